@@ -1,0 +1,243 @@
+#!/usr/bin/env python3
+"""bench.py — RHO radix hash join (+ predicate scan) on MI355X, BASELINE.json's metric.
+
+Step = one full RHO join (partition pass 1 + pass 2 + build/probe, count-only) over
+|R| = |S| = 2^28 uniform tuples per GPU (BASELINE config 2; weak scaling: with N GPUs
+the global relations are N * 2^28 and are radix-sharded with one RCCL all-to-all per
+relation, sgxamd.dist).  Inputs are resident in HBM before the timed region.
+
+One JSON line (rank 0):
+  value = probed tuples (|S|, all ranks) per second over the whole join, in millions;
+  roofline = the dominant kernel's algorithmic bytes / its HIP-event time vs 8 TB/s;
+  cpu_baseline = the oracle's restated reference RHO (oracle/rho_oracle.c, pthreads)
+  on a bounded sample of reference-generated relations on this host's cores.
+The scan (BASELINE config 3: 2^30 int32, 10 % selectivity) is measured in the same run
+and reported under "scan".
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "sgxv2-analytical-query-processing-benchmarks_amd")
+sys.path.insert(0, os.path.join(PKG, "python"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+METRIC = "M probed tuples/sec (RHO join) + scan GB/s vs HBM roofline, 1/2/4/8 MI355X"
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic_r01.json")
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def algorithmic_bytes(kernel: str, nR: int, nS: int) -> int:
+    """Bytes a kernel must move per launch (DESIGN.md 'Kernels and their rooflines')."""
+    n = nR if kernel.startswith("R_") else nS
+    if kernel.endswith("_hist"):
+        return 8 * n          # read every tuple once (key only used, AoS line read)
+    if kernel.endswith("_scatter"):
+        return 16 * n         # read + write every tuple
+    if kernel == "join_build_probe":
+        return 8 * (nR + nS)  # every partitioned tuple read once
+    return 0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--log2n", type=int, default=28, help="per-GPU |R| = |S| = 2^log2n")
+    ap.add_argument("--no-scan", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import sgxamd
+    from sgxamd.dist import sharded_rho_join
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    def max_over_ranks(x: float) -> float:
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    stream = torch.cuda.current_stream().cuda_stream
+    sgxamd.set_stream(stream)
+
+    # ---------------- RHO workload: rank slice of global pk(N n) and fk(N n, N n)
+    n = 1 << args.log2n
+    N_glob = n * world
+    R = torch.empty(n, dtype=torch.int64, device=dev)
+    S = torch.empty(n, dtype=torch.int64, device=dev)
+    sgxamd.gen_pk_dev(R, n, rank * n, N_glob, 11111, stream)
+    sgxamd.gen_fk_dev(S, n, rank * n, N_glob, 22222, stream)
+    torch.cuda.synchronize()
+
+    def step():
+        return sharded_rho_join(R, S)
+
+    for _ in range(args.warmup):
+        res = step()
+        assert res.matches == N_glob, (res.matches, N_glob)
+    barrier()
+    per_kernel: dict[str, list[float]] = {}
+    results = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+        results.append(res)
+        for name, ms in sgxamd.timings():
+            per_kernel.setdefault(name, []).append(ms)
+    barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0)
+    ok = all(r.matches == N_glob for r in results)
+    value = N_glob * args.steps / elapsed / 1e6  # M probed tuples/s, all ranks
+    ms_per_step = elapsed / args.steps * 1e3
+
+    # roofline of the dominant kernel (this rank's event times; rank 0 reports)
+    nR = results[-1].recv_r
+    nS = results[-1].recv_s
+    avg = {k: statistics.mean(v) for k, v in per_kernel.items()}
+    byte_kernels = {k: v for k, v in avg.items() if algorithmic_bytes(k, nR, nS) > 0}
+    dom = max(byte_kernels, key=byte_kernels.get)
+    achieved = algorithmic_bytes(dom, nR, nS) / (avg[dom] * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(TRAFFIC_FILE):
+        try:
+            tf = json.load(open(TRAFFIC_FILE))
+            if tf.get("log2n") == args.log2n and dom in tf.get("bytes_per_launch", {}):
+                traffic = tf["bytes_per_launch"][dom]
+        except (OSError, ValueError):
+            traffic = None
+    roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "avg_ms": round(avg[dom], 4), "algorithmic_bytes": algorithmic_bytes(dom, nR, nS)}
+    probe_gbs = algorithmic_bytes("join_build_probe", nR, nS) / (avg["join_build_probe"] * 1e-3) / 1e9
+    phase = {k: round(v, 4) for k, v in sorted(avg.items())}
+    ls = results[-1].local_stats
+    rho_info = {
+        "matches_ok": ok, "matches": results[-1].matches,
+        "M_rec_per_s_reference_formula": round(2 * N_glob * args.steps / elapsed / 1e6, 1),
+        "probe_phase_M_probed_tuples_per_s": round(nS / (avg["join_build_probe"] * 1e-3) / 1e6, 1),
+        "probe_roofline": {"achieved": round(probe_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": round(probe_gbs / HBM_PEAK_GBS, 4)},
+        "kernel_ms_avg": phase,
+        "radix_bits": ls.get("radix_bits"), "passes": ls.get("passes"),
+        "step_ms_breakdown": {k: round(v, 3) for k, v in results[-1].ms.items()},
+    }
+    del R, S
+    torch.cuda.empty_cache()
+
+    # ---------------- scan (BASELINE config 3): 2^30 int32, [0, 26] = 10 % (types.hpp:134)
+    scan_info = None
+    if not args.no_scan:
+        ns = 1 << 30
+        col = torch.empty(ns, dtype=torch.int32, device=dev)
+        sgxamd.gen_scan_dev(col, ns, 0, 0, "i32", stream)
+        exp = ns // 256 * 27
+        bv = torch.empty(ns // 64, dtype=torch.int64, device=dev)
+        idx = torch.empty(exp, dtype=torch.int64, device=dev)
+        scan_info = {"rows": ns, "dtype": "i32", "predicate": [0, 26], "matches": exp}
+        for kind in ("count", "bitvector", "index"):
+            def run():
+                if kind == "count":
+                    assert sgxamd.scan_count(0, 26, col, ns) == exp
+                elif kind == "bitvector":
+                    sgxamd.scan_bitvector(0, 26, col, ns, bv)
+                else:
+                    assert sgxamd.scan_index(0, 26, col, ns, idx, exp) == exp
+            for _ in range(max(1, args.warmup)):
+                run()
+            barrier()
+            kt = {}
+            t1 = time.perf_counter()
+            for _ in range(args.steps):
+                run()
+                for name, ms in sgxamd.timings():
+                    kt.setdefault(name, []).append(ms)
+            barrier()
+            el = max_over_ranks(time.perf_counter() - t1)
+            out_bytes = {"count": 0, "bitvector": ns // 8, "index": 8 * exp}[kind]
+            scan_info[kind] = {
+                "input_GB_per_s": round(world * 4 * ns * args.steps / el / 1e9, 1),
+                "total_GB_per_s": round(world * (4 * ns + out_bytes) * args.steps / el / 1e9, 1),
+                "ms_per_call": round(el / args.steps * 1e3, 4),
+                "kernel_ms_avg": {k: round(statistics.mean(v), 4) for k, v in kt.items()},
+            }
+        pk = "scan_bitvector"
+        k_ms = scan_info["bitvector"]["kernel_ms_avg"].get(pk)
+        if k_ms:
+            gbs = (4 * ns + ns // 8) / (k_ms * 1e-3) / 1e9
+            scan_info["bitvector_kernel_roofline"] = {"achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+                                                      "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4)}
+        del col, bv, idx
+        torch.cuda.empty_cache()
+
+    # ---------------- CPU baseline: restated reference RHO on this host, rank 0 at N=1
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+
+        threads = args.cpu_threads
+        cn = 1 << 26
+        Rh, Sh = sgxamd.reference_relations(cn, cn, nthreads=threads)
+        tp = []
+        t_start = time.perf_counter()
+        while time.perf_counter() - t_start < args.cpu_seconds and len(tp) < 30:
+            m, t = oracle.rho_join(Rh, Sh, threads)
+            assert m == cn
+            tp.append(cn / t["s_total"] / 1e6)
+        cpu = {"value": round(statistics.median(tp), 1), "unit": "M probed tuples/s", "cores": threads,
+               "kind": "port",
+               "sample": f"oracle RHO (radix_join.cpp restated, pthreads) on reference-generated "
+                         f"pk/fk |R|=|S|=2^26 (native.cpp seeds), median of {len(tp)} joins",
+               "M_rec_per_s_reference_formula": round(2 * statistics.median(tp), 1)}
+        del Rh, Sh
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "M probed tuples/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic: device-generated pk (shuffled 1..N) and fk (shuffled 1..N) relations, "
+                    "8-byte {key, payload} tuples",
+            "config": {"workload": f"RHO join |R|=|S|=2^{args.log2n} uniform per GPU (BASELINE config 2)",
+                       "global_R": N_glob, "global_S": N_glob, "parallelism": f"radix-shard{world}"},
+            "roofline": roofline, "cpu_baseline": cpu, "rho": rho_info, "scan": scan_info,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

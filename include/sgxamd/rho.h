@@ -1,0 +1,114 @@
+/*
+ * sgxamd/rho.h — C-ABI of the MI355X radix hash join (RHO).
+ *
+ * Drop-in boundary.  The reference exposes RHO as
+ *     result_t *RHO(const table_t *relR, const table_t *relS, const joinconfig_t *config);
+ * (Join-Benchmarks/lib/Joins/include/radix/radix_join.h:29-30, implemented at
+ *  lib/Joins/src/radix/radix_join.cpp:1640-1643) and dispatches it by name through
+ *     void run_join(result_t*, const table_t*, const table_t*, const char*, const joinconfig_t*);
+ * (lib/Joins/src/joins.cpp:55-78, table entry {"RHO", RHO} at :42).
+ *
+ * This header declares the plain-C entry points a cgo / ctypes / JNI binding
+ * would bind.  The C++-linkage adapters with the reference's exact (mangled)
+ * signatures, RHO() and run_join(), live in sgxamd/joins.hpp.
+ *
+ * Pointers: every tuple pointer may be host memory or device (hipMalloc /
+ * torch) memory; the library classifies it with hipPointerGetAttributes and
+ * stages host buffers through HBM.  All calls are blocking, like the reference.
+ */
+#ifndef SGXAMD_RHO_H
+#define SGXAMD_RHO_H
+
+#include "sgxamd/data_types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Status codes returned by every mi355_* entry point (0 = success). */
+#define MI355_OK 0
+#define MI355_ERR_INVALID (-1)   /* bad argument (null pointer, size, capacity) */
+#define MI355_ERR_NO_DEVICE (-2) /* no gfx950 device visible */
+#define MI355_ERR_HIP (-3)       /* a HIP runtime call failed; see mi355_last_error() */
+#define MI355_ERR_OOM (-4)       /* device allocation failed */
+#define MI355_ERR_CAPACITY (-5)  /* output buffer too small; required size reported */
+
+/* Options of one join call (NULL = defaults). */
+typedef struct mi355_rho_opts {
+    int radix_bits;      /* total radix bits; 0 = GPU policy (DESIGN.md "partitioning policy") */
+    int passes;          /* 1 or 2; 0 = policy */
+    uint32_t key_shift;  /* low key bits already fixed by a shard exchange (multi-GPU); 0 otherwise */
+    int materialize;     /* reserved (count-only in this round); must be 0 */
+    int timing;          /* 1 = record per-kernel HIP events (mi355_timing_* below) */
+    int reserved;
+    void *stream;        /* hipStream_t to launch on; NULL = the library's stream */
+} mi355_rho_opts;
+
+/* What one join call did. */
+typedef struct mi355_rho_stats {
+    uint64_t matches;         /* join cardinality (bit-exact vs the reference's totalresults) */
+    uint32_t radix_bits;      /* total bits used */
+    uint32_t passes;          /* partition passes */
+    uint32_t pass1_bits;
+    uint32_t pass2_bits;
+    uint64_t num_partitions;  /* 2^radix_bits */
+    uint64_t num_tasks;       /* build/probe tasks (partition x S-chunk) */
+    uint64_t max_part_r;      /* largest R partition (tuples) */
+    uint64_t max_part_s;      /* largest S partition (tuples) */
+    double ms_h2d;            /* host->device staging (0 when inputs were resident) */
+    double ms_partition;      /* partition phase (pass 1 + pass 2), device time */
+    double ms_pass1;
+    double ms_pass2;
+    double ms_join;           /* build + probe ("Build+Join Overall"), device time */
+    double ms_total;          /* partition + join, device time */
+} mi355_rho_stats;
+
+/* Number of gfx950 devices visible (0 on a CPU-only host). */
+int mi355_device_count(void);
+
+/* Text of the last error on this thread. */
+const char *mi355_last_error(void);
+
+/* Library version string. */
+const char *mi355_version(void);
+
+/*
+ * RHO join with the reference's semantics (count-only, MATERIALIZE must be 0).
+ * Replaces RHO() at radix_join.cpp:1640 / radix_join.h:29.  Fills out->totalresults,
+ * nthreads (= config->NTHREADS), materialized, result (NULL), result_type (0) and
+ * throughput (M rec/s = (|R|+|S|) / join time, which the reference leaves unset).
+ */
+int mi355_rho_join(const struct table_t *relR, const struct table_t *relS,
+                   const struct joinconfig_t *config, struct result_t *out);
+
+/* Same join on raw tuple arrays with explicit options and per-phase statistics. */
+int mi355_rho_join_ex(const struct row_t *R, uint64_t nR, const struct row_t *S, uint64_t nS,
+                      const mi355_rho_opts *opts, mi355_rho_stats *stats);
+
+/*
+ * Multi-GPU shard step: stable radix partition of n device-resident tuples by
+ * destination d = (key >> key_shift) & (2^dest_bits - 1) into `out` (device,
+ * n tuples), destination-major.  dest_counts (host, 2^dest_bits entries) receives
+ * the tuple count per destination, i.e. the send split of the all-to-all.
+ */
+int mi355_rho_shard_partition(const struct row_t *in, uint64_t n, uint32_t key_shift,
+                              uint32_t dest_bits, struct row_t *out, uint64_t *dest_counts,
+                              void *stream);
+
+/*
+ * Per-kernel timing of the last call on this thread that ran with timing
+ * enabled (opts->timing or mi355_timing_enable(1)): names and milliseconds
+ * of every recorded kernel, in launch order.  Returns the number of records
+ * (up to `cap` are copied).
+ */
+void mi355_timing_enable(int on);
+int mi355_timing_get(const char **names, double *ms, int cap);
+
+/* Stream used by calls that take no explicit stream (NULL = library stream). */
+void mi355_set_stream(void *stream);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* SGXAMD_RHO_H */

@@ -1,0 +1,59 @@
+/*
+ * sgxamd/scan.h — C-ABI of the MI355X predicate column scan.
+ *
+ * Replaces the reference's AVX-512 scan functions in namespace SIMD512
+ * (Scan-Micro-Benchmarks/shared_libraries/SimdScan/include/SIMD512.hpp:39-84,
+ *  implemented in src/SIMD512.cpp):
+ *   count                          SIMD512.cpp:7-32    -> mi355_scan_count_*
+ *   bitvector_scan                 SIMD512.cpp:210-222 -> mi355_scan_bitvector_*
+ *   implicit_index_scan(_self_alloc) SIMD512.cpp:225-287 -> mi355_scan_index_*
+ *   scan (value materialisation)   SIMD512.cpp:91-150  -> mi355_scan_values_*
+ * Predicate semantics: lo <= v <= hi, inclusive; unsigned compare for u8
+ * (_mm512_cmpge_epu8_mask / cmple), signed compare for i32.
+ *
+ * Unlike the AVX-512 code, which silently ignores the n % 64 tail
+ * (loops run to input_size / 64), these entry points scan all n values.  The
+ * header-only C++ adapter sgxamd/SIMD512_mi355.hpp restores the reference's
+ * tail behaviour for drop-in callers.
+ *
+ * Pointers may be host or device memory (classified per call).  Blocking.
+ */
+#ifndef SGXAMD_SCAN_H
+#define SGXAMD_SCAN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Number of values v[i] with lo <= v[i] <= hi. */
+int mi355_scan_count_u8(uint8_t lo, uint8_t hi, const uint8_t *in, size_t n, uint64_t *count);
+int mi355_scan_count_i32(int32_t lo, int32_t hi, const int32_t *in, size_t n, uint64_t *count);
+
+/* One bit per row: bit j of word i <-> row 64*i + j (the _store_mask64 layout,
+ * SIMD512.cpp:219).  out holds ceil(n/64) words; bits past n are zero. */
+int mi355_scan_bitvector_u8(uint8_t lo, uint8_t hi, const uint8_t *in, size_t n, uint64_t *out_words);
+int mi355_scan_bitvector_i32(int32_t lo, int32_t hi, const int32_t *in, size_t n, uint64_t *out_words);
+
+/* Ascending uint64 row indexes (relative to `in`) of all matches.  Writes at
+ * most cap indexes; *n_out = number of matches.  Returns MI355_ERR_CAPACITY
+ * (with *n_out set) when cap < matches. */
+int mi355_scan_index_u8(uint8_t lo, uint8_t hi, const uint8_t *in, size_t n,
+                        uint64_t *out, size_t cap, uint64_t *n_out);
+int mi355_scan_index_i32(int32_t lo, int32_t hi, const int32_t *in, size_t n,
+                         uint64_t *out, size_t cap, uint64_t *n_out);
+
+/* Matching values in row order: u8 codes zero-extended to uint32 (SIMD512::scan),
+ * i32 values as int32. */
+int mi355_scan_values_u8(uint8_t lo, uint8_t hi, const uint8_t *in, size_t n,
+                         uint32_t *out, size_t cap, uint64_t *n_out);
+int mi355_scan_values_i32(int32_t lo, int32_t hi, const int32_t *in, size_t n,
+                          int32_t *out, size_t cap, uint64_t *n_out);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* SGXAMD_SCAN_H */

@@ -1,0 +1,80 @@
+/*
+ * oracle/oracle.h — CPU restatement of the reference's hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (the HIP library under
+ * sgxv2-analytical-query-processing-benchmarks_amd/) links or calls this code.
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg load
+ * liboracle.so, and only as the checker / the timed CPU baseline.
+ *
+ * Pinning (see DESIGN.md "Oracle"): building or running the reference itself
+ * was denied in this pipeline, so there is no oracle/_ref.
+ * The join restatement is pinned by the analytical known-answer tests derived
+ * from the reference's generators (pk ⋈ fk → |S|, fk_sel jump rule, Zipf → |S|)
+ * and by an independent sort-merge cardinality counter; the scan restatement
+ * by the reference's own Catch2 KATs (testsimdscan.cpp: count = N/256 · width
+ * over the i % 256 column).  Join parity is therefore "pinned by KATs", not by
+ * reference-produced golden vectors.
+ */
+#ifndef SGXAMD_ORACLE_H
+#define SGXAMD_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "sgxamd/data_types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct oracle_rho_timing {
+    uint32_t radix_bits;
+    uint32_t passes;
+    uint64_t join_tasks;
+    double s_total;      /* max over threads of total_timer (radix_join.cpp:1108,1353) */
+    double s_partition;  /* partitioning_total_timer */
+    double s_pass1;
+    double s_pass2;
+    double s_join;       /* join_total_timer ("Build+Join Overall") */
+} oracle_rho_timing;
+
+/* radix_join.cpp:295-317 (L2_CACHE_SIZE 1280 KiB, CACHE_DIVISOR 4). */
+uint32_t oracle_calc_num_radix_bits(uint64_t num_r, uint64_t nthreads);
+/* radix_join.cpp:319-329 */
+uint32_t oracle_calc_num_passes(uint32_t num_radix_bits);
+
+/*
+ * RHO = join_init_run(R, S, bucket_chaining_join, cfg) (radix_join.cpp:1369-1643),
+ * count-only, with nthreads pthreads.  force_two_passes mirrors -DFORCE_2_PHASES.
+ * Returns the match count (the reference's result_t.totalresults).
+ */
+int64_t oracle_rho_join(const struct row_t *R, uint64_t nR, const struct row_t *S, uint64_t nS,
+                        int nthreads, int force_two_passes, oracle_rho_timing *timing);
+
+/* Independent check: sum_k cnt_R(k) * cnt_S(k) by sorting the keys. */
+int64_t oracle_count_join_sort(const struct row_t *R, uint64_t nR, const struct row_t *S, uint64_t nS);
+
+/* Stable single-pass radix partition of `in` by bin = (key >> shift) & (2^bits-1)
+ * with the reference's per-thread histogram/offset rule (radix_join.cpp:851-931)
+ * for `nthreads` contiguous slices, without padding.  out: n tuples;
+ * bin_start: 2^bits + 1 entries. */
+void oracle_radix_partition(const struct row_t *in, uint64_t n, int nthreads, uint32_t shift,
+                            uint32_t bits, struct row_t *out, uint64_t *bin_start);
+
+/* Scalar scans (SIMD512.cpp:7-32, 210-287; ScalarScan.hpp:8-18) over all n values. */
+uint64_t oracle_scan_count_u8(uint8_t lo, uint8_t hi, const uint8_t *in, size_t n);
+uint64_t oracle_scan_count_i32(int32_t lo, int32_t hi, const int32_t *in, size_t n);
+void oracle_scan_bitvector_u8(uint8_t lo, uint8_t hi, const uint8_t *in, size_t n, uint64_t *out);
+void oracle_scan_bitvector_i32(int32_t lo, int32_t hi, const int32_t *in, size_t n, uint64_t *out);
+uint64_t oracle_scan_index_u8(uint8_t lo, uint8_t hi, const uint8_t *in, size_t n, uint64_t *out);
+uint64_t oracle_scan_index_i32(int32_t lo, int32_t hi, const int32_t *in, size_t n, uint64_t *out);
+uint64_t oracle_scan_values_u8(uint8_t lo, uint8_t hi, const uint8_t *in, size_t n, uint32_t *out);
+uint64_t oracle_scan_values_i32(int32_t lo, int32_t hi, const int32_t *in, size_t n, int32_t *out);
+/* Multithreaded count for the CPU baseline (contiguous slices, like scan_wrapper). */
+uint64_t oracle_scan_count_i32_mt(int32_t lo, int32_t hi, const int32_t *in, size_t n, int nthreads);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SGXAMD_ORACLE_H */

@@ -1,0 +1,119 @@
+"""ctypes wrapper of liboracle.so — the CPU restatement of the reference's RHO join
+and predicate scans (oracle/rho_oracle.c, oracle/scan_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py, as the checker / the timed CPU baseline.  The
+product (libsgxamd.so and its Python binding) never imports this module.
+Parity pinning: see oracle.h and DESIGN.md ("Oracle").
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def _load() -> C.CDLL:
+    if not os.path.exists(LIB):
+        build()
+    lib = C.CDLL(LIB)
+    P = C.c_void_p
+    U64P = C.POINTER(C.c_uint64)
+
+    class Timing(C.Structure):
+        _fields_ = [("radix_bits", C.c_uint32), ("passes", C.c_uint32), ("join_tasks", C.c_uint64),
+                    ("s_total", C.c_double), ("s_partition", C.c_double), ("s_pass1", C.c_double),
+                    ("s_pass2", C.c_double), ("s_join", C.c_double)]
+
+    lib.Timing = Timing
+    sig = {
+        "oracle_calc_num_radix_bits": (C.c_uint32, [C.c_uint64, C.c_uint64]),
+        "oracle_calc_num_passes": (C.c_uint32, [C.c_uint32]),
+        "oracle_rho_join": (C.c_int64, [P, C.c_uint64, P, C.c_uint64, C.c_int, C.c_int, C.POINTER(Timing)]),
+        "oracle_count_join_sort": (C.c_int64, [P, C.c_uint64, P, C.c_uint64]),
+        "oracle_radix_partition": (None, [P, C.c_uint64, C.c_int, C.c_uint32, C.c_uint32, P, U64P]),
+        "oracle_scan_count_u8": (C.c_uint64, [C.c_uint8, C.c_uint8, P, C.c_size_t]),
+        "oracle_scan_count_i32": (C.c_uint64, [C.c_int32, C.c_int32, P, C.c_size_t]),
+        "oracle_scan_bitvector_u8": (None, [C.c_uint8, C.c_uint8, P, C.c_size_t, P]),
+        "oracle_scan_bitvector_i32": (None, [C.c_int32, C.c_int32, P, C.c_size_t, P]),
+        "oracle_scan_index_u8": (C.c_uint64, [C.c_uint8, C.c_uint8, P, C.c_size_t, P]),
+        "oracle_scan_index_i32": (C.c_uint64, [C.c_int32, C.c_int32, P, C.c_size_t, P]),
+        "oracle_scan_values_u8": (C.c_uint64, [C.c_uint8, C.c_uint8, P, C.c_size_t, P]),
+        "oracle_scan_values_i32": (C.c_uint64, [C.c_int32, C.c_int32, P, C.c_size_t, P]),
+        "oracle_scan_count_i32_mt": (C.c_uint64, [C.c_int32, C.c_int32, P, C.c_size_t, C.c_int]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def _p(a) -> int:
+    if hasattr(a, "data_ptr"):
+        return a.data_ptr()
+    return a.ctypes.data
+
+
+def rho_join(R, S, nthreads: int = 1, force_two_passes: bool = False) -> tuple[int, dict]:
+    """Reference RHO (count-only) on numpy row_t arrays; returns (matches, timing)."""
+    t = lib.Timing()
+    m = lib.oracle_rho_join(_p(R), len(R), _p(S), len(S), nthreads, 1 if force_two_passes else 0, C.byref(t))
+    return int(m), {f: getattr(t, f) for f, _ in t._fields_}
+
+
+def count_join_sort(R, S) -> int:
+    return int(lib.oracle_count_join_sort(_p(R), len(R), _p(S), len(S)))
+
+
+def calc_num_radix_bits(num_r: int, nthreads: int) -> int:
+    return int(lib.oracle_calc_num_radix_bits(num_r, nthreads))
+
+
+def calc_num_passes(bits: int) -> int:
+    return int(lib.oracle_calc_num_passes(bits))
+
+
+def radix_partition(inp, nthreads: int, shift: int, bits: int):
+    import numpy as np
+
+    out = np.empty_like(inp)
+    starts = np.zeros((1 << bits) + 1, dtype=np.uint64)
+    lib.oracle_radix_partition(_p(inp), len(inp), nthreads, shift, bits, _p(out),
+                               starts.ctypes.data_as(C.POINTER(C.c_uint64)))
+    return out, starts
+
+
+def scan(kind: str, dtype: str, lo: int, hi: int, col):
+    """kind in count/bitvector/index/values; dtype u8/i32; col a numpy array."""
+    import numpy as np
+
+    n = len(col)
+    fn = getattr(lib, f"oracle_scan_{kind}_{dtype}")
+    if kind == "count":
+        return int(fn(lo, hi, _p(col), n))
+    if kind == "bitvector":
+        out = np.zeros((n + 63) // 64, dtype=np.uint64)
+        fn(lo, hi, _p(col), n, _p(out))
+        return out
+    if kind == "index":
+        out = np.empty(max(n, 1), dtype=np.uint64)
+        k = fn(lo, hi, _p(col), n, _p(out))
+        return out[:k]
+    out = np.empty(max(n, 1), dtype=np.uint32 if dtype == "u8" else np.int32)
+    k = fn(lo, hi, _p(col), n, _p(out))
+    return out[:k]
+
+
+def scan_count_mt(lo: int, hi: int, col, nthreads: int) -> int:
+    return int(lib.oracle_scan_count_i32_mt(lo, hi, _p(col), len(col), nthreads))

@@ -1,0 +1,110 @@
+/*
+ * oracle/scan_oracle.c — scalar restatement of the reference's predicate scans.
+ *
+ * TEST INFRASTRUCTURE ONLY (see oracle.h).
+ *
+ * Semantics follow Scan-Micro-Benchmarks/shared_libraries/SimdScan/src/SIMD512.cpp:
+ *   count            :7-32     popcount of (v >= lo) & (v <= hi), unsigned bytes
+ *   bitvector_scan   :210-222  bit j of word i <-> row 64i+j (_store_mask64)
+ *   implicit_index_scan(_self_alloc) :225-287  ascending row indexes (uint64)
+ *   scan             :91-150   matching values zero-extended to uint32
+ * and the scalar driver mode microbenchmarks/SimdScanMulti/shared/ScalarScan.hpp:8-18.
+ * All n values are scanned (the AVX-512 code drops the n % 64 tail; callers
+ * that want that pass n rounded down).  i32 variants compare signed.
+ */
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "oracle.h"
+
+#define PRED(v) ((v) >= lo && (v) <= hi)
+
+uint64_t oracle_scan_count_u8(uint8_t lo, uint8_t hi, const uint8_t *in, size_t n) {
+    uint64_t c = 0;
+    for (size_t i = 0; i < n; i++) c += PRED(in[i]);
+    return c;
+}
+
+uint64_t oracle_scan_count_i32(int32_t lo, int32_t hi, const int32_t *in, size_t n) {
+    uint64_t c = 0;
+    for (size_t i = 0; i < n; i++) c += PRED(in[i]);
+    return c;
+}
+
+void oracle_scan_bitvector_u8(uint8_t lo, uint8_t hi, const uint8_t *in, size_t n, uint64_t *out) {
+    memset(out, 0, ((n + 63) / 64) * sizeof(uint64_t));
+    for (size_t i = 0; i < n; i++)
+        if (PRED(in[i])) out[i / 64] |= 1ull << (i % 64);
+}
+
+void oracle_scan_bitvector_i32(int32_t lo, int32_t hi, const int32_t *in, size_t n, uint64_t *out) {
+    memset(out, 0, ((n + 63) / 64) * sizeof(uint64_t));
+    for (size_t i = 0; i < n; i++)
+        if (PRED(in[i])) out[i / 64] |= 1ull << (i % 64);
+}
+
+uint64_t oracle_scan_index_u8(uint8_t lo, uint8_t hi, const uint8_t *in, size_t n, uint64_t *out) {
+    uint64_t k = 0;
+    for (size_t i = 0; i < n; i++)
+        if (PRED(in[i])) out[k++] = i;
+    return k;
+}
+
+uint64_t oracle_scan_index_i32(int32_t lo, int32_t hi, const int32_t *in, size_t n, uint64_t *out) {
+    uint64_t k = 0;
+    for (size_t i = 0; i < n; i++)
+        if (PRED(in[i])) out[k++] = i;
+    return k;
+}
+
+uint64_t oracle_scan_values_u8(uint8_t lo, uint8_t hi, const uint8_t *in, size_t n, uint32_t *out) {
+    uint64_t k = 0;
+    for (size_t i = 0; i < n; i++)
+        if (PRED(in[i])) out[k++] = in[i];
+    return k;
+}
+
+uint64_t oracle_scan_values_i32(int32_t lo, int32_t hi, const int32_t *in, size_t n, int32_t *out) {
+    uint64_t k = 0;
+    for (size_t i = 0; i < n; i++)
+        if (PRED(in[i])) out[k++] = in[i];
+    return k;
+}
+
+typedef struct {
+    int32_t lo, hi;
+    const int32_t *in;
+    size_t n;
+    uint64_t result;
+} count_arg;
+
+static void *count_worker(void *p) {
+    count_arg *a = (count_arg *)p;
+    a->result = oracle_scan_count_i32(a->lo, a->hi, a->in, a->n);
+    return NULL;
+}
+
+/* Contiguous per-thread slices as in scan_wrapper (multithreadedscan.cpp:227-236). */
+uint64_t oracle_scan_count_i32_mt(int32_t lo, int32_t hi, const int32_t *in, size_t n, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    pthread_t *th = (pthread_t *)calloc(nthreads, sizeof(pthread_t));
+    count_arg *args = (count_arg *)calloc(nthreads, sizeof(count_arg));
+    size_t per = n / nthreads;
+    for (int t = 0; t < nthreads; t++) {
+        args[t].lo = lo;
+        args[t].hi = hi;
+        args[t].in = in + t * per;
+        args[t].n = (t == nthreads - 1) ? n - t * per : per;
+        pthread_create(&th[t], NULL, count_worker, &args[t]);
+    }
+    uint64_t total = 0;
+    for (int t = 0; t < nthreads; t++) {
+        pthread_join(th[t], NULL);
+        total += args[t].result;
+    }
+    free(th);
+    free(args);
+    return total;
+}

@@ -1,0 +1,98 @@
+// Shared host/device helpers for the MI355X (gfx950) kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+namespace sgxamd {
+
+constexpr int kWave = 64;  // CDNA wavefront width (never 32)
+
+// ---------------------------------------------------------------- device ---
+
+__device__ __forceinline__ uint64_t lanemask_lt() {
+    const uint32_t lane = __lane_id();
+    return lane == 0 ? 0ull : (~0ull >> (64 - lane));
+}
+
+__device__ __forceinline__ uint32_t popc64(uint64_t x) { return __popcll(x); }
+
+// Sum of a 64-bit value over the wave (result valid in every lane).
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+    return v;
+}
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+    return v;
+}
+
+// Inclusive prefix sum over the wave.
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
+    const uint32_t lane = __lane_id();
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+        uint32_t t = __shfl_up(v, off, kWave);
+        if (lane >= (uint32_t)off) v += t;
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint64_t wave_incl_scan_u64(uint64_t v) {
+    const uint32_t lane = __lane_id();
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+        uint64_t t = __shfl_up(v, off, kWave);
+        if (lane >= (uint32_t)off) v += t;
+    }
+    return v;
+}
+
+// Block-wide exclusive scan of one u64 per thread (blockDim.x <= 1024, multiple of 64).
+// `scratch` must hold blockDim.x / 64 + 1 entries.  Returns the exclusive prefix;
+// *total receives the block sum.  Contains __syncthreads().
+__device__ __forceinline__ uint64_t block_excl_scan_u64(uint64_t v, uint64_t *scratch, uint64_t *total) {
+    const uint32_t lane = __lane_id();
+    const uint32_t wave = threadIdx.x / kWave;
+    const uint32_t nwaves = blockDim.x / kWave;
+    uint64_t incl = wave_incl_scan_u64(v);
+    if (lane == kWave - 1) scratch[wave] = incl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t acc = 0;
+        for (uint32_t w = 0; w < nwaves; ++w) {
+            uint64_t t = scratch[w];
+            scratch[w] = acc;
+            acc += t;
+        }
+        scratch[nwaves] = acc;
+    }
+    __syncthreads();
+    uint64_t r = scratch[wave] + incl - v;
+    *total = scratch[nwaves];
+    __syncthreads();
+    return r;
+}
+
+// ------------------------------------------------------------------ host ---
+
+// Thread-local error text, exposed through mi355_last_error().
+void set_last_error(const std::string &msg);
+const char *last_error();
+
+}  // namespace sgxamd
+
+// Evaluate a HIP call; on failure record the error and return MI355_ERR_HIP.
+#define SGX_HIP(call)                                                                     \
+    do {                                                                                  \
+        hipError_t _e = (call);                                                           \
+        if (_e != hipSuccess) {                                                           \
+            ::sgxamd::set_last_error(std::string(#call) + ": " + hipGetErrorString(_e)); \
+            return (_e == hipErrorOutOfMemory) ? MI355_ERR_OOM : MI355_ERR_HIP;          \
+        }                                                                                 \
+    } while (0)

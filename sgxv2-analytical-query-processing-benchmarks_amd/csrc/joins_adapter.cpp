@@ -1,0 +1,96 @@
+// C++-linkage drop-ins RHO() and run_join() (declared in sgxamd/joins.hpp).
+//
+// RHO: radix_join.cpp:1640-1643 -> mi355_rho_join, plus the reference's
+//      print_timing log lines (radix_join.cpp:252-293) so that
+//      SGXv2Scripts/scripts/helpers/runner.py:14-55 parses our output unchanged.
+// run_join: joins.cpp:55-78 (strcmp lookup in an algorithm table, memcpy of the
+//      result; like the reference, the callee's result_t is not freed).
+#include <chrono>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+#include "sgxamd/joins.hpp"
+#include "sgxamd/rho.h"
+
+namespace {
+
+const auto g_log_start = std::chrono::steady_clock::now();
+
+// Logger.cpp:53-76 format: "<color>[%8.4f][%5s] msg<reset>\n"
+void logger(const char *level, const char *color, const char *fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    const double t = std::chrono::duration<double>(std::chrono::steady_clock::now() - g_log_start).count();
+    std::printf("%s[%8.4f][%5s] %s\x1b[0m\n", color, t, level, buf);
+}
+
+#define LOG_INFO(...) logger("INFO", "\x1b[32m", __VA_ARGS__)
+#define LOG_ERROR(...) logger("ERROR", "\x1b[31m", __VA_ARGS__)
+
+uint64_t cpms() {  // CYCLES_PER_MICROSECOND of the reference build (J/CMakeLists.txt:17)
+    const char *e = std::getenv("SGXAMD_CPMS");
+    return e ? std::strtoull(e, nullptr, 10) : 2900ull;
+}
+
+const algorithm_t mi355_algorithms[] = {
+    {"RHO", RHO},
+    {"", nullptr},
+};
+
+}  // namespace
+
+result_t *RHO(const table_t *relR, const table_t *relS, const joinconfig_t *config) {
+    mi355_rho_stats st{};
+    LOG_INFO("Running RHO on MI355X (%s)", mi355_version());
+    const int rc = mi355_rho_join_ex(relR->tuples, relR->num_tuples, relS->tuples, relS->num_tuples, nullptr, &st);
+    if (rc != MI355_OK) {
+        LOG_ERROR("RHO failed (%d): %s", rc, mi355_last_error());
+        std::exit(EXIT_FAILURE);
+    }
+    auto *res = static_cast<result_t *>(std::malloc(sizeof(result_t)));
+    const uint64_t num = relR->num_tuples + relS->num_tuples;
+    const double us = st.ms_total * 1000.0;
+    res->totalresults = static_cast<int64_t>(st.matches);
+    res->nthreads = config ? config->NTHREADS : 1;
+    res->throughput = us > 0 ? num / us : 0.0;
+    res->materialized = 0;
+    res->result = nullptr;
+    res->result_type = 0;
+
+    const uint64_t C = cpms();
+    auto cyc = [&](double ms) { return static_cast<unsigned long>(ms * 1000.0 * C); };
+    LOG_INFO("Running RHO with %u passes and %u radix bits", st.passes, st.radix_bits);
+    LOG_INFO("Total input tuples : %lu", (unsigned long)num);
+    LOG_INFO("Result tuples : %ld", (long)st.matches);
+    LOG_INFO("Total Join Time (cycles)    : %lu", cyc(st.ms_total));
+    LOG_INFO("Partition Overall (cycles)  : %lu", cyc(st.ms_partition));
+    LOG_INFO("Partition Pass One (cycles) : %lu", cyc(st.ms_pass1));
+    LOG_INFO("Partition Pass Two (cycles) : %lu", cyc(st.ms_pass2));
+    LOG_INFO("Build+Join Overall (cycles) : %lu", cyc(st.ms_join));
+    LOG_INFO("Pure Join Runtime (us) : %lu ", (unsigned long)us);
+    LOG_INFO("Throughput (M rec/sec) : %.2lf", res->throughput);
+    LOG_INFO("Host->device staging (us) : %lu ", (unsigned long)(st.ms_h2d * 1000.0));
+    return res;
+}
+
+void run_join(result_t *res, const table_t *relR, const table_t *relS, const char *algorithm_name,
+              const joinconfig_t *config) {
+    const algorithm_t *alg = nullptr;
+    for (int i = 0; mi355_algorithms[i].join; ++i) {
+        if (std::strcmp(algorithm_name, mi355_algorithms[i].name) == 0) {
+            alg = &mi355_algorithms[i];
+            break;
+        }
+    }
+    if (!alg) {
+        LOG_ERROR("Algorithm not found: %s", algorithm_name);
+        std::exit(EXIT_FAILURE);
+    }
+    result_t *tmp = alg->join(relR, relS, config);
+    if (tmp) std::memcpy(res, tmp, sizeof(result_t));
+}

@@ -1,0 +1,353 @@
+// Host orchestration of the MI355X RHO join: partitioning policy, workspace,
+// kernel sequence and the C-ABI entry points of sgxamd/rho.h.
+//
+// Mirrors the phase structure of join_init_run / prj_thread
+// (radix_join.cpp:1369-1638 / :1067-1356): pass-1 partition of R then S, optional
+// pass 2, then build+probe of every partition pair; but each phase is a sequence
+// of device-wide kernels instead of T pthreads with barriers, and partitions are
+// sized for the LDS of a CU rather than for L2 (calc_num_radix_bits :295-317).
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <string>
+
+#include "common.hpp"
+#include "rho_internal.hpp"
+#include "runtime.hpp"
+#include "sgxamd/rho.h"
+
+namespace sgxamd {
+namespace rho {
+
+namespace {
+
+constexpr uint64_t kTargetPartition = 4096;  // R tuples per partition (= RCAP of an 8192-slot table)
+constexpr uint32_t kMaxBits = 18;
+constexpr uint32_t kSegTarget = 2048;        // workgroups per partition pass and relation
+
+inline uint32_t ceil_log2(uint64_t x) {
+    uint32_t b = 0;
+    while ((1ull << b) < x) ++b;
+    return b;
+}
+
+struct Policy {
+    uint32_t bits, passes, b1, b2, table_slots;
+};
+
+Policy choose_policy(uint64_t nR, const mi355_rho_opts *o) {
+    Policy p{};
+    if (o && o->radix_bits > 0) {
+        p.bits = std::min<uint32_t>((uint32_t)o->radix_bits, kMaxBits);
+    } else {
+        const uint64_t need = (nR + kTargetPartition - 1) / kTargetPartition;
+        p.bits = std::min(ceil_log2(std::max<uint64_t>(need, 1)), kMaxBits);
+    }
+    p.passes = (o && o->passes > 0) ? (uint32_t)o->passes : (p.bits <= 9 ? 1u : 2u);
+    if (p.passes > 2) p.passes = 2;
+    if (p.bits > 9 && p.passes == 1) p.passes = 2;  // one pass is limited to kMaxF = 2^9 bins
+    if (p.passes == 2 && p.bits < 2) p.passes = 1;
+    if (p.passes == 1) {
+        p.b1 = p.bits;
+        p.b2 = 0;
+    } else {
+        p.b1 = (p.bits + 1) / 2;
+        p.b2 = p.bits - p.b1;
+    }
+    // table large enough that the average partition needs one R chunk
+    const uint64_t avg = (nR >> p.bits) + 1;
+    p.table_slots = avg > 4096 ? 16384 : (avg > 2048 ? 8192 : 8192);
+    return p;
+}
+
+inline uint64_t seg_size_for(uint64_t n) {
+    uint64_t s = (n + kSegTarget - 1) / kSegTarget;
+    s = (s + kTile - 1) / kTile * kTile;
+    return std::max<uint64_t>(s, kTile);
+}
+
+struct RelPlan {
+    uint64_t n;
+    uint64_t seg1;
+    uint32_t nseg1;
+    uint64_t seg2;
+    uint32_t grid2;
+    // scratch offsets
+    size_t hist1, tot1, start1, cnt1, segbase2, hist2, pstart, pcnt;
+};
+
+#define RHO_HIP(call)                                                                      \
+    do {                                                                                   \
+        hipError_t _e = (call);                                                            \
+        if (_e != hipSuccess) {                                                            \
+            set_last_error(std::string(#call) + ": " + hipGetErrorString(_e));             \
+            return (_e == hipErrorOutOfMemory) ? MI355_ERR_OOM : MI355_ERR_HIP;            \
+        }                                                                                  \
+    } while (0)
+
+// One relation through pass 1 (and pass 2).  Returns the final buffer and
+// partition table pointers through *final / *pstart / *pcnt.
+int partition_relation(Context *ctx, hipStream_t s, Timer &tm, const char *tag, const row_t *in, row_t *t1,
+                       row_t *t2, RelPlan &rp, const Policy &pol, uint32_t key_shift, const row_t **final_rel,
+                       const uint64_t **pstart, const uint64_t **pcnt, bool pass2_now) {
+    Arena &A = ctx->scratch;
+    uint64_t *hist1 = A.at<uint64_t>(rp.hist1);
+    uint64_t *tot1 = A.at<uint64_t>(rp.tot1);
+    uint64_t *start1 = A.at<uint64_t>(rp.start1);
+    uint64_t *cnt1 = A.at<uint64_t>(rp.cnt1);
+    uint32_t *segbase2 = A.at<uint32_t>(rp.segbase2);
+    std::string t(tag);
+    if (!pass2_now) {
+        SegMap m1{nullptr, nullptr, nullptr, 1, rp.seg1, rp.n};
+        tm.mark((t + "pass1_hist").c_str());
+        RHO_HIP(launch_hist(in, m1, rp.nseg1, key_shift, pol.b1, hist1, kDigitMajor, rp.nseg1, s));
+        tm.mark((t + "pass1_scan").c_str());
+        RHO_HIP(launch_scan_single(hist1, rp.nseg1, pol.b1, tot1, start1, cnt1, 0,
+                                   pol.passes == 2 ? segbase2 : nullptr, rp.seg2, s));
+        tm.mark((t + "pass1_scatter").c_str());
+        RHO_HIP(launch_scatter(in, t1, m1, rp.nseg1, key_shift, pol.b1, hist1, kDigitMajor, rp.nseg1, start1, s));
+        *final_rel = t1;
+        *pstart = start1;
+        *pcnt = cnt1;
+        return MI355_OK;
+    }
+    uint64_t *hist2 = A.at<uint64_t>(rp.hist2);
+    uint64_t *ps = A.at<uint64_t>(rp.pstart);
+    uint64_t *pc = A.at<uint64_t>(rp.pcnt);
+    const uint32_t F1 = 1u << pol.b1;
+    SegMap m2{start1, cnt1, segbase2, F1, rp.seg2, rp.n};
+    const uint32_t shift2 = key_shift + pol.b1;
+    tm.mark((t + "pass2_hist").c_str());
+    RHO_HIP(launch_hist(t1, m2, rp.grid2, shift2, pol.b2, hist2, kSegMajor, 0, s));
+    tm.mark((t + "pass2_scan").c_str());
+    RHO_HIP(launch_scan_regions(hist2, segbase2, start1, F1, pol.b2, ps, pc, s));
+    tm.mark((t + "pass2_scatter").c_str());
+    RHO_HIP(launch_scatter(t1, t2, m2, rp.grid2, shift2, pol.b2, hist2, kSegMajor, 0, nullptr, s));
+    *final_rel = t2;
+    *pstart = ps;
+    *pcnt = pc;
+    return MI355_OK;
+}
+
+void plan_relation(Arena &A, RelPlan &rp, uint64_t n, const Policy &pol) {
+    rp.n = n;
+    rp.seg1 = seg_size_for(n);
+    rp.nseg1 = (uint32_t)((n + rp.seg1 - 1) / rp.seg1);
+    const uint32_t F1 = 1u << pol.b1, F2 = 1u << pol.b2;
+    rp.seg2 = seg_size_for(n);
+    rp.grid2 = (uint32_t)((n + rp.seg2 - 1) / rp.seg2) + F1;
+    rp.hist1 = A.reserve(sizeof(uint64_t) * (size_t)F1 * std::max<uint32_t>(rp.nseg1, 1));
+    rp.tot1 = A.reserve(sizeof(uint64_t) * F1);
+    rp.start1 = A.reserve(sizeof(uint64_t) * F1);
+    rp.cnt1 = A.reserve(sizeof(uint64_t) * F1);
+    rp.segbase2 = A.reserve(sizeof(uint32_t) * (F1 + 1));
+    if (pol.passes == 2) {
+        rp.hist2 = A.reserve(sizeof(uint64_t) * (size_t)rp.grid2 * F2);
+        rp.pstart = A.reserve(sizeof(uint64_t) * (size_t)F1 * F2);
+        rp.pcnt = A.reserve(sizeof(uint64_t) * (size_t)F1 * F2);
+    }
+}
+
+}  // namespace
+
+// The whole join on device-resident inputs.  Caller holds ctx->mu.
+int join_device(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const row_t *dS, uint64_t nS,
+                const mi355_rho_opts *opts, mi355_rho_stats *st) {
+    const uint32_t key_shift = opts ? opts->key_shift : 0;
+    const Policy pol = choose_policy(nR, opts);
+    if (key_shift + pol.bits > 31) {
+        set_last_error("key_shift + radix bits must stay below 32");
+        return MI355_ERR_INVALID;
+    }
+    Timer &tm = thread_timer();
+    const bool user_timing = (opts && opts->timing) || thread_timing_enabled();
+    tm.begin_call(s, true);  // phase events are always recorded (throughput in result_t)
+
+    RHO_HIP(ctx->t1R.ensure(std::max<uint64_t>(nR, 1) * sizeof(row_t)));
+    RHO_HIP(ctx->t1S.ensure(std::max<uint64_t>(nS, 1) * sizeof(row_t)));
+    if (pol.passes == 2) {
+        RHO_HIP(ctx->t2R.ensure(std::max<uint64_t>(nR, 1) * sizeof(row_t)));
+        RHO_HIP(ctx->t2S.ensure(std::max<uint64_t>(nS, 1) * sizeof(row_t)));
+    }
+    Arena &A = ctx->scratch;
+    A.reset();
+    RelPlan pr{}, ps{};
+    plan_relation(A, pr, nR, pol);
+    plan_relation(A, ps, nS, pol);
+    const uint64_t P = 1ull << pol.bits;
+    const uint32_t join_grid = (uint32_t)std::min<uint64_t>(P, 2048);
+    const size_t off_partials = A.reserve(sizeof(uint64_t) * join_grid);
+    const size_t off_result = A.reserve(sizeof(uint64_t) * 4);
+    RHO_HIP(A.buf.ensure(A.used));
+
+    const row_t *fR = nullptr, *fS = nullptr;
+    const uint64_t *psR = nullptr, *pcR = nullptr, *psS = nullptr, *pcS = nullptr;
+    int rc;
+    if ((rc = partition_relation(ctx, s, tm, "R_", dR, ctx->t1R.as<row_t>(), ctx->t2R.as<row_t>(), pr, pol, key_shift,
+                                 &fR, &psR, &pcR, false)))
+        return rc;
+    if ((rc = partition_relation(ctx, s, tm, "S_", dS, ctx->t1S.as<row_t>(), ctx->t2S.as<row_t>(), ps, pol, key_shift,
+                                 &fS, &psS, &pcS, false)))
+        return rc;
+    if (pol.passes == 2) {
+        if ((rc = partition_relation(ctx, s, tm, "R_", dR, ctx->t1R.as<row_t>(), ctx->t2R.as<row_t>(), pr, pol,
+                                     key_shift, &fR, &psR, &pcR, true)))
+            return rc;
+        if ((rc = partition_relation(ctx, s, tm, "S_", dS, ctx->t1S.as<row_t>(), ctx->t2S.as<row_t>(), ps, pol,
+                                     key_shift, &fS, &psS, &pcS, true)))
+            return rc;
+    }
+    uint64_t *partials = A.at<uint64_t>(off_partials);
+    uint64_t *result = A.at<uint64_t>(off_result);
+    tm.mark("join_build_probe");
+    RHO_HIP(launch_join(fR, fS, psR, pcR, psS, pcS, P, key_shift + pol.bits, pol.table_slots, join_grid, partials,
+                        s));
+    tm.mark("join_reduce");
+    RHO_HIP(launch_reduce(partials, join_grid, result, s));
+    tm.end_call();
+    RHO_HIP(launch_max(pcR, P, result + 1, s));
+    RHO_HIP(launch_max(pcS, P, result + 2, s));
+    RHO_HIP(hipMemcpyAsync(ctx->host_result, result, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    RHO_HIP(hipStreamSynchronize(s));
+    tm.collect();
+
+    if (st) {
+        st->matches = ctx->host_result[0];
+        st->radix_bits = pol.bits;
+        st->passes = pol.passes;
+        st->pass1_bits = pol.b1;
+        st->pass2_bits = pol.b2;
+        st->num_partitions = P;
+        st->num_tasks = P;
+        st->max_part_r = ctx->host_result[1];
+        st->max_part_s = ctx->host_result[2];
+        st->ms_pass1 = tm.ms_of_prefix("R_pass1") + tm.ms_of_prefix("S_pass1");
+        st->ms_pass2 = tm.ms_of_prefix("R_pass2") + tm.ms_of_prefix("S_pass2");
+        st->ms_partition = st->ms_pass1 + st->ms_pass2;
+        st->ms_join = tm.ms_of_prefix("join_");
+        st->ms_total = st->ms_partition + st->ms_join;
+    }
+    (void)user_timing;
+    return MI355_OK;
+}
+
+// Stable partition by destination shard (multi-GPU exchange step).
+int shard_partition_device(Context *ctx, hipStream_t s, const row_t *in, uint64_t n, uint32_t key_shift,
+                           uint32_t dest_bits, row_t *out, uint64_t *dest_counts) {
+    Policy pol{};
+    pol.bits = pol.b1 = dest_bits;
+    pol.passes = 1;
+    Arena &A = ctx->scratch;
+    A.reset();
+    RelPlan rp{};
+    plan_relation(A, rp, n, pol);
+    RHO_HIP(A.buf.ensure(A.used));
+    Timer &tm = thread_timer();
+    tm.begin_call(s, thread_timing_enabled());
+    const row_t *f;
+    const uint64_t *pst, *pcn;
+    int rc = partition_relation(ctx, s, tm, "shard_", in, out, nullptr, rp, pol, key_shift, &f, &pst, &pcn, false);
+    if (rc) return rc;
+    tm.end_call();
+    const uint32_t F = 1u << dest_bits;
+    RHO_HIP(hipMemcpyAsync(dest_counts, pcn, F * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    RHO_HIP(hipStreamSynchronize(s));
+    tm.collect();
+    return MI355_OK;
+}
+
+}  // namespace rho
+}  // namespace sgxamd
+
+using namespace sgxamd;
+
+extern "C" {
+
+int mi355_rho_join_ex(const row_t *R, uint64_t nR, const row_t *S, uint64_t nS, const mi355_rho_opts *opts,
+                      mi355_rho_stats *stats) {
+    if ((!R && nR) || (!S && nS)) {
+        set_last_error("null relation");
+        return MI355_ERR_INVALID;
+    }
+    if (opts && opts->materialize) {
+        set_last_error("materialisation is not supported by this build (count-only)");
+        return MI355_ERR_INVALID;
+    }
+    int status = MI355_OK;
+    Context *ctx = current_context(&status);
+    if (!ctx) return status;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    hipStream_t s = thread_stream(ctx, opts ? opts->stream : nullptr);
+    mi355_rho_stats local{};
+    mi355_rho_stats *st = stats ? stats : &local;
+    std::memset(st, 0, sizeof(*st));
+    if (nR == 0 || nS == 0) return MI355_OK;
+
+    const row_t *dR = R, *dS = S;
+    const auto t0 = std::chrono::steady_clock::now();
+    bool staged = false;
+    if (!is_device_pointer(R)) {
+        RHO_HIP(ctx->inR.ensure(nR * sizeof(row_t)));
+        RHO_HIP(hipMemcpyAsync(ctx->inR.ptr, R, nR * sizeof(row_t), hipMemcpyHostToDevice, s));
+        dR = ctx->inR.as<row_t>();
+        staged = true;
+    }
+    if (!is_device_pointer(S)) {
+        RHO_HIP(ctx->inS.ensure(nS * sizeof(row_t)));
+        RHO_HIP(hipMemcpyAsync(ctx->inS.ptr, S, nS * sizeof(row_t), hipMemcpyHostToDevice, s));
+        dS = ctx->inS.as<row_t>();
+        staged = true;
+    }
+    if (staged) {
+        RHO_HIP(hipStreamSynchronize(s));
+        st->ms_h2d = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    return rho::join_device(ctx, s, dR, nR, dS, nS, opts, st);
+}
+
+// Drop-in for RHO() (radix_join.cpp:1640-1643), count-only.
+int mi355_rho_join(const table_t *relR, const table_t *relS, const joinconfig_t *config, result_t *out) {
+    if (!relR || !relS || !out) {
+        set_last_error("null argument");
+        return MI355_ERR_INVALID;
+    }
+    if (config && config->MATERIALIZE) {
+        set_last_error("MATERIALIZE=1 is not supported by this build (count-only)");
+        return MI355_ERR_INVALID;
+    }
+    mi355_rho_stats st{};
+    int rc = mi355_rho_join_ex(relR->tuples, relR->num_tuples, relS->tuples, relS->num_tuples, nullptr, &st);
+    if (rc) return rc;
+    out->totalresults = (int64_t)st.matches;
+    out->nthreads = config ? config->NTHREADS : 1;
+    const double us = st.ms_total * 1000.0;
+    out->throughput = us > 0 ? (double)(relR->num_tuples + relS->num_tuples) / us : 0.0;  // M rec/s
+    out->materialized = 0;
+    out->result = nullptr;
+    out->result_type = 0;
+    return MI355_OK;
+}
+
+int mi355_rho_shard_partition(const row_t *in, uint64_t n, uint32_t key_shift, uint32_t dest_bits, row_t *out,
+                              uint64_t *dest_counts, void *stream) {
+    if ((!in && n) || !out || !dest_counts || dest_bits > 9 || key_shift + dest_bits > 32) {
+        set_last_error("invalid shard_partition arguments");
+        return MI355_ERR_INVALID;
+    }
+    if (!is_device_pointer(in) || !is_device_pointer(out)) {
+        set_last_error("shard_partition needs device-resident in/out");
+        return MI355_ERR_INVALID;
+    }
+    int status = MI355_OK;
+    Context *ctx = current_context(&status);
+    if (!ctx) return status;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    hipStream_t s = thread_stream(ctx, stream);
+    if (n == 0) {
+        std::memset(dest_counts, 0, sizeof(uint64_t) << dest_bits);
+        return MI355_OK;
+    }
+    return rho::shard_partition_device(ctx, s, in, n, key_shift, dest_bits, out, dest_counts);
+}
+
+}  // extern "C"

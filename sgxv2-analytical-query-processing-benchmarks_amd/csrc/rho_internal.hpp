@@ -1,0 +1,68 @@
+// Internal interface between the RHO kernels (rho_kernels.hip) and the host
+// orchestration (rho_host.cpp).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "sgxamd/data_types.h"
+
+namespace sgxamd {
+namespace rho {
+
+constexpr int kBlock = 256;   // threads per workgroup for partition/join kernels
+constexpr int kMaxF = 512;    // max fanout of one partition pass (9 radix bits)
+constexpr int kScatterItems = 8;                      // tuples per thread per tile
+constexpr int kTile = kBlock * kScatterItems;         // tuples per scatter tile
+constexpr uint32_t kEmptyKey = 0xFFFFFFFFu;           // LDS hash-table empty marker
+
+// Which contiguous slice of the input a partition workgroup owns.  Regions are
+// the bins of the previous pass (or the whole relation); each region is cut into
+// segments of seg_size tuples, one workgroup per segment.
+struct SegMap {
+    const uint64_t *reg_start;  // nullptr => one region [0, single_n)
+    const uint64_t *reg_count;
+    const uint32_t *seg_base;   // nreg + 1 prefix of segments per region (device)
+    uint32_t nreg;
+    uint64_t seg_size;
+    uint64_t single_n;
+};
+
+// Histogram layout selector: digit-major [d][g] (single region: column scans)
+// or segment-major [g][d] (many regions: per-region scans).
+enum HistLayout : int { kDigitMajor = 0, kSegMajor = 1 };
+
+hipError_t launch_hist(const row_t *in, const SegMap &m, uint32_t grid, uint32_t shift, uint32_t bits,
+                       uint64_t *hist, HistLayout layout, uint32_t nseg_stride, hipStream_t s);
+
+// Single-region scan: hist [F][nseg] -> exclusive per-digit column prefix (in place);
+// then digit starts/counts, and (optionally) the segment table of the next pass.
+hipError_t launch_scan_single(uint64_t *hist, uint32_t nseg, uint32_t bits, uint64_t *totals,
+                              uint64_t *out_start, uint64_t *out_count, uint64_t base,
+                              uint32_t *next_seg_base, uint64_t next_seg_size, hipStream_t s);
+
+// Multi-region scan: hist [g][F] -> absolute write cursors (in place) and the
+// (region, digit) partition table part_start/part_count [nreg * F].
+hipError_t launch_scan_regions(uint64_t *hist, const uint32_t *seg_base, const uint64_t *reg_start,
+                               uint32_t nreg, uint32_t bits, uint64_t *part_start, uint64_t *part_count,
+                               hipStream_t s);
+
+// Stable scatter of every segment into `out` at the cursors of the scan.
+// digit_base (nullable) is added to the cursors: base[r * F + d].
+hipError_t launch_scatter(const row_t *in, row_t *out, const SegMap &m, uint32_t grid, uint32_t shift,
+                          uint32_t bits, const uint64_t *cursors, HistLayout layout, uint32_t nseg_stride,
+                          const uint64_t *digit_base, hipStream_t s);
+
+// Build + probe over P partitions; writes one partial count per workgroup.
+hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, const uint64_t *r_count,
+                       const uint64_t *s_start, const uint64_t *s_count, uint64_t P, uint32_t hash_shift,
+                       uint32_t table_slots, uint32_t grid, uint64_t *partials, hipStream_t s);
+
+hipError_t launch_reduce(const uint64_t *partials, uint32_t n, uint64_t *result, hipStream_t s);
+
+// max over an array of counts (diagnostics: largest partition)
+hipError_t launch_max(const uint64_t *v, uint64_t n, uint64_t *result, hipStream_t s);
+
+}  // namespace rho
+}  // namespace sgxamd

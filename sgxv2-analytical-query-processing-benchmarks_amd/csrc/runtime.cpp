@@ -1,0 +1,178 @@
+// Per-device runtime (see runtime.hpp) and the error / timing C-ABI.
+#include "runtime.hpp"
+
+#include <map>
+#include <memory>
+
+#include "common.hpp"
+#include "sgxamd/rho.h"
+
+namespace sgxamd {
+
+namespace {
+thread_local std::string t_last_error;
+thread_local bool t_timing = false;
+thread_local void *t_stream = nullptr;
+thread_local Timer t_timer;
+std::mutex g_ctx_mu;
+std::map<int, std::unique_ptr<Context>> g_ctx;
+}  // namespace
+
+void set_last_error(const std::string &msg) { t_last_error = msg; }
+const char *last_error() { return t_last_error.c_str(); }
+
+hipError_t DeviceBuffer::ensure(size_t n) {
+    if (n <= bytes && ptr) return hipSuccess;
+    release();
+    size_t want = n < 256 ? 256 : n;
+    hipError_t e = hipMalloc(&ptr, want);
+    if (e != hipSuccess) {
+        ptr = nullptr;
+        bytes = 0;
+        return e;
+    }
+    bytes = want;
+    return hipSuccess;
+}
+
+void DeviceBuffer::release() {
+    if (ptr) (void)hipFree(ptr);
+    ptr = nullptr;
+    bytes = 0;
+}
+
+hipEvent_t Timer::get_event() {
+    if (used_ == pool_.size()) {
+        hipEvent_t ev = nullptr;
+        if (hipEventCreate(&ev) != hipSuccess) return nullptr;
+        pool_.push_back(ev);
+    }
+    return pool_[used_++];
+}
+
+void Timer::begin_call(hipStream_t s, bool enabled) {
+    enabled_ = enabled;
+    stream_ = s;
+    used_ = 0;
+    spans_.clear();
+    records_.clear();
+    open_name_.clear();
+    open_ev_ = nullptr;
+}
+
+void Timer::mark(const char *name) {
+    if (!enabled_) return;
+    hipEvent_t ev = get_event();
+    if (!ev) return;
+    (void)hipEventRecord(ev, stream_);
+    if (open_ev_) spans_.push_back({open_name_, {open_ev_, ev}});
+    open_name_ = name;
+    open_ev_ = ev;
+}
+
+void Timer::end_call() {
+    if (!enabled_ || !open_ev_) return;
+    hipEvent_t ev = get_event();
+    if (!ev) return;
+    (void)hipEventRecord(ev, stream_);
+    spans_.push_back({open_name_, {open_ev_, ev}});
+    open_ev_ = nullptr;
+}
+
+void Timer::collect() {
+    records_.clear();
+    for (auto &s : spans_) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, s.second.first, s.second.second) != hipSuccess) ms = 0.f;
+        records_.push_back({s.first, (double)ms});
+    }
+}
+
+double Timer::ms_of_prefix(const std::string &prefix) const {
+    double t = 0;
+    for (auto &r : records_)
+        if (r.first.compare(0, prefix.size(), prefix) == 0) t += r.second;
+    return t;
+}
+
+Timer &thread_timer() { return t_timer; }
+bool thread_timing_enabled() { return t_timing; }
+
+Context *current_context(int *status) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        (void)hipGetLastError();
+        set_last_error("no HIP device visible (mi355_* needs a gfx950 GPU)");
+        if (status) *status = MI355_ERR_NO_DEVICE;
+        return nullptr;
+    }
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) {
+        set_last_error("hipGetDevice failed");
+        if (status) *status = MI355_ERR_HIP;
+        return nullptr;
+    }
+    std::lock_guard<std::mutex> lk(g_ctx_mu);
+    auto it = g_ctx.find(dev);
+    if (it != g_ctx.end()) return it->second.get();
+    auto ctx = std::make_unique<Context>();
+    ctx->device = dev;
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void **>(&ctx->host_result), 64 * sizeof(uint64_t)) != hipSuccess) {
+        set_last_error("stream / pinned allocation failed");
+        if (status) *status = MI355_ERR_HIP;
+        return nullptr;
+    }
+    Context *raw = ctx.get();
+    g_ctx[dev] = std::move(ctx);
+    return raw;
+}
+
+hipStream_t thread_stream(Context *ctx, void *explicit_stream) {
+    if (explicit_stream) return static_cast<hipStream_t>(explicit_stream);
+    if (t_stream) return static_cast<hipStream_t>(t_stream);
+    return ctx->stream;
+}
+
+bool is_device_pointer(const void *p) {
+    if (!p) return false;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
+}
+
+}  // namespace sgxamd
+
+extern "C" {
+
+const char *mi355_last_error(void) { return sgxamd::last_error(); }
+
+const char *mi355_version(void) { return "sgxamd-mi355 0.1 (gfx950)"; }
+
+int mi355_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return n;
+}
+
+void mi355_timing_enable(int on) { sgxamd::t_timing = on != 0; }
+
+int mi355_timing_get(const char **names, double *ms, int cap) {
+    const auto &rec = sgxamd::t_timer.records();
+    const int n = (int)rec.size();
+    for (int i = 0; i < n && i < cap; ++i) {
+        if (names) names[i] = rec[i].first.c_str();
+        if (ms) ms[i] = rec[i].second;
+    }
+    return n;
+}
+
+void mi355_set_stream(void *stream) { sgxamd::t_stream = stream; }
+
+}  // extern "C"

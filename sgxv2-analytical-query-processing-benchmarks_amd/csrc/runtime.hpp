@@ -1,0 +1,88 @@
+// Per-device runtime: library stream, grow-only device buffers, per-kernel
+// event timing and pointer classification.  Native replacement for the
+// reference's per-call aligned_alloc/memset workspace (radix_join.cpp:1419-1450)
+// and its rdtscp phase timers (rdtscpWrapper.h:6-35).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <mutex>
+#include <string>
+#include <vector>
+
+namespace sgxamd {
+
+// Grow-only device allocation (HBM).  Never shrinks; freed with the context.
+struct DeviceBuffer {
+    void *ptr = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t n);
+    void release();
+    template <typename T>
+    T *as() const { return static_cast<T *>(ptr); }
+};
+
+// Bump allocator over one DeviceBuffer (256-B aligned slices).
+struct Arena {
+    DeviceBuffer buf;
+    size_t used = 0;
+    std::vector<std::pair<size_t, size_t>> plan;
+    void reset() { used = 0; }
+    size_t reserve(size_t bytes) {
+        size_t off = (used + 255) & ~size_t(255);
+        used = off + bytes;
+        return off;
+    }
+    template <typename T>
+    T *at(size_t off) const { return reinterpret_cast<T *>(static_cast<char *>(buf.ptr) + off); }
+};
+
+// Per-kernel HIP event timing, enabled per thread.
+class Timer {
+   public:
+    void begin_call(hipStream_t s, bool enabled);
+    void mark(const char *name);  // closes the previous span, opens `name`
+    void end_call();              // closes the last span (before the final sync)
+    // after the stream synchronised: fold event pairs into (name, ms)
+    void collect();
+    const std::vector<std::pair<std::string, double>> &records() const { return records_; }
+    double ms_of_prefix(const std::string &prefix) const;
+    bool enabled() const { return enabled_; }
+
+   private:
+    hipEvent_t get_event();
+    bool enabled_ = false;
+    hipStream_t stream_ = nullptr;
+    std::vector<hipEvent_t> pool_;
+    size_t used_ = 0;
+    std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> spans_;
+    std::vector<std::pair<std::string, double>> records_;
+    std::string open_name_;
+    hipEvent_t open_ev_ = nullptr;
+};
+
+struct Context {
+    int device = -1;
+    hipStream_t stream = nullptr;  // library stream (non-blocking)
+    std::mutex mu;                 // one call at a time per device context
+    // join workspace
+    DeviceBuffer inR, inS;         // staging of host relations
+    DeviceBuffer t1R, t1S, t2R, t2S;
+    Arena scratch;
+    // scan workspace
+    DeviceBuffer scan_in, scan_out, scan_aux;
+    uint64_t *host_result = nullptr;  // pinned 64 x u64
+};
+
+// Context of the calling thread's current HIP device (created on first use).
+// Returns nullptr (and sets the last error) when no device is available.
+Context *current_context(int *status);
+
+Timer &thread_timer();
+bool thread_timing_enabled();
+hipStream_t thread_stream(Context *ctx, void *explicit_stream);
+
+bool is_device_pointer(const void *p);
+
+}  // namespace sgxamd

@@ -1,0 +1,323 @@
+"""ctypes binding of libsgxamd.so, the MI355X RHO join + predicate scan C-ABI.
+
+This is the Python side of the drop-in boundary declared in include/sgxamd/*.h:
+the same entry points a cgo / JNI / ctypes caller of the reference would bind
+(see INTEGRATION.md).  Arguments are raw pointers and sizes; torch tensors and
+numpy arrays are accepted and passed by address (device tensors stay in HBM).
+
+The library is built in-tree by ``make`` in the package directory (or
+``__graft_entry__.build()``).  There is no CPU fallback: if libsgxamd.so is
+missing, importing this module raises, and every compute call on a host
+without a gfx950 device returns MI355_ERR_NO_DEVICE (raised as Mi355Error).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+LIB_PATH = os.path.join(PKG_DIR, "libsgxamd.so")
+
+MI355_OK = 0
+MI355_ERR_INVALID = -1
+MI355_ERR_NO_DEVICE = -2
+MI355_ERR_HIP = -3
+MI355_ERR_OOM = -4
+MI355_ERR_CAPACITY = -5
+
+
+class Mi355Error(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"mi355 error {code}: {msg}")
+        self.code = code
+
+
+class row_t(C.Structure):
+    _fields_ = [("key", C.c_uint32), ("payload", C.c_uint32)]
+
+
+class table_t(C.Structure):
+    _fields_ = [("tuples", C.c_void_p), ("num_tuples", C.c_uint64), ("ratio_holes", C.c_int), ("sorted", C.c_int)]
+
+
+class result_t(C.Structure):
+    _fields_ = [
+        ("totalresults", C.c_int64),
+        ("nthreads", C.c_int),
+        ("throughput", C.c_double),
+        ("materialized", C.c_int),
+        ("result", C.c_void_p),
+        ("result_type", C.c_int),
+    ]
+
+
+class joinconfig_t(C.Structure):
+    _fields_ = [
+        (n, C.c_int)
+        for n in (
+            "NTHREADS", "PARTFANOUT", "SCALARSORT", "SCALARMERGE", "MWAYMERGEBUFFERSIZE", "NUMASTRATEGY",
+            "RADIXBITS", "WRITETOFILE", "MATERIALIZE", "PRINT", "CRACKING_THRESHOLD", "ALLOC_CORE",
+        )
+    ]
+
+
+class rho_opts(C.Structure):
+    _fields_ = [
+        ("radix_bits", C.c_int),
+        ("passes", C.c_int),
+        ("key_shift", C.c_uint32),
+        ("materialize", C.c_int),
+        ("timing", C.c_int),
+        ("reserved", C.c_int),
+        ("stream", C.c_void_p),
+    ]
+
+
+class rho_stats(C.Structure):
+    _fields_ = [
+        ("matches", C.c_uint64),
+        ("radix_bits", C.c_uint32),
+        ("passes", C.c_uint32),
+        ("pass1_bits", C.c_uint32),
+        ("pass2_bits", C.c_uint32),
+        ("num_partitions", C.c_uint64),
+        ("num_tasks", C.c_uint64),
+        ("max_part_r", C.c_uint64),
+        ("max_part_s", C.c_uint64),
+        ("ms_h2d", C.c_double),
+        ("ms_partition", C.c_double),
+        ("ms_pass1", C.c_double),
+        ("ms_pass2", C.c_double),
+        ("ms_join", C.c_double),
+        ("ms_total", C.c_double),
+    ]
+
+    def as_dict(self) -> dict:
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+# Every symbol declared in include/sgxamd/*.h with its (restype, argtypes).
+_P = C.c_void_p
+_U64P = C.POINTER(C.c_uint64)
+SIGNATURES = {
+    # rho.h
+    "mi355_device_count": (C.c_int, []),
+    "mi355_last_error": (C.c_char_p, []),
+    "mi355_version": (C.c_char_p, []),
+    "mi355_rho_join": (C.c_int, [C.POINTER(table_t), C.POINTER(table_t), C.POINTER(joinconfig_t), C.POINTER(result_t)]),
+    "mi355_rho_join_ex": (C.c_int, [_P, C.c_uint64, _P, C.c_uint64, C.POINTER(rho_opts), C.POINTER(rho_stats)]),
+    "mi355_rho_shard_partition": (C.c_int, [_P, C.c_uint64, C.c_uint32, C.c_uint32, _P, _U64P, _P]),
+    "mi355_timing_enable": (None, [C.c_int]),
+    "mi355_timing_get": (C.c_int, [C.POINTER(C.c_char_p), C.POINTER(C.c_double), C.c_int]),
+    "mi355_set_stream": (None, [_P]),
+    # scan.h
+    "mi355_scan_count_u8": (C.c_int, [C.c_uint8, C.c_uint8, _P, C.c_size_t, _U64P]),
+    "mi355_scan_count_i32": (C.c_int, [C.c_int32, C.c_int32, _P, C.c_size_t, _U64P]),
+    "mi355_scan_bitvector_u8": (C.c_int, [C.c_uint8, C.c_uint8, _P, C.c_size_t, _P]),
+    "mi355_scan_bitvector_i32": (C.c_int, [C.c_int32, C.c_int32, _P, C.c_size_t, _P]),
+    "mi355_scan_index_u8": (C.c_int, [C.c_uint8, C.c_uint8, _P, C.c_size_t, _P, C.c_size_t, _U64P]),
+    "mi355_scan_index_i32": (C.c_int, [C.c_int32, C.c_int32, _P, C.c_size_t, _P, C.c_size_t, _U64P]),
+    "mi355_scan_values_u8": (C.c_int, [C.c_uint8, C.c_uint8, _P, C.c_size_t, _P, C.c_size_t, _U64P]),
+    "mi355_scan_values_i32": (C.c_int, [C.c_int32, C.c_int32, _P, C.c_size_t, _P, C.c_size_t, _U64P]),
+    # generator.h
+    "mi355_gen_seed": (None, [C.c_uint]),
+    "mi355_gen_rand": (C.c_int, []),
+    "mi355_gen_pk": (C.c_int, [_P, C.c_uint64]),
+    "mi355_gen_fk": (C.c_int, [_P, C.c_uint64, C.c_int64]),
+    "mi355_gen_fk_sel": (C.c_int, [_P, C.c_uint64, C.c_int64]),
+    "mi355_gen_zipf": (C.c_int, [_P, C.c_uint64, C.c_uint32, C.c_double, C.c_uint64, C.c_int]),
+    "mi355_gen_scan_u8": (C.c_int, [_P, C.c_size_t]),
+    "mi355_gen_scan_i32": (C.c_int, [_P, C.c_size_t]),
+    "mi355_gen_pk_dev": (C.c_int, [_P, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, _P]),
+    "mi355_gen_fk_dev": (C.c_int, [_P, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, _P]),
+    "mi355_gen_scan_u8_dev": (C.c_int, [_P, C.c_size_t, C.c_int, C.c_uint64, _P]),
+    "mi355_gen_scan_i32_dev": (C.c_int, [_P, C.c_size_t, C.c_int, C.c_uint64, _P]),
+}
+
+
+def _load() -> C.CDLL:
+    # PyTorch-ROCm ships its own libamdhip64 / libhsa-runtime64 (SONAME libamdhip64.so.7).
+    # Loading torch first makes libsgxamd.so bind to that same HIP runtime instead of
+    # /opt/rocm's, so one process never holds two HIP runtimes (torch tensors are then
+    # device pointers of our runtime too).  Without torch, /opt/rocm's runtime is used.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `make -C {PKG_DIR}` or __graft_entry__.build(); "
+            "there is no CPU fallback for the MI355X kernels"
+        )
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def last_error() -> str:
+    return (lib.mi355_last_error() or b"").decode()
+
+
+def _check(rc: int) -> None:
+    if rc != MI355_OK:
+        raise Mi355Error(rc, last_error())
+
+
+def ptr(x) -> int:
+    """Address of a torch tensor, numpy array, ctypes object or int."""
+    if x is None:
+        return 0
+    if isinstance(x, int):
+        return x
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
+    if hasattr(x, "ctypes"):
+        return x.ctypes.data
+    return C.addressof(x)
+
+
+def device_count() -> int:
+    return lib.mi355_device_count()
+
+
+def version() -> str:
+    return lib.mi355_version().decode()
+
+
+# ------------------------------------------------------------------ join ---
+@dataclass
+class JoinResult:
+    matches: int
+    stats: dict
+
+
+def rho_join(R, nR: int, S, nS: int, *, radix_bits: int = 0, passes: int = 0, key_shift: int = 0,
+             timing: bool = False, stream: int | None = None) -> JoinResult:
+    """RHO join of nR R-tuples and nS S-tuples (8-byte {key, payload}; host or device)."""
+    o = rho_opts(radix_bits, passes, key_shift, 0, 1 if timing else 0, 0, stream or None)
+    st = rho_stats()
+    _check(lib.mi355_rho_join_ex(ptr(R), nR, ptr(S), nS, C.byref(o), C.byref(st)))
+    return JoinResult(int(st.matches), st.as_dict())
+
+
+def rho_join_tables(R, nR: int, S, nS: int, nthreads: int = 1) -> result_t:
+    """The drop-in mi355_rho_join(table_t*, table_t*, joinconfig_t*, result_t*)."""
+    tR = table_t(ptr(R), nR, 0, 0)
+    tS = table_t(ptr(S), nS, 0, 0)
+    cfg = joinconfig_t()
+    cfg.NTHREADS = nthreads
+    out = result_t()
+    _check(lib.mi355_rho_join(C.byref(tR), C.byref(tS), C.byref(cfg), C.byref(out)))
+    return out
+
+
+def shard_partition(inp, n: int, key_shift: int, dest_bits: int, out, stream: int | None = None) -> list[int]:
+    counts = (C.c_uint64 * (1 << dest_bits))()
+    _check(lib.mi355_rho_shard_partition(ptr(inp), n, key_shift, dest_bits, ptr(out), counts, stream or None))
+    return [int(c) for c in counts]
+
+
+def timing_enable(on: bool = True) -> None:
+    lib.mi355_timing_enable(1 if on else 0)
+
+
+def timings() -> list[tuple[str, float]]:
+    cap = 256
+    names = (C.c_char_p * cap)()
+    ms = (C.c_double * cap)()
+    n = lib.mi355_timing_get(names, ms, cap)
+    return [(names[i].decode(), ms[i]) for i in range(min(n, cap))]
+
+
+def set_stream(stream: int | None) -> None:
+    lib.mi355_set_stream(stream or None)
+
+
+# ------------------------------------------------------------------ scan ---
+def _scan_fn(kind: str, dtype: str):
+    return getattr(lib, f"mi355_scan_{kind}_{dtype}")
+
+
+def scan_count(lo: int, hi: int, col, n: int, dtype: str = "i32") -> int:
+    c = C.c_uint64()
+    _check(_scan_fn("count", dtype)(lo, hi, ptr(col), n, C.byref(c)))
+    return int(c.value)
+
+
+def scan_bitvector(lo: int, hi: int, col, n: int, out_words, dtype: str = "i32") -> None:
+    _check(_scan_fn("bitvector", dtype)(lo, hi, ptr(col), n, ptr(out_words)))
+
+
+def scan_index(lo: int, hi: int, col, n: int, out, cap: int, dtype: str = "i32") -> int:
+    c = C.c_uint64()
+    _check(_scan_fn("index", dtype)(lo, hi, ptr(col), n, ptr(out), cap, C.byref(c)))
+    return int(c.value)
+
+
+def scan_values(lo: int, hi: int, col, n: int, out, cap: int, dtype: str = "i32") -> int:
+    c = C.c_uint64()
+    _check(_scan_fn("values", dtype)(lo, hi, ptr(col), n, ptr(out), cap, C.byref(c)))
+    return int(c.value)
+
+
+# ------------------------------------------------------------- generators ---
+def gen_seed(seed: int) -> None:
+    lib.mi355_gen_seed(seed)
+
+
+def gen_pk(out, n: int) -> None:
+    _check(lib.mi355_gen_pk(ptr(out), n))
+
+
+def gen_fk(out, n: int, maxid: int) -> None:
+    _check(lib.mi355_gen_fk(ptr(out), n, maxid))
+
+
+def gen_fk_sel(out, n: int, maxid: int) -> None:
+    _check(lib.mi355_gen_fk_sel(ptr(out), n, maxid))
+
+
+def gen_zipf(out, n: int, alphabet: int, theta: float, seed: int, nthreads: int = 8) -> None:
+    _check(lib.mi355_gen_zipf(ptr(out), n, alphabet, theta, seed, nthreads))
+
+
+def gen_pk_dev(out, count: int, first: int, n: int, seed: int, stream: int | None = None) -> None:
+    _check(lib.mi355_gen_pk_dev(ptr(out), count, first, n, seed, stream or None))
+
+
+def gen_fk_dev(out, count: int, first: int, maxid: int, seed: int, stream: int | None = None) -> None:
+    _check(lib.mi355_gen_fk_dev(ptr(out), count, first, maxid, seed, stream or None))
+
+
+def gen_scan_dev(out, n: int, mode: int, seed: int, dtype: str = "i32", stream: int | None = None) -> None:
+    _check(getattr(lib, f"mi355_gen_scan_{dtype}_dev")(ptr(out), n, mode, seed, stream or None))
+
+
+def reference_relations(nR: int, nS: int, *, selectivity: int = 100, skew: float = 0.0,
+                        r_seed: int = 11111, s_seed: int = 22222, zipf_seed: int | None = None,
+                        nthreads: int = 8):
+    """R and S exactly as the reference's native driver builds them (native.cpp:62-101),
+    as numpy structured arrays of row_t (payload = row index)."""
+    import numpy as np
+
+    dt = np.dtype([("key", "<u4"), ("payload", "<u4")])
+    R = np.empty(nR, dtype=dt)
+    S = np.empty(nS, dtype=dt)
+    gen_seed(r_seed)
+    gen_pk(R, nR)
+    gen_seed(s_seed)
+    if skew > 0:
+        gen_zipf(S, nS, nR, skew, s_seed if zipf_seed is None else zipf_seed, nthreads)
+    elif selectivity != 100:
+        maxid = (100 * nR // selectivity) & 0xFFFFFFFF if selectivity else 0
+        gen_fk_sel(S, nS, maxid)
+    else:
+        gen_fk(S, nS, nR)
+    return R, S

@@ -1,0 +1,162 @@
+"""RHO join on the MI355X vs the CPU oracle: bit-exact match counts.
+
+The oracle (oracle/rho_oracle.c) restates radix_join.cpp; relations come from the
+restated reference generators (native.cpp:62-101 seeds and shapes)."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import PKG
+
+pytestmark = pytest.mark.gpu
+
+DT = np.dtype([("key", "<u4"), ("payload", "<u4")])
+
+
+def rel(keys):
+    x = np.empty(len(keys), dtype=DT)
+    x["key"] = keys
+    x["payload"] = np.arange(len(keys), dtype=np.uint32)
+    return x
+
+
+def gpu_join(sgx, R, S, **kw):
+    return sgx.rho_join(R, len(R), S, len(S), **kw)
+
+
+@pytest.mark.parametrize("n", [1 << 10, 1 << 16, 1 << 20])
+def test_reference_pk_fk(sgx, orc, gpu, n):
+    R, S = sgx.reference_relations(n, n)
+    exp, _ = orc.rho_join(R, S, 4)
+    assert exp == n
+    res = gpu_join(sgx, R, S)
+    assert res.matches == exp
+    assert res.stats["ms_total"] > 0
+
+
+def test_config1_native_cpu_shape(sgx, orc, gpu):
+    # BASELINE config 1: |R| = |S| = 2^20 uniform; reference policy 5 bits / 1 pass
+    R, S = sgx.reference_relations(1 << 20, 1 << 20)
+    exp, t = orc.rho_join(R, S, 2)
+    assert (t["radix_bits"], t["passes"]) == (5, 1)
+    for bits, passes in [(0, 0), (5, 1), (8, 1), (9, 1), (12, 2), (16, 2), (18, 2)]:
+        assert gpu_join(sgx, R, S, radix_bits=bits, passes=passes).matches == exp, (bits, passes)
+
+
+@pytest.mark.parametrize("sel", [50, 10, 1])
+def test_fk_sel(sgx, orc, gpu, sel):
+    R, S = sgx.reference_relations(1 << 18, 1 << 18, selectivity=sel)
+    assert gpu_join(sgx, R, S).matches == orc.rho_join(R, S, 4)[0]
+
+
+def test_fk_multiple_copies(sgx, orc, gpu):
+    R, S = sgx.reference_relations(1 << 16, 1 << 19)
+    assert gpu_join(sgx, R, S).matches == 1 << 19
+
+
+def test_zipf(sgx, orc, gpu):
+    n = 1 << 18
+    R, S = sgx.reference_relations(n, n, skew=0.75)
+    res = gpu_join(sgx, R, S)
+    assert res.matches == orc.rho_join(R, S, 4)[0] == n
+    assert res.stats["max_part_s"] > 1.5 * (n >> res.stats["radix_bits"])  # skew reaches the partitions
+
+
+@pytest.mark.parametrize("seed,nR,nS,kmax", [(1, 5000, 7000, 300), (2, 1 << 17, 1 << 15, 1 << 12),
+                                             (3, 100_003, 77_777, 2**32 - 1), (4, 3, 5, 2)])
+def test_random_with_duplicates(sgx, orc, gpu, seed, nR, nS, kmax):
+    rng = np.random.default_rng(seed)
+    R = rel(rng.integers(0, kmax + 1, nR, dtype=np.uint64).astype(np.uint32))
+    S = rel(rng.integers(0, kmax + 1, nS, dtype=np.uint64).astype(np.uint32))
+    exp = orc.count_join_sort(R, S)
+    for bits, passes in [(0, 0), (4, 1), (14, 2)]:
+        assert gpu_join(sgx, R, S, radix_bits=bits, passes=passes).matches == exp
+
+
+def test_extreme_keys(sgx, orc, gpu):
+    # 0 and 0xFFFFFFFF (the LDS empty marker) must join like any other key
+    keys = np.array([0, 0xFFFFFFFF, 0xFFFFFFFF, 1, 0x80000000, 0xFFFFFFFE] * 50, dtype=np.uint32)
+    R = rel(keys)
+    S = rel(np.concatenate([keys[::-1], np.array([0xFFFFFFFF] * 7, dtype=np.uint32)]))
+    exp = orc.count_join_sort(R, S)
+    for bits in (0, 3, 10):
+        assert gpu_join(sgx, R, S, radix_bits=bits).matches == exp
+
+
+def test_skewed_build_side_chunks(sgx, orc, gpu):
+    # one R partition far larger than an LDS table (R chunking) plus a hot S key
+    R = rel(np.concatenate([np.full(20_000, 7, np.uint32), np.arange(1, 5001, dtype=np.uint32)]))
+    S = rel(np.concatenate([np.full(1000, 7, np.uint32), np.arange(1, 90_001, dtype=np.uint32)]))
+    exp = orc.count_join_sort(R, S)
+    assert exp == 20_000 * 1000 + 20_000 + 4999
+    assert gpu_join(sgx, R, S).matches == exp
+    assert gpu_join(sgx, R, S, radix_bits=2).matches == exp
+
+
+@pytest.mark.parametrize("nR,nS", [(0, 10), (10, 0), (1, 1), (63, 2049), (2049, 63)])
+def test_empty_and_ragged(sgx, orc, gpu, nR, nS):
+    R, _ = sgx.reference_relations(max(nR, 1), 1)
+    R = R[:nR]
+    S = rel(np.arange(1, nS + 1, dtype=np.uint32) % max(nR, 1) + 1)
+    exp = orc.count_join_sort(R, S) if nR and nS else 0
+    assert gpu_join(sgx, R, S).matches == exp
+
+
+def test_device_resident_inputs(sgx, orc, gpu):
+    import torch
+
+    R, S = sgx.reference_relations(1 << 18, 1 << 18)
+    dR = torch.from_numpy(R.view(np.int64)).to(gpu)
+    dS = torch.from_numpy(S.view(np.int64)).to(gpu)
+    res = sgx.rho_join(dR, len(R), dS, len(S))
+    assert res.matches == 1 << 18 and res.stats["ms_h2d"] == 0.0
+    # inputs are const: untouched
+    assert np.array_equal(dR.cpu().numpy().view(DT), R)
+
+
+def test_dropin_table_api(sgx, gpu):
+    R, S = sgx.reference_relations(1 << 16, 1 << 16)
+    out = sgx.rho_join_tables(R, len(R), S, len(S), nthreads=16)
+    assert out.totalresults == 1 << 16
+    assert out.nthreads == 16 and out.materialized == 0 and out.result_type == 0
+    assert out.throughput > 0
+
+
+def test_shard_partition_is_stable_radix_partition(sgx, orc, gpu):
+    import torch
+
+    rng = np.random.default_rng(5)
+    x = rel(rng.integers(0, 2**32, 300_001, dtype=np.uint64).astype(np.uint32))
+    dx = torch.from_numpy(x.view(np.int64)).to(gpu)
+    out = torch.empty_like(dx)
+    for shift, bits in [(0, 3), (0, 1), (5, 9)]:
+        counts = sgx.shard_partition(dx, len(x), shift, bits, out)
+        ref, starts = orc.radix_partition(x, 1, shift, bits)
+        assert counts == np.diff(starts).tolist()
+        assert np.array_equal(out.cpu().numpy().view(DT), ref)
+
+
+def test_full_size_config2_property(sgx, gpu):
+    """BASELINE config 2 size (|R| = |S| = 2^28) on device-generated pk/fk: matches == |S|."""
+    import torch
+
+    n = 1 << 28
+    R = torch.empty(n, dtype=torch.int64, device=gpu)
+    S = torch.empty(n, dtype=torch.int64, device=gpu)
+    sgx.gen_pk_dev(R, n, 0, n, 11111)
+    sgx.gen_fk_dev(S, n, 0, n, 22222)
+    res = sgx.rho_join(R, n, S, n)
+    assert res.matches == n
+    assert res.stats["radix_bits"] == 16 and res.stats["passes"] == 2
+    del R, S
+    torch.cuda.empty_cache()
+
+
+def test_native_driver_binary(gpu):
+    exe = os.path.join(PKG, "bin", "native_mi355")
+    out = subprocess.run([exe, "-a", "RHO", "-r", str(1 << 20), "-s", str(1 << 20), "-n", "2"],
+                         capture_output=True, text=True, timeout=300, check=True).stdout
+    assert "Matches = 1048576" in out
+    assert "Throughput (M rec/sec)" in out
