@@ -91,6 +91,7 @@ def main():
 
     stream = torch.cuda.current_stream().cuda_stream
     sgxamd.set_stream(stream)
+    sgxamd.timing_enable(True)  # per-kernel HIP events on `stream` (roofline "achieved")
 
     # ---------------- RHO workload: rank slice of global pk(N n) and fk(N n, N n)
     n = 1 << args.log2n

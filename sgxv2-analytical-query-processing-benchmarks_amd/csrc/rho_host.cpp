@@ -32,7 +32,7 @@ inline uint32_t ceil_log2(uint64_t x) {
 }
 
 struct Policy {
-    uint32_t bits, passes, b1, b2, table_slots;
+    uint32_t bits, passes, b1, b2, rcap;
 };
 
 Policy choose_policy(uint64_t nR, const mi355_rho_opts *o) {
@@ -43,7 +43,7 @@ Policy choose_policy(uint64_t nR, const mi355_rho_opts *o) {
         const uint64_t need = (nR + kTargetPartition - 1) / kTargetPartition;
         p.bits = std::min(ceil_log2(std::max<uint64_t>(need, 1)), kMaxBits);
     }
-    p.passes = (o && o->passes > 0) ? (uint32_t)o->passes : (p.bits <= 9 ? 1u : 2u);
+    p.passes = (o && o->passes > 0) ? (uint32_t)o->passes : (p.bits <= 8 ? 1u : 2u);
     if (p.passes > 2) p.passes = 2;
     if (p.bits > 9 && p.passes == 1) p.passes = 2;  // one pass is limited to kMaxF = 2^9 bins
     if (p.passes == 2 && p.bits < 2) p.passes = 1;
@@ -54,9 +54,9 @@ Policy choose_policy(uint64_t nR, const mi355_rho_opts *o) {
         p.b1 = (p.bits + 1) / 2;
         p.b2 = p.bits - p.b1;
     }
-    // table large enough that the average partition needs one R chunk
-    const uint64_t avg = (nR >> p.bits) + 1;
-    p.table_slots = avg > 4096 ? 16384 : (avg > 2048 ? 8192 : 8192);
+    // chain table large enough that the average partition needs one R chunk
+    const uint64_t avg = (nR + (1ull << p.bits) - 1) >> p.bits;
+    p.rcap = avg <= 2048 ? 2048 : (avg <= 4096 ? 4096 : 8192);
     return p;
 }
 
@@ -200,7 +200,7 @@ int join_device(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const
     uint64_t *partials = A.at<uint64_t>(off_partials);
     uint64_t *result = A.at<uint64_t>(off_result);
     tm.mark("join_build_probe");
-    RHO_HIP(launch_join(fR, fS, psR, pcR, psS, pcS, P, key_shift + pol.bits, pol.table_slots, join_grid, partials,
+    RHO_HIP(launch_join(fR, fS, psR, pcR, psS, pcS, P, key_shift + pol.bits, pol.rcap, join_grid, partials,
                         s));
     tm.mark("join_reduce");
     RHO_HIP(launch_reduce(partials, join_grid, result, s));

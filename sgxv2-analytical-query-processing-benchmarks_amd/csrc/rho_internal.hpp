@@ -13,9 +13,10 @@ namespace rho {
 
 constexpr int kBlock = 256;   // threads per workgroup for partition/join kernels
 constexpr int kMaxF = 512;    // max fanout of one partition pass (9 radix bits)
+constexpr int kScatterThreads = 256;                  // threads per scatter workgroup
 constexpr int kScatterItems = 8;                      // tuples per thread per tile
-constexpr int kTile = kBlock * kScatterItems;         // tuples per scatter tile
-constexpr uint32_t kEmptyKey = 0xFFFFFFFFu;           // LDS hash-table empty marker
+constexpr int kTile = kScatterThreads * kScatterItems;  // tuples per scatter tile
+constexpr int kScatterSegTuples = 16;                 // write-combining granule: 16 tuples = 128 B
 
 // Which contiguous slice of the input a partition workgroup owns.  Regions are
 // the bins of the previous pass (or the whole relation); each region is cut into
@@ -55,9 +56,10 @@ hipError_t launch_scatter(const row_t *in, row_t *out, const SegMap &m, uint32_t
                           const uint64_t *digit_base, hipStream_t s);
 
 // Build + probe over P partitions; writes one partial count per workgroup.
+// rcap (2048 / 4096 / 8192) = R tuples per LDS chain table; LDS = 10 * rcap bytes.
 hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, const uint64_t *r_count,
                        const uint64_t *s_start, const uint64_t *s_count, uint64_t P, uint32_t hash_shift,
-                       uint32_t table_slots, uint32_t grid, uint64_t *partials, hipStream_t s);
+                       uint32_t rcap, uint32_t grid, uint64_t *partials, hipStream_t s);
 
 hipError_t launch_reduce(const uint64_t *partials, uint32_t n, uint64_t *result, hipStream_t s);
 

@@ -3,10 +3,10 @@
 // The reference's CPU hot loops and what replaces them here:
 //   partition_hist[_unrolled]   radix_join.cpp:617-654  -> k_hist
 //   local/global prefix         radix_join.cpp:886-915  -> k_scan_cols / k_scan_digits / k_scan_regions
-//   partition_copy[_unrolled]   radix_join.cpp:659-697  -> k_scatter (stable LDS multisplit, the
-//                               GPU analogue of the SWWC variant at :961-1056)
-//   bucket_chaining_join        radix_join.cpp:359-458  -> k_join (LDS linear-probing table per
-//                               partition, S streamed, one partial count per workgroup)
+//   partition_copy[_unrolled]   radix_join.cpp:659-697  -> k_scatter (LDS counting sort per tile with
+//                               64-B write combining, the SWWC variant at :961-1056)
+//   bucket_chaining_join        radix_join.cpp:359-458  -> k_join (the same bucket chains in LDS,
+//                               S streamed, one partial count per workgroup)
 // Radix digits are taken as (key >> shift) & (F - 1) with the pass-1 digit in the
 // low bits, exactly like HASH_BIT_MODULO(key, MASK, R) (:47) with R = shift.
 // All work is integer; HBM bandwidth is the roofline.
@@ -177,140 +177,264 @@ hipError_t launch_scan_regions(uint64_t *hist, const uint32_t *seg_base, const u
 }
 
 // --------------------------------------------------------------- scatter ---
-// Stable multisplit of tiles of kTile tuples.  Wave w owns tile rows
-// [w*64*ITEMS, (w+1)*64*ITEMS); item k of lane l is row w*64*ITEMS + k*64 + l, so
-// (wave, item, lane) order is input order.  Equal-digit peers in a wave are found
-// with one ballot per digit bit; per-wave LDS counters give stable ranks; the tile
-// is reordered by digit in LDS and written as contiguous per-digit runs that
-// continue where the previous tile of this workgroup stopped.
-template <int ITEMS>
-__global__ __launch_bounds__(kBlock) void k_scatter(const uint64_t *__restrict__ in, uint64_t *__restrict__ out,
-                                                    SegMap m, uint32_t shift, uint32_t bits,
-                                                    const uint64_t *__restrict__ cur_init, HistLayout layout,
-                                                    uint32_t nseg_stride, const uint64_t *__restrict__ digit_base) {
-    constexpr int TILE = kBlock * ITEMS;
-    __shared__ uint32_t sbase[kMaxF + 1];
-    __shared__ uint32_t wcnt[kWaves][kMaxF];
-    __shared__ uint32_t tcnt[kMaxF];
-    __shared__ uint32_t toff[kMaxF];
-    __shared__ uint64_t cursor[kMaxF];
-    __shared__ uint64_t scratch[kWaves + 1];
-    __shared__ uint64_t stage[TILE];
+// Partition copy of one segment per workgroup (partition_copy, radix_join.cpp:659-697),
+// organised like the reference's software write-combining variant
+// parallel_radix_partition_optimized (:961-1056): every digit keeps its unfinished
+// output segment (SEGT tuples, 128 B) and only whole, aligned segments go to HBM.
+// Thread d owns digit d: its pending carry (< SEGT tuples) and its write cursor
+// live in that thread's registers, not in LDS.  Per tile of NT * ITEMS tuples:
+//   1. each tuple takes a slot of its digit with one LDS atomic (tile histogram and
+//      in-tile rank at once; order inside a digit is arrival order, the join count
+//      does not depend on it);
+//   2. per digit: pending = carried tuples + this tile's tuples; the prefix that ends
+//      on a segment boundary is written, the rest (< SEGT tuples) is carried on;
+//   3. tuples are placed in LDS as [all written tuples, digit-major | new carries]
+//      and the written block goes out with consecutive lanes on consecutive addresses.
+// The next tile's tuples are already loading while a tile is processed (two
+// register sets).  The last carries of the segment are flushed at the end.
+template <int BITS, int ITEMS, int NT, int SEGT>
+struct ScatterLds {
+    static constexpr uint32_t F = 1u << BITS;
+    static constexpr uint32_t TILE = NT * ITEMS;
+    static constexpr uint32_t NW = NT / kWave;
+    uint32_t cnt[F];     // tile count -> sequence position of the tile's first tuple of d
+    uint32_t cbase[F];   // stage index of sequence position 0 of d in the carry block (minus wcount)
+    uint32_t wbase[F];   // stage index of sequence position 0 of d in the write block
+    uint32_t wcount[F];  // tuples of d written this tile
+    uint64_t ob[F];      // output base of d: global position = ob[d] + stage index
+    uint32_t wtot[NW][2];
+    union {
+        uint32_t sbase[kMaxF + 1];  // segment table (only before the first tile)
+        uint64_t stage[TILE + (SEGT - 1) * F];
+    };
+};
 
+template <int ITEMS, int NT>
+__device__ __forceinline__ void load_tile(const uint64_t *__restrict__ in, uint64_t tb, uint64_t e,
+                                          uint64_t (&dst)[ITEMS]) {
+    constexpr uint32_t TILE = NT * ITEMS;
+    if (tb + TILE <= e) {
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) dst[k] = __builtin_nontemporal_load(in + tb + threadIdx.x + k * NT);
+    } else {
+        const uint32_t tn = (uint32_t)(e - tb);
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) {
+            const uint32_t li = threadIdx.x + k * NT;
+            dst[k] = li < tn ? in[tb + li] : 0ull;
+        }
+    }
+}
+
+// Block-wide exclusive scan of two u32 counters at once (one __syncthreads).
+template <int NW>
+__device__ __forceinline__ void block_scan2(uint32_t a, uint32_t b, uint32_t (&wt)[NW][2], uint32_t &ea,
+                                            uint32_t &eb, uint32_t &ta, uint32_t &tb) {
+    const uint32_t lane = __lane_id(), wave = threadIdx.x / kWave;
+    const uint32_t ia = wave_incl_scan_u32(a), ib = wave_incl_scan_u32(b);
+    if (lane == kWave - 1) {
+        wt[wave][0] = ia;
+        wt[wave][1] = ib;
+    }
+    __syncthreads();
+    uint32_t pa = 0, pb = 0;
+    ta = 0;
+    tb = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+        const uint32_t x = wt[w][0], y = wt[w][1];
+        if (w < (int)wave) {
+            pa += x;
+            pb += y;
+        }
+        ta += x;
+        tb += y;
+    }
+    ea = pa + ia - a;
+    eb = pb + ib - b;
+}
+
+// Per-digit state held in the registers of the digit's owner thread.
+template <int SEGT>
+struct DigitState {
+    uint64_t pend;           // global position of the first pending tuple
+    uint32_t c;              // carried tuples
+    uint64_t carry[SEGT - 1];
+};
+
+template <int BITS, int ITEMS, int NT, int SEGT>
+__device__ __forceinline__ void scatter_tile(ScatterLds<BITS, ITEMS, NT, SEGT> &L, DigitState<SEGT> &ds,
+                                             const uint64_t (&v)[ITEMS], uint64_t *__restrict__ out, uint32_t tn,
+                                             uint32_t shift) {
+    constexpr uint32_t F = 1u << BITS, mask = F - 1;
+    const uint32_t tid = threadIdx.x;
+    const bool owner = tid < F;  // thread tid owns digit tid
+    // 1. slot of every tuple inside its digit
+    uint32_t slot[ITEMS];
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {
+        if (tid + k * NT < tn) slot[k] = atomicAdd(&L.cnt[((uint32_t)v[k] >> shift) & mask], 1u);
+    }
+    __syncthreads();
+    // 2. per digit: what is written now, what is carried on
+    uint32_t w = 0, r = 0, c = 0;
+    if (owner) {
+        const uint32_t t = L.cnt[tid];
+        c = ds.c;
+        const uint64_t end = ds.pend + c + t;
+        const uint64_t aligned = end & ~uint64_t(SEGT - 1);
+        w = aligned > ds.pend ? (uint32_t)(aligned - ds.pend) : 0u;
+        r = c + t - w;
+    }
+    uint32_t we, re, W, R;
+    block_scan2(w, r, L.wtot, we, re, W, R);
+    if (owner) {
+        L.wbase[tid] = we;
+        L.cbase[tid] = W + re - w;
+        L.wcount[tid] = w;
+        L.ob[tid] = ds.pend - we;
+        L.cnt[tid] = c;  // sequence position of the tile's first tuple
+        // old carries open the digit's sequence
+#pragma unroll
+        for (int s = 0; s < SEGT - 1; ++s)
+            if ((uint32_t)s < c) L.stage[(uint32_t)s < w ? we + s : W + re - w + s] = ds.carry[s];
+        ds.pend += w;
+        ds.c = r;
+    }
+    __syncthreads();
+    // 3. place the tile's tuples behind the carries
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {
+        if (tid + k * NT < tn) {
+            const uint32_t d = ((uint32_t)v[k] >> shift) & mask;
+            const uint32_t s = L.cnt[d] + slot[k];
+            L.stage[s < L.wcount[d] ? L.wbase[d] + s : L.cbase[d] + s] = v[k];
+        }
+    }
+    __syncthreads();
+    // 4. write whole segments; collect the new carries; reset the counters
+    for (uint32_t i = tid; i < W; i += NT) {
+        const uint64_t x = L.stage[i];
+        out[L.ob[((uint32_t)x >> shift) & mask] + i] = x;
+    }
+    if (owner) {
+#pragma unroll
+        for (int s = 0; s < SEGT - 1; ++s)
+            if ((uint32_t)s < r) ds.carry[s] = L.stage[W + re + s];
+        L.cnt[tid] = 0;
+    }
+    __syncthreads();
+}
+
+template <int BITS, int ITEMS, int NT, int SEGT>
+__global__ __launch_bounds__(NT) void k_scatter(const uint64_t *__restrict__ in, uint64_t *__restrict__ out,
+                                                SegMap m, uint32_t shift, const uint64_t *__restrict__ cur_init,
+                                                HistLayout layout, uint32_t nseg_stride,
+                                                const uint64_t *__restrict__ digit_base) {
+    constexpr uint32_t TILE = NT * ITEMS;
+    constexpr uint32_t F = 1u << BITS;
+    static_assert(F <= NT, "one owner thread per digit");
+    __shared__ ScatterLds<BITS, ITEMS, NT, SEGT> L;
     const uint32_t g = blockIdx.x;
     uint32_t r;
     uint64_t b, e;
-    if (!seg_lookup(m, g, sbase, r, b, e)) return;
-    const uint32_t F = 1u << bits, mask = F - 1;
-    const uint32_t tid = threadIdx.x, lane = __lane_id(), wave = tid / kWave;
-    for (uint32_t d = tid; d < F; d += kBlock)
-        cursor[d] = cur_init[hist_index(layout, g, d, F, nseg_stride)] +
-                    (digit_base ? digit_base[(uint64_t)r * F + d] : 0);
-
-    const uint64_t lt = lanemask_lt();
-    for (uint64_t tb = b; tb < e; tb += TILE) {
-        const uint32_t tn = (uint32_t)((e - tb) < (uint64_t)TILE ? (e - tb) : (uint64_t)TILE);
-        for (uint32_t i = tid; i < kWaves * F; i += kBlock) (&wcnt[0][0])[(i / F) * kMaxF + (i % F)] = 0;
-        uint64_t v[ITEMS];
-#pragma unroll
-        for (int k = 0; k < ITEMS; ++k) {
-            const uint32_t li = wave * kWave * ITEMS + k * kWave + lane;
-            v[k] = li < tn ? in[tb + li] : 0ull;
-        }
-        __syncthreads();
-        uint32_t dig[ITEMS], rank[ITEMS];
-#pragma unroll
-        for (int k = 0; k < ITEMS; ++k) {
-            const uint32_t li = wave * kWave * ITEMS + k * kWave + lane;
-            const bool valid = li < tn;
-            const uint32_t d = valid ? (((uint32_t)v[k] >> shift) & mask) : 0u;
-            uint64_t peers = __ballot(valid);
-            for (uint32_t bit = 0; bit < bits; ++bit) {
-                const bool set = (d >> bit) & 1u;
-                const uint64_t bb = __ballot(set);
-                peers &= set ? bb : ~bb;
-            }
-            uint32_t rk = 0;
-            if (valid) {
-                const uint32_t old = wcnt[wave][d];
-                const uint64_t below = peers & lt;
-                rk = old + popc64(below);
-                if (below == 0) wcnt[wave][d] = old + popc64(peers);
-            }
-            dig[k] = d;
-            rank[k] = rk;
-        }
-        __syncthreads();
-        // per digit: exclusive prefix across waves (in place) and the tile count
-        for (uint32_t d = tid; d < F; d += kBlock) {
-            uint32_t acc = 0;
-#pragma unroll
-            for (int w = 0; w < kWaves; ++w) {
-                const uint32_t t = wcnt[w][d];
-                wcnt[w][d] = acc;
-                acc += t;
-            }
-            tcnt[d] = acc;
-        }
-        __syncthreads();
-        // exclusive scan over digits (F <= 2 * kBlock): two digits per thread
-        {
-            const uint32_t d0 = 2 * tid, d1 = 2 * tid + 1;
-            const uint32_t c0 = d0 < F ? tcnt[d0] : 0u, c1 = d1 < F ? tcnt[d1] : 0u;
-            uint64_t tot;
-            const uint64_t ex = block_excl_scan_u64((uint64_t)c0 + c1, scratch, &tot);
-            if (d0 < F) toff[d0] = (uint32_t)ex;
-            if (d1 < F) toff[d1] = (uint32_t)ex + c0;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < ITEMS; ++k) {
-            const uint32_t li = wave * kWave * ITEMS + k * kWave + lane;
-            if (li < tn) stage[toff[dig[k]] + wcnt[wave][dig[k]] + rank[k]] = v[k];
-        }
-        __syncthreads();
-        for (uint32_t i = tid; i < tn; i += kBlock) {
-            const uint64_t x = stage[i];
-            const uint32_t d = ((uint32_t)x >> shift) & mask;
-            out[cursor[d] + (i - toff[d])] = x;
-        }
-        __syncthreads();
-        for (uint32_t d = tid; d < F; d += kBlock) cursor[d] += tcnt[d];
-        __syncthreads();
+    if (!seg_lookup(m, g, L.sbase, r, b, e)) return;
+    DigitState<SEGT> ds;
+    ds.c = 0;
+    ds.pend = 0;
+    const uint32_t tid = threadIdx.x;
+    if (tid < F) {
+        ds.pend = cur_init[hist_index(layout, g, tid, F, nseg_stride)] +
+                  (digit_base ? digit_base[(uint64_t)r * F + tid] : 0);
+        L.cnt[tid] = 0;
     }
+    __syncthreads();  // sbase (aliased with stage) is dead from here on
+    uint64_t va[ITEMS], vb[ITEMS];
+    load_tile<ITEMS, NT>(in, b, e, va);
+    for (uint64_t tb = b; tb < e; tb += 2 * TILE) {
+        if (tb + TILE < e) load_tile<ITEMS, NT>(in, tb + TILE, e, vb);
+        scatter_tile<BITS, ITEMS, NT, SEGT>(L, ds, va, out, (uint32_t)min<uint64_t>(TILE, e - tb), shift);
+        if (tb + TILE >= e) break;
+        const uint64_t t2 = tb + TILE;
+        if (t2 + TILE < e) load_tile<ITEMS, NT>(in, t2 + TILE, e, va);
+        scatter_tile<BITS, ITEMS, NT, SEGT>(L, ds, vb, out, (uint32_t)min<uint64_t>(TILE, e - t2), shift);
+    }
+    // flush the carried (partial) segments
+    if (tid < F) {
+#pragma unroll
+        for (int s = 0; s < SEGT - 1; ++s)
+            if ((uint32_t)s < ds.c) out[ds.pend + s] = ds.carry[s];
+    }
+}
+
+template <int ITEMS, int NT, int SEGT>
+hipError_t launch_scatter_items(const uint64_t *in, uint64_t *out, const SegMap &m, uint32_t grid, uint32_t shift,
+                                uint32_t bits, const uint64_t *cursors, HistLayout layout, uint32_t nseg_stride,
+                                const uint64_t *digit_base, hipStream_t s) {
+#define SCATTER_CASE(B)                                                                                    \
+    case B:                                                                                                \
+        if constexpr (sizeof(ScatterLds<B, ITEMS, NT, SEGT>) <= 160 * 1024 && (1 << B) <= NT) {             \
+            hipLaunchKernelGGL((k_scatter<B, ITEMS, NT, SEGT>), dim3(grid), dim3(NT), 0, s, in, out, m, shift, \
+                               cursors, layout, nseg_stride, digit_base);                                  \
+            break;                                                                                         \
+        } else {                                                                                           \
+            return hipErrorInvalidValue;                                                                   \
+        }
+    switch (bits) {
+        SCATTER_CASE(0)
+        SCATTER_CASE(1)
+        SCATTER_CASE(2)
+        SCATTER_CASE(3)
+        SCATTER_CASE(4)
+        SCATTER_CASE(5)
+        SCATTER_CASE(6)
+        SCATTER_CASE(7)
+        SCATTER_CASE(8)
+        SCATTER_CASE(9)
+        default:
+            return hipErrorInvalidValue;
+    }
+#undef SCATTER_CASE
+    return hipGetLastError();
 }
 
 hipError_t launch_scatter(const row_t *in, row_t *out, const SegMap &m, uint32_t grid, uint32_t shift,
                           uint32_t bits, const uint64_t *cursors, HistLayout layout, uint32_t nseg_stride,
                           const uint64_t *digit_base, hipStream_t s) {
     if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_scatter<kScatterItems>, dim3(grid), dim3(kBlock), 0, s,
-                       reinterpret_cast<const uint64_t *>(in), reinterpret_cast<uint64_t *>(out), m, shift, bits,
-                       cursors, layout, nseg_stride, digit_base);
-    return hipGetLastError();
+    const uint64_t *i64 = reinterpret_cast<const uint64_t *>(in);
+    uint64_t *o64 = reinterpret_cast<uint64_t *>(out);
+    if (bits > 8)  // 512 digit owners: 512-thread workgroups with the same tile size, 64-B granules (LDS)
+        return launch_scatter_items<kTile / 512, 512, 8>(i64, o64, m, grid, shift, bits, cursors, layout,
+                                                         nseg_stride, digit_base, s);
+    return launch_scatter_items<kScatterItems, kScatterThreads, kScatterSegTuples>(
+        i64, o64, m, grid, shift, bits, cursors, layout, nseg_stride, digit_base, s);
 }
 
 // ------------------------------------------------------------ build+probe ---
-// One partition per loop iteration.  R keys go into an LDS linear-probing table of
-// T = nextpow2(2 |R_chunk|) slots (load factor <= 1/2); R chunks larger than
-// TMAX / 2 are built one after another and S is re-probed per chunk.  Duplicate R
-// keys occupy separate slots, so a probe counts every equal key in its cluster,
-// which is what walking the reference's bucket chain does (:429-436).  The slot
-// of a key is its bits above the radix bits, HASH_BIT_MODULO(key, (N-1)<<bits, bits)
-// of bucket_chaining_join (:378,:388).  A key equal to the empty marker is counted
-// on the side.
-template <int TMAX>
+// bucket_chaining_join (radix_join.cpp:359-458) per partition, in LDS.  For an R
+// chunk of nrc <= RCAP tuples: N = nextpow2(nrc) bucket heads, bucket of a key =
+// HASH_BIT_MODULO(key, (N-1) << bits, bits) = (key >> bits) & (N-1) exactly as
+// the reference (:374-378, :388); keys[] and 16-bit next[] hold the chains with
+// 1-based positions (:393 "we start pos's from 1").  The build links tuple i with
+// one LDS atomic exchange on its bucket head (chain order differs from the
+// reference's serial build; the count does not).  The probe walks every chain and
+// counts key equality (:429-436).  Each thread handles U = RCAP / kBlock tuples at
+// a time; their chain walks advance in lockstep so the LDS reads of independent
+// tuples overlap.  Partitions whose R side exceeds RCAP are built chunk by chunk
+// with S re-probed per chunk.  One partial count per workgroup.
+template <int RCAP>
 __global__ __launch_bounds__(kBlock) void k_join(const uint32_t *__restrict__ Rw, const uint32_t *__restrict__ Sw,
                                                  const uint64_t *__restrict__ r_start,
                                                  const uint64_t *__restrict__ r_count,
                                                  const uint64_t *__restrict__ s_start,
                                                  const uint64_t *__restrict__ s_count, uint64_t P,
                                                  uint32_t hash_shift, uint64_t *__restrict__ partials) {
-    __shared__ __attribute__((aligned(16))) uint32_t table[TMAX];
-    __shared__ uint32_t s_empty;
-    __shared__ uint64_t red[kWaves];
-    constexpr uint32_t RCAP = TMAX / 2;
-    constexpr int U = 4;
+    constexpr int U = RCAP / kBlock;
+    __shared__ __attribute__((aligned(16))) uint32_t head[RCAP];
+    __shared__ uint32_t keys[RCAP];
+    __shared__ uint16_t next[RCAP];
+    uint64_t *red = reinterpret_cast<uint64_t *>(head);  // reused after the last table (keeps LDS = 10 * RCAP)
     const uint32_t tid = threadIdx.x;
     uint64_t matches = 0;
     for (uint64_t p = blockIdx.x; p < P; p += gridDim.x) {
@@ -319,64 +443,61 @@ __global__ __launch_bounds__(kBlock) void k_join(const uint32_t *__restrict__ Rw
         const uint64_t rb = r_start[p], sb = s_start[p];
         for (uint64_t rc = 0; rc < nR; rc += RCAP) {
             const uint32_t nrc = (uint32_t)((nR - rc) < RCAP ? (nR - rc) : RCAP);
-            uint32_t T = 64;
-            while (T < 2 * nrc) T <<= 1;
-            const uint32_t tmask = T - 1;
-            for (uint32_t i = tid; i < T / 4; i += kBlock)
-                reinterpret_cast<uint4 *>(table)[i] = make_uint4(kEmptyKey, kEmptyKey, kEmptyKey, kEmptyKey);
-            if (tid == 0) s_empty = 0;
-            __syncthreads();
-            // build
+            uint32_t N = 1;
+            while (N < nrc) N <<= 1;  // NEXT_POW_2(numR)
+            const uint32_t hmask = N - 1;
             const uint32_t *rk = Rw + 2 * (rb + rc);
-            for (uint32_t i = tid; i < nrc; i += kBlock) {
-                const uint32_t k = rk[2 * i];
-                if (k == kEmptyKey) {
-                    atomicAdd(&s_empty, 1u);
-                    continue;
+            uint32_t kr[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t i = tid + u * kBlock;
+                kr[u] = i < nrc ? rk[2 * i] : 0u;
+            }
+            for (uint32_t i = tid; i < (N + 3) / 4; i += kBlock)
+                reinterpret_cast<uint4 *>(head)[i] = make_uint4(0, 0, 0, 0);
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < U; ++u) {  // BUILD-LOOP (:407-411)
+                const uint32_t i = tid + u * kBlock;
+                if (i < nrc) {
+                    keys[i] = kr[u];
+                    const uint32_t prev = atomicExch(&head[(kr[u] >> hash_shift) & hmask], i + 1);
+                    next[i] = (uint16_t)prev;
                 }
-                uint32_t h = (k >> hash_shift) & tmask;
-                while (atomicCAS(&table[h], kEmptyKey, k) != kEmptyKey) h = (h + 1) & tmask;
             }
             __syncthreads();
-            const uint32_t n_empty = s_empty;
-            // probe
             const uint32_t *sk = Sw + 2 * sb;
-            uint64_t i = tid;
-            for (; i + (U - 1) * kBlock < nS; i += U * kBlock) {
-                uint32_t k[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) k[u] = sk[2 * (i + u * kBlock)];
+            for (uint64_t s0 = 0; s0 < nS; s0 += RCAP) {  // PROBE-LOOP (:429-436)
+                uint32_t ks[U], cur[U];
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
-                    if (k[u] == kEmptyKey) {
-                        matches += n_empty;
-                        continue;
-                    }
-                    uint32_t h = (k[u] >> hash_shift) & tmask;
-                    uint32_t t;
-                    while ((t = table[h]) != kEmptyKey) {
-                        matches += (t == k[u]);
-                        h = (h + 1) & tmask;
-                    }
+                    const uint64_t i = s0 + tid + u * kBlock;
+                    ks[u] = i < nS ? sk[2 * i] : 0u;
                 }
-            }
-            for (; i < nS; i += kBlock) {
-                const uint32_t k = sk[2 * i];
-                if (k == kEmptyKey) {
-                    matches += n_empty;
-                    continue;
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const uint64_t i = s0 + tid + u * kBlock;
+                    cur[u] = i < nS ? head[(ks[u] >> hash_shift) & hmask] : 0u;
                 }
-                uint32_t h = (k >> hash_shift) & tmask;
-                uint32_t t;
-                while ((t = table[h]) != kEmptyKey) {
-                    matches += (t == k);
-                    h = (h + 1) & tmask;
+                bool more = true;
+                while (more) {
+                    more = false;
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        if (cur[u]) {
+                            const uint32_t e = cur[u] - 1;
+                            matches += (keys[e] == ks[u]);
+                            cur[u] = next[e];
+                            more |= cur[u] != 0;
+                        }
+                    }
                 }
             }
             __syncthreads();
         }
     }
     matches = wave_sum_u64(matches);
+    __syncthreads();
     if (__lane_id() == 0) red[tid / kWave] = matches;
     __syncthreads();
     if (tid == 0) {
@@ -388,20 +509,20 @@ __global__ __launch_bounds__(kBlock) void k_join(const uint32_t *__restrict__ Rw
 
 hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, const uint64_t *r_count,
                        const uint64_t *s_start, const uint64_t *s_count, uint64_t P, uint32_t hash_shift,
-                       uint32_t table_slots, uint32_t grid, uint64_t *partials, hipStream_t s) {
+                       uint32_t rcap, uint32_t grid, uint64_t *partials, hipStream_t s) {
     const uint32_t *Rw = reinterpret_cast<const uint32_t *>(R);
     const uint32_t *Sw = reinterpret_cast<const uint32_t *>(S);
-    switch (table_slots) {
+    switch (rcap) {
+        case 2048:
+            hipLaunchKernelGGL(k_join<2048>, dim3(grid), dim3(kBlock), 0, s, Rw, Sw, r_start, r_count, s_start,
+                               s_count, P, hash_shift, partials);
+            break;
         case 4096:
             hipLaunchKernelGGL(k_join<4096>, dim3(grid), dim3(kBlock), 0, s, Rw, Sw, r_start, r_count, s_start,
                                s_count, P, hash_shift, partials);
             break;
         case 8192:
             hipLaunchKernelGGL(k_join<8192>, dim3(grid), dim3(kBlock), 0, s, Rw, Sw, r_start, r_count, s_start,
-                               s_count, P, hash_shift, partials);
-            break;
-        case 16384:
-            hipLaunchKernelGGL(k_join<16384>, dim3(grid), dim3(kBlock), 0, s, Rw, Sw, r_start, r_count, s_start,
                                s_count, P, hash_shift, partials);
             break;
         default:
