@@ -12,6 +12,18 @@ constexpr int kWave = 64;  // CDNA wavefront width (never 32)
 
 // ---------------------------------------------------------------- device ---
 
+// Streaming (non-temporal) 16-B / 8-B accesses: once-touched HBM data.  On gfx950
+// the nt load path reads ~10 % faster than the default policy for a pure stream
+// (tools/bw_lab), and nt stores help the partition scatter's 128-B granules.
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld_nt(const uint4 *p) {
+    const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t *>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint64_t ld_nt(const uint64_t *p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ void st_nt(uint64_t *p, uint64_t v) { __builtin_nontemporal_store(v, p); }
+__device__ __forceinline__ void st_nt(uint32_t *p, uint32_t v) { __builtin_nontemporal_store(v, p); }
+
 __device__ __forceinline__ uint64_t lanemask_lt() {
     const uint32_t lane = __lane_id();
     return lane == 0 ? 0ull : (~0ull >> (64 - lane));

@@ -13,10 +13,9 @@ namespace rho {
 
 constexpr int kBlock = 256;   // threads per workgroup for partition/join kernels
 constexpr int kMaxF = 512;    // max fanout of one partition pass (9 radix bits)
-constexpr int kScatterThreads = 256;                  // threads per scatter workgroup
+constexpr int kScatterThreads = 512;                  // threads per scatter workgroup
 constexpr int kScatterItems = 8;                      // tuples per thread per tile
 constexpr int kTile = kScatterThreads * kScatterItems;  // tuples per scatter tile
-constexpr int kScatterSegTuples = 16;                 // write-combining granule: 16 tuples = 128 B
 
 // Which contiguous slice of the input a partition workgroup owns.  Regions are
 // the bins of the previous pass (or the whole relation); each region is cut into

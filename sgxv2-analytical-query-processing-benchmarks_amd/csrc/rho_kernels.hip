@@ -63,16 +63,33 @@ __global__ __launch_bounds__(kBlock) void k_hist(const uint32_t *__restrict__ in
     const uint32_t F = 1u << bits, mask = F - 1;
     for (uint32_t d = threadIdx.x; d < F; d += kBlock) h[d] = 0;
     __syncthreads();
-    constexpr int U = 8;
-    uint64_t i = b + threadIdx.x;
-    for (; i + (U - 1) * kBlock < e; i += U * kBlock) {
-        uint32_t k[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) k[u] = in_words[2 * (i + u * kBlock)];
-#pragma unroll
-        for (int u = 0; u < U; ++u) atomicAdd(&h[(k[u] >> shift) & mask], 1u);
+    // 16-B non-temporal loads (two tuples per lane); an odd leading tuple first
+    const uint64_t *in64 = reinterpret_cast<const uint64_t *>(in_words);
+    uint64_t b2 = b;
+    if ((b & 1) && b < e) {
+        if (threadIdx.x == 0) atomicAdd(&h[(in_words[2 * b] >> shift) & mask], 1u);
+        b2 = b + 1;
     }
-    for (; i < e; i += kBlock) atomicAdd(&h[(in_words[2 * i] >> shift) & mask], 1u);
+    const uint4 *pairs = reinterpret_cast<const uint4 *>(in64 + b2);
+    const uint64_t np = (e - b2) / 2;
+    constexpr int U = 8;
+    uint64_t i = threadIdx.x;
+    for (; i + (U - 1) * kBlock < np; i += U * kBlock) {
+        uint4 q[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) q[u] = ld_nt(pairs + i + u * kBlock);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            atomicAdd(&h[(q[u].x >> shift) & mask], 1u);
+            atomicAdd(&h[(q[u].z >> shift) & mask], 1u);
+        }
+    }
+    for (; i < np; i += kBlock) {
+        const uint4 q = ld_nt(pairs + i);
+        atomicAdd(&h[(q.x >> shift) & mask], 1u);
+        atomicAdd(&h[(q.z >> shift) & mask], 1u);
+    }
+    if (((e - b2) & 1) && threadIdx.x == 0) atomicAdd(&h[(in_words[2 * (e - 1)] >> shift) & mask], 1u);
     __syncthreads();
     for (uint32_t d = threadIdx.x; d < F; d += kBlock) hist[hist_index(layout, g, d, F, nseg_stride)] = h[d];
 }
@@ -180,34 +197,52 @@ hipError_t launch_scan_regions(uint64_t *hist, const uint32_t *seg_base, const u
 // Partition copy of one segment per workgroup (partition_copy, radix_join.cpp:659-697),
 // organised like the reference's software write-combining variant
 // parallel_radix_partition_optimized (:961-1056): every digit keeps its unfinished
-// output segment (SEGT tuples, 128 B) and only whole, aligned segments go to HBM.
-// Thread d owns digit d: its pending carry (< SEGT tuples) and its write cursor
-// live in that thread's registers, not in LDS.  Per tile of NT * ITEMS tuples:
-//   1. each tuple takes a slot of its digit with one LDS atomic (tile histogram and
+// 128-B output granule (kGran tuples) in LDS and only whole, aligned granules go to
+// HBM, so no HBM line is written twice.  Per tile of NT * ITEMS tuples:
+//   A. every tuple takes a slot of its digit with one LDS atomic (tile histogram and
 //      in-tile rank at once; order inside a digit is arrival order, the join count
 //      does not depend on it);
-//   2. per digit: pending = carried tuples + this tile's tuples; the prefix that ends
-//      on a segment boundary is written, the rest (< SEGT tuples) is carried on;
-//   3. tuples are placed in LDS as [all written tuples, digit-major | new carries]
-//      and the written block goes out with consecutive lanes on consecutive addresses.
+//   B. owner thread d: pending = carried + tile tuples of d; the prefix that ends on a
+//      granule boundary is written now (w), the rest (r < kGran) is carried.  One
+//      block scan gives the digit-sorted tile offsets and the granule descriptors;
+//   C. the tile is placed digit-sorted in LDS (one LDS read of tbase[d] per tuple);
+//   D. 16-lane groups write whole granules: carried tuples first, then the tile's;
+//   E. 16-lane groups move each digit's new carries (< kGran) into its carry slots.
+// The ablation measurements behind this layout (LDS-bound, not HBM-bound, with the
+// carries in registers and four random metadata reads per tuple) are in DESIGN.md.
 // The next tile's tuples are already loading while a tile is processed (two
 // register sets).  The last carries of the segment are flushed at the end.
-template <int BITS, int ITEMS, int NT, int SEGT>
+constexpr uint32_t kGran = 16;  // tuples per output granule = one 128-B line
+
+template <int BITS, int ITEMS, int NT>
 struct ScatterLds {
     static constexpr uint32_t F = 1u << BITS;
     static constexpr uint32_t TILE = NT * ITEMS;
     static constexpr uint32_t NW = NT / kWave;
-    uint32_t cnt[F];     // tile count -> sequence position of the tile's first tuple of d
-    uint32_t cbase[F];   // stage index of sequence position 0 of d in the carry block (minus wcount)
-    uint32_t wbase[F];   // stage index of sequence position 0 of d in the write block
-    uint32_t wcount[F];  // tuples of d written this tile
-    uint64_t ob[F];      // output base of d: global position = ob[d] + stage index
-    uint32_t wtot[NW][2];
+    static constexpr uint32_t MAXDESC = (TILE + (kGran - 1) * F) / kGran + F;
     union {
         uint32_t sbase[kMaxF + 1];  // segment table (only before the first tile)
-        uint64_t stage[TILE + (SEGT - 1) * F];
+        uint64_t tile[TILE];        // this tile's tuples, digit-sorted
     };
+    uint64_t carry[F * (kGran - 1)];  // digit d: slots [d*(kGran-1), (d+1)*(kGran-1))
+    uint64_t pend[F];                 // global position of d's first pending (carried) tuple
+    uint2 meta[F];                    // {tbase, c | r << 8 | w << 16} of the current tile
+    uint32_t cnt[F];                  // tile histogram (phase A), zero between tiles
+    uint32_t tbase[F];                // digit-sorted tile offset of d
+    uint32_t gbase[F];                // first granule descriptor of d
+    uint16_t desc[MAXDESC];           // granule j belongs to digit desc[j]
+    uint32_t wt[NW][2];
 };
+
+// Waves per SIMD that the LDS footprint allows (__launch_bounds__ second argument:
+// k workgroups per CU of NT threads <=> k * NT / 256 waves per SIMD), so the
+// register allocation never becomes the tighter occupancy limit.
+template <int BITS, int ITEMS, int NT>
+constexpr int scatter_waves_per_simd() {
+    constexpr int k = (160 * 1024) / (int)sizeof(ScatterLds<BITS, ITEMS, NT>);
+    constexpr int w = (k < 1 ? 1 : k) * NT / 256;
+    return w < 1 ? 1 : (w > 8 ? 8 : w);
+}
 
 template <int ITEMS, int NT>
 __device__ __forceinline__ void load_tile(const uint64_t *__restrict__ in, uint64_t tb, uint64_t e,
@@ -215,7 +250,7 @@ __device__ __forceinline__ void load_tile(const uint64_t *__restrict__ in, uint6
     constexpr uint32_t TILE = NT * ITEMS;
     if (tb + TILE <= e) {
 #pragma unroll
-        for (int k = 0; k < ITEMS; ++k) dst[k] = __builtin_nontemporal_load(in + tb + threadIdx.x + k * NT);
+        for (int k = 0; k < ITEMS; ++k) dst[k] = ld_nt(in + tb + threadIdx.x + k * NT);
     } else {
         const uint32_t tn = (uint32_t)(e - tb);
 #pragma unroll
@@ -254,131 +289,152 @@ __device__ __forceinline__ void block_scan2(uint32_t a, uint32_t b, uint32_t (&w
     eb = pb + ib - b;
 }
 
-// Per-digit state held in the registers of the digit's owner thread.
-template <int SEGT>
-struct DigitState {
-    uint64_t pend;           // global position of the first pending tuple
-    uint32_t c;              // carried tuples
-    uint64_t carry[SEGT - 1];
-};
-
-template <int BITS, int ITEMS, int NT, int SEGT>
-__device__ __forceinline__ void scatter_tile(ScatterLds<BITS, ITEMS, NT, SEGT> &L, DigitState<SEGT> &ds,
+template <int BITS, int ITEMS, int NT>
+__device__ __forceinline__ void scatter_tile(ScatterLds<BITS, ITEMS, NT> &L, uint64_t &pend, uint32_t &carried,
                                              const uint64_t (&v)[ITEMS], uint64_t *__restrict__ out, uint32_t tn,
-                                             uint32_t shift) {
-    constexpr uint32_t F = 1u << BITS, mask = F - 1;
+                                             uint32_t shift, uint64_t tbase_global) {
+    constexpr uint32_t F = 1u << BITS, mask = F - 1, NG = NT / kGran, NW = NT / kWave;
+    constexpr uint32_t CS = kGran - 1;
     const uint32_t tid = threadIdx.x;
-    const bool owner = tid < F;  // thread tid owns digit tid
-    // 1. slot of every tuple inside its digit
+#ifdef SGXAMD_ABLATE_NOSORT  // development ablation (tools/part_bench): the memory pipeline alone
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k)
+        if (tid + k * NT < tn) st_nt(out + tbase_global + tid + k * NT, v[k]);
+    return;
+#endif
+    (void)tbase_global;
+    // A. slot of every tuple inside its digit
     uint32_t slot[ITEMS];
 #pragma unroll
-    for (int k = 0; k < ITEMS; ++k) {
+    for (int k = 0; k < ITEMS; ++k)
         if (tid + k * NT < tn) slot[k] = atomicAdd(&L.cnt[((uint32_t)v[k] >> shift) & mask], 1u);
-    }
     __syncthreads();
-    // 2. per digit: what is written now, what is carried on
-    uint32_t w = 0, r = 0, c = 0;
-    if (owner) {
-        const uint32_t t = L.cnt[tid];
-        c = ds.c;
-        const uint64_t end = ds.pend + c + t;
-        const uint64_t aligned = end & ~uint64_t(SEGT - 1);
-        w = aligned > ds.pend ? (uint32_t)(aligned - ds.pend) : 0u;
+    // B. per digit: what is written now (w), what is carried on (r), granules touched (g)
+    uint32_t t = 0, g = 0, w = 0, r = 0, c = 0;
+    uint64_t p0 = 0;
+    if (tid < F) {
+        t = L.cnt[tid];
+        L.cnt[tid] = 0;
+        c = carried;
+        p0 = pend;
+        const uint64_t aligned = (p0 + c + t) & ~uint64_t(kGran - 1);
+        if (aligned > p0) {
+            w = (uint32_t)(aligned - p0);
+            g = (uint32_t)(aligned / kGran - p0 / kGran);
+        }
         r = c + t - w;
     }
-    uint32_t we, re, W, R;
-    block_scan2(w, r, L.wtot, we, re, W, R);
-    if (owner) {
-        L.wbase[tid] = we;
-        L.cbase[tid] = W + re - w;
-        L.wcount[tid] = w;
-        L.ob[tid] = ds.pend - we;
-        L.cnt[tid] = c;  // sequence position of the tile's first tuple
-        // old carries open the digit's sequence
-#pragma unroll
-        for (int s = 0; s < SEGT - 1; ++s)
-            if ((uint32_t)s < c) L.stage[(uint32_t)s < w ? we + s : W + re - w + s] = ds.carry[s];
-        ds.pend += w;
-        ds.c = r;
+    uint32_t tb, gb, ttot, gtot;
+    block_scan2<NW>(t, g, L.wt, tb, gb, ttot, gtot);
+    (void)ttot;
+    if (tid < F) {
+        L.tbase[tid] = tb;
+        L.gbase[tid] = gb;
+        L.meta[tid] = make_uint2(tb, c | (r << 8) | (w << 16));
+        L.pend[tid] = p0;
+        for (uint32_t j = 0; j < g; ++j) L.desc[gb + j] = (uint16_t)tid;
+        pend = p0 + w;
+        carried = r;
     }
     __syncthreads();
-    // 3. place the tile's tuples behind the carries
+    // C. the tile, digit-sorted
 #pragma unroll
     for (int k = 0; k < ITEMS; ++k) {
         if (tid + k * NT < tn) {
             const uint32_t d = ((uint32_t)v[k] >> shift) & mask;
-            const uint32_t s = L.cnt[d] + slot[k];
-            L.stage[s < L.wcount[d] ? L.wbase[d] + s : L.cbase[d] + s] = v[k];
+            L.tile[L.tbase[d] + slot[k]] = v[k];
         }
     }
     __syncthreads();
-    // 4. write whole segments; collect the new carries; reset the counters
-    for (uint32_t i = tid; i < W; i += NT) {
-        const uint64_t x = L.stage[i];
-        out[L.ob[((uint32_t)x >> shift) & mask] + i] = x;
-    }
-    if (owner) {
-#pragma unroll
-        for (int s = 0; s < SEGT - 1; ++s)
-            if ((uint32_t)s < r) ds.carry[s] = L.stage[W + re + s];
-        L.cnt[tid] = 0;
+    // D. whole granules, 16 lanes (one 128-B line) per granule
+    const uint32_t lane = tid & (kGran - 1), grp = tid / kGran;
+    for (uint32_t j = grp; j < gtot; j += NG) {
+        const uint32_t d = L.desc[j];
+        const uint2 m = L.meta[d];
+        const uint64_t pd = L.pend[d];
+        const uint32_t cd = m.y & 0xFFu, wd = m.y >> 16;
+        const uint64_t a = (pd / kGran + (j - L.gbase[d])) * kGran + lane;
+        const uint64_t q = a - pd;  // sequence position inside d (wraps when a < pd)
+        if (a >= pd && q < wd) {
+            const uint64_t x = q < cd ? L.carry[d * CS + q] : L.tile[m.x + q - cd];
+#ifdef SGXAMD_ABLATE_NOSTORE  // development ablation: everything but the global stores
+            if (x == ~0ull) out[0] = x;
+#elif defined(SGXAMD_PLAIN_STORE)
+            out[a] = x;
+#else
+            st_nt(out + a, x);
+#endif
+        }
     }
     __syncthreads();
+    // E. new carries (the next tile's phase A touches only cnt; C/D come after barriers)
+    for (uint32_t d = grp; d < F; d += NG) {
+        const uint2 m = L.meta[d];
+        const uint32_t cd = m.y & 0xFFu, rd = (m.y >> 8) & 0xFFu, wd = m.y >> 16;
+        if (wd > 0) {
+            if (lane < rd) L.carry[d * CS + lane] = L.tile[m.x + wd - cd + lane];
+        } else if (lane < rd - cd) {
+            L.carry[d * CS + cd + lane] = L.tile[m.x + lane];
+        }
+    }
 }
 
-template <int BITS, int ITEMS, int NT, int SEGT>
-__global__ __launch_bounds__(NT) void k_scatter(const uint64_t *__restrict__ in, uint64_t *__restrict__ out,
+template <int BITS, int ITEMS, int NT>
+__global__ __launch_bounds__(NT, (scatter_waves_per_simd<BITS, ITEMS, NT>())) void k_scatter(const uint64_t *__restrict__ in, uint64_t *__restrict__ out,
                                                 SegMap m, uint32_t shift, const uint64_t *__restrict__ cur_init,
                                                 HistLayout layout, uint32_t nseg_stride,
                                                 const uint64_t *__restrict__ digit_base) {
     constexpr uint32_t TILE = NT * ITEMS;
-    constexpr uint32_t F = 1u << BITS;
+    constexpr uint32_t F = 1u << BITS, NG = NT / kGran, CS = kGran - 1;
     static_assert(F <= NT, "one owner thread per digit");
-    __shared__ ScatterLds<BITS, ITEMS, NT, SEGT> L;
+    __shared__ ScatterLds<BITS, ITEMS, NT> L;
     const uint32_t g = blockIdx.x;
     uint32_t r;
     uint64_t b, e;
     if (!seg_lookup(m, g, L.sbase, r, b, e)) return;
-    DigitState<SEGT> ds;
-    ds.c = 0;
-    ds.pend = 0;
+    uint64_t pend = 0;
+    uint32_t carried = 0;
     const uint32_t tid = threadIdx.x;
     if (tid < F) {
-        ds.pend = cur_init[hist_index(layout, g, tid, F, nseg_stride)] +
-                  (digit_base ? digit_base[(uint64_t)r * F + tid] : 0);
+        pend = cur_init[hist_index(layout, g, tid, F, nseg_stride)] +
+               (digit_base ? digit_base[(uint64_t)r * F + tid] : 0);
         L.cnt[tid] = 0;
     }
-    __syncthreads();  // sbase (aliased with stage) is dead from here on
+    __syncthreads();  // sbase (aliased with tile) is dead from here on
     uint64_t va[ITEMS], vb[ITEMS];
     load_tile<ITEMS, NT>(in, b, e, va);
     for (uint64_t tb = b; tb < e; tb += 2 * TILE) {
         if (tb + TILE < e) load_tile<ITEMS, NT>(in, tb + TILE, e, vb);
-        scatter_tile<BITS, ITEMS, NT, SEGT>(L, ds, va, out, (uint32_t)min<uint64_t>(TILE, e - tb), shift);
+        scatter_tile<BITS, ITEMS, NT>(L, pend, carried, va, out, (uint32_t)min<uint64_t>(TILE, e - tb), shift, tb);
         if (tb + TILE >= e) break;
         const uint64_t t2 = tb + TILE;
         if (t2 + TILE < e) load_tile<ITEMS, NT>(in, t2 + TILE, e, va);
-        scatter_tile<BITS, ITEMS, NT, SEGT>(L, ds, vb, out, (uint32_t)min<uint64_t>(TILE, e - t2), shift);
+        scatter_tile<BITS, ITEMS, NT>(L, pend, carried, vb, out, (uint32_t)min<uint64_t>(TILE, e - t2), shift, t2);
     }
-    // flush the carried (partial) segments
+    // flush the carried (partial) granules
+    __syncthreads();
     if (tid < F) {
-#pragma unroll
-        for (int s = 0; s < SEGT - 1; ++s)
-            if ((uint32_t)s < ds.c) out[ds.pend + s] = ds.carry[s];
+        L.pend[tid] = pend;
+        L.cnt[tid] = carried;
     }
+    __syncthreads();
+    const uint32_t lane = tid & (kGran - 1);
+    for (uint32_t d = tid / kGran; d < F; d += NG)
+        if (lane < L.cnt[d]) out[L.pend[d] + lane] = L.carry[d * CS + lane];
 }
 
-template <int ITEMS, int NT, int SEGT>
+template <int ITEMS, int NT>
 hipError_t launch_scatter_items(const uint64_t *in, uint64_t *out, const SegMap &m, uint32_t grid, uint32_t shift,
                                 uint32_t bits, const uint64_t *cursors, HistLayout layout, uint32_t nseg_stride,
                                 const uint64_t *digit_base, hipStream_t s) {
-#define SCATTER_CASE(B)                                                                                    \
-    case B:                                                                                                \
-        if constexpr (sizeof(ScatterLds<B, ITEMS, NT, SEGT>) <= 160 * 1024 && (1 << B) <= NT) {             \
-            hipLaunchKernelGGL((k_scatter<B, ITEMS, NT, SEGT>), dim3(grid), dim3(NT), 0, s, in, out, m, shift, \
-                               cursors, layout, nseg_stride, digit_base);                                  \
-            break;                                                                                         \
-        } else {                                                                                           \
-            return hipErrorInvalidValue;                                                                   \
+#define SCATTER_CASE(B)                                                                                  \
+    case B:                                                                                              \
+        if constexpr (sizeof(ScatterLds<B, ITEMS, NT>) <= 160 * 1024 && (1 << B) <= NT) {                  \
+            hipLaunchKernelGGL((k_scatter<B, ITEMS, NT>), dim3(grid), dim3(NT), 0, s, in, out, m, shift,   \
+                               cursors, layout, nseg_stride, digit_base);                                \
+            break;                                                                                       \
+        } else {                                                                                         \
+            return hipErrorInvalidValue;                                                                 \
         }
     switch (bits) {
         SCATTER_CASE(0)
@@ -404,11 +460,8 @@ hipError_t launch_scatter(const row_t *in, row_t *out, const SegMap &m, uint32_t
     if (grid == 0) return hipSuccess;
     const uint64_t *i64 = reinterpret_cast<const uint64_t *>(in);
     uint64_t *o64 = reinterpret_cast<uint64_t *>(out);
-    if (bits > 8)  // 512 digit owners: 512-thread workgroups with the same tile size, 64-B granules (LDS)
-        return launch_scatter_items<kTile / 512, 512, 8>(i64, o64, m, grid, shift, bits, cursors, layout,
-                                                         nseg_stride, digit_base, s);
-    return launch_scatter_items<kScatterItems, kScatterThreads, kScatterSegTuples>(
-        i64, o64, m, grid, shift, bits, cursors, layout, nseg_stride, digit_base, s);
+    return launch_scatter_items<kScatterItems, kScatterThreads>(i64, o64, m, grid, shift, bits, cursors, layout,
+                                                                nseg_stride, digit_base, s);
 }
 
 // ------------------------------------------------------------ build+probe ---
@@ -451,7 +504,7 @@ __global__ __launch_bounds__(kBlock) void k_join(const uint32_t *__restrict__ Rw
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const uint32_t i = tid + u * kBlock;
-                kr[u] = i < nrc ? rk[2 * i] : 0u;
+                kr[u] = i < nrc ? (uint32_t)ld_nt(reinterpret_cast<const uint64_t *>(rk) + i) : 0u;
             }
             for (uint32_t i = tid; i < (N + 3) / 4; i += kBlock)
                 reinterpret_cast<uint4 *>(head)[i] = make_uint4(0, 0, 0, 0);
@@ -472,7 +525,7 @@ __global__ __launch_bounds__(kBlock) void k_join(const uint32_t *__restrict__ Rw
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     const uint64_t i = s0 + tid + u * kBlock;
-                    ks[u] = i < nS ? sk[2 * i] : 0u;
+                    ks[u] = i < nS ? (uint32_t)ld_nt(reinterpret_cast<const uint64_t *>(sk) + i) : 0u;
                 }
 #pragma unroll
                 for (int u = 0; u < U; ++u) {

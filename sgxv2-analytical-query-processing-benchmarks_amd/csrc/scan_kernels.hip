@@ -71,7 +71,7 @@ __global__ __launch_bounds__(kBlock) void k_predicate(const T *__restrict__ in, 
         for (int u = 0; u < kUnroll; ++u) {
             const uint64_t row = base + u * STEP + (uint64_t)lane * V;
             if (row + V <= r1) {
-                q[u] = *reinterpret_cast<const uint4 *>(in + row);
+                q[u] = ld_nt(reinterpret_cast<const uint4 *>(in + row));
                 valid[u] = FULL;
             } else if (row < r1) {  // ragged tail: element loads packed like a uint4
                 uint32_t w[4] = {0, 0, 0, 0};
@@ -194,7 +194,7 @@ __global__ __launch_bounds__(kBlock) void k_expand(const uint64_t *__restrict__ 
     uint64_t base = chunk_off[blockIdx.x];
     for (uint64_t wb = w0; wb < w1; wb += kWaves * 64) {
         const uint64_t wi = wb + (uint64_t)wave * 64 + lane;
-        const uint64_t x = wi < w1 ? bv[wi] : 0ull;
+        const uint64_t x = wi < w1 ? ld_nt(bv + wi) : 0ull;
         const uint32_t c = __popcll(x);
         const uint32_t incl = wave_incl_scan_u32(c);
         incl_s[wave][lane] = incl;
