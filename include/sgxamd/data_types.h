@@ -46,6 +46,21 @@ struct output_triple_t {
     type_value Spayload;
 };
 
+/* data-types.h:78-92: the reference's CHUNKED_TABLE result (CSKB = 16). */
+#define SGXAMD_CHUNK_SIZE (1024 * 16)
+#define SGXAMD_TUPLES_PER_CHUNK ((SGXAMD_CHUNK_SIZE - 8) / sizeof(struct output_triple_t))
+struct table_chunk_t {
+    uint64_t num_tuples;
+    struct output_triple_t tuples[SGXAMD_TUPLES_PER_CHUNK];
+};
+struct chunked_table_t {
+    struct table_chunk_t **chunks; /* pointers to the chunks */
+    uint64_t current_chunk;        /* the chunk that is currently being filled */
+    uint64_t num_chunks;           /* allocated chunks (non-null pointers in chunks) */
+    uint64_t chunk_capacity;       /* pointers that fit into chunks */
+    uint64_t num_tuples;           /* total tuples over all chunks */
+};
+
 /* data-types.h:107-114: join result (48 bytes with padding). */
 struct result_t {
     int64_t totalresults;
@@ -94,6 +109,8 @@ SGXAMD_STATIC_ASSERT(offsetof(struct row_t, payload) == 4, "row_t.payload at 4")
 SGXAMD_STATIC_ASSERT(sizeof(struct table_t) == 24, "table_t must be 24 bytes");
 SGXAMD_STATIC_ASSERT(offsetof(struct table_t, num_tuples) == 8, "table_t.num_tuples at 8");
 SGXAMD_STATIC_ASSERT(sizeof(struct output_triple_t) == 12, "output_triple_t must be 12 bytes");
+SGXAMD_STATIC_ASSERT(sizeof(struct table_chunk_t) == 16376, "table_chunk_t: 8 + 1364 * 12 bytes");
+SGXAMD_STATIC_ASSERT(sizeof(struct chunked_table_t) == 40, "chunked_table_t must be 40 bytes");
 SGXAMD_STATIC_ASSERT(sizeof(struct result_t) == 48, "result_t must be 48 bytes");
 SGXAMD_STATIC_ASSERT(offsetof(struct result_t, throughput) == 16, "result_t.throughput at 16");
 SGXAMD_STATIC_ASSERT(offsetof(struct result_t, result) == 32, "result_t.result at 32");

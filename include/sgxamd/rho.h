@@ -38,10 +38,14 @@ typedef struct mi355_rho_opts {
     int radix_bits;      /* total radix bits; 0 = GPU policy (DESIGN.md "partitioning policy") */
     int passes;          /* 1 or 2; 0 = policy */
     uint32_t key_shift;  /* low key bits already fixed by a shard exchange (multi-GPU); 0 otherwise */
-    int materialize;     /* reserved (count-only in this round); must be 0 */
+    int materialize;     /* 1 = write every match to out (radix_join.cpp:437-446, MATERIALIZE) */
     int timing;          /* 1 = record per-kernel HIP events (mi355_timing_* below) */
     int reserved;
     void *stream;        /* hipStream_t to launch on; NULL = the library's stream */
+    struct output_triple_t *out; /* materialize: {key, R payload, S payload} per match, host or
+                                    device memory; order unspecified (the reference's is per thread) */
+    uint64_t out_capacity;       /* triples that fit in out; if fewer than the matches, the call
+                                    returns MI355_ERR_CAPACITY with stats->matches = required */
 } mi355_rho_opts;
 
 /* What one join call did. */
@@ -73,13 +77,21 @@ const char *mi355_last_error(void);
 const char *mi355_version(void);
 
 /*
- * RHO join with the reference's semantics (count-only, MATERIALIZE must be 0).
- * Replaces RHO() at radix_join.cpp:1640 / radix_join.h:29.  Fills out->totalresults,
- * nthreads (= config->NTHREADS), materialized, result (NULL), result_type (0) and
- * throughput (M rec/s = (|R|+|S|) / join time, which the reference leaves unset).
+ * RHO join with the reference's semantics.  Replaces RHO() at radix_join.cpp:1640 /
+ * radix_join.h:29.  Fills out->totalresults, nthreads (= config->NTHREADS),
+ * materialized, result, result_type and throughput (M rec/s = (|R|+|S|) / join
+ * time, which the reference leaves unset).  With config->MATERIALIZE = 1 the
+ * matches come back as a host chunked_table_t (result_type 1, as the reference's
+ * CHUNKED_TABLE build, radix_join.cpp:1554-1557); free it with
+ * mi355_free_chunked_table.  Otherwise result = NULL, result_type = 0.
  */
 int mi355_rho_join(const struct table_t *relR, const struct table_t *relS,
                    const struct joinconfig_t *config, struct result_t *out);
+
+/* Frees the chunked_table_t that mi355_rho_join / RHO() return in result->result
+ * when config->MATERIALIZE = 1 (result_type 1, the reference's CHUNKED_TABLE form,
+ * ChunkedTable.cpp:21-171).  NULL is ignored. */
+void mi355_free_chunked_table(struct chunked_table_t *table);
 
 /* Same join on raw tuple arrays with explicit options and per-phase statistics. */
 int mi355_rho_join_ex(const struct row_t *R, uint64_t nR, const struct row_t *S, uint64_t nS,

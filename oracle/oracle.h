@@ -52,6 +52,12 @@ int64_t oracle_rho_join(const struct row_t *R, uint64_t nR, const struct row_t *
                         int nthreads, int force_two_passes, oracle_rho_timing *timing);
 
 /* Independent check: sum_k cnt_R(k) * cnt_S(k) by sorting the keys. */
+/* The same join with MATERIALIZE = 1 (radix_join.cpp:437-446): every match as
+ * {S key, R payload, S payload}, per-thread outputs concatenated in thread order
+ * into out (at most cap triples written).  Returns the match count. */
+int64_t oracle_rho_join_mat(const struct row_t *R, uint64_t nR, const struct row_t *S, uint64_t nS, int nthreads,
+                            int force_two_passes, struct output_triple_t *out, uint64_t cap);
+
 int64_t oracle_count_join_sort(const struct row_t *R, uint64_t nR, const struct row_t *S, uint64_t nS);
 
 /* Stable single-pass radix partition of `in` by bin = (key >> shift) & (2^bits-1)

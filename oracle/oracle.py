@@ -12,6 +12,8 @@ import ctypes as C
 import os
 import subprocess
 
+import numpy as np
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "liboracle.so")
 
@@ -37,6 +39,7 @@ def _load() -> C.CDLL:
         "oracle_calc_num_radix_bits": (C.c_uint32, [C.c_uint64, C.c_uint64]),
         "oracle_calc_num_passes": (C.c_uint32, [C.c_uint32]),
         "oracle_rho_join": (C.c_int64, [P, C.c_uint64, P, C.c_uint64, C.c_int, C.c_int, C.POINTER(Timing)]),
+        "oracle_rho_join_mat": (C.c_int64, [P, C.c_uint64, P, C.c_uint64, C.c_int, C.c_int, P, C.c_uint64]),
         "oracle_count_join_sort": (C.c_int64, [P, C.c_uint64, P, C.c_uint64]),
         "oracle_radix_partition": (None, [P, C.c_uint64, C.c_int, C.c_uint32, C.c_uint32, P, U64P]),
         "oracle_scan_count_u8": (C.c_uint64, [C.c_uint8, C.c_uint8, P, C.c_size_t]),
@@ -70,6 +73,16 @@ def rho_join(R, S, nthreads: int = 1, force_two_passes: bool = False) -> tuple[i
     t = lib.Timing()
     m = lib.oracle_rho_join(_p(R), len(R), _p(S), len(S), nthreads, 1 if force_two_passes else 0, C.byref(t))
     return int(m), {f: getattr(t, f) for f, _ in t._fields_}
+
+
+def rho_join_triples(R, S, nthreads: int = 1, force_two_passes: bool = False):
+    """Materialising RHO (radix_join.cpp:437-446): (n, 3) uint32 {key, R payload,
+    S payload} in the restatement's per-thread order."""
+    m = lib.oracle_rho_join(_p(R), len(R), _p(S), len(S), nthreads, 1 if force_two_passes else 0, None)
+    out = np.zeros((max(m, 1), 3), dtype=np.uint32)
+    got = lib.oracle_rho_join_mat(_p(R), len(R), _p(S), len(S), nthreads, 1 if force_two_passes else 0, _p(out), m)
+    assert got == m
+    return out[:m]
 
 
 def count_join_sort(R, S) -> int:

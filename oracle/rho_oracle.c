@@ -55,9 +55,28 @@ static inline uint32_t padding_tuples(uint32_t bits, uint32_t passes) {
     return (uint32_t)SMALL_PADDING_TUPLES * (fanout_pass_2(bits, passes) + 1);
 }
 
-/* bucket_chaining_join (:359-458), count-only branch (:428-436). */
+/* Per-thread materialisation output: the reference's insert_output into a
+ * chunked table (ChunkedTable.cpp:21-171); here one growable array per thread. */
+typedef struct out_buf {
+    struct output_triple_t *t;
+    uint64_t n, cap;
+} out_buf;
+
+static void out_push(out_buf *o, uint32_t key, uint32_t rpay, uint32_t spay) {
+    if (o->n == o->cap) {
+        o->cap = o->cap ? 2 * o->cap : 1024;
+        o->t = (struct output_triple_t *)realloc(o->t, o->cap * sizeof(struct output_triple_t));
+    }
+    o->t[o->n].key = key;
+    o->t[o->n].Rpayload = rpay;
+    o->t[o->n].Spayload = spay;
+    o->n++;
+}
+
+/* bucket_chaining_join (:359-458): count-only branch (:428-436) and, with an
+ * output buffer, the materialising branch (:437-446). */
 static int64_t bucket_chaining_join(const struct row_t *R, uint64_t numR, const struct row_t *S,
-                                    uint64_t numS, uint32_t num_radix_bits) {
+                                    uint64_t numS, uint32_t num_radix_bits, out_buf *out) {
     uint32_t N = (uint32_t)numR;
     /* NEXT_POW_2 (:55-64) */
     N--; N |= N >> 1; N |= N >> 2; N |= N >> 4; N |= N >> 8; N |= N >> 16; N++;
@@ -70,10 +89,22 @@ static int64_t bucket_chaining_join(const struct row_t *R, uint64_t numR, const 
         bucket[idx] = ++i; /* positions start at 1 */
     }
     int64_t matches = 0;
-    for (uint32_t i = 0; i < numS; i++) {
-        uint32_t idx = HASH_BIT_MODULO(S[i].key, MASK, num_radix_bits);
-        for (uint32_t hit = bucket[idx]; hit > 0; hit = next[hit - 1]) {
-            if (S[i].key == R[hit - 1].key) matches++;
+    if (!out) {
+        for (uint32_t i = 0; i < numS; i++) {
+            uint32_t idx = HASH_BIT_MODULO(S[i].key, MASK, num_radix_bits);
+            for (uint32_t hit = bucket[idx]; hit > 0; hit = next[hit - 1]) {
+                if (S[i].key == R[hit - 1].key) matches++;
+            }
+        }
+    } else {
+        for (uint32_t i = 0; i < numS; i++) {
+            uint32_t idx = HASH_BIT_MODULO(S[i].key, MASK, num_radix_bits);
+            for (uint32_t hit = bucket[idx]; hit > 0; hit = next[hit - 1]) {
+                if (S[i].key == R[hit - 1].key) {
+                    matches++;
+                    out_push(out, S[i].key, R[hit - 1].payload, S[i].payload);
+                }
+            }
         }
     }
     free(bucket);
@@ -168,6 +199,7 @@ typedef struct shared_t {
     struct row_t *tmpR, *tmpS, *tmpR2, *tmpS2;
     uint64_t totalR, totalS;
     uint32_t bits, passes;
+    int materialize;
     task_array part_queue, join_queue;
 } shared_t;
 
@@ -177,6 +209,7 @@ typedef struct arg_t {
     const struct row_t *relR, *relS;
     uint64_t numR, numS;
     int64_t result;
+    out_buf out;
     double t_total, t_part, t_pass1, t_pass2, t_join;
 } arg_t;
 
@@ -256,7 +289,8 @@ static void *prj_thread(void *param) {
     int64_t results = 0;
     task_t task;
     while (ta_pop(join_queue, &task))
-        results += bucket_chaining_join(task.relR, task.nR, task.relS, task.nS, bits);
+        results += bucket_chaining_join(task.relR, task.nR, task.relS, task.nS, bits,
+                                        sh->materialize ? &a->out : NULL);
     double t3 = now_s();
     a->result = results;
     a->t_total = t3 - t0;
@@ -267,9 +301,26 @@ static void *prj_thread(void *param) {
     return NULL;
 }
 
-/* join_init_run (:1369-1638) with jf = bucket_chaining_join, i.e. RHO (:1640-1643). */
+/* join_init_run (:1369-1638) with jf = bucket_chaining_join, i.e. RHO (:1640-1643).
+ * With out != NULL the join materialises (config->MATERIALIZE): the per-thread
+ * triples are concatenated in thread order into out (up to cap of them). */
+static int64_t rho_join_impl(const struct row_t *R, uint64_t nR, const struct row_t *S, uint64_t nS, int nthreads,
+                             int force_two_passes, oracle_rho_timing *timing, struct output_triple_t *out,
+                             uint64_t cap, int materialize);
+
 int64_t oracle_rho_join(const struct row_t *R, uint64_t nR, const struct row_t *S, uint64_t nS, int nthreads,
                         int force_two_passes, oracle_rho_timing *timing) {
+    return rho_join_impl(R, nR, S, nS, nthreads, force_two_passes, timing, NULL, 0, 0);
+}
+
+int64_t oracle_rho_join_mat(const struct row_t *R, uint64_t nR, const struct row_t *S, uint64_t nS, int nthreads,
+                            int force_two_passes, struct output_triple_t *out, uint64_t cap) {
+    return rho_join_impl(R, nR, S, nS, nthreads, force_two_passes, NULL, out, cap, 1);
+}
+
+static int64_t rho_join_impl(const struct row_t *R, uint64_t nR, const struct row_t *S, uint64_t nS, int nthreads,
+                             int force_two_passes, oracle_rho_timing *timing, struct output_triple_t *out,
+                             uint64_t cap, int materialize) {
     if (nthreads < 1) nthreads = 1;
     shared_t sh;
     memset(&sh, 0, sizeof(sh));
@@ -277,6 +328,7 @@ int64_t oracle_rho_join(const struct row_t *R, uint64_t nR, const struct row_t *
     sh.passes = force_two_passes ? 2 : oracle_calc_num_passes(sh.bits);
     sh.totalR = nR;
     sh.totalS = nS;
+    sh.materialize = materialize;
     const uint64_t fan1 = fanout_pass_1(sh.bits, sh.passes);
     const uint64_t rel_padding = (uint64_t)padding_tuples(sh.bits, sh.passes) * fan1 * sizeof(struct row_t);
     const uint64_t rsz = nR * sizeof(struct row_t) + rel_padding;
@@ -332,6 +384,11 @@ int64_t oracle_rho_join(const struct row_t *R, uint64_t nR, const struct row_t *
             if (args[i].t_pass2 > timing->s_pass2) timing->s_pass2 = args[i].t_pass2;
             if (args[i].t_join > timing->s_join) timing->s_join = args[i].t_join;
         }
+    }
+    uint64_t w = 0;
+    for (int i = 0; i < nthreads; i++) { /* concatenate the threads' outputs (:1554-1557) */
+        for (uint64_t j = 0; j < args[i].out.n && w < cap; ++j) out[w++] = args[i].out.t[j];
+        free(args[i].out.t);
     }
     for (int i = 0; i < nthreads; i++) { free(sh.histR[i]); free(sh.histS[i]); }
     free(sh.histR); free(sh.histS);

@@ -8,6 +8,7 @@
 // sized for the LDS of a CU rather than for L2 (calc_num_radix_bits :295-317).
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -151,16 +152,19 @@ void plan_relation(Arena &A, RelPlan &rp, uint64_t n, const Policy &pol) {
 }  // namespace
 
 // The whole join on device-resident inputs.  Caller holds ctx->mu.
+// Materialisation (opts->materialize): a per-task count pass, an exclusive scan of
+// the task counts into output offsets, then a write pass; `out` must be device
+// memory with room for out_cap triples (MI355_ERR_CAPACITY otherwise).
 int join_device(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const row_t *dS, uint64_t nS,
-                const mi355_rho_opts *opts, mi355_rho_stats *st) {
+                const mi355_rho_opts *opts, mi355_rho_stats *st, output_triple_t *out, uint64_t out_cap) {
     const uint32_t key_shift = opts ? opts->key_shift : 0;
+    const bool materialize = opts && opts->materialize;
     const Policy pol = choose_policy(nR, opts);
     if (key_shift + pol.bits > 31) {
         set_last_error("key_shift + radix bits must stay below 32");
         return MI355_ERR_INVALID;
     }
     Timer &tm = thread_timer();
-    const bool user_timing = (opts && opts->timing) || thread_timing_enabled();
     tm.begin_call(s, true);  // phase events are always recorded (throughput in result_t)
 
     RHO_HIP(ctx->t1R.ensure(std::max<uint64_t>(nR, 1) * sizeof(row_t)));
@@ -176,7 +180,11 @@ int join_device(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const
     plan_relation(A, ps, nS, pol);
     const uint64_t P = 1ull << pol.bits;
     const uint32_t join_grid = (uint32_t)std::min<uint64_t>(P, 2048);
-    const size_t off_partials = A.reserve(sizeof(uint64_t) * join_grid);
+    const uint32_t over_cap = (uint32_t)(nS / kSChunk + 1);
+    const size_t off_over = A.reserve(sizeof(uint64_t) * over_cap);
+    const size_t off_nover = A.reserve(sizeof(uint32_t));
+    const size_t off_counts = A.reserve(sizeof(uint64_t) * (materialize ? P + over_cap : join_grid));
+    const size_t off_toff = A.reserve(sizeof(uint64_t) * (materialize ? P + over_cap : 1));
     const size_t off_result = A.reserve(sizeof(uint64_t) * 4);
     RHO_HIP(A.buf.ensure(A.used));
 
@@ -197,17 +205,45 @@ int join_device(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const
                                      key_shift, &fS, &psS, &pcS, true)))
             return rc;
     }
-    uint64_t *partials = A.at<uint64_t>(off_partials);
+    uint64_t *over = A.at<uint64_t>(off_over);
+    uint32_t *n_over = A.at<uint32_t>(off_nover);
+    uint64_t *counts = A.at<uint64_t>(off_counts);
+    uint64_t *task_off = A.at<uint64_t>(off_toff);
     uint64_t *result = A.at<uint64_t>(off_result);
-    tm.mark("join_build_probe");
-    RHO_HIP(launch_join(fR, fS, psR, pcR, psS, pcS, P, key_shift + pol.bits, pol.rcap, join_grid, partials,
-                        s));
-    tm.mark("join_reduce");
-    RHO_HIP(launch_reduce(partials, join_grid, result, s));
+    const uint32_t hash_shift = key_shift + pol.bits;
+    tm.mark("join_tasks");
+    RHO_HIP(launch_make_tasks(pcR, pcS, P, over, over_cap, n_over, s));
+    if (!materialize) {
+        tm.mark("join_build_probe");
+        RHO_HIP(launch_join(fR, fS, psR, pcR, psS, pcS, P, over, n_over, hash_shift, pol.rcap, join_grid, kJoinCount,
+                            counts, nullptr, nullptr, s));
+        tm.mark("join_reduce");
+        RHO_HIP(launch_reduce(counts, join_grid, result, s));
+    } else {
+        tm.mark("join_build_probe");
+        RHO_HIP(launch_join(fR, fS, psR, pcR, psS, pcS, P, over, n_over, hash_shift, pol.rcap, join_grid,
+                            kJoinTaskCount, counts, nullptr, nullptr, s));
+        tm.mark("join_offsets");
+        RHO_HIP(launch_excl_scan(counts, n_over, P, task_off, result, s));
+        RHO_HIP(hipMemcpyAsync(ctx->host_result, result, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+        RHO_HIP(hipStreamSynchronize(s));
+        const uint64_t total = ctx->host_result[0];
+        if (total > out_cap || (total > 0 && out == nullptr)) {
+            tm.end_call();
+            tm.collect();
+            if (st) st->matches = total;
+            set_last_error("materialisation output too small: " + std::to_string(total) + " triples needed");
+            return MI355_ERR_CAPACITY;
+        }
+        tm.mark("join_materialize");
+        RHO_HIP(launch_join(fR, fS, psR, pcR, psS, pcS, P, over, n_over, hash_shift, pol.rcap, join_grid, kJoinWrite,
+                            counts, task_off, out, s));
+    }
     tm.end_call();
     RHO_HIP(launch_max(pcR, P, result + 1, s));
     RHO_HIP(launch_max(pcS, P, result + 2, s));
     RHO_HIP(hipMemcpyAsync(ctx->host_result, result, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    RHO_HIP(hipMemcpyAsync(ctx->host_result + 3, n_over, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     RHO_HIP(hipStreamSynchronize(s));
     tm.collect();
 
@@ -218,7 +254,7 @@ int join_device(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const
         st->pass1_bits = pol.b1;
         st->pass2_bits = pol.b2;
         st->num_partitions = P;
-        st->num_tasks = P;
+        st->num_tasks = P + (uint32_t)ctx->host_result[3];
         st->max_part_r = ctx->host_result[1];
         st->max_part_s = ctx->host_result[2];
         st->ms_pass1 = tm.ms_of_prefix("R_pass1") + tm.ms_of_prefix("S_pass1");
@@ -227,7 +263,6 @@ int join_device(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const
         st->ms_join = tm.ms_of_prefix("join_");
         st->ms_total = st->ms_partition + st->ms_join;
     }
-    (void)user_timing;
     return MI355_OK;
 }
 
@@ -269,8 +304,9 @@ int mi355_rho_join_ex(const row_t *R, uint64_t nR, const row_t *S, uint64_t nS, 
         set_last_error("null relation");
         return MI355_ERR_INVALID;
     }
-    if (opts && opts->materialize) {
-        set_last_error("materialisation is not supported by this build (count-only)");
+    const bool materialize = opts && opts->materialize;
+    if (materialize && opts->out_capacity > 0 && opts->out == nullptr) {
+        set_last_error("materialize: out is NULL");
         return MI355_ERR_INVALID;
     }
     int status = MI355_OK;
@@ -302,29 +338,106 @@ int mi355_rho_join_ex(const row_t *R, uint64_t nR, const row_t *S, uint64_t nS, 
         RHO_HIP(hipStreamSynchronize(s));
         st->ms_h2d = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
-    return rho::join_device(ctx, s, dR, nR, dS, nS, opts, st);
+    if (!materialize) return rho::join_device(ctx, s, dR, nR, dS, nS, opts, st, nullptr, 0);
+    // materialise: straight into a device buffer, or through the context's buffer into host memory
+    const uint64_t cap = opts->out_capacity;
+    if (opts->out == nullptr || is_device_pointer(opts->out))
+        return rho::join_device(ctx, s, dR, nR, dS, nS, opts, st, opts->out, cap);
+    RHO_HIP(ctx->mat.ensure(std::max<uint64_t>(cap, 1) * sizeof(output_triple_t)));
+    int rc = rho::join_device(ctx, s, dR, nR, dS, nS, opts, st, ctx->mat.as<output_triple_t>(), cap);
+    if (rc) return rc;
+    RHO_HIP(hipMemcpyAsync(opts->out, ctx->mat.ptr, st->matches * sizeof(output_triple_t), hipMemcpyDeviceToHost, s));
+    RHO_HIP(hipStreamSynchronize(s));
+    return MI355_OK;
 }
 
-// Drop-in for RHO() (radix_join.cpp:1640-1643), count-only.
+// Host chunked table of n triples (ChunkedTable.cpp layout: TUPLES_PER_CHUNK per chunk).
+static chunked_table_t *make_chunked_table(const output_triple_t *src, uint64_t n) {
+    auto *t = static_cast<chunked_table_t *>(std::calloc(1, sizeof(chunked_table_t)));
+    if (!t) return nullptr;
+    const uint64_t per = SGXAMD_TUPLES_PER_CHUNK;
+    const uint64_t nchunks = std::max<uint64_t>((n + per - 1) / per, 1);
+    t->chunks = static_cast<table_chunk_t **>(std::calloc(nchunks, sizeof(table_chunk_t *)));
+    if (!t->chunks) {
+        std::free(t);
+        return nullptr;
+    }
+    t->chunk_capacity = nchunks;
+    for (uint64_t c = 0; c < nchunks; ++c) {
+        auto *ch = static_cast<table_chunk_t *>(std::malloc(sizeof(table_chunk_t)));
+        if (!ch) {
+            t->num_chunks = c;
+            mi355_free_chunked_table(t);
+            return nullptr;
+        }
+        const uint64_t k = std::min<uint64_t>(per, n - std::min<uint64_t>(n, c * per));
+        ch->num_tuples = k;
+        if (k) std::memcpy(ch->tuples, src + c * per, k * sizeof(output_triple_t));
+        t->chunks[c] = ch;
+    }
+    t->num_chunks = nchunks;
+    t->current_chunk = nchunks - 1;
+    t->num_tuples = n;
+    return t;
+}
+
+void mi355_free_chunked_table(chunked_table_t *table) {
+    if (!table) return;
+    for (uint64_t c = 0; c < table->num_chunks; ++c) std::free(table->chunks[c]);
+    std::free(table->chunks);
+    std::free(table);
+}
+
+// Drop-in for RHO() (radix_join.cpp:1640-1643).
 int mi355_rho_join(const table_t *relR, const table_t *relS, const joinconfig_t *config, result_t *out) {
     if (!relR || !relS || !out) {
         set_last_error("null argument");
         return MI355_ERR_INVALID;
     }
-    if (config && config->MATERIALIZE) {
-        set_last_error("MATERIALIZE=1 is not supported by this build (count-only)");
-        return MI355_ERR_INVALID;
-    }
+    const bool materialize = config && config->MATERIALIZE;
     mi355_rho_stats st{};
-    int rc = mi355_rho_join_ex(relR->tuples, relR->num_tuples, relS->tuples, relS->num_tuples, nullptr, &st);
-    if (rc) return rc;
+    int rc;
+    output_triple_t *host = nullptr;
+    if (!materialize) {
+        rc = mi355_rho_join_ex(relR->tuples, relR->num_tuples, relS->tuples, relS->num_tuples, nullptr, &st);
+    } else {
+        // count first (capacity 0 -> MI355_ERR_CAPACITY with the size), then materialise
+        mi355_rho_opts o{};
+        o.materialize = 1;
+        rc = mi355_rho_join_ex(relR->tuples, relR->num_tuples, relS->tuples, relS->num_tuples, &o, &st);
+        if (rc == MI355_ERR_CAPACITY || (rc == MI355_OK && st.matches > 0)) {
+            const uint64_t need = st.matches;
+            host = static_cast<output_triple_t *>(std::malloc(std::max<uint64_t>(need, 1) * sizeof(output_triple_t)));
+            if (!host) {
+                set_last_error("host allocation of the materialised result failed");
+                return MI355_ERR_OOM;
+            }
+            o.out = host;
+            o.out_capacity = need;
+            rc = mi355_rho_join_ex(relR->tuples, relR->num_tuples, relS->tuples, relS->num_tuples, &o, &st);
+        }
+    }
+    if (rc) {
+        std::free(host);
+        return rc;
+    }
     out->totalresults = (int64_t)st.matches;
     out->nthreads = config ? config->NTHREADS : 1;
     const double us = st.ms_total * 1000.0;
     out->throughput = us > 0 ? (double)(relR->num_tuples + relS->num_tuples) / us : 0.0;  // M rec/s
-    out->materialized = 0;
+    out->materialized = materialize ? 1 : 0;
     out->result = nullptr;
     out->result_type = 0;
+    if (materialize) {
+        chunked_table_t *t = make_chunked_table(host, st.matches);
+        std::free(host);
+        if (!t) {
+            set_last_error("host allocation of the chunked table failed");
+            return MI355_ERR_OOM;
+        }
+        out->result = t;
+        out->result_type = 1;
+    }
     return MI355_OK;
 }
 

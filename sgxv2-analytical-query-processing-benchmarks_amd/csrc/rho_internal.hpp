@@ -54,11 +54,24 @@ hipError_t launch_scatter(const row_t *in, row_t *out, const SegMap &m, uint32_t
                           uint32_t bits, const uint64_t *cursors, HistLayout layout, uint32_t nseg_stride,
                           const uint64_t *digit_base, hipStream_t s);
 
-// Build + probe over P partitions; writes one partial count per workgroup.
-// rcap (2048 / 4096 / 8192) = R tuples per LDS chain table; LDS = 10 * rcap bytes.
+// Build + probe over tasks (partition x S chunk of at most kSChunk tuples).
+// Tasks 0..P-1 are the partitions' first chunks; over[0 .. *n_over) holds the
+// further chunks of large S partitions as p | chunk << 32 (launch_make_tasks).
+// rcap (2048 / 4096 / 8192) = R tuples per LDS chain table.
+// mode 0: counts[blockIdx] = per-workgroup partial count (grid entries);
+// mode 1: counts[t] = per-task count (P + *n_over entries);
+// mode 2: write every match to out[task_off[t] + ...] as output_triple_t.
+constexpr uint64_t kSChunk = 8192;
+enum JoinMode : int { kJoinCount = 0, kJoinTaskCount = 1, kJoinWrite = 2 };
+hipError_t launch_make_tasks(const uint64_t *r_count, const uint64_t *s_count, uint64_t P, uint64_t *over,
+                             uint32_t over_cap, uint32_t *n_over, hipStream_t s);
 hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, const uint64_t *r_count,
-                       const uint64_t *s_start, const uint64_t *s_count, uint64_t P, uint32_t hash_shift,
-                       uint32_t rcap, uint32_t grid, uint64_t *partials, hipStream_t s);
+                       const uint64_t *s_start, const uint64_t *s_count, uint64_t P, const uint64_t *over,
+                       const uint32_t *n_over, uint32_t hash_shift, uint32_t rcap, uint32_t grid, int mode,
+                       uint64_t *counts, const uint64_t *task_off, output_triple_t *out, hipStream_t s);
+// One-block exclusive scan of n_base + *n_extra values; *total = their sum.
+hipError_t launch_excl_scan(const uint64_t *in, const uint32_t *n_extra, uint64_t n_base, uint64_t *out,
+                            uint64_t *total, hipStream_t s);
 
 hipError_t launch_reduce(const uint64_t *partials, uint32_t n, uint64_t *result, hipStream_t s);
 

@@ -465,9 +465,15 @@ hipError_t launch_scatter(const row_t *in, row_t *out, const SegMap &m, uint32_t
 }
 
 // ------------------------------------------------------------ build+probe ---
-// bucket_chaining_join (radix_join.cpp:359-458) per partition, in LDS.  For an R
-// chunk of nrc <= RCAP tuples: N = nextpow2(nrc) bucket heads, bucket of a key =
-// HASH_BIT_MODULO(key, (N-1) << bits, bits) = (key >> bits) & (N-1) exactly as
+// bucket_chaining_join (radix_join.cpp:359-458) per task, in LDS.  A task is a
+// partition p and one chunk of at most kSChunk of its S tuples: S partitions
+// larger than kSChunk (skew, e.g. a Zipf hot key) are split over several tasks so
+// that no single workgroup is left with a hot partition (the reference has no
+// skew handling, prj_params.h:69-71).  Task t < P is (p = t, chunk 0); the extra
+// chunks of large partitions follow as overflow entries {p, chunk}.
+//
+// For an R chunk of nrc <= RCAP tuples: N = nextpow2(nrc) bucket heads, bucket of a
+// key = HASH_BIT_MODULO(key, (N-1) << bits, bits) = (key >> bits) & (N-1) exactly as
 // the reference (:374-378, :388); keys[] and 16-bit next[] hold the chains with
 // 1-based positions (:393 "we start pos's from 1").  The build links tuple i with
 // one LDS atomic exchange on its bucket head (chain order differs from the
@@ -475,112 +481,268 @@ hipError_t launch_scatter(const row_t *in, row_t *out, const SegMap &m, uint32_t
 // counts key equality (:429-436).  Each thread handles U = RCAP / kBlock tuples at
 // a time; their chain walks advance in lockstep so the LDS reads of independent
 // tuples overlap.  Partitions whose R side exceeds RCAP are built chunk by chunk
-// with S re-probed per chunk.  One partial count per workgroup.
+// with the task's S chunk re-probed per R chunk.
+//
+// MODE kJoinCount     one partial count per workgroup (count-only join);
+// MODE kJoinTaskCount one count per task (first pass of materialisation);
+// MODE kJoinWrite     every match as an output_triple_t {key, R payload, S payload}
+//                     (radix_join.cpp:437-446) at task_off[t] + a task-local slot
+//                     taken with one LDS atomic per wave and chain step.
+
+__device__ __forceinline__ void decode_task(uint64_t t, uint64_t P, const uint64_t *__restrict__ over, uint64_t &p,
+                                            uint64_t &chunk) {
+    if (t < P) {
+        p = t;
+        chunk = 0;
+    } else {
+        const uint64_t e = over[t - P];
+        p = e & 0xFFFFFFFFull;
+        chunk = e >> 32;
+    }
+}
+
+// LDS of one build/probe workgroup: exactly 10 * RCAP bytes when counting (4
+// workgroups per CU at RCAP 4096), + 4 * RCAP of R payloads when writing.  The
+// reduction slots reuse the bucket heads, which are dead after each probe.
+template <int RCAP, int MODE>
+struct JoinLds {
+    union {
+        __attribute__((aligned(16))) uint32_t head[RCAP];
+        uint64_t red[kWaves];
+    };
+    uint32_t keys[RCAP];
+    uint16_t next[RCAP];
+};
 template <int RCAP>
-__global__ __launch_bounds__(kBlock) void k_join(const uint32_t *__restrict__ Rw, const uint32_t *__restrict__ Sw,
+struct JoinLds<RCAP, kJoinWrite> {
+    union {
+        __attribute__((aligned(16))) uint32_t head[RCAP];
+        uint64_t red[kWaves];
+    };
+    uint32_t keys[RCAP];
+    uint16_t next[RCAP];
+    uint32_t rpay[RCAP];
+    uint32_t cursor;
+};
+
+template <int RCAP, int MODE>
+__global__ __launch_bounds__(kBlock) void k_join(const uint64_t *__restrict__ R, const uint64_t *__restrict__ S,
                                                  const uint64_t *__restrict__ r_start,
                                                  const uint64_t *__restrict__ r_count,
                                                  const uint64_t *__restrict__ s_start,
                                                  const uint64_t *__restrict__ s_count, uint64_t P,
-                                                 uint32_t hash_shift, uint64_t *__restrict__ partials) {
+                                                 const uint64_t *__restrict__ over,
+                                                 const uint32_t *__restrict__ n_over, uint32_t hash_shift,
+                                                 uint64_t *__restrict__ counts,
+                                                 const uint64_t *__restrict__ task_off,
+                                                 output_triple_t *__restrict__ out) {
     constexpr int U = RCAP / kBlock;
-    __shared__ __attribute__((aligned(16))) uint32_t head[RCAP];
-    __shared__ uint32_t keys[RCAP];
-    __shared__ uint16_t next[RCAP];
-    uint64_t *red = reinterpret_cast<uint64_t *>(head);  // reused after the last table (keeps LDS = 10 * RCAP)
-    const uint32_t tid = threadIdx.x;
+    __shared__ JoinLds<RCAP, MODE> L;
+    const uint32_t tid = threadIdx.x, lane = __lane_id();
+    const uint64_t T = P + *n_over;
     uint64_t matches = 0;
-    for (uint64_t p = blockIdx.x; p < P; p += gridDim.x) {
-        const uint64_t nR = r_count[p], nS = s_count[p];
-        if (nR == 0 || nS == 0) continue;
-        const uint64_t rb = r_start[p], sb = s_start[p];
-        for (uint64_t rc = 0; rc < nR; rc += RCAP) {
-            const uint32_t nrc = (uint32_t)((nR - rc) < RCAP ? (nR - rc) : RCAP);
-            uint32_t N = 1;
-            while (N < nrc) N <<= 1;  // NEXT_POW_2(numR)
-            const uint32_t hmask = N - 1;
-            const uint32_t *rk = Rw + 2 * (rb + rc);
-            uint32_t kr[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint32_t i = tid + u * kBlock;
-                kr[u] = i < nrc ? (uint32_t)ld_nt(reinterpret_cast<const uint64_t *>(rk) + i) : 0u;
-            }
-            for (uint32_t i = tid; i < (N + 3) / 4; i += kBlock)
-                reinterpret_cast<uint4 *>(head)[i] = make_uint4(0, 0, 0, 0);
-            __syncthreads();
-#pragma unroll
-            for (int u = 0; u < U; ++u) {  // BUILD-LOOP (:407-411)
-                const uint32_t i = tid + u * kBlock;
-                if (i < nrc) {
-                    keys[i] = kr[u];
-                    const uint32_t prev = atomicExch(&head[(kr[u] >> hash_shift) & hmask], i + 1);
-                    next[i] = (uint16_t)prev;
-                }
-            }
-            __syncthreads();
-            const uint32_t *sk = Sw + 2 * sb;
-            for (uint64_t s0 = 0; s0 < nS; s0 += RCAP) {  // PROBE-LOOP (:429-436)
-                uint32_t ks[U], cur[U];
+    for (uint64_t t = blockIdx.x; t < T; t += gridDim.x) {
+        uint64_t p, chunk;
+        decode_task(t, P, over, p, chunk);
+        const uint64_t nR = r_count[p], nSp = s_count[p];
+        const uint64_t s_lo = chunk * kSChunk;
+        const uint64_t nS = (nR == 0 || s_lo >= nSp) ? 0 : min<uint64_t>(nSp - s_lo, kSChunk);
+        uint64_t tmatch = 0;
+        if constexpr (MODE == kJoinWrite) {
+            if (tid == 0) L.cursor = 0;
+        }
+        if (nS > 0) {
+            const uint64_t *rp = R + r_start[p];
+            const uint64_t *sp = S + s_start[p] + s_lo;
+            for (uint64_t rc = 0; rc < nR; rc += RCAP) {
+                const uint32_t nrc = (uint32_t)((nR - rc) < RCAP ? (nR - rc) : RCAP);
+                uint32_t N = 1;
+                while (N < nrc) N <<= 1;  // NEXT_POW_2(numR)
+                const uint32_t hmask = N - 1;
+                uint64_t kr[U];
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
-                    const uint64_t i = s0 + tid + u * kBlock;
-                    ks[u] = i < nS ? (uint32_t)ld_nt(reinterpret_cast<const uint64_t *>(sk) + i) : 0u;
+                    const uint32_t i = tid + u * kBlock;
+                    kr[u] = i < nrc ? ld_nt(rp + rc + i) : 0ull;
                 }
+                for (uint32_t i = tid; i < (N + 3) / 4; i += kBlock)
+                    reinterpret_cast<uint4 *>(L.head)[i] = make_uint4(0, 0, 0, 0);
+                __syncthreads();
 #pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const uint64_t i = s0 + tid + u * kBlock;
-                    cur[u] = i < nS ? head[(ks[u] >> hash_shift) & hmask] : 0u;
+                for (int u = 0; u < U; ++u) {  // BUILD-LOOP (:407-411)
+                    const uint32_t i = tid + u * kBlock;
+                    if (i < nrc) {
+                        const uint32_t k = (uint32_t)kr[u];
+                        L.keys[i] = k;
+                        if constexpr (MODE == kJoinWrite) L.rpay[i] = (uint32_t)(kr[u] >> 32);
+                        const uint32_t prev = atomicExch(&L.head[(k >> hash_shift) & hmask], i + 1);
+                        L.next[i] = (uint16_t)prev;
+                    }
                 }
-                bool more = true;
-                while (more) {
-                    more = false;
+                __syncthreads();
+                for (uint64_t s0 = 0; s0 < nS; s0 += RCAP) {  // PROBE-LOOP (:429-436)
+                    uint32_t ks[U], cur[U];
+                    uint32_t sv[MODE == kJoinWrite ? U : 1];
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
-                        if (cur[u]) {
-                            const uint32_t e = cur[u] - 1;
-                            matches += (keys[e] == ks[u]);
-                            cur[u] = next[e];
-                            more |= cur[u] != 0;
+                        const uint64_t i = s0 + tid + u * kBlock;
+                        const uint64_t x = i < nS ? ld_nt(sp + i) : 0ull;
+                        ks[u] = (uint32_t)x;
+                        if constexpr (MODE == kJoinWrite) sv[u] = (uint32_t)(x >> 32);
+                    }
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const uint64_t i = s0 + tid + u * kBlock;
+                        cur[u] = i < nS ? L.head[(ks[u] >> hash_shift) & hmask] : 0u;
+                    }
+                    bool more = true;
+                    while (more) {
+                        more = false;
+#pragma unroll
+                        for (int u = 0; u < U; ++u) {
+                            if constexpr (MODE == kJoinWrite) {
+                                // ballot over the active lanes, one LDS atomic per wave
+                                bool m = false;
+                                uint32_t e = 0;
+                                if (cur[u]) {
+                                    e = cur[u] - 1;
+                                    m = L.keys[e] == ks[u];
+                                }
+                                // the chain-walk loop diverges: lanes whose chains ended have left
+                                // it, so the slot is taken by the lowest still-active lane
+                                const uint64_t bal = __ballot(m);
+                                if (bal) {
+                                    const int leader = __ffsll((unsigned long long)__ballot(1)) - 1;
+                                    uint32_t base = 0;
+                                    if ((int)lane == leader) base = atomicAdd(&L.cursor, (uint32_t)__popcll(bal));
+                                    base = __shfl(base, leader, kWave);
+                                    if (m) {
+                                        const uint64_t o = task_off[t] + base + __popcll(bal & lanemask_lt());
+                                        uint32_t *w = reinterpret_cast<uint32_t *>(out + o);
+                                        w[0] = ks[u];
+                                        w[1] = L.rpay[e];
+                                        w[2] = sv[u];
+                                    }
+                                }
+                                if (cur[u]) {
+                                    cur[u] = L.next[e];
+                                    more |= cur[u] != 0;
+                                }
+                            } else if (cur[u] != 0) {
+                                const uint32_t e = cur[u] - 1;
+                                tmatch += (L.keys[e] == ks[u]);
+                                cur[u] = L.next[e];
+                                more |= cur[u] != 0;
+                            }
                         }
                     }
                 }
+                __syncthreads();
+            }
+        }
+        if constexpr (MODE == kJoinTaskCount) {
+            const uint64_t wsum = wave_sum_u64(tmatch);
+            __syncthreads();  // red aliases head
+            if (lane == 0) L.red[tid / kWave] = wsum;
+            __syncthreads();
+            if (tid == 0) {
+                uint64_t acc = 0;
+                for (int w = 0; w < kWaves; ++w) acc += L.red[w];
+                counts[t] = acc;
             }
             __syncthreads();
+        } else if constexpr (MODE == kJoinWrite) {
+            __syncthreads();  // the task's cursor is re-armed only after every wave wrote
         }
+        matches += tmatch;
     }
-    matches = wave_sum_u64(matches);
-    __syncthreads();
-    if (__lane_id() == 0) red[tid / kWave] = matches;
-    __syncthreads();
-    if (tid == 0) {
-        uint64_t acc = 0;
-        for (int w = 0; w < kWaves; ++w) acc += red[w];
-        partials[blockIdx.x] = acc;
+    if constexpr (MODE == kJoinCount) {
+        matches = wave_sum_u64(matches);
+        __syncthreads();
+        if (lane == 0) L.red[tid / kWave] = matches;
+        __syncthreads();
+        if (tid == 0) {
+            uint64_t acc = 0;
+            for (int w = 0; w < kWaves; ++w) acc += L.red[w];
+            counts[blockIdx.x] = acc;
+        }
     }
 }
 
 hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, const uint64_t *r_count,
-                       const uint64_t *s_start, const uint64_t *s_count, uint64_t P, uint32_t hash_shift,
-                       uint32_t rcap, uint32_t grid, uint64_t *partials, hipStream_t s) {
-    const uint32_t *Rw = reinterpret_cast<const uint32_t *>(R);
-    const uint32_t *Sw = reinterpret_cast<const uint32_t *>(S);
+                       const uint64_t *s_start, const uint64_t *s_count, uint64_t P, const uint64_t *over,
+                       const uint32_t *n_over, uint32_t hash_shift, uint32_t rcap, uint32_t grid, int mode,
+                       uint64_t *counts, const uint64_t *task_off, output_triple_t *out, hipStream_t s) {
+    const uint64_t *R64 = reinterpret_cast<const uint64_t *>(R);
+    const uint64_t *S64 = reinterpret_cast<const uint64_t *>(S);
+#define JOIN_LAUNCH(RC, MD)                                                                                 \
+    hipLaunchKernelGGL((k_join<RC, MD>), dim3(grid), dim3(kBlock), 0, s, R64, S64, r_start, r_count, s_start, \
+                       s_count, P, over, n_over, hash_shift, counts, task_off, out)
+#define JOIN_MODES(RC)                                        \
+    case RC:                                                  \
+        if (mode == kJoinCount) JOIN_LAUNCH(RC, kJoinCount);  \
+        else if (mode == kJoinTaskCount) JOIN_LAUNCH(RC, kJoinTaskCount); \
+        else JOIN_LAUNCH(RC, kJoinWrite);                     \
+        break;
     switch (rcap) {
-        case 2048:
-            hipLaunchKernelGGL(k_join<2048>, dim3(grid), dim3(kBlock), 0, s, Rw, Sw, r_start, r_count, s_start,
-                               s_count, P, hash_shift, partials);
-            break;
-        case 4096:
-            hipLaunchKernelGGL(k_join<4096>, dim3(grid), dim3(kBlock), 0, s, Rw, Sw, r_start, r_count, s_start,
-                               s_count, P, hash_shift, partials);
-            break;
-        case 8192:
-            hipLaunchKernelGGL(k_join<8192>, dim3(grid), dim3(kBlock), 0, s, Rw, Sw, r_start, r_count, s_start,
-                               s_count, P, hash_shift, partials);
-            break;
+        JOIN_MODES(2048)
+        JOIN_MODES(4096)
+        JOIN_MODES(8192)
         default:
             return hipErrorInvalidValue;
     }
+#undef JOIN_MODES
+#undef JOIN_LAUNCH
+    return hipGetLastError();
+}
+
+// Overflow tasks: the S chunks 1.. of every partition whose S side exceeds kSChunk
+// (and whose R side is not empty).
+__global__ __launch_bounds__(kBlock) void k_make_tasks(const uint64_t *__restrict__ r_count,
+                                                       const uint64_t *__restrict__ s_count, uint64_t P,
+                                                       uint64_t *__restrict__ over, uint32_t over_cap,
+                                                       uint32_t *__restrict__ n_over) {
+    for (uint64_t p = blockIdx.x * (uint64_t)kBlock + threadIdx.x; p < P; p += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t nS = s_count[p];
+        if (r_count[p] == 0 || nS <= kSChunk) continue;
+        const uint32_t k = (uint32_t)((nS + kSChunk - 1) / kSChunk) - 1;
+        const uint32_t base = atomicAdd(n_over, k);
+        for (uint32_t j = 0; j < k && base + j < over_cap; ++j) over[base + j] = p | ((uint64_t)(j + 1) << 32);
+    }
+}
+
+hipError_t launch_make_tasks(const uint64_t *r_count, const uint64_t *s_count, uint64_t P, uint64_t *over,
+                             uint32_t over_cap, uint32_t *n_over, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(n_over, 0, sizeof(uint32_t), s);
+    if (e != hipSuccess) return e;
+    uint64_t blocks = (P + kBlock - 1) / kBlock;
+    if (blocks > 1024) blocks = 1024;
+    hipLaunchKernelGGL(k_make_tasks, dim3((uint32_t)blocks), dim3(kBlock), 0, s, r_count, s_count, P, over, over_cap,
+                       n_over);
+    return hipGetLastError();
+}
+
+// One block: exclusive scan of n u64 values (task counts -> output offsets), total in *total.
+__global__ __launch_bounds__(1024) void k_excl_scan(const uint64_t *__restrict__ in, const uint32_t *__restrict__ n_extra,
+                                                    uint64_t n_base, uint64_t *__restrict__ out,
+                                                    uint64_t *__restrict__ total) {
+    __shared__ uint64_t scratch[1024 / kWave + 1];
+    const uint64_t n = n_base + (n_extra ? *n_extra : 0);
+    uint64_t carry = 0;
+    for (uint64_t b = 0; b < n; b += 1024) {
+        const uint64_t i = b + threadIdx.x;
+        const uint64_t v = i < n ? in[i] : 0;
+        uint64_t tot;
+        const uint64_t ex = block_excl_scan_u64(v, scratch, &tot);
+        if (i < n) out[i] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) *total = carry;
+}
+
+hipError_t launch_excl_scan(const uint64_t *in, const uint32_t *n_extra, uint64_t n_base, uint64_t *out,
+                            uint64_t *total, hipStream_t s) {
+    hipLaunchKernelGGL(k_excl_scan, dim3(1), dim3(1024), 0, s, in, n_extra, n_base, out, total);
     return hipGetLastError();
 }
 

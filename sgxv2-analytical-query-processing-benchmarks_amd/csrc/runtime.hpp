@@ -70,6 +70,7 @@ struct Context {
     DeviceBuffer inR, inS;         // staging of host relations
     DeviceBuffer t1R, t1S, t2R, t2S;
     Arena scratch;
+    DeviceBuffer mat;              // materialised output_triple_t (when the caller's buffer is host memory)
     // scan workspace
     DeviceBuffer scan_in, scan_out, scan_aux;
     uint64_t *host_result = nullptr;  // pinned 64 x u64

@@ -71,7 +71,23 @@ class rho_opts(C.Structure):
         ("timing", C.c_int),
         ("reserved", C.c_int),
         ("stream", C.c_void_p),
+        ("out", C.c_void_p),
+        ("out_capacity", C.c_uint64),
     ]
+
+
+class chunked_table_t(C.Structure):
+    """data-types.h:86-92 (ChunkedTable.cpp): the MATERIALIZE=1 result of RHO."""
+    _fields_ = [
+        ("chunks", C.POINTER(C.c_void_p)),
+        ("current_chunk", C.c_uint64),
+        ("num_chunks", C.c_uint64),
+        ("chunk_capacity", C.c_uint64),
+        ("num_tuples", C.c_uint64),
+    ]
+
+
+TUPLES_PER_CHUNK = (16 * 1024 - 8) // 12  # data-types.h:80-81 with CSKB = 16
 
 
 class rho_stats(C.Structure):
@@ -107,6 +123,7 @@ SIGNATURES = {
     "mi355_version": (C.c_char_p, []),
     "mi355_rho_join": (C.c_int, [C.POINTER(table_t), C.POINTER(table_t), C.POINTER(joinconfig_t), C.POINTER(result_t)]),
     "mi355_rho_join_ex": (C.c_int, [_P, C.c_uint64, _P, C.c_uint64, C.POINTER(rho_opts), C.POINTER(rho_stats)]),
+    "mi355_free_chunked_table": (None, [_P]),
     "mi355_rho_shard_partition": (C.c_int, [_P, C.c_uint64, C.c_uint32, C.c_uint32, _P, _U64P, _P]),
     "mi355_timing_enable": (None, [C.c_int]),
     "mi355_timing_get": (C.c_int, [C.POINTER(C.c_char_p), C.POINTER(C.c_double), C.c_int]),
@@ -199,23 +216,58 @@ class JoinResult:
 
 
 def rho_join(R, nR: int, S, nS: int, *, radix_bits: int = 0, passes: int = 0, key_shift: int = 0,
-             timing: bool = False, stream: int | None = None) -> JoinResult:
-    """RHO join of nR R-tuples and nS S-tuples (8-byte {key, payload}; host or device)."""
-    o = rho_opts(radix_bits, passes, key_shift, 0, 1 if timing else 0, 0, stream or None)
+             timing: bool = False, stream: int | None = None, out=None, out_capacity: int = 0) -> JoinResult:
+    """RHO join of nR R-tuples and nS S-tuples (8-byte {key, payload}; host or device).
+
+    With `out` (host or device buffer of out_capacity 12-byte triples) every match is
+    materialised as {key, R payload, S payload}; a too-small buffer raises Mi355Error
+    with code MI355_ERR_CAPACITY (-5)."""
+    o = rho_opts(radix_bits, passes, key_shift, 1 if out is not None else 0, 1 if timing else 0, 0, stream or None,
+                 ptr(out) if out is not None else None, out_capacity)
     st = rho_stats()
-    _check(lib.mi355_rho_join_ex(ptr(R), nR, ptr(S), nS, C.byref(o), C.byref(st)))
+    rc = lib.mi355_rho_join_ex(ptr(R), nR, ptr(S), nS, C.byref(o), C.byref(st))
+    if rc == -5:
+        raise Mi355Error(rc, f"capacity: {int(st.matches)} triples needed")
+    _check(rc)
     return JoinResult(int(st.matches), st.as_dict())
 
 
-def rho_join_tables(R, nR: int, S, nS: int, nthreads: int = 1) -> result_t:
-    """The drop-in mi355_rho_join(table_t*, table_t*, joinconfig_t*, result_t*)."""
+def rho_join_tables(R, nR: int, S, nS: int, nthreads: int = 1, materialize: bool = False) -> result_t:
+    """The drop-in mi355_rho_join(table_t*, table_t*, joinconfig_t*, result_t*).
+
+    With materialize, result.result is a chunked_table_t* (result_type 1): read it
+    with chunked_table_triples() and release it with free_result()."""
     tR = table_t(ptr(R), nR, 0, 0)
     tS = table_t(ptr(S), nS, 0, 0)
     cfg = joinconfig_t()
     cfg.NTHREADS = nthreads
+    cfg.MATERIALIZE = 1 if materialize else 0
     out = result_t()
     _check(lib.mi355_rho_join(C.byref(tR), C.byref(tS), C.byref(cfg), C.byref(out)))
     return out
+
+
+def chunked_table_triples(res: result_t):
+    """numpy (n, 3) uint32 array of the {key, Rpayload, Spayload} triples of a
+    materialised result (chunk order)."""
+    import numpy as np
+
+    if not res.materialized or res.result_type != 1 or not res.result:
+        return np.zeros((0, 3), dtype=np.uint32)
+    t = C.cast(res.result, C.POINTER(chunked_table_t)).contents
+    parts = []
+    for c in range(t.num_chunks):
+        base = t.chunks[c]
+        k = C.c_uint64.from_address(base).value
+        if k:
+            parts.append(np.frombuffer(C.string_at(base + 8, 12 * k), dtype=np.uint32).reshape(k, 3))
+    return np.concatenate(parts) if parts else np.zeros((0, 3), dtype=np.uint32)
+
+
+def free_result(res: result_t) -> None:
+    if res.result and res.result_type == 1:
+        lib.mi355_free_chunked_table(res.result)
+        res.result = None
 
 
 def shard_partition(inp, n: int, key_shift: int, dest_bits: int, out, stream: int | None = None) -> list[int]:

@@ -122,3 +122,29 @@ def test_scan_signed_i32(orc):
     col = np.array([-5, -1, 0, 3, 2**31 - 1, -(2**31)], dtype=np.int32)
     assert orc.scan("count", "i32", -1, 3, col) == 3
     assert orc.scan("index", "i32", -(2**31), -1, col).tolist() == [0, 1, 5]
+
+
+def test_oracle_materialize_vs_pair_enumeration():
+    """oracle_rho_join_mat (radix_join.cpp:437-446) emits exactly the equi-join pairs."""
+    import oracle
+
+    rng = np.random.default_rng(3)
+    dt = np.dtype([("key", "<u4"), ("payload", "<u4")])
+    for nR, nS, kmax in [(3000, 4000, 500), (1 << 14, 1 << 12, 1 << 20)]:
+        R = np.empty(nR, dt)
+        S = np.empty(nS, dt)
+        R["key"] = rng.integers(0, kmax, nR)
+        S["key"] = rng.integers(0, kmax, nS)
+        R["payload"] = np.arange(nR)
+        S["payload"] = np.arange(nS)
+        got = oracle.rho_join_triples(R, S, 3)
+        # independent: for each S row all R rows with the same key
+        order = np.argsort(R["key"], kind="stable")
+        rk = R["key"][order]
+        lo = np.searchsorted(rk, S["key"], "left")
+        hi = np.searchsorted(rk, S["key"], "right")
+        exp = [(S["key"][j], order[i], j) for j in range(nS) for i in range(lo[j], hi[j])]
+        exp = np.array(exp, dtype=np.uint32).reshape(-1, 3)
+        key = lambda t: t[np.lexsort((t[:, 2], t[:, 1], t[:, 0]))]
+        assert got.shape == exp.shape
+        assert np.array_equal(key(got), key(exp))

@@ -166,3 +166,95 @@ def test_native_driver_binary(gpu):
                          capture_output=True, text=True, timeout=300, check=True).stdout
     assert "Matches = 1048576" in out
     assert "Throughput (M rec/sec)" in out
+
+
+# ---------------------------------------------------------------- materialisation
+def sorted_triples(t):
+    t = np.asarray(t, dtype=np.uint32).reshape(-1, 3)
+    return t[np.lexsort((t[:, 2], t[:, 1], t[:, 0]))]
+
+
+def gpu_triples(sgx, R, S, **kw):
+    m = sgx.rho_join(R, len(R), S, len(S)).matches
+    out = np.zeros((max(m, 1), 3), dtype=np.uint32)
+    res = sgx.rho_join(R, len(R), S, len(S), out=out, out_capacity=m, **kw)
+    assert res.matches == m
+    return out[:m]
+
+
+@pytest.mark.parametrize("case", ["pk_fk_sel50", "fk_copies", "dups", "hot_key"])
+def test_materialize_matches_oracle(sgx, orc, gpu, case):
+    """MATERIALIZE = 1 (radix_join.cpp:437-446): the same multiset of {key, R payload, S payload}."""
+    rng = np.random.default_rng(11)
+    if case == "pk_fk_sel50":
+        R, S = sgx.reference_relations(1 << 16, 1 << 16, selectivity=50)
+    elif case == "fk_copies":
+        R, S = sgx.reference_relations(1 << 14, 1 << 17)
+    elif case == "dups":
+        R = rel(rng.integers(0, 3000, 20_000).astype(np.uint32))
+        S = rel(rng.integers(0, 3000, 30_000).astype(np.uint32))
+    else:  # hot S key split over several build/probe tasks, duplicated R key
+        R = rel(np.concatenate([np.full(3, 9, np.uint32), np.arange(100, 20_100, dtype=np.uint32)]))
+        S = rel(np.concatenate([np.full(40_000, 9, np.uint32), rng.integers(0, 30_000, 50_000).astype(np.uint32)]))
+    exp = orc.rho_join_triples(R, S, 4)
+    for bits, passes in [(0, 0), (6, 1), (14, 2)]:
+        got = gpu_triples(sgx, R, S, radix_bits=bits, passes=passes)
+        assert got.shape == exp.shape
+        assert np.array_equal(sorted_triples(got), sorted_triples(exp)), (case, bits, passes)
+
+
+def test_materialize_capacity_and_device_output(sgx, gpu):
+    import torch
+
+    R, S = sgx.reference_relations(1 << 15, 1 << 15)
+    with pytest.raises(sgx.Mi355Error) as ei:
+        sgx.rho_join(R, len(R), S, len(S), out=np.zeros((10, 3), np.uint32), out_capacity=10)
+    assert ei.value.code == -5 and str(1 << 15) in str(ei.value)
+    d = torch.zeros((1 << 15) * 3, dtype=torch.int32, device=gpu)
+    res = sgx.rho_join(R, len(R), S, len(S), out=d, out_capacity=1 << 15)
+    t = d.cpu().numpy().view(np.uint32).reshape(-1, 3)
+    assert res.matches == 1 << 15
+    assert (R["key"][t[:, 1]] == t[:, 0]).all() and (S["key"][t[:, 2]] == t[:, 0]).all()
+    assert np.array_equal(np.sort(t[:, 2]), np.arange(1 << 15, dtype=np.uint32))
+
+
+def test_dropin_materialize_chunked_table(sgx, orc, gpu):
+    R, S = sgx.reference_relations(1 << 12, 1 << 13, selectivity=50)
+    res = sgx.rho_join_tables(R, len(R), S, len(S), nthreads=4, materialize=True)
+    try:
+        assert res.materialized == 1 and res.result_type == 1
+        got = sgx.chunked_table_triples(res)
+        exp = orc.rho_join_triples(R, S, 4)
+        assert res.totalresults == len(exp) == len(got)
+        assert np.array_equal(sorted_triples(got), sorted_triples(exp))
+    finally:
+        sgx.free_result(res)
+
+
+def test_skew_splits_hot_partition(sgx, orc, gpu):
+    """A hot S partition (200k copies of one key) is split over several build/probe tasks."""
+    R = rel(np.concatenate([np.full(2, 5, np.uint32), np.arange(1000, 60_000, dtype=np.uint32)]))
+    S = rel(np.concatenate([np.full(200_000, 5, np.uint32), np.arange(1000, 50_000, dtype=np.uint32)]))
+    res = gpu_join(sgx, R, S)
+    assert res.matches == orc.count_join_sort(R, S) == 2 * 200_000 + 49_000
+    assert res.stats["num_tasks"] >= res.stats["num_partitions"] + 200_000 // 8192
+
+
+def test_full_size_materialize_property(sgx, gpu):
+    """|R| = |S| = 2^26 device pk/fk, materialised on the device: every S row matches once,
+    and each triple's payloads point at rows holding its key."""
+    import torch
+
+    n = 1 << 26
+    R = torch.empty(n, dtype=torch.int64, device=gpu)
+    S = torch.empty(n, dtype=torch.int64, device=gpu)
+    sgx.gen_pk_dev(R, n, 0, n, 11111)
+    sgx.gen_fk_dev(S, n, 0, n, 22222)
+    out = torch.empty(n * 3, dtype=torch.int32, device=gpu)
+    assert sgx.rho_join(R, n, S, n, out=out, out_capacity=n).matches == n
+    t = out.view(n, 3).to(torch.int64) & 0xFFFFFFFF
+    rk, sk = R & 0xFFFFFFFF, S & 0xFFFFFFFF
+    assert torch.equal(rk[t[:, 1]], t[:, 0]) and torch.equal(sk[t[:, 2]], t[:, 0])
+    assert torch.equal(torch.sort(t[:, 2]).values, torch.arange(n, device=gpu))
+    del R, S, out, t, rk, sk
+    torch.cuda.empty_cache()
