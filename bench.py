@@ -53,7 +53,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--log2n", type=int, default=28, help="per-GPU |R| = |S| = 2^log2n")
+    ap.add_argument("--log2n", type=int, default=28, help="c2: per-GPU |R| = |S| = 2^log2n")
+    ap.add_argument("--workload", choices=["c2", "c4", "c5"], default="c2",
+                    help="BASELINE config: c2 = pk/fk 2^28 per GPU (weak), c4 = |R| 2^27 x |S| 2^30 "
+                         "global (strong), c5 = Zipf 0.75 |R| = |S| = 2^28 global (strong)")
     ap.add_argument("--no-scan", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -93,13 +96,28 @@ def main():
     sgxamd.set_stream(stream)
     sgxamd.timing_enable(True)  # per-kernel HIP events on `stream` (roofline "achieved")
 
-    # ---------------- RHO workload: rank slice of global pk(N n) and fk(N n, N n)
-    n = 1 << args.log2n
-    N_glob = n * world
-    R = torch.empty(n, dtype=torch.int64, device=dev)
-    S = torch.empty(n, dtype=torch.int64, device=dev)
-    sgxamd.gen_pk_dev(R, n, rank * n, N_glob, 11111, stream)
-    sgxamd.gen_fk_dev(S, n, rank * n, N_glob, 22222, stream)
+    # ---------------- RHO workload: this rank's slice of the global relations
+    if args.workload == "c2":  # weak: pk(N n) and fk(N n, maxid N n), n per GPU
+        n = 1 << args.log2n
+        gR = gS = n * world
+        workload = f"RHO join |R|=|S|=2^{args.log2n} uniform per GPU (BASELINE config 2)"
+    elif args.workload == "c4":  # strong: pk(2^27) and fk(2^30, maxid 2^27) = 8 shuffled copies
+        gR, gS = 1 << 27, 1 << 30
+        workload = "RHO join |R|=2^27 |S|=2^30 uniform, global (BASELINE config 4)"
+    else:  # strong: pk(2^28) and Zipf(0.75) over 1..2^28
+        gR = gS = 1 << 28
+        workload = "RHO join |R|=|S|=2^28, S Zipf theta=0.75, global (BASELINE config 5)"
+    if gR % world or gS % world:
+        raise SystemExit("relation sizes must divide by the number of GPUs")
+    nR_loc, nS_loc = gR // world, gS // world
+    R = torch.empty(nR_loc, dtype=torch.int64, device=dev)
+    S = torch.empty(nS_loc, dtype=torch.int64, device=dev)
+    sgxamd.gen_pk_dev(R, nR_loc, rank * nR_loc, gR, 11111, stream)
+    if args.workload == "c5":
+        sgxamd.gen_zipf_dev(S, nS_loc, rank * nS_loc, gR, 0.75, 22222, stream)
+    else:
+        sgxamd.gen_fk_dev(S, nS_loc, rank * nS_loc, gR, 22222, stream)
+    N_glob = gS  # every S tuple matches exactly one R tuple in all three configs
     torch.cuda.synchronize()
 
     def step():
@@ -134,7 +152,8 @@ def main():
     if os.path.exists(TRAFFIC_FILE):
         try:
             tf = json.load(open(TRAFFIC_FILE))
-            if tf.get("log2n") == args.log2n and dom in tf.get("bytes_per_launch", {}):
+            if (args.workload == "c2" and tf.get("log2n") == args.log2n
+                    and dom in tf.get("bytes_per_launch", {})):
                 traffic = tf["bytes_per_launch"][dom]
         except (OSError, ValueError):
             traffic = None
@@ -146,7 +165,7 @@ def main():
     ls = results[-1].local_stats
     rho_info = {
         "matches_ok": ok, "matches": results[-1].matches,
-        "M_rec_per_s_reference_formula": round(2 * N_glob * args.steps / elapsed / 1e6, 1),
+        "M_rec_per_s_reference_formula": round((gR + gS) * args.steps / elapsed / 1e6, 1),
         "probe_phase_M_probed_tuples_per_s": round(nS / (avg["join_build_probe"] * 1e-3) / 1e6, 1),
         "probe_roofline": {"achieved": round(probe_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                            "frac": round(probe_gbs / HBM_PEAK_GBS, 4)},
@@ -154,12 +173,26 @@ def main():
         "radix_bits": ls.get("radix_bits"), "passes": ls.get("passes"),
         "step_ms_breakdown": {k: round(v, 3) for k, v in results[-1].ms.items()},
     }
+    if args.workload == "c5":  # per-partition / per-GPU load report (skew)
+        rs = torch.tensor([float(nS)], dtype=torch.float64, device=dev)
+        if world > 1:
+            allr = [torch.zeros_like(rs) for _ in range(world)]
+            dist.all_gather(allr, rs)
+            recv = [float(x.item()) for x in allr]
+        else:
+            recv = [float(nS)]
+        P = ls.get("num_partitions") or 1
+        rho_info["load_report"] = {
+            "recv_S_per_gpu_max": max(recv), "recv_S_per_gpu_mean": sum(recv) / len(recv),
+            "S_partition_max": ls.get("max_part_s"), "S_partition_mean": round(nS / P, 1),
+            "partitions": P, "build_probe_tasks": ls.get("num_tasks"),
+        }
     del R, S
     torch.cuda.empty_cache()
 
     # ---------------- scan (BASELINE config 3): 2^30 int32, [0, 26] = 10 % (types.hpp:134)
     scan_info = None
-    if not args.no_scan:
+    if not args.no_scan and args.workload == "c2":
         ns = 1 << 30
         col = torch.empty(ns, dtype=torch.int32, device=dev)
         sgxamd.gen_scan_dev(col, ns, 0, 0, "i32", stream)
@@ -228,11 +261,13 @@ def main():
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "M probed tuples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
-            "data": "synthetic: device-generated pk (shuffled 1..N) and fk (shuffled 1..N) relations, "
-                    "8-byte {key, payload} tuples",
-            "config": {"workload": f"RHO join |R|=|S|=2^{args.log2n} uniform per GPU (BASELINE config 2)",
-                       "global_R": N_glob, "global_S": N_glob, "parallelism": f"radix-shard{world}"},
+            "higher_is_better": True, "scaling": "weak" if args.workload == "c2" else "strong",
+            "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic: device-generated pk (shuffled 1..|R|) and "
+                    + ("Zipf(0.75) over 1..|R|" if args.workload == "c5" else "fk (shuffled copies of 1..|R|)")
+                    + " relations, 8-byte {key, payload} tuples",
+            "config": {"workload": workload, "global_R": gR, "global_S": gS,
+                       "parallelism": f"radix-shard{world}"},
             "roofline": roofline, "cpu_baseline": cpu, "rho": rho_info, "scan": scan_info,
         }
         print(json.dumps(line), flush=True)

@@ -56,6 +56,12 @@ int mi355_gen_pk_dev(struct row_t *out, uint64_t count, uint64_t first, uint64_t
                      uint64_t seed, void *stream);
 int mi355_gen_fk_dev(struct row_t *out, uint64_t count, uint64_t first, uint64_t maxid,
                      uint64_t seed, void *stream);
+/* Zipf(theta) keys over the alphabet 1..alphabet_size (genzipf.cpp:87-144 on the
+ * device: CDF lookup table, binary search of a uniform draw, random alphabet
+ * permutation); rows [first, first + count) of the same global relation for a
+ * given seed, so ranks can generate disjoint slices.  payload = row index. */
+int mi355_gen_zipf_dev(struct row_t *out, uint64_t count, uint64_t first, uint32_t alphabet_size, double theta,
+                       uint64_t seed, void *stream);
 /* Device scan columns: mode 0 = i % 256 (reference), mode 1 = keyed uniform random. */
 int mi355_gen_scan_u8_dev(uint8_t *out, size_t n, int mode, uint64_t seed, void *stream);
 int mi355_gen_scan_i32_dev(int32_t *out, size_t n, int mode, uint64_t seed, void *stream);

@@ -148,6 +148,7 @@ SIGNATURES = {
     "mi355_gen_scan_i32": (C.c_int, [_P, C.c_size_t]),
     "mi355_gen_pk_dev": (C.c_int, [_P, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, _P]),
     "mi355_gen_fk_dev": (C.c_int, [_P, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, _P]),
+    "mi355_gen_zipf_dev": (C.c_int, [_P, C.c_uint64, C.c_uint64, C.c_uint32, C.c_double, C.c_uint64, _P]),
     "mi355_gen_scan_u8_dev": (C.c_int, [_P, C.c_size_t, C.c_int, C.c_uint64, _P]),
     "mi355_gen_scan_i32_dev": (C.c_int, [_P, C.c_size_t, C.c_int, C.c_uint64, _P]),
 }
@@ -346,6 +347,12 @@ def gen_pk_dev(out, count: int, first: int, n: int, seed: int, stream: int | Non
 
 def gen_fk_dev(out, count: int, first: int, maxid: int, seed: int, stream: int | None = None) -> None:
     _check(lib.mi355_gen_fk_dev(ptr(out), count, first, maxid, seed, stream or None))
+
+
+def gen_zipf_dev(out, count: int, first: int, alphabet: int, theta: float, seed: int,
+                 stream: int | None = None) -> None:
+    """Rows [first, first+count) of a device Zipf(theta) relation over keys 1..alphabet."""
+    _check(lib.mi355_gen_zipf_dev(ptr(out), count, first, alphabet, theta, seed, stream or None))
 
 
 def gen_scan_dev(out, n: int, mode: int, seed: int, dtype: str = "i32", stream: int | None = None) -> None:
