@@ -57,6 +57,8 @@ def main():
     ap.add_argument("--workload", choices=["c2", "c4", "c5"], default="c2",
                     help="BASELINE config: c2 = pk/fk 2^28 per GPU (weak), c4 = |R| 2^27 x |S| 2^30 "
                          "global (strong), c5 = Zipf 0.75 |R| = |S| = 2^28 global (strong)")
+    ap.add_argument("--algorithm", choices=["RHO", "RHT"], default="RHO",
+                    help="build/probe: RHO bucket chaining (headline) or RHT histogram join")
     ap.add_argument("--no-scan", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -121,7 +123,7 @@ def main():
     torch.cuda.synchronize()
 
     def step():
-        return sharded_rho_join(R, S)
+        return sharded_rho_join(R, S, algorithm=args.algorithm)
 
     for _ in range(args.warmup):
         res = step()
@@ -266,7 +268,7 @@ def main():
             "data": "synthetic: device-generated pk (shuffled 1..|R|) and "
                     + ("Zipf(0.75) over 1..|R|" if args.workload == "c5" else "fk (shuffled copies of 1..|R|)")
                     + " relations, 8-byte {key, payload} tuples",
-            "config": {"workload": workload, "global_R": gR, "global_S": gS,
+            "config": {"workload": workload, "algorithm": args.algorithm, "global_R": gR, "global_S": gS,
                        "parallelism": f"radix-shard{world}"},
             "roofline": roofline, "cpu_baseline": cpu, "rho": rho_info, "scan": scan_info,
         }

@@ -33,6 +33,10 @@ extern "C" {
 #define MI355_ERR_OOM (-4)       /* device allocation failed */
 #define MI355_ERR_CAPACITY (-5)  /* output buffer too small; required size reported */
 
+/* Build/probe algorithm over the radix partitions (joins.cpp:42-43 table names). */
+#define MI355_ALGO_RHO 0 /* bucket_chaining_join, radix_join.cpp:359-458 */
+#define MI355_ALGO_RHT 1 /* histogram_join, radix_join.cpp:463-612 */
+
 /* Options of one join call (NULL = defaults). */
 typedef struct mi355_rho_opts {
     int radix_bits;      /* total radix bits; 0 = GPU policy (DESIGN.md "partitioning policy") */
@@ -40,7 +44,7 @@ typedef struct mi355_rho_opts {
     uint32_t key_shift;  /* low key bits already fixed by a shard exchange (multi-GPU); 0 otherwise */
     int materialize;     /* 1 = write every match to out (radix_join.cpp:437-446, MATERIALIZE) */
     int timing;          /* 1 = record per-kernel HIP events (mi355_timing_* below) */
-    int reserved;
+    int algorithm;       /* MI355_ALGO_RHO (bucket chaining) or MI355_ALGO_RHT (histogram join) */
     void *stream;        /* hipStream_t to launch on; NULL = the library's stream */
     struct output_triple_t *out; /* materialize: {key, R payload, S payload} per match, host or
                                     device memory; order unspecified (the reference's is per thread) */
@@ -87,6 +91,15 @@ const char *mi355_version(void);
  */
 int mi355_rho_join(const struct table_t *relR, const struct table_t *relS,
                    const struct joinconfig_t *config, struct result_t *out);
+
+/* Drop-in for RHT() (radix_join.cpp:1645-1648, radix_join.h): the same radix
+ * partitioning with the histogram build/probe of histogram_join.  Same result
+ * contract as mi355_rho_join. */
+int mi355_rht_join(const struct table_t *relR, const struct table_t *relS,
+                   const struct joinconfig_t *config, struct result_t *out);
+
+/* Statistics of the last join call made on this thread (any entry point). */
+int mi355_last_join_stats(mi355_rho_stats *out);
 
 /* Frees the chunked_table_t that mi355_rho_join / RHO() return in result->result
  * when config->MATERIALIZE = 1 (result_type 1, the reference's CHUNKED_TABLE form,

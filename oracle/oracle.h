@@ -58,6 +58,11 @@ int64_t oracle_rho_join(const struct row_t *R, uint64_t nR, const struct row_t *
 int64_t oracle_rho_join_mat(const struct row_t *R, uint64_t nR, const struct row_t *S, uint64_t nS, int nthreads,
                             int force_two_passes, struct output_triple_t *out, uint64_t cap);
 
+/* RHT (radix_join.cpp:1645-1648): the same partitioning with histogram_join
+ * (:463-612); out = NULL counts only, else materialises like oracle_rho_join_mat. */
+int64_t oracle_rht_join(const struct row_t *R, uint64_t nR, const struct row_t *S, uint64_t nS, int nthreads,
+                        int force_two_passes, struct output_triple_t *out, uint64_t cap);
+
 int64_t oracle_count_join_sort(const struct row_t *R, uint64_t nR, const struct row_t *S, uint64_t nS);
 
 /* Stable single-pass radix partition of `in` by bin = (key >> shift) & (2^bits-1)

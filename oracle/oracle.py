@@ -40,6 +40,7 @@ def _load() -> C.CDLL:
         "oracle_calc_num_passes": (C.c_uint32, [C.c_uint32]),
         "oracle_rho_join": (C.c_int64, [P, C.c_uint64, P, C.c_uint64, C.c_int, C.c_int, C.POINTER(Timing)]),
         "oracle_rho_join_mat": (C.c_int64, [P, C.c_uint64, P, C.c_uint64, C.c_int, C.c_int, P, C.c_uint64]),
+        "oracle_rht_join": (C.c_int64, [P, C.c_uint64, P, C.c_uint64, C.c_int, C.c_int, P, C.c_uint64]),
         "oracle_count_join_sort": (C.c_int64, [P, C.c_uint64, P, C.c_uint64]),
         "oracle_radix_partition": (None, [P, C.c_uint64, C.c_int, C.c_uint32, C.c_uint32, P, U64P]),
         "oracle_scan_count_u8": (C.c_uint64, [C.c_uint8, C.c_uint8, P, C.c_size_t]),
@@ -81,6 +82,19 @@ def rho_join_triples(R, S, nthreads: int = 1, force_two_passes: bool = False):
     m = lib.oracle_rho_join(_p(R), len(R), _p(S), len(S), nthreads, 1 if force_two_passes else 0, None)
     out = np.zeros((max(m, 1), 3), dtype=np.uint32)
     got = lib.oracle_rho_join_mat(_p(R), len(R), _p(S), len(S), nthreads, 1 if force_two_passes else 0, _p(out), m)
+    assert got == m
+    return out[:m]
+
+
+def rht_join(R, S, nthreads: int = 1, force_two_passes: bool = False) -> int:
+    """RHT (histogram_join) match count."""
+    return int(lib.oracle_rht_join(_p(R), len(R), _p(S), len(S), nthreads, 1 if force_two_passes else 0, None, 0))
+
+
+def rht_join_triples(R, S, nthreads: int = 1, force_two_passes: bool = False):
+    m = rht_join(R, S, nthreads, force_two_passes)
+    out = np.zeros((max(m, 1), 3), dtype=np.uint32)
+    got = lib.oracle_rht_join(_p(R), len(R), _p(S), len(S), nthreads, 1 if force_two_passes else 0, _p(out), m)
     assert got == m
     return out[:m]
 

@@ -112,6 +112,44 @@ static int64_t bucket_chaining_join(const struct row_t *R, uint64_t numR, const 
     return matches;
 }
 
+/* histogram_join (:463-612), RHT's build/probe: Nhist = get_hist_size(numR)
+ * (:462-467), histogram + prefix sum, R re-ordered by bucket into tmp, probe
+ * scans the S key's bucket.  The non-UNROLL path is restated (the UNROLL tail at
+ * :556-560 drops the "+ 1" of the bucket index; the plain loops do not). */
+static int64_t histogram_join(const struct row_t *R, uint64_t numR, const struct row_t *S, uint64_t numS,
+                              uint32_t num_radix_bits, out_buf *out) {
+    uint32_t N = (uint32_t)numR;
+    N--; N |= N >> 1; N |= N >> 2; N |= N >> 4; N |= N >> 8; N |= N >> 16; N++;
+    uint32_t Nhist = N >> 2;
+    if (Nhist < 4) Nhist = 4;
+    const uint32_t MASK = (Nhist - 1) << num_radix_bits;
+    int32_t *hist = (int32_t *)calloc(Nhist + 2, sizeof(int32_t));
+    struct row_t *tmp = (struct row_t *)malloc(sizeof(struct row_t) * (numR ? numR : 1));
+    for (uint32_t i = 0; i < numR; i++) ++hist[HASH_BIT_MODULO(R[i].key, MASK, num_radix_bits) + 2];
+    for (uint32_t i = 2, sum = 0; i < Nhist + 2; i++) {
+        sum += (uint32_t)hist[i];
+        hist[i] = (int32_t)sum;
+    }
+    for (uint32_t i = 0; i < numR; i++) {
+        const uint32_t idx = HASH_BIT_MODULO(R[i].key, MASK, num_radix_bits) + 1;
+        tmp[hist[idx]] = R[i];
+        hist[idx]++;
+    }
+    int64_t match = 0;
+    for (uint32_t i = 0; i < numS; ++i) {
+        const uint32_t idx = HASH_BIT_MODULO(S[i].key, MASK, num_radix_bits);
+        for (int j = hist[idx], end = hist[idx + 1]; j < end; j++) {
+            if (S[i].key == tmp[j].key) {
+                ++match;
+                if (out) out_push(out, S[i].key, tmp[j].payload, S[i].payload);
+            }
+        }
+    }
+    free(hist);
+    free(tmp);
+    return match;
+}
+
 static void partition_hist(const struct row_t *rel, uint32_t size, uint32_t *hist, uint32_t MASK, int32_t R) {
     for (uint32_t i = 0; i < size; ++i) ++hist[(rel[i].key & MASK) >> R];
 }
@@ -200,6 +238,7 @@ typedef struct shared_t {
     uint64_t totalR, totalS;
     uint32_t bits, passes;
     int materialize;
+    int rht; /* 1 = histogram_join (RHT), 0 = bucket_chaining_join (RHO) */
     task_array part_queue, join_queue;
 } shared_t;
 
@@ -289,8 +328,8 @@ static void *prj_thread(void *param) {
     int64_t results = 0;
     task_t task;
     while (ta_pop(join_queue, &task))
-        results += bucket_chaining_join(task.relR, task.nR, task.relS, task.nS, bits,
-                                        sh->materialize ? &a->out : NULL);
+        results += (sh->rht ? histogram_join : bucket_chaining_join)(task.relR, task.nR, task.relS, task.nS, bits,
+                                                                     sh->materialize ? &a->out : NULL);
     double t3 = now_s();
     a->result = results;
     a->t_total = t3 - t0;
@@ -306,21 +345,27 @@ static void *prj_thread(void *param) {
  * triples are concatenated in thread order into out (up to cap of them). */
 static int64_t rho_join_impl(const struct row_t *R, uint64_t nR, const struct row_t *S, uint64_t nS, int nthreads,
                              int force_two_passes, oracle_rho_timing *timing, struct output_triple_t *out,
-                             uint64_t cap, int materialize);
+                             uint64_t cap, int materialize, int rht);
 
 int64_t oracle_rho_join(const struct row_t *R, uint64_t nR, const struct row_t *S, uint64_t nS, int nthreads,
                         int force_two_passes, oracle_rho_timing *timing) {
-    return rho_join_impl(R, nR, S, nS, nthreads, force_two_passes, timing, NULL, 0, 0);
+    return rho_join_impl(R, nR, S, nS, nthreads, force_two_passes, timing, NULL, 0, 0, 0);
+}
+
+/* RHT (:1645-1648): join_init_run with histogram_join; out may be NULL (count only). */
+int64_t oracle_rht_join(const struct row_t *R, uint64_t nR, const struct row_t *S, uint64_t nS, int nthreads,
+                        int force_two_passes, struct output_triple_t *out, uint64_t cap) {
+    return rho_join_impl(R, nR, S, nS, nthreads, force_two_passes, NULL, out, cap, out != NULL, 1);
 }
 
 int64_t oracle_rho_join_mat(const struct row_t *R, uint64_t nR, const struct row_t *S, uint64_t nS, int nthreads,
                             int force_two_passes, struct output_triple_t *out, uint64_t cap) {
-    return rho_join_impl(R, nR, S, nS, nthreads, force_two_passes, NULL, out, cap, 1);
+    return rho_join_impl(R, nR, S, nS, nthreads, force_two_passes, NULL, out, cap, 1, 0);
 }
 
 static int64_t rho_join_impl(const struct row_t *R, uint64_t nR, const struct row_t *S, uint64_t nS, int nthreads,
                              int force_two_passes, oracle_rho_timing *timing, struct output_triple_t *out,
-                             uint64_t cap, int materialize) {
+                             uint64_t cap, int materialize, int rht) {
     if (nthreads < 1) nthreads = 1;
     shared_t sh;
     memset(&sh, 0, sizeof(sh));
@@ -329,6 +374,7 @@ static int64_t rho_join_impl(const struct row_t *R, uint64_t nR, const struct ro
     sh.totalR = nR;
     sh.totalS = nS;
     sh.materialize = materialize;
+    sh.rht = rht;
     const uint64_t fan1 = fanout_pass_1(sh.bits, sh.passes);
     const uint64_t rel_padding = (uint64_t)padding_tuples(sh.bits, sh.passes) * fan1 * sizeof(struct row_t);
     const uint64_t rsz = nR * sizeof(struct row_t) + rel_padding;

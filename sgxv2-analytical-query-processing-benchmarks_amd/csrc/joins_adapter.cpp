@@ -1,6 +1,6 @@
 // C++-linkage drop-ins RHO() and run_join() (declared in sgxamd/joins.hpp).
 //
-// RHO: radix_join.cpp:1640-1643 -> mi355_rho_join, plus the reference's
+// RHO / RHT: radix_join.cpp:1640-1648 -> mi355_rho_join / mi355_rht_join, plus the reference's
 //      print_timing log lines (radix_join.cpp:252-293) so that
 //      SGXv2Scripts/scripts/helpers/runner.py:14-55 parses our output unchanged.
 // run_join: joins.cpp:55-78 (strcmp lookup in an algorithm table, memcpy of the
@@ -37,34 +37,29 @@ uint64_t cpms() {  // CYCLES_PER_MICROSECOND of the reference build (J/CMakeList
     return e ? std::strtoull(e, nullptr, 10) : 2900ull;
 }
 
-const algorithm_t mi355_algorithms[] = {
+const algorithm_t mi355_algorithms[] = {  // joins.cpp:33-53, the radix joins this library replaces
     {"RHO", RHO},
+    {"RHT", RHT},
     {"", nullptr},
 };
 
-}  // namespace
-
-result_t *RHO(const table_t *relR, const table_t *relS, const joinconfig_t *config) {
-    mi355_rho_stats st{};
-    LOG_INFO("Running RHO on MI355X (%s)", mi355_version());
-    const int rc = mi355_rho_join_ex(relR->tuples, relR->num_tuples, relS->tuples, relS->num_tuples, nullptr, &st);
+result_t *radix_dropin(const char *name, const table_t *relR, const table_t *relS, const joinconfig_t *config,
+                       int (*join)(const table_t *, const table_t *, const joinconfig_t *, result_t *)) {
+    LOG_INFO("Running %s on MI355X (%s)", name, mi355_version());
+    auto *res = static_cast<result_t *>(std::malloc(sizeof(result_t)));
+    const int rc = join(relR, relS, config, res);
     if (rc != MI355_OK) {
-        LOG_ERROR("RHO failed (%d): %s", rc, mi355_last_error());
+        LOG_ERROR("%s failed (%d): %s", name, rc, mi355_last_error());
         std::exit(EXIT_FAILURE);
     }
-    auto *res = static_cast<result_t *>(std::malloc(sizeof(result_t)));
+    mi355_rho_stats st{};
+    mi355_last_join_stats(&st);
     const uint64_t num = relR->num_tuples + relS->num_tuples;
     const double us = st.ms_total * 1000.0;
-    res->totalresults = static_cast<int64_t>(st.matches);
-    res->nthreads = config ? config->NTHREADS : 1;
-    res->throughput = us > 0 ? num / us : 0.0;
-    res->materialized = 0;
-    res->result = nullptr;
-    res->result_type = 0;
 
     const uint64_t C = cpms();
     auto cyc = [&](double ms) { return static_cast<unsigned long>(ms * 1000.0 * C); };
-    LOG_INFO("Running RHO with %u passes and %u radix bits", st.passes, st.radix_bits);
+    LOG_INFO("Running %s with %u passes and %u radix bits", name, st.passes, st.radix_bits);
     LOG_INFO("Total input tuples : %lu", (unsigned long)num);
     LOG_INFO("Result tuples : %ld", (long)st.matches);
     LOG_INFO("Total Join Time (cycles)    : %lu", cyc(st.ms_total));
@@ -76,6 +71,16 @@ result_t *RHO(const table_t *relR, const table_t *relS, const joinconfig_t *conf
     LOG_INFO("Throughput (M rec/sec) : %.2lf", res->throughput);
     LOG_INFO("Host->device staging (us) : %lu ", (unsigned long)(st.ms_h2d * 1000.0));
     return res;
+}
+
+}  // namespace
+
+result_t *RHO(const table_t *relR, const table_t *relS, const joinconfig_t *config) {
+    return radix_dropin("RHO", relR, relS, config, mi355_rho_join);
+}
+
+result_t *RHT(const table_t *relR, const table_t *relS, const joinconfig_t *config) {
+    return radix_dropin("RHT", relR, relS, config, mi355_rht_join);
 }
 
 void run_join(result_t *res, const table_t *relR, const table_t *relS, const char *algorithm_name,

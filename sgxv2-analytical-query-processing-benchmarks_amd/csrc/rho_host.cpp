@@ -159,6 +159,7 @@ int join_device(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const
                 const mi355_rho_opts *opts, mi355_rho_stats *st, output_triple_t *out, uint64_t out_cap) {
     const uint32_t key_shift = opts ? opts->key_shift : 0;
     const bool materialize = opts && opts->materialize;
+    const int algo = (opts && opts->algorithm == MI355_ALGO_RHT) ? kAlgoHistogram : kAlgoChaining;
     const Policy pol = choose_policy(nR, opts);
     if (key_shift + pol.bits > 31) {
         set_last_error("key_shift + radix bits must stay below 32");
@@ -216,13 +217,13 @@ int join_device(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const
     if (!materialize) {
         tm.mark("join_build_probe");
         RHO_HIP(launch_join(fR, fS, psR, pcR, psS, pcS, P, over, n_over, hash_shift, pol.rcap, join_grid, kJoinCount,
-                            counts, nullptr, nullptr, s));
+                            algo, counts, nullptr, nullptr, s));
         tm.mark("join_reduce");
         RHO_HIP(launch_reduce(counts, join_grid, result, s));
     } else {
         tm.mark("join_build_probe");
         RHO_HIP(launch_join(fR, fS, psR, pcR, psS, pcS, P, over, n_over, hash_shift, pol.rcap, join_grid,
-                            kJoinTaskCount, counts, nullptr, nullptr, s));
+                            kJoinTaskCount, algo, counts, nullptr, nullptr, s));
         tm.mark("join_offsets");
         RHO_HIP(launch_excl_scan(counts, n_over, P, task_off, result, s));
         RHO_HIP(hipMemcpyAsync(ctx->host_result, result, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
@@ -237,7 +238,7 @@ int join_device(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const
         }
         tm.mark("join_materialize");
         RHO_HIP(launch_join(fR, fS, psR, pcR, psS, pcS, P, over, n_over, hash_shift, pol.rcap, join_grid, kJoinWrite,
-                            counts, task_off, out, s));
+                            algo, counts, task_off, out, s));
     }
     tm.end_call();
     RHO_HIP(launch_max(pcR, P, result + 1, s));
@@ -296,7 +297,17 @@ int shard_partition_device(Context *ctx, hipStream_t s, const row_t *in, uint64_
 
 using namespace sgxamd;
 
+namespace {
+thread_local mi355_rho_stats g_last_stats{};
+}
+
 extern "C" {
+
+int mi355_last_join_stats(mi355_rho_stats *out) {
+    if (!out) return MI355_ERR_INVALID;
+    *out = g_last_stats;
+    return MI355_OK;
+}
 
 int mi355_rho_join_ex(const row_t *R, uint64_t nR, const row_t *S, uint64_t nS, const mi355_rho_opts *opts,
                       mi355_rho_stats *stats) {
@@ -317,7 +328,14 @@ int mi355_rho_join_ex(const row_t *R, uint64_t nR, const row_t *S, uint64_t nS, 
     mi355_rho_stats local{};
     mi355_rho_stats *st = stats ? stats : &local;
     std::memset(st, 0, sizeof(*st));
-    if (nR == 0 || nS == 0) return MI355_OK;
+    if (nR == 0 || nS == 0) {
+        g_last_stats = *st;
+        return MI355_OK;
+    }
+    struct Remember {  // publish the stats of this call on every return path
+        mi355_rho_stats *st;
+        ~Remember() { g_last_stats = *st; }
+    } remember{st};
 
     const row_t *dR = R, *dS = S;
     const auto t0 = std::chrono::steady_clock::now();
@@ -388,8 +406,10 @@ void mi355_free_chunked_table(chunked_table_t *table) {
     std::free(table);
 }
 
-// Drop-in for RHO() (radix_join.cpp:1640-1643).
-int mi355_rho_join(const table_t *relR, const table_t *relS, const joinconfig_t *config, result_t *out) {
+// Drop-ins for RHO() / RHT() (radix_join.cpp:1640-1648): join_init_run with
+// bucket_chaining_join or histogram_join.
+static int table_join(const table_t *relR, const table_t *relS, const joinconfig_t *config, result_t *out,
+                      int algorithm) {
     if (!relR || !relS || !out) {
         set_last_error("null argument");
         return MI355_ERR_INVALID;
@@ -398,11 +418,12 @@ int mi355_rho_join(const table_t *relR, const table_t *relS, const joinconfig_t 
     mi355_rho_stats st{};
     int rc;
     output_triple_t *host = nullptr;
+    mi355_rho_opts o{};
+    o.algorithm = algorithm;
     if (!materialize) {
-        rc = mi355_rho_join_ex(relR->tuples, relR->num_tuples, relS->tuples, relS->num_tuples, nullptr, &st);
+        rc = mi355_rho_join_ex(relR->tuples, relR->num_tuples, relS->tuples, relS->num_tuples, &o, &st);
     } else {
         // count first (capacity 0 -> MI355_ERR_CAPACITY with the size), then materialise
-        mi355_rho_opts o{};
         o.materialize = 1;
         rc = mi355_rho_join_ex(relR->tuples, relR->num_tuples, relS->tuples, relS->num_tuples, &o, &st);
         if (rc == MI355_ERR_CAPACITY || (rc == MI355_OK && st.matches > 0)) {
@@ -439,6 +460,14 @@ int mi355_rho_join(const table_t *relR, const table_t *relS, const joinconfig_t 
         out->result_type = 1;
     }
     return MI355_OK;
+}
+
+int mi355_rho_join(const table_t *relR, const table_t *relS, const joinconfig_t *config, result_t *out) {
+    return table_join(relR, relS, config, out, MI355_ALGO_RHO);
+}
+
+int mi355_rht_join(const table_t *relR, const table_t *relS, const joinconfig_t *config, result_t *out) {
+    return table_join(relR, relS, config, out, MI355_ALGO_RHT);
 }
 
 int mi355_rho_shard_partition(const row_t *in, uint64_t n, uint32_t key_shift, uint32_t dest_bits, row_t *out,

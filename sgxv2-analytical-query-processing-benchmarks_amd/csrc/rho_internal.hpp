@@ -63,12 +63,14 @@ hipError_t launch_scatter(const row_t *in, row_t *out, const SegMap &m, uint32_t
 // mode 2: write every match to out[task_off[t] + ...] as output_triple_t.
 constexpr uint64_t kSChunk = 8192;
 enum JoinMode : int { kJoinCount = 0, kJoinTaskCount = 1, kJoinWrite = 2 };
+// Build/probe algorithm of one task: RHO's bucket chaining or RHT's histogram join.
+enum JoinAlgo : int { kAlgoChaining = 0, kAlgoHistogram = 1 };
 hipError_t launch_make_tasks(const uint64_t *r_count, const uint64_t *s_count, uint64_t P, uint64_t *over,
                              uint32_t over_cap, uint32_t *n_over, hipStream_t s);
 hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, const uint64_t *r_count,
                        const uint64_t *s_start, const uint64_t *s_count, uint64_t P, const uint64_t *over,
                        const uint32_t *n_over, uint32_t hash_shift, uint32_t rcap, uint32_t grid, int mode,
-                       uint64_t *counts, const uint64_t *task_off, output_triple_t *out, hipStream_t s);
+                       int algo, uint64_t *counts, const uint64_t *task_off, output_triple_t *out, hipStream_t s);
 // One-block exclusive scan of n_base + *n_extra values; *total = their sum.
 hipError_t launch_excl_scan(const uint64_t *in, const uint32_t *n_extra, uint64_t n_base, uint64_t *out,
                             uint64_t *total, hipStream_t s);

@@ -669,27 +669,220 @@ __global__ __launch_bounds__(kBlock) void k_join(const uint64_t *__restrict__ R,
     }
 }
 
+// ------------------------------------------------------- histogram join (RHT) ---
+// histogram_join (radix_join.cpp:463-612), the build/probe of RHT (:1645-1648), per
+// task in LDS.  For an R chunk of nrc tuples: Nhist = max(nextpow2(nrc) / 4, 4)
+// buckets (get_hist_size :462-467), bucket = HASH_BIT_MODULO(key, (Nhist-1) << bits,
+// bits); an LDS histogram (one atomic per tuple, which is also the tuple's rank in
+// its bucket), an exclusive scan into bucket offsets (:520-524), and the R keys
+// re-ordered bucket-contiguous in LDS (:527-561).  The probe compares each S key
+// with its bucket's contiguous run [off[b], off[b+1]) (:574-600).  The reference's
+// unrolled re-order tail drops the "+ 1" of the bucket index (:556-560); that slip
+// is not restated here, every R tuple lands in its own bucket.
+template <int RCAP, int MODE>
+struct HistJoinLds {
+    static constexpr int NB = RCAP / 4;  // max buckets of one chunk
+    uint32_t off[NB + 1];
+    uint32_t keys[RCAP];
+    uint32_t rpay[MODE == kJoinWrite ? RCAP : 1];
+    uint32_t cursor;
+    uint64_t red[kWaves];
+};
+
+template <int RCAP, int MODE>
+__global__ __launch_bounds__(kBlock) void k_join_hist(const uint64_t *__restrict__ R, const uint64_t *__restrict__ S,
+                                                      const uint64_t *__restrict__ r_start,
+                                                      const uint64_t *__restrict__ r_count,
+                                                      const uint64_t *__restrict__ s_start,
+                                                      const uint64_t *__restrict__ s_count, uint64_t P,
+                                                      const uint64_t *__restrict__ over,
+                                                      const uint32_t *__restrict__ n_over, uint32_t hash_shift,
+                                                      uint64_t *__restrict__ counts,
+                                                      const uint64_t *__restrict__ task_off,
+                                                      output_triple_t *__restrict__ out) {
+    constexpr int U = RCAP / kBlock;
+    constexpr int NB = HistJoinLds<RCAP, MODE>::NB;
+    __shared__ HistJoinLds<RCAP, MODE> L;
+    __shared__ uint64_t scan_scratch[kWaves + 1];
+    const uint32_t tid = threadIdx.x, lane = __lane_id();
+    const uint64_t T = P + *n_over;
+    uint64_t matches = 0;
+    for (uint64_t t = blockIdx.x; t < T; t += gridDim.x) {
+        uint64_t p, chunk;
+        decode_task(t, P, over, p, chunk);
+        const uint64_t nR = r_count[p], nSp = s_count[p];
+        const uint64_t s_lo = chunk * kSChunk;
+        const uint64_t nS = (nR == 0 || s_lo >= nSp) ? 0 : min<uint64_t>(nSp - s_lo, kSChunk);
+        uint64_t tmatch = 0;
+        if constexpr (MODE == kJoinWrite) {
+            if (tid == 0) L.cursor = 0;
+        }
+        if (nS > 0) {
+            const uint64_t *rp = R + r_start[p];
+            const uint64_t *sp = S + s_start[p] + s_lo;
+            for (uint64_t rc = 0; rc < nR; rc += RCAP) {
+                const uint32_t nrc = (uint32_t)((nR - rc) < RCAP ? (nR - rc) : RCAP);
+                uint32_t N = 1;
+                while (N < nrc) N <<= 1;
+                uint32_t nh = N >> 2;
+                if (nh < 4) nh = 4;  // get_hist_size
+                const uint32_t hmask = nh - 1;
+                uint64_t kr[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t i = tid + u * kBlock;
+                    kr[u] = i < nrc ? ld_nt(rp + rc + i) : 0ull;
+                }
+                for (uint32_t i = tid; i <= nh; i += kBlock) L.off[i] = 0;
+                __syncthreads();
+                uint32_t slot[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {  // HISTOGRAM CREATION (:489-517)
+                    const uint32_t i = tid + u * kBlock;
+                    if (i < nrc) slot[u] = atomicAdd(&L.off[((uint32_t)kr[u] >> hash_shift) & hmask], 1u);
+                }
+                __syncthreads();
+                {  // prefix sum on histogram (:520-524): thread tid owns buckets [tid*E, tid*E + E)
+                    const uint32_t E = (nh + kBlock - 1) / kBlock;
+                    uint32_t loc[NB / kBlock > 0 ? NB / kBlock : 1];
+                    uint32_t sum = 0;
+                    for (uint32_t j = 0; j < E; ++j) {
+                        const uint32_t b = tid * E + j;
+                        const uint32_t c = b < nh ? L.off[b] : 0u;
+                        loc[j] = sum;
+                        sum += c;
+                    }
+                    uint64_t tot;
+                    const uint32_t base = (uint32_t)block_excl_scan_u64(sum, scan_scratch, &tot);
+                    for (uint32_t j = 0; j < E; ++j) {
+                        const uint32_t b = tid * E + j;
+                        if (b < nh) L.off[b] = base + loc[j];
+                    }
+                    if (tid == 0) L.off[nh] = (uint32_t)tot;
+                }
+                __syncthreads();
+#pragma unroll
+                for (int u = 0; u < U; ++u) {  // BUILD PHASE: re-order (:527-561)
+                    const uint32_t i = tid + u * kBlock;
+                    if (i < nrc) {
+                        const uint32_t pos = L.off[((uint32_t)kr[u] >> hash_shift) & hmask] + slot[u];
+                        L.keys[pos] = (uint32_t)kr[u];
+                        if constexpr (MODE == kJoinWrite) L.rpay[pos] = (uint32_t)(kr[u] >> 32);
+                    }
+                }
+                __syncthreads();
+                for (uint64_t s0 = 0; s0 < nS; s0 += RCAP) {  // PROBE PHASE (:570-600)
+                    uint32_t ks[U], j[U], end[U];
+                    uint32_t sv[MODE == kJoinWrite ? U : 1];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const uint64_t i = s0 + tid + u * kBlock;
+                        const uint64_t x = i < nS ? ld_nt(sp + i) : 0ull;
+                        ks[u] = (uint32_t)x;
+                        if constexpr (MODE == kJoinWrite) sv[u] = (uint32_t)(x >> 32);
+                    }
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const uint64_t i = s0 + tid + u * kBlock;
+                        const uint32_t b = (ks[u] >> hash_shift) & hmask;
+                        j[u] = i < nS ? L.off[b] : 0u;
+                        end[u] = i < nS ? L.off[b + 1] : 0u;
+                    }
+                    bool more = true;
+                    while (more) {
+                        more = false;
+#pragma unroll
+                        for (int u = 0; u < U; ++u) {
+                            if constexpr (MODE == kJoinWrite) {
+                                const bool live = j[u] < end[u];
+                                const bool m = live && L.keys[j[u]] == ks[u];
+                                const uint64_t bal = __ballot(m);
+                                if (bal) {
+                                    const int leader = __ffsll((unsigned long long)__ballot(1)) - 1;
+                                    uint32_t base = 0;
+                                    if ((int)lane == leader) base = atomicAdd(&L.cursor, (uint32_t)__popcll(bal));
+                                    base = __shfl(base, leader, kWave);
+                                    if (m) {
+                                        const uint64_t o = task_off[t] + base + __popcll(bal & lanemask_lt());
+                                        uint32_t *w = reinterpret_cast<uint32_t *>(out + o);
+                                        w[0] = ks[u];
+                                        w[1] = L.rpay[j[u]];
+                                        w[2] = sv[u];
+                                    }
+                                }
+                                if (live) {
+                                    ++j[u];
+                                    more |= j[u] < end[u];
+                                }
+                            } else if (j[u] < end[u]) {
+                                tmatch += (L.keys[j[u]] == ks[u]);
+                                ++j[u];
+                                more |= j[u] < end[u];
+                            }
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        if constexpr (MODE == kJoinTaskCount) {
+            const uint64_t wsum = wave_sum_u64(tmatch);
+            if (lane == 0) L.red[tid / kWave] = wsum;
+            __syncthreads();
+            if (tid == 0) {
+                uint64_t acc = 0;
+                for (int w = 0; w < kWaves; ++w) acc += L.red[w];
+                counts[t] = acc;
+            }
+            __syncthreads();
+        } else if constexpr (MODE == kJoinWrite) {
+            __syncthreads();
+        }
+        matches += tmatch;
+    }
+    if constexpr (MODE == kJoinCount) {
+        matches = wave_sum_u64(matches);
+        if (lane == 0) L.red[tid / kWave] = matches;
+        __syncthreads();
+        if (tid == 0) {
+            uint64_t acc = 0;
+            for (int w = 0; w < kWaves; ++w) acc += L.red[w];
+            counts[blockIdx.x] = acc;
+        }
+    }
+}
+
 hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, const uint64_t *r_count,
                        const uint64_t *s_start, const uint64_t *s_count, uint64_t P, const uint64_t *over,
                        const uint32_t *n_over, uint32_t hash_shift, uint32_t rcap, uint32_t grid, int mode,
-                       uint64_t *counts, const uint64_t *task_off, output_triple_t *out, hipStream_t s) {
+                       int algo, uint64_t *counts, const uint64_t *task_off, output_triple_t *out, hipStream_t s) {
     const uint64_t *R64 = reinterpret_cast<const uint64_t *>(R);
     const uint64_t *S64 = reinterpret_cast<const uint64_t *>(S);
-#define JOIN_LAUNCH(RC, MD)                                                                                 \
-    hipLaunchKernelGGL((k_join<RC, MD>), dim3(grid), dim3(kBlock), 0, s, R64, S64, r_start, r_count, s_start, \
+#define JOIN_LAUNCH(K, RC, MD)                                                                             \
+    hipLaunchKernelGGL((K<RC, MD>), dim3(grid), dim3(kBlock), 0, s, R64, S64, r_start, r_count, s_start,    \
                        s_count, P, over, n_over, hash_shift, counts, task_off, out)
-#define JOIN_MODES(RC)                                        \
-    case RC:                                                  \
-        if (mode == kJoinCount) JOIN_LAUNCH(RC, kJoinCount);  \
-        else if (mode == kJoinTaskCount) JOIN_LAUNCH(RC, kJoinTaskCount); \
-        else JOIN_LAUNCH(RC, kJoinWrite);                     \
+#define JOIN_MODES(K, RC)                                                    \
+    case RC:                                                                 \
+        if (mode == kJoinCount) JOIN_LAUNCH(K, RC, kJoinCount);              \
+        else if (mode == kJoinTaskCount) JOIN_LAUNCH(K, RC, kJoinTaskCount); \
+        else JOIN_LAUNCH(K, RC, kJoinWrite);                                 \
         break;
-    switch (rcap) {
-        JOIN_MODES(2048)
-        JOIN_MODES(4096)
-        JOIN_MODES(8192)
-        default:
-            return hipErrorInvalidValue;
+    if (algo == kAlgoHistogram) {
+        switch (rcap) {
+            JOIN_MODES(k_join_hist, 2048)
+            JOIN_MODES(k_join_hist, 4096)
+            JOIN_MODES(k_join_hist, 8192)
+            default:
+                return hipErrorInvalidValue;
+        }
+    } else {
+        switch (rcap) {
+            JOIN_MODES(k_join, 2048)
+            JOIN_MODES(k_join, 4096)
+            JOIN_MODES(k_join, 8192)
+            default:
+                return hipErrorInvalidValue;
+        }
     }
 #undef JOIN_MODES
 #undef JOIN_LAUNCH

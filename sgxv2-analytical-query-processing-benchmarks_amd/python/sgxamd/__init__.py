@@ -69,7 +69,7 @@ class rho_opts(C.Structure):
         ("key_shift", C.c_uint32),
         ("materialize", C.c_int),
         ("timing", C.c_int),
-        ("reserved", C.c_int),
+        ("algorithm", C.c_int),
         ("stream", C.c_void_p),
         ("out", C.c_void_p),
         ("out_capacity", C.c_uint64),
@@ -124,6 +124,8 @@ SIGNATURES = {
     "mi355_rho_join": (C.c_int, [C.POINTER(table_t), C.POINTER(table_t), C.POINTER(joinconfig_t), C.POINTER(result_t)]),
     "mi355_rho_join_ex": (C.c_int, [_P, C.c_uint64, _P, C.c_uint64, C.POINTER(rho_opts), C.POINTER(rho_stats)]),
     "mi355_free_chunked_table": (None, [_P]),
+    "mi355_rht_join": (C.c_int, [C.POINTER(table_t), C.POINTER(table_t), C.POINTER(joinconfig_t), C.POINTER(result_t)]),
+    "mi355_last_join_stats": (C.c_int, [C.POINTER(rho_stats)]),
     "mi355_rho_shard_partition": (C.c_int, [_P, C.c_uint64, C.c_uint32, C.c_uint32, _P, _U64P, _P]),
     "mi355_timing_enable": (None, [C.c_int]),
     "mi355_timing_get": (C.c_int, [C.POINTER(C.c_char_p), C.POINTER(C.c_double), C.c_int]),
@@ -216,15 +218,19 @@ class JoinResult:
     stats: dict
 
 
+ALGORITHMS = {"RHO": 0, "RHT": 1}  # MI355_ALGO_RHO / MI355_ALGO_RHT
+
+
 def rho_join(R, nR: int, S, nS: int, *, radix_bits: int = 0, passes: int = 0, key_shift: int = 0,
-             timing: bool = False, stream: int | None = None, out=None, out_capacity: int = 0) -> JoinResult:
+             timing: bool = False, stream: int | None = None, out=None, out_capacity: int = 0,
+             algorithm: str = "RHO") -> JoinResult:
     """RHO join of nR R-tuples and nS S-tuples (8-byte {key, payload}; host or device).
 
     With `out` (host or device buffer of out_capacity 12-byte triples) every match is
     materialised as {key, R payload, S payload}; a too-small buffer raises Mi355Error
     with code MI355_ERR_CAPACITY (-5)."""
-    o = rho_opts(radix_bits, passes, key_shift, 1 if out is not None else 0, 1 if timing else 0, 0, stream or None,
-                 ptr(out) if out is not None else None, out_capacity)
+    o = rho_opts(radix_bits, passes, key_shift, 1 if out is not None else 0, 1 if timing else 0,
+                 ALGORITHMS[algorithm], stream or None, ptr(out) if out is not None else None, out_capacity)
     st = rho_stats()
     rc = lib.mi355_rho_join_ex(ptr(R), nR, ptr(S), nS, C.byref(o), C.byref(st))
     if rc == -5:
@@ -233,7 +239,8 @@ def rho_join(R, nR: int, S, nS: int, *, radix_bits: int = 0, passes: int = 0, ke
     return JoinResult(int(st.matches), st.as_dict())
 
 
-def rho_join_tables(R, nR: int, S, nS: int, nthreads: int = 1, materialize: bool = False) -> result_t:
+def rho_join_tables(R, nR: int, S, nS: int, nthreads: int = 1, materialize: bool = False,
+                    algorithm: str = "RHO") -> result_t:
     """The drop-in mi355_rho_join(table_t*, table_t*, joinconfig_t*, result_t*).
 
     With materialize, result.result is a chunked_table_t* (result_type 1): read it
@@ -244,7 +251,8 @@ def rho_join_tables(R, nR: int, S, nS: int, nthreads: int = 1, materialize: bool
     cfg.NTHREADS = nthreads
     cfg.MATERIALIZE = 1 if materialize else 0
     out = result_t()
-    _check(lib.mi355_rho_join(C.byref(tR), C.byref(tS), C.byref(cfg), C.byref(out)))
+    fn = lib.mi355_rht_join if algorithm == "RHT" else lib.mi355_rho_join
+    _check(fn(C.byref(tR), C.byref(tS), C.byref(cfg), C.byref(out)))
     return out
 
 

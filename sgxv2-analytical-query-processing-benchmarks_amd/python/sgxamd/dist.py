@@ -53,9 +53,10 @@ def _default_partition(t: torch.Tensor, n: int, dest_bits: int):
     return out, counts
 
 
-def _default_local_join(R: torch.Tensor, nR: int, S: torch.Tensor, nS: int, key_shift: int):
+def _default_local_join(R: torch.Tensor, nR: int, S: torch.Tensor, nS: int, key_shift: int,
+                        algorithm: str = "RHO"):
     stream = torch.cuda.current_stream().cuda_stream if R.is_cuda else None
-    res = rho_join(R, nR, S, nS, key_shift=key_shift, stream=stream)
+    res = rho_join(R, nR, S, nS, key_shift=key_shift, stream=stream, algorithm=algorithm)
     return res.matches, res.stats
 
 
@@ -73,14 +74,16 @@ def _exchange(t: torch.Tensor, send_counts: list[int], group) -> tuple[torch.Ten
 
 
 def sharded_rho_join(R: torch.Tensor, S: torch.Tensor, *, group=None, partition_fn=None,
-                     local_join_fn=None) -> ShardedJoinResult:
+                     local_join_fn=None, algorithm: str = "RHO") -> ShardedJoinResult:
     """Global RHO join of the row slices R and S (int64 tensors, one tuple each).
 
     Collective: every rank of `group` must call it.  Returns the global match count
     on every rank.
     """
     partition_fn = partition_fn or _default_partition
-    local_join_fn = local_join_fn or _default_local_join
+    if local_join_fn is None:
+        def local_join_fn(R_, nR_, S_, nS_, shift_):
+            return _default_local_join(R_, nR_, S_, nS_, shift_, algorithm)
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     dest_bits = _log2_exact(world)
     ms = {}

@@ -148,3 +148,20 @@ def test_oracle_materialize_vs_pair_enumeration():
         key = lambda t: t[np.lexsort((t[:, 2], t[:, 1], t[:, 0]))]
         assert got.shape == exp.shape
         assert np.array_equal(key(got), key(exp))
+
+
+def test_oracle_rht_equals_rho_and_sort_counter():
+    """RHT (histogram_join) and RHO (bucket chaining) count the same equi-join."""
+    import oracle
+
+    rng = np.random.default_rng(9)
+    dt = np.dtype([("key", "<u4"), ("payload", "<u4")])
+    for nR, nS, kmax in [(5000, 9000, 700), (1 << 15, 1 << 15, 1 << 31), (3, 7, 2)]:
+        R = np.zeros(nR, dt)
+        S = np.zeros(nS, dt)
+        R["key"] = rng.integers(0, kmax, nR)
+        S["key"] = rng.integers(0, kmax, nS)
+        exp = oracle.count_join_sort(R, S)
+        for threads, two in [(1, False), (4, False), (3, True)]:
+            assert oracle.rht_join(R, S, threads, two) == exp
+            assert oracle.rho_join(R, S, threads, two)[0] == exp

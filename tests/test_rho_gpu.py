@@ -258,3 +258,43 @@ def test_full_size_materialize_property(sgx, gpu):
     assert torch.equal(torch.sort(t[:, 2]).values, torch.arange(n, device=gpu))
     del R, S, out, t, rk, sk
     torch.cuda.empty_cache()
+
+
+# ------------------------------------------------------------------ RHT
+@pytest.mark.parametrize("case", ["pk_fk", "sel10", "dups", "hot_key"])
+def test_rht_matches_oracle(sgx, orc, gpu, case):
+    """RHT (histogram_join, radix_join.cpp:463-612): counts and triples equal the oracle's RHT."""
+    rng = np.random.default_rng(7)
+    if case == "pk_fk":
+        R, S = sgx.reference_relations(1 << 18, 1 << 18)
+    elif case == "sel10":
+        R, S = sgx.reference_relations(1 << 16, 1 << 16, selectivity=10)
+    elif case == "dups":
+        R = rel(rng.integers(0, 5000, 30_000).astype(np.uint32))
+        S = rel(rng.integers(0, 5000, 20_000).astype(np.uint32))
+    else:
+        R = rel(np.concatenate([np.full(4, 3, np.uint32), np.arange(10, 40_010, dtype=np.uint32)]))
+        S = rel(np.concatenate([np.full(30_000, 3, np.uint32), rng.integers(0, 50_000, 40_000).astype(np.uint32)]))
+    exp = orc.rht_join(R, S, 4)
+    assert exp == orc.count_join_sort(R, S)
+    for bits, passes in [(0, 0), (5, 1), (13, 2)]:
+        assert gpu_join(sgx, R, S, radix_bits=bits, passes=passes, algorithm="RHT").matches == exp
+    if len(R) <= 1 << 16:
+        got = gpu_triples(sgx, R, S, algorithm="RHT")
+        assert np.array_equal(sorted_triples(got), sorted_triples(orc.rht_join_triples(R, S, 4)))
+
+
+def test_rht_dropin_and_full_size(sgx, gpu):
+    import torch
+
+    R, S = sgx.reference_relations(1 << 16, 1 << 16)
+    out = sgx.rho_join_tables(R, len(R), S, len(S), nthreads=8, algorithm="RHT")
+    assert out.totalresults == 1 << 16 and out.result_type == 0
+    n = 1 << 28
+    dR = torch.empty(n, dtype=torch.int64, device=gpu)
+    dS = torch.empty(n, dtype=torch.int64, device=gpu)
+    sgx.gen_pk_dev(dR, n, 0, n, 11111)
+    sgx.gen_fk_dev(dS, n, 0, n, 22222)
+    assert sgx.rho_join(dR, n, dS, n, algorithm="RHT").matches == n
+    del dR, dS
+    torch.cuda.empty_cache()
