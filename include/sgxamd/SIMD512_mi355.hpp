@@ -84,4 +84,57 @@ inline size_t scan(pred_t lo, pred_t hi, const void *input_compressed, size_t in
     return n;
 }
 
+// SIMD512.cpp:34-88: sum of the matching codes.
+inline size_t sum(pred_t lo, pred_t hi, const void *input_compressed, size_t input_size) {
+    uint64_t v = 0;
+    detail::check(mi355_scan_sum_u8(lo, hi, static_cast<const uint8_t *>(input_compressed), detail::whole(input_size),
+                                    &v),
+                  "sum");
+    return v;
+}
+
+namespace detail {
+// Dictionary scans: the reference processes input_size / BLOCK whole blocks
+// (64 / 32 / 16 codes per 512-bit register) and sizes the output vector itself.
+template <typename Vec, typename F>
+inline void dict_into(Vec &out, size_t max_matches, F &&call, bool trim) {
+    if (out.size() < max_matches) out.resize(max_matches);
+    uint64_t n = 0;
+    check(call(reinterpret_cast<int64_t *>(out.data()), out.size(), &n), "dict_scan");
+    if (trim) out.resize(n);
+}
+}  // namespace detail
+
+// SIMD512.cpp:289-338
+template <typename Vec>
+inline void dict_scan_8bit_64bit(int64_t lo, int64_t hi, const int64_t *dict, const void *input_compressed,
+                                 size_t input_size, Vec &output_buffer, bool cut = false) {
+    const size_t m = input_size / 64 * 64;
+    detail::dict_into(output_buffer, m, [&](int64_t *o, size_t cap, uint64_t *n) {
+        return mi355_dict_scan_8bit_64bit(lo, hi, dict, static_cast<const uint8_t *>(input_compressed), m, o, cap, n);
+    }, cut);
+}
+
+// SIMD512.cpp:531-579 (always trims, like the reference)
+template <typename Vec>
+inline void dict_scan_16bit_64bit(int64_t lo, int64_t hi, const int64_t *dict, const void *input_compressed,
+                                  size_t input_size, Vec &output_buffer) {
+    const size_t m = input_size / 32 * 32;
+    detail::dict_into(output_buffer, m, [&](int64_t *o, size_t cap, uint64_t *n) {
+        return mi355_dict_scan_16bit_64bit(lo, hi, dict, static_cast<const uint16_t *>(input_compressed), m, o, cap,
+                                           n);
+    }, true);
+}
+
+// SIMD512.cpp:581-629 (always trims, like the reference)
+template <typename Vec>
+inline void dict_scan_32bit_64bit(int64_t lo, int64_t hi, const int64_t *dict, size_t dict_size,
+                                  const void *input_compressed, size_t input_size, Vec &output_buffer) {
+    const size_t m = input_size / 16 * 16;
+    detail::dict_into(output_buffer, m, [&](int64_t *o, size_t cap, uint64_t *n) {
+        return mi355_dict_scan_32bit_64bit(lo, hi, dict, dict_size, static_cast<const uint32_t *>(input_compressed),
+                                           m, o, cap, n);
+    }, true);
+}
+
 }  // namespace SIMD512

@@ -8,6 +8,10 @@
  *   bitvector_scan                 SIMD512.cpp:210-222 -> mi355_scan_bitvector_*
  *   implicit_index_scan(_self_alloc) SIMD512.cpp:225-287 -> mi355_scan_index_*
  *   scan (value materialisation)   SIMD512.cpp:91-150  -> mi355_scan_values_*
+ *   sum                            SIMD512.cpp:34-88   -> mi355_scan_sum_u8
+ *   dict_scan_8bit_64bit           SIMD512.cpp:289-338 -> mi355_dict_scan_8bit_64bit
+ *   dict_scan_16bit_64bit          SIMD512.cpp:531-579 -> mi355_dict_scan_16bit_64bit
+ *   dict_scan_32bit_64bit          SIMD512.cpp:581-629 -> mi355_dict_scan_32bit_64bit
  * Predicate semantics: lo <= v <= hi, inclusive; unsigned compare for u8
  * (_mm512_cmpge_epu8_mask / cmple), signed compare for i32.
  *
@@ -51,6 +55,26 @@ int mi355_scan_values_u8(uint8_t lo, uint8_t hi, const uint8_t *in, size_t n,
                          uint32_t *out, size_t cap, uint64_t *n_out);
 int mi355_scan_values_i32(int32_t lo, int32_t hi, const int32_t *in, size_t n,
                           int32_t *out, size_t cap, uint64_t *n_out);
+
+/* Sum of the u8 codes v[i] with lo <= v[i] <= hi (SIMD512::sum). */
+int mi355_scan_sum_u8(uint8_t lo, uint8_t hi, const uint8_t *in, size_t n, uint64_t *sum);
+
+/*
+ * Dictionary scans: codes index a dictionary of int64 values; the value predicate
+ * [lo, hi] is turned into a code range the way the reference does (first index
+ * with dict[i] >= lo; first index after it with dict[j] > hi, minus one; cast to
+ * the code width, uint16_t for the 32-bit variant as at SIMD512.cpp:588-589, so
+ * out-of-dictionary predicates wrap exactly like the reference's), and every
+ * matching row's dict[code] is written in row order.  At most cap values are
+ * written; *n_out = matches (MI355_ERR_CAPACITY when cap < matches).  dict has
+ * 256 / 65536 / dict_size entries (host or device).
+ */
+int mi355_dict_scan_8bit_64bit(int64_t lo, int64_t hi, const int64_t *dict, const uint8_t *in, size_t n,
+                               int64_t *out, size_t cap, uint64_t *n_out);
+int mi355_dict_scan_16bit_64bit(int64_t lo, int64_t hi, const int64_t *dict, const uint16_t *in, size_t n,
+                                int64_t *out, size_t cap, uint64_t *n_out);
+int mi355_dict_scan_32bit_64bit(int64_t lo, int64_t hi, const int64_t *dict, size_t dict_size, const uint32_t *in,
+                                size_t n, int64_t *out, size_t cap, uint64_t *n_out);
 
 #ifdef __cplusplus
 } /* extern "C" */

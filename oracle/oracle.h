@@ -82,6 +82,12 @@ uint64_t oracle_scan_index_i32(int32_t lo, int32_t hi, const int32_t *in, size_t
 uint64_t oracle_scan_values_u8(uint8_t lo, uint8_t hi, const uint8_t *in, size_t n, uint32_t *out);
 uint64_t oracle_scan_values_i32(int32_t lo, int32_t hi, const int32_t *in, size_t n, int32_t *out);
 /* Multithreaded count for the CPU baseline (contiguous slices, like scan_wrapper). */
+/* SIMD512::sum (SIMD512.cpp:34-88). */
+uint64_t oracle_scan_sum_u8(uint8_t lo, uint8_t hi, const uint8_t *in, size_t n);
+/* dict_scan_{8,16,32}bit_64bit (SIMD512.cpp:289-629): code range via the dictionary with
+ * the reference's casts, then dict[code] of every matching row; returns the matches. */
+uint64_t oracle_dict_scan(int64_t lo, int64_t hi, const int64_t *dict, uint64_t dict_size, const void *codes,
+                          int code_bytes, size_t n, int64_t *out);
 uint64_t oracle_scan_count_i32_mt(int32_t lo, int32_t hi, const int32_t *in, size_t n, int nthreads);
 
 #ifdef __cplusplus

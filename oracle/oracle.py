@@ -52,6 +52,8 @@ def _load() -> C.CDLL:
         "oracle_scan_values_u8": (C.c_uint64, [C.c_uint8, C.c_uint8, P, C.c_size_t, P]),
         "oracle_scan_values_i32": (C.c_uint64, [C.c_int32, C.c_int32, P, C.c_size_t, P]),
         "oracle_scan_count_i32_mt": (C.c_uint64, [C.c_int32, C.c_int32, P, C.c_size_t, C.c_int]),
+        "oracle_scan_sum_u8": (C.c_uint64, [C.c_uint8, C.c_uint8, P, C.c_size_t]),
+        "oracle_dict_scan": (C.c_uint64, [C.c_int64, C.c_int64, P, C.c_uint64, P, C.c_int, C.c_size_t, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -144,3 +146,17 @@ def scan(kind: str, dtype: str, lo: int, hi: int, col):
 
 def scan_count_mt(lo: int, hi: int, col, nthreads: int) -> int:
     return int(lib.oracle_scan_count_i32_mt(lo, hi, _p(col), len(col), nthreads))
+
+
+def scan_sum_u8(lo: int, hi: int, col) -> int:
+    return int(lib.oracle_scan_sum_u8(lo, hi, _p(col), len(col)))
+
+
+def dict_scan(lo: int, hi: int, dictionary, codes):
+    """dict_scan_{8,16,32}bit_64bit restated: int64 values dict[code] of the matching rows."""
+    d = np.ascontiguousarray(dictionary, dtype=np.int64)
+    c = np.ascontiguousarray(codes)
+    k = int(lib.oracle_dict_scan(lo, hi, _p(d), len(d), _p(c), c.dtype.itemsize, len(c), None))
+    out = np.zeros(max(k, 1), dtype=np.int64)
+    lib.oracle_dict_scan(lo, hi, _p(d), len(d), _p(c), c.dtype.itemsize, len(c), _p(out))
+    return out[:k]

@@ -108,3 +108,46 @@ uint64_t oracle_scan_count_i32_mt(int32_t lo, int32_t hi, const int32_t *in, siz
     free(args);
     return total;
 }
+
+/* SIMD512::sum (SIMD512.cpp:34-88), scalar: sum of the u8 codes in [lo, hi]. */
+uint64_t oracle_scan_sum_u8(uint8_t lo, uint8_t hi, const uint8_t *in, size_t n) {
+    uint64_t s = 0;
+    for (size_t i = 0; i < n; i++)
+        if (in[i] >= lo && in[i] <= hi) s += in[i];
+    return s;
+}
+
+/* dict_scan_{8,16,32}bit_64bit (SIMD512.cpp:289-338, 531-579, 581-629) in the
+ * scalar form of dict_scan_8bit_64bit_scalar (:505-529): the predicate's code
+ * range comes from two std::find_if passes over the dictionary (:297-302), cast to
+ * uint8_t (8-bit codes) or uint16_t (16- and 32-bit codes, :588-589); matching
+ * rows are decoded to dict[code] in row order.  code_bytes = 1, 2 or 4.  Scans all
+ * n codes (the vector versions' block tails are the caller's business). */
+uint64_t oracle_dict_scan(int64_t lo, int64_t hi, const int64_t *dict, uint64_t dict_size, const void *codes,
+                          int code_bytes, size_t n, int64_t *out) {
+    uint64_t low = 0;
+    while (low < dict_size && !(dict[low] >= lo)) low++;
+    uint64_t end = low;
+    while (end < dict_size && !(dict[end] > hi)) end++;
+    const int64_t high = (int64_t)end - 1;
+    uint32_t clo, chi;
+    if (code_bytes == 1) {
+        clo = (uint8_t)low;
+        chi = (uint8_t)(high & 0xff);
+    } else {
+        clo = (uint16_t)low;
+        chi = (uint16_t)high;
+    }
+    uint64_t k = 0;
+    for (size_t i = 0; i < n; i++) {
+        uint32_t c;
+        if (code_bytes == 1) c = ((const uint8_t *)codes)[i];
+        else if (code_bytes == 2) c = ((const uint16_t *)codes)[i];
+        else c = ((const uint32_t *)codes)[i];
+        if (c >= clo && c <= chi) {
+            if (out) out[k] = dict[c];
+            k++;
+        }
+    }
+    return k;
+}

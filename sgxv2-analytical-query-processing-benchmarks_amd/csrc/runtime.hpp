@@ -72,7 +72,7 @@ struct Context {
     Arena scratch;
     DeviceBuffer mat;              // materialised output_triple_t (when the caller's buffer is host memory)
     // scan workspace
-    DeviceBuffer scan_in, scan_out, scan_aux;
+    DeviceBuffer scan_in, scan_out, scan_aux, scan_dict;
     uint64_t *host_result = nullptr;  // pinned 64 x u64
 };
 

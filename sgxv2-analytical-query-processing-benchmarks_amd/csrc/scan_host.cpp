@@ -137,6 +137,111 @@ int run(Op op, T lo, T hi, const T *in, size_t n, void *out, size_t cap, uint64_
     return MI355_OK;
 }
 
+// SIMD512::sum (SIMD512.cpp:34-88): sum of the u8 codes in [lo, hi].
+int run_sum_u8(uint8_t lo, uint8_t hi, const uint8_t *in, size_t n, uint64_t *sum) {
+    int status = MI355_OK;
+    Context *ctx = current_context(&status);
+    if (!ctx) return status;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    hipStream_t s = thread_stream(ctx, nullptr);
+    Timer &tm = thread_timer();
+    tm.begin_call(s, thread_timing_enabled());
+    const uint8_t *din = nullptr;
+    int rc = stage_input(ctx, s, in, n, &din);
+    if (rc) return rc;
+    const Geometry g = geometry(n);
+    Arena &A = ctx->scratch;
+    A.reset();
+    const size_t o_counts = A.reserve(sizeof(uint64_t) * g.nchunks);
+    const size_t o_res = A.reserve(sizeof(uint64_t) * 2);
+    SCAN_HIP(A.buf.ensure(A.used));
+    tm.mark("scan_sum_values");
+    SCAN_HIP(launch_sum_u8(din, n, lo, hi, g.rows_per_chunk, g.nchunks, A.at<uint64_t>(o_counts), s));
+    tm.mark("scan_sum");
+    SCAN_HIP(launch_sum(A.at<uint64_t>(o_counts), g.nchunks, A.at<uint64_t>(o_res), s));
+    tm.end_call();
+    SCAN_HIP(hipMemcpyAsync(ctx->host_result, A.at<uint64_t>(o_res), sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    SCAN_HIP(hipStreamSynchronize(s));
+    tm.collect();
+    *sum = ctx->host_result[0];
+    return MI355_OK;
+}
+
+// dict_scan_{8,16,32}bit_64bit (SIMD512.cpp:289-338, 531-579, 581-629): the value
+// predicate [lo, hi] becomes a code range through the dictionary exactly as the
+// reference computes it, including its casts: codes [(C)lo_idx, (C)(hi_end - 1)]
+// with C = uint8_t / uint16_t / uint16_t (the 32-bit variant casts its indexes to
+// uint16_t too, :588-589); then the matching codes are decoded to dict[code] in
+// row order.  CodeT is the code width, CastT the reference's index cast.
+template <typename CodeT, typename CastT>
+int run_dict(int64_t lo, int64_t hi, const int64_t *dict, uint64_t dict_size, const CodeT *in, size_t n,
+             int64_t *out, size_t cap, uint64_t *n_out) {
+    int status = MI355_OK;
+    Context *ctx = current_context(&status);
+    if (!ctx) return status;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    hipStream_t s = thread_stream(ctx, nullptr);
+    Timer &tm = thread_timer();
+    tm.begin_call(s, thread_timing_enabled());
+
+    const int64_t *ddict = dict;
+    if (!is_device_pointer(dict)) {
+        SCAN_HIP(ctx->scan_dict.ensure(dict_size * sizeof(int64_t)));
+        SCAN_HIP(hipMemcpyAsync(ctx->scan_dict.ptr, dict, dict_size * sizeof(int64_t), hipMemcpyHostToDevice, s));
+        ddict = ctx->scan_dict.as<int64_t>();
+    }
+    const CodeT *din = nullptr;
+    int rc = stage_input(ctx, s, in, n, &din);
+    if (rc) return rc;
+    const Geometry g = geometry(n);
+    const uint64_t nwords = (n + 63) / 64;
+    Arena &A = ctx->scratch;
+    A.reset();
+    const size_t o_counts = A.reserve(sizeof(uint64_t) * g.nchunks);
+    const size_t o_offs = A.reserve(sizeof(uint64_t) * g.nchunks);
+    const size_t o_res = A.reserve(sizeof(uint64_t) * 2);
+    const size_t o_range = A.reserve(sizeof(uint64_t) * 2);
+    SCAN_HIP(A.buf.ensure(A.used));
+    uint64_t *range = A.at<uint64_t>(o_range);
+    tm.mark("dict_range");
+    const uint64_t init[2] = {dict_size, dict_size};
+    SCAN_HIP(hipMemcpyAsync(range, init, sizeof(init), hipMemcpyHostToDevice, s));
+    SCAN_HIP(launch_dict_range(ddict, dict_size, lo, hi, range, s));
+    SCAN_HIP(hipMemcpyAsync(ctx->host_result, range, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    SCAN_HIP(hipStreamSynchronize(s));
+    const CodeT clo = (CodeT)(CastT)ctx->host_result[0];
+    const CodeT chi = (CodeT)(CastT)(int64_t)(ctx->host_result[1] - 1);
+
+    SCAN_HIP(ctx->scan_aux.ensure(std::max<uint64_t>(nwords, 1) * sizeof(uint64_t)));
+    uint64_t *bv = ctx->scan_aux.as<uint64_t>();
+    uint64_t *counts = A.at<uint64_t>(o_counts), *offs = A.at<uint64_t>(o_offs), *res = A.at<uint64_t>(o_res);
+    tm.mark("dict_bitvector");
+    SCAN_HIP(launch_predicate<CodeT>(din, n, clo, chi, g.rows_per_chunk, g.nchunks, bv, counts, s));
+    tm.mark("dict_chunk_scan");
+    SCAN_HIP(launch_chunk_scan(counts, g.nchunks, offs, res, s));
+    const bool out_dev = out && is_device_pointer(out);
+    int64_t *o = out;
+    if (!out_dev) {
+        SCAN_HIP(ctx->scan_out.ensure(std::max<size_t>(cap, 1) * sizeof(int64_t)));
+        o = ctx->scan_out.as<int64_t>();
+    }
+    tm.mark("dict_decode");
+    SCAN_HIP((launch_expand<CodeT, int64_t, 2>(bv, din, n, g.rows_per_chunk, g.nchunks, offs, o, cap, s, ddict)));
+    tm.end_call();
+    SCAN_HIP(hipMemcpyAsync(ctx->host_result, res, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    SCAN_HIP(hipStreamSynchronize(s));
+    const uint64_t total = ctx->host_result[0];
+    *n_out = total;
+    if (!out_dev && out && total) SCAN_HIP(hipMemcpy(out, o, std::min<uint64_t>(total, cap) * sizeof(int64_t),
+                                                     hipMemcpyDeviceToHost));
+    tm.collect();
+    if (total > cap) {
+        set_last_error("output capacity " + std::to_string(cap) + " < " + std::to_string(total) + " matches");
+        return MI355_ERR_CAPACITY;
+    }
+    return MI355_OK;
+}
+
 inline bool bad(const void *in, size_t n, const void *out, bool need_out) {
     if (!in && n) return true;
     if (need_out && !out && n) return true;
@@ -150,6 +255,7 @@ inline bool bad(const void *in, size_t n, const void *out, bool need_out) {
 using sgxamd::set_last_error;
 using sgxamd::scan::Op;
 using sgxamd::scan::run;
+using sgxamd::scan::run_dict;
 
 #define SCAN_ARGCHECK(cond)                     \
     do {                                        \
@@ -211,6 +317,33 @@ int mi355_scan_values_i32(int32_t lo, int32_t hi, const int32_t *in, size_t n, i
     SCAN_ARGCHECK(sgxamd::scan::bad(in, n, out, cap > 0) || !n_out);
     if (n == 0) { *n_out = 0; return MI355_OK; }
     return run<int32_t, int32_t>(Op::kValues, lo, hi, in, n, out, cap, n_out);
+}
+
+int mi355_scan_sum_u8(uint8_t lo, uint8_t hi, const uint8_t *in, size_t n, uint64_t *sum) {
+    SCAN_ARGCHECK(sgxamd::scan::bad(in, n, sum, true) || !sum);
+    if (n == 0) { *sum = 0; return MI355_OK; }
+    return sgxamd::scan::run_sum_u8(lo, hi, in, n, sum);
+}
+
+int mi355_dict_scan_8bit_64bit(int64_t lo, int64_t hi, const int64_t *dict, const uint8_t *in, size_t n,
+                               int64_t *out, size_t cap, uint64_t *n_out) {
+    SCAN_ARGCHECK(sgxamd::scan::bad(in, n, out, cap > 0) || !n_out || !dict);
+    if (n == 0) { *n_out = 0; return MI355_OK; }
+    return run_dict<uint8_t, uint8_t>(lo, hi, dict, 256, in, n, out, cap, n_out);
+}
+
+int mi355_dict_scan_16bit_64bit(int64_t lo, int64_t hi, const int64_t *dict, const uint16_t *in, size_t n,
+                                int64_t *out, size_t cap, uint64_t *n_out) {
+    SCAN_ARGCHECK(sgxamd::scan::bad(in, n, out, cap > 0) || !n_out || !dict);
+    if (n == 0) { *n_out = 0; return MI355_OK; }
+    return run_dict<uint16_t, uint16_t>(lo, hi, dict, 65536, in, n, out, cap, n_out);
+}
+
+int mi355_dict_scan_32bit_64bit(int64_t lo, int64_t hi, const int64_t *dict, size_t dict_size, const uint32_t *in,
+                                size_t n, int64_t *out, size_t cap, uint64_t *n_out) {
+    SCAN_ARGCHECK(sgxamd::scan::bad(in, n, out, cap > 0) || !n_out || !dict || dict_size == 0);
+    if (n == 0) { *n_out = 0; return MI355_OK; }
+    return run_dict<uint32_t, uint16_t>(lo, hi, dict, dict_size, in, n, out, cap, n_out);
 }
 
 }  // extern "C"

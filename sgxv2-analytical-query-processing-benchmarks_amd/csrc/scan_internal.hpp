@@ -18,10 +18,21 @@ hipError_t launch_predicate(const T *in, uint64_t n, T lo, T hi, uint64_t rows_p
 hipError_t launch_chunk_scan(const uint64_t *counts, uint32_t nchunks, uint64_t *offsets, uint64_t *total,
                              hipStream_t s);
 
-// MODE 0: row indexes (OutT = uint64_t); MODE 1: values (u8 -> uint32_t, i32 -> int32_t)
+// MODE 0: row indexes (OutT = uint64_t); MODE 1: values (u8 -> uint32_t, i32 -> int32_t);
+// MODE 2: dictionary-decoded values dict[code] (OutT = int64_t).
 template <typename T, typename OutT, int MODE>
 hipError_t launch_expand(const uint64_t *bv, const T *in, uint64_t n, uint64_t rows_per_chunk, uint32_t nchunks,
-                         const uint64_t *chunk_off, OutT *out, uint64_t cap, hipStream_t s);
+                         const uint64_t *chunk_off, OutT *out, uint64_t cap, hipStream_t s,
+                         const int64_t *dict = nullptr);
+
+// Per-chunk sums of the u8 codes in [lo, hi] (SIMD512::sum).
+hipError_t launch_sum_u8(const uint8_t *in, uint64_t n, uint8_t lo, uint8_t hi, uint64_t rows_per_chunk,
+                         uint32_t nchunks, uint64_t *chunk_sums, hipStream_t s);
+
+// range[0] = first i with dict[i] >= lo, range[1] = first j >= range[0] with dict[j] > hi
+// (each dict_size when none); both must be preset to dict_size.
+hipError_t launch_dict_range(const int64_t *dict, uint64_t n, int64_t lo, int64_t hi, uint64_t *range,
+                             hipStream_t s);
 
 hipError_t launch_sum(const uint64_t *v, uint32_t n, uint64_t *out, hipStream_t s);
 

@@ -48,9 +48,45 @@ __device__ __forceinline__ uint32_t match_mask<int32_t>(const uint4 &q, int32_t 
     return m & valid;
 }
 
+// 8 uint16 dictionary codes -> 8-bit mask (unsigned, _mm512_cmpge/le_epu16_mask).
+template <>
+__device__ __forceinline__ uint32_t match_mask<uint16_t>(const uint4 &q, uint16_t lo, uint16_t hi, uint32_t valid) {
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+    uint32_t m = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const uint32_t c = __builtin_amdgcn_ubfe(w[j >> 1], (j & 1) * 16, 16);
+        m |= (uint32_t)(c >= lo && c <= hi) << j;
+    }
+    return m & valid;
+}
+
+// 4 uint32 dictionary codes -> 4-bit mask (unsigned, _mm512_cmpge/le_epu32_mask).
+template <>
+__device__ __forceinline__ uint32_t match_mask<uint32_t>(const uint4 &q, uint32_t lo, uint32_t hi, uint32_t valid) {
+    uint32_t m = (uint32_t)(q.x >= lo && q.x <= hi) | ((uint32_t)(q.y >= lo && q.y <= hi) << 1) |
+                 ((uint32_t)(q.z >= lo && q.z <= hi) << 2) | ((uint32_t)(q.w >= lo && q.w <= hi) << 3);
+    return m & valid;
+}
+
+// Sum of the matching values of one 16-byte lane load (SIMD512::sum, u8 codes).
+template <typename T>
+__device__ __forceinline__ uint64_t match_sum(const uint4 &q, uint32_t m) {
+    constexpr uint32_t V = 16 / sizeof(T), B = 8 * sizeof(T);
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+    uint64_t acc = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < V; ++j) {
+        const uint32_t v = B == 32 ? w[j] : __builtin_amdgcn_ubfe(w[(j * B) / 32], (j * B) % 32, B);
+        acc += (m >> j) & 1u ? (uint64_t)v : 0ull;
+    }
+    return acc;
+}
+
 // Count (WRITE=false) or bitvector + count (WRITE=true) of one chunk per workgroup.
 // rows_per_chunk is a multiple of kWaves * 64 * V * kUnroll.
-template <typename T, bool WRITE>
+// SUM=true accumulates the matching values instead of counting them (SIMD512::sum).
+template <typename T, bool WRITE, bool SUM = false>
 __global__ __launch_bounds__(kBlock) void k_predicate(const T *__restrict__ in, uint64_t n, T lo, T hi,
                                                       uint64_t rows_per_chunk, uint64_t *__restrict__ bv,
                                                       uint64_t *__restrict__ chunk_counts) {
@@ -78,8 +114,9 @@ __global__ __launch_bounds__(kBlock) void k_predicate(const T *__restrict__ in, 
 #pragma unroll
                 for (uint32_t j = 0; j < V; ++j) {
                     const uint32_t val = (row + j < r1) ? (uint32_t)in[row + j] : 0u;
-                    if (sizeof(T) == 1) w[j / 4] |= (val & 0xFFu) << (8 * (j % 4));
-                    else w[j] = val;
+                    constexpr uint32_t B = 8 * sizeof(T);
+                    constexpr uint32_t VM = B == 32 ? 0xFFFFFFFFu : ((1u << B) - 1u);
+                    w[(j * B) / 32] |= (val & VM) << ((j * B) % 32);
                 }
                 q[u] = make_uint4(w[0], w[1], w[2], w[3]);
                 valid[u] = (1u << (uint32_t)(r1 - row)) - 1u;
@@ -91,7 +128,8 @@ __global__ __launch_bounds__(kBlock) void k_predicate(const T *__restrict__ in, 
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) {
             const uint32_t m = match_mask<T>(q[u], lo, hi, valid[u]);
-            count += __popc(m);
+            if (SUM) count += match_sum<T>(q[u], m);
+            else count += __popc(m);
             if (WRITE) {
                 uint64_t x = (uint64_t)m << (V * (lane % LPW));
 #pragma unroll
@@ -126,6 +164,18 @@ hipError_t launch_predicate(const T *in, uint64_t n, T lo, T hi, uint64_t rows_p
 
 template hipError_t launch_predicate<uint8_t>(const uint8_t *, uint64_t, uint8_t, uint8_t, uint64_t, uint32_t,
                                               uint64_t *, uint64_t *, hipStream_t);
+template hipError_t launch_predicate<uint16_t>(const uint16_t *, uint64_t, uint16_t, uint16_t, uint64_t, uint32_t,
+                                               uint64_t *, uint64_t *, hipStream_t);
+template hipError_t launch_predicate<uint32_t>(const uint32_t *, uint64_t, uint32_t, uint32_t, uint64_t, uint32_t,
+                                               uint64_t *, uint64_t *, hipStream_t);
+
+hipError_t launch_sum_u8(const uint8_t *in, uint64_t n, uint8_t lo, uint8_t hi, uint64_t rows_per_chunk,
+                         uint32_t nchunks, uint64_t *chunk_sums, hipStream_t s) {
+    if (nchunks == 0) return hipSuccess;
+    hipLaunchKernelGGL((k_predicate<uint8_t, false, true>), dim3(nchunks), dim3(kBlock), 0, s, in, n, lo, hi,
+                       rows_per_chunk, nullptr, chunk_sums);
+    return hipGetLastError();
+}
 template hipError_t launch_predicate<int32_t>(const int32_t *, uint64_t, int32_t, int32_t, uint64_t, uint32_t,
                                               uint64_t *, uint64_t *, hipStream_t);
 
@@ -174,7 +224,8 @@ __device__ __forceinline__ uint32_t select_bit(uint64_t x, uint32_t r) {
     return pos;
 }
 
-// Expand the bitvector of one chunk into row indexes (MODE 0) or values (MODE 1).
+// Expand the bitvector of one chunk into row indexes (MODE 0), values (MODE 1) or
+// dictionary-decoded values dict[code] (MODE 2, the dict_scan_* family).
 // Waves take 64 words at a time; lane j of a wave writes the wave's j-th, (j+64)-th,
 // ... output, locating its set bit by binary search over the wave's inclusive
 // word-popcount prefix held in LDS.
@@ -182,7 +233,7 @@ template <typename T, typename OutT, int MODE>
 __global__ __launch_bounds__(kBlock) void k_expand(const uint64_t *__restrict__ bv, const T *__restrict__ in,
                                                    uint64_t n, uint64_t rows_per_chunk,
                                                    const uint64_t *__restrict__ chunk_off, OutT *__restrict__ out,
-                                                   uint64_t cap) {
+                                                   uint64_t cap, const int64_t *__restrict__ dict) {
     __shared__ uint32_t incl_s[kWaves][64];
     __shared__ uint64_t word_s[kWaves][64];
     __shared__ uint32_t wtot_s[kWaves];
@@ -223,7 +274,8 @@ __global__ __launch_bounds__(kBlock) void k_expand(const uint64_t *__restrict__ 
             const uint64_t o = woff + m;
             if (o < cap) {
                 if (MODE == 0) out[o] = (OutT)row;
-                else out[o] = (OutT)in[row];
+                else if (MODE == 1) out[o] = (OutT)in[row];
+                else out[o] = (OutT)dict[in[row]];
             }
         }
         base += all;
@@ -233,25 +285,62 @@ __global__ __launch_bounds__(kBlock) void k_expand(const uint64_t *__restrict__ 
 
 template <typename T, typename OutT, int MODE>
 hipError_t launch_expand(const uint64_t *bv, const T *in, uint64_t n, uint64_t rows_per_chunk, uint32_t nchunks,
-                         const uint64_t *chunk_off, OutT *out, uint64_t cap, hipStream_t s) {
+                         const uint64_t *chunk_off, OutT *out, uint64_t cap, hipStream_t s, const int64_t *dict) {
     if (nchunks == 0) return hipSuccess;
     hipLaunchKernelGGL((k_expand<T, OutT, MODE>), dim3(nchunks), dim3(kBlock), 0, s, bv, in, n, rows_per_chunk,
-                       chunk_off, out, cap);
+                       chunk_off, out, cap, dict);
     return hipGetLastError();
 }
 
 template hipError_t launch_expand<uint8_t, uint64_t, 0>(const uint64_t *, const uint8_t *, uint64_t, uint64_t,
                                                         uint32_t, const uint64_t *, uint64_t *, uint64_t,
-                                                        hipStream_t);
+                                                        hipStream_t, const int64_t *);
 template hipError_t launch_expand<int32_t, uint64_t, 0>(const uint64_t *, const int32_t *, uint64_t, uint64_t,
                                                         uint32_t, const uint64_t *, uint64_t *, uint64_t,
-                                                        hipStream_t);
+                                                        hipStream_t, const int64_t *);
 template hipError_t launch_expand<uint8_t, uint32_t, 1>(const uint64_t *, const uint8_t *, uint64_t, uint64_t,
                                                         uint32_t, const uint64_t *, uint32_t *, uint64_t,
-                                                        hipStream_t);
+                                                        hipStream_t, const int64_t *);
 template hipError_t launch_expand<int32_t, int32_t, 1>(const uint64_t *, const int32_t *, uint64_t, uint64_t,
                                                        uint32_t, const uint64_t *, int32_t *, uint64_t,
-                                                       hipStream_t);
+                                                       hipStream_t, const int64_t *);
+
+template hipError_t launch_expand<uint8_t, int64_t, 2>(const uint64_t *, const uint8_t *, uint64_t, uint64_t,
+                                                       uint32_t, const uint64_t *, int64_t *, uint64_t, hipStream_t,
+                                                       const int64_t *);
+template hipError_t launch_expand<uint16_t, int64_t, 2>(const uint64_t *, const uint16_t *, uint64_t, uint64_t,
+                                                        uint32_t, const uint64_t *, int64_t *, uint64_t, hipStream_t,
+                                                        const int64_t *);
+template hipError_t launch_expand<uint32_t, int64_t, 2>(const uint64_t *, const uint32_t *, uint64_t, uint64_t,
+                                                        uint32_t, const uint64_t *, int64_t *, uint64_t, hipStream_t,
+                                                        const int64_t *);
+
+// Dictionary code range of a predicate on values (dict_scan_* prologue,
+// SIMD512.cpp:297-305): lo_idx = first i with dict[i] >= lo (else dict_size),
+// hi_end = first j >= lo_idx with dict[j] > hi (else dict_size).  Two passes of
+// atomicMin; range[0] / range[1] must be preset to dict_size.
+__global__ __launch_bounds__(kBlock) void k_dict_low(const int64_t *__restrict__ dict, uint64_t n, int64_t lo,
+                                                     unsigned long long *__restrict__ range) {
+    for (uint64_t i = blockIdx.x * (uint64_t)kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock)
+        if (dict[i] >= lo) atomicMin(&range[0], (unsigned long long)i);
+}
+__global__ __launch_bounds__(kBlock) void k_dict_high(const int64_t *__restrict__ dict, uint64_t n, int64_t hi,
+                                                      unsigned long long *__restrict__ range) {
+    const uint64_t lo_idx = range[0];
+    for (uint64_t i = lo_idx + blockIdx.x * (uint64_t)kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock)
+        if (dict[i] > hi) atomicMin(&range[1], (unsigned long long)i);
+}
+
+hipError_t launch_dict_range(const int64_t *dict, uint64_t n, int64_t lo, int64_t hi, uint64_t *range,
+                             hipStream_t s) {
+    uint64_t blocks = (n + kBlock - 1) / kBlock;
+    if (blocks > 1024) blocks = 1024;
+    if (blocks == 0) blocks = 1;
+    auto *r = reinterpret_cast<unsigned long long *>(range);
+    hipLaunchKernelGGL(k_dict_low, dim3((uint32_t)blocks), dim3(kBlock), 0, s, dict, n, lo, r);
+    hipLaunchKernelGGL(k_dict_high, dim3((uint32_t)blocks), dim3(kBlock), 0, s, dict, n, hi, r);
+    return hipGetLastError();
+}
 
 // Sum of chunk counts (count-only path).
 __global__ __launch_bounds__(kBlock) void k_sum(const uint64_t *__restrict__ v, uint32_t n,

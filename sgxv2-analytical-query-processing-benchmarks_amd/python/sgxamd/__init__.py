@@ -139,6 +139,11 @@ SIGNATURES = {
     "mi355_scan_index_i32": (C.c_int, [C.c_int32, C.c_int32, _P, C.c_size_t, _P, C.c_size_t, _U64P]),
     "mi355_scan_values_u8": (C.c_int, [C.c_uint8, C.c_uint8, _P, C.c_size_t, _P, C.c_size_t, _U64P]),
     "mi355_scan_values_i32": (C.c_int, [C.c_int32, C.c_int32, _P, C.c_size_t, _P, C.c_size_t, _U64P]),
+    "mi355_scan_sum_u8": (C.c_int, [C.c_uint8, C.c_uint8, _P, C.c_size_t, _U64P]),
+    "mi355_dict_scan_8bit_64bit": (C.c_int, [C.c_int64, C.c_int64, _P, _P, C.c_size_t, _P, C.c_size_t, _U64P]),
+    "mi355_dict_scan_16bit_64bit": (C.c_int, [C.c_int64, C.c_int64, _P, _P, C.c_size_t, _P, C.c_size_t, _U64P]),
+    "mi355_dict_scan_32bit_64bit": (C.c_int, [C.c_int64, C.c_int64, _P, C.c_size_t, _P, C.c_size_t, _P, C.c_size_t,
+                                              _U64P]),
     # generator.h
     "mi355_gen_seed": (None, [C.c_uint]),
     "mi355_gen_rand": (C.c_int, []),
@@ -329,6 +334,27 @@ def scan_values(lo: int, hi: int, col, n: int, out, cap: int, dtype: str = "i32"
 
 
 # ------------------------------------------------------------- generators ---
+def scan_sum_u8(lo: int, hi: int, col, n: int) -> int:
+    out = C.c_uint64()
+    _check(lib.mi355_scan_sum_u8(lo, hi, ptr(col), n, C.byref(out)))
+    return int(out.value)
+
+
+def dict_scan(lo: int, hi: int, dictionary, codes, n: int, out, cap: int, code_bits: int,
+              dict_size: int | None = None) -> int:
+    """dict_scan_{8,16,32}bit_64bit: writes dict[code] (int64) of the matching rows to out."""
+    cnt = C.c_uint64()
+    if code_bits == 8:
+        rc = lib.mi355_dict_scan_8bit_64bit(lo, hi, ptr(dictionary), ptr(codes), n, ptr(out), cap, C.byref(cnt))
+    elif code_bits == 16:
+        rc = lib.mi355_dict_scan_16bit_64bit(lo, hi, ptr(dictionary), ptr(codes), n, ptr(out), cap, C.byref(cnt))
+    else:
+        rc = lib.mi355_dict_scan_32bit_64bit(lo, hi, ptr(dictionary), dict_size, ptr(codes), n, ptr(out), cap,
+                                             C.byref(cnt))
+    _check(rc)
+    return int(cnt.value)
+
+
 def gen_seed(seed: int) -> None:
     lib.mi355_gen_seed(seed)
 

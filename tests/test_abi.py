@@ -73,7 +73,15 @@ def test_static_asserts_compile_as_c_and_cxx(tmp_path):
     subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(tmp_path / "a")],
                    check=True)
     cpp = tmp_path / "t.cpp"
-    cpp.write_text('#include "sgxamd/joins.hpp"\n#include "sgxamd/SIMD512_mi355.hpp"\nint main(){return 0;}\n')
+    # instantiate every adapter template the way a reference caller would (compile only)
+    cpp.write_text('#include <vector>\n#include "sgxamd/joins.hpp"\n#include "sgxamd/SIMD512_mi355.hpp"\n'
+                   'void use(const void *in, const int64_t *d, std::vector<int64_t> &v, std::vector<size_t> &ix) {\n'
+                   '  SIMD512::dict_scan_8bit_64bit(0, 1, d, in, 64, v, true);\n'
+                   '  SIMD512::dict_scan_16bit_64bit(0, 1, d, in, 64, v);\n'
+                   '  SIMD512::dict_scan_32bit_64bit(0, 1, d, 99, in, 64, v);\n'
+                   '  SIMD512::implicit_index_scan_self_alloc(0, 1, in, 64, ix, true);\n'
+                   '  (void)SIMD512::sum(0, 1, in, 64); (void)SIMD512::count(0, 1, in, 64);\n}\n'
+                   'int main(){return 0;}\n')
     subprocess.run(["g++", "-std=c++17", "-c", "-I", os.path.join(ROOT, "include"), str(cpp), "-o",
                     str(tmp_path / "b.o")], check=True)
 

@@ -165,3 +165,27 @@ def test_oracle_rht_equals_rho_and_sort_counter():
         for threads, two in [(1, False), (4, False), (3, True)]:
             assert oracle.rht_join(R, S, threads, two) == exp
             assert oracle.rho_join(R, S, threads, two)[0] == exp
+
+
+def test_oracle_dict_scan_reference_kats():
+    """oracle_dict_scan against every dictionary-scan KAT of testsimdscan.cpp."""
+    import oracle
+    from dict_kats import cases
+
+    for name, codes, dictionary, lo, hi, size, probes in cases():
+        got = oracle.dict_scan(lo, hi, dictionary, codes)
+        assert len(got) == size, name
+        for i, v in probes.items():
+            assert got[i] == v, (name, i)
+
+
+def test_oracle_dict_scan_wraps_like_reference():
+    """Predicates outside the dictionary wrap through the reference's casts
+    (SIMD512.cpp:297-305): no value >= lo -> code range [0, 255] for 8-bit codes."""
+    import oracle
+
+    d = np.arange(256, dtype=np.int64)
+    codes = (np.arange(4096) % 256).astype(np.uint8)
+    assert len(oracle.dict_scan(1000, 2000, d, codes)) == 4096
+    assert len(oracle.dict_scan(-100, -50, d, codes)) == 4096  # hi below dict[0]: high index -1 -> 255
+    assert oracle.scan_sum_u8(0, 26, codes) == 16 * sum(range(27))

@@ -94,3 +94,46 @@ def test_config3_full_size(sgx, gpu):
     assert int(bv[0]) == (1 << 27) - 1 and int(bv[4]) == (1 << 27) - 1 and int(bv[1]) == 0
     del col, idx, bv
     torch.cuda.empty_cache()
+
+
+# ------------------------------------------------------------- dictionary scans
+def test_dict_scan_reference_kats(sgx, orc, gpu):
+    """dict_scan_{8,16,32}bit_64bit on the GPU == the oracle on every testsimdscan.cpp dictionary KAT."""
+    from dict_kats import cases
+
+    for name, codes, dictionary, lo, hi, size, probes in cases():
+        bits = codes.dtype.itemsize * 8
+        out = np.zeros(size + 16, dtype=np.int64)
+        n = sgx.dict_scan(lo, hi, dictionary, codes, len(codes), out, len(out), bits, len(dictionary))
+        assert n == size, name
+        assert np.array_equal(out[:n], orc.dict_scan(lo, hi, dictionary, codes)), name
+        for i, v in probes.items():
+            assert out[i] == v, (name, i)
+
+
+@pytest.mark.parametrize("bits", [8, 16, 32])
+def test_dict_scan_random_vs_oracle(sgx, orc, gpu, bits, seed=3):
+    import torch
+
+    rng = np.random.default_rng(seed + bits)
+    dsize = {8: 256, 16: 1 << 16, 32: 70_000}[bits]
+    dt = {8: np.uint8, 16: np.uint16, 32: np.uint32}[bits]
+    dictionary = rng.integers(-10**12, 10**12, dsize)  # unsorted: find_if semantics, not a sorted range
+    dictionary[: dsize // 2].sort()
+    n = 1_000_003
+    codes = rng.integers(0, dsize, n).astype(dt)
+    dcodes = torch.from_numpy(codes.view(np.int8 if bits == 8 else (np.int16 if bits == 16 else np.int32))).to(gpu)
+    for lo, hi in [(-10**11, 3 * 10**11), (0, 10**12), (10**13, 10**14), (-10**13, -10**12 - 1), (5, 5)]:
+        exp = orc.dict_scan(lo, hi, dictionary, codes)
+        out = torch.zeros(len(exp) + 1, dtype=torch.int64, device=gpu)
+        k = sgx.dict_scan(lo, hi, dictionary, dcodes, n, out, len(exp) + 1, bits, dsize)
+        assert k == len(exp)
+        assert np.array_equal(out[:k].cpu().numpy(), exp), (bits, lo, hi)
+    with pytest.raises(sgx.Mi355Error):
+        sgx.dict_scan(-10**13, 10**13, dictionary, codes, n, np.zeros(10, np.int64), 10, bits, dsize)
+
+
+def test_scan_sum_u8(sgx, orc, gpu):
+    col = (np.arange((1 << 20) + 77) % 256).astype(np.uint8)
+    for lo, hi in [(0, 26), (0, 255), (200, 255), (7, 7), (9, 3)]:
+        assert sgx.scan_sum_u8(lo, hi, col, len(col)) == orc.scan_sum_u8(lo, hi, col)
