@@ -1,5 +1,6 @@
 // native_mi355 — the reference's native join driver (Join-Benchmarks/App/TEEBench/native.cpp)
-// running RHO on an MI355X through run_join() of libsgxamd.so.
+// running RHO or RHT (-a) on an MI355X through run_join() of libsgxamd.so; -m materialises
+// the result into the reference's chunked table (CHUNKED_TABLE build).
 //
 // Same CLI (commons.cpp:10-190 getopt "a:c:d:e:l:n:mr:s:t:u:x:y:z:hv"), the same
 // relation generation (seeds 11111 / 22222, pk R, fk / fk_sel / Zipf S: native.cpp:62-101,
@@ -46,7 +47,7 @@ int main(int argc, char **argv) {
             case 'x': r_size = std::strtoull(optarg, nullptr, 10) * 1024 * 1024 / 8; break;
             case 'y': s_size = std::strtoull(optarg, nullptr, 10) * 1024 * 1024 / 8; break;
             case 'z': skew = std::atof(optarg); break;
-            case 'h': std::printf("native_mi355 -a RHO -r N -s N [-l sel] [-z theta] [-n threads]\n"); return 0;
+            case 'h': std::printf("native_mi355 -a RHO|RHT -r N -s N [-l sel] [-z theta] [-n threads] [-m]\n"); return 0;
             default: break;
         }
     }
@@ -78,5 +79,11 @@ int main(int argc, char **argv) {
     std::printf("[INFO] Total join runtime: %.2fs\n", time_s);
     std::printf("[INFO] throughput = %.2lf [M rec / s]\n", (double)(r_size + s_size) / time_s);
     std::printf("[INFO] Matches = %lu\n", (unsigned long)res.totalresults);
+    if (res.materialized && res.result_type == 1) {
+        auto *t = static_cast<chunked_table_t *>(res.result);
+        std::printf("[INFO] Materialized %lu tuples in %lu chunks\n", (unsigned long)t->num_tuples,
+                    (unsigned long)t->num_chunks);
+        mi355_free_chunked_table(t);
+    }
     return 0;
 }

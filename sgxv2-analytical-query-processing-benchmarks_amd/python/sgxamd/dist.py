@@ -10,7 +10,8 @@ tmpR/tmpS arrays (:1421-1433) across sockets:
      d = key & (G - 1) (the low log2(G) key bits, i.e. pass-1 radix bits of
      radix_join.cpp:1118-1119 taken by the shard level);
   2. split exchange: all_to_all of the G per-destination counts;
-  3. tuple exchange: all_to_all_single of the 8-byte tuples (viewed as int64);
+  3. tuple exchange: all_to_all_single of the 8-byte tuples (viewed as int64); R's
+     exchange is left in flight while S is shard-partitioned;
   4. local join of the received R' and S' with key_shift = log2(G) (all their keys
      agree on the low bits, so the local radix bits start above them);
   5. all_reduce(sum) of the match counts (exact: integer sum).
@@ -60,7 +61,9 @@ def _default_local_join(R: torch.Tensor, nR: int, S: torch.Tensor, nS: int, key_
     return res.matches, res.stats
 
 
-def _exchange(t: torch.Tensor, send_counts: list[int], group) -> tuple[torch.Tensor, int]:
+def _exchange(t: torch.Tensor, send_counts: list[int], group, async_op: bool = False):
+    """all_to_all of the per-destination counts (blocking, tiny), then of the tuples.
+    With async_op the tuple exchange is left in flight: (out, total, work)."""
     world = dist.get_world_size(group)
     dev = t.device
     sc = torch.tensor(send_counts, dtype=torch.int64, device=dev)
@@ -69,7 +72,9 @@ def _exchange(t: torch.Tensor, send_counts: list[int], group) -> tuple[torch.Ten
     recv_counts = [int(x) for x in rc.tolist()]
     total = sum(recv_counts)
     out = torch.empty(max(total, 1), dtype=torch.int64, device=dev)
-    dist.all_to_all_single(out[:total], t, recv_counts, send_counts, group=group)
+    work = dist.all_to_all_single(out[:total], t, recv_counts, send_counts, group=group, async_op=async_op)
+    if async_op:
+        return out, total, work
     return out, total
 
 
@@ -95,13 +100,16 @@ def sharded_rho_join(R: torch.Tensor, S: torch.Tensor, *, group=None, partition_
         ms["local_join"] = (time.perf_counter() - t0) * 1e3
         return ShardedJoinResult(int(local), int(local), R.numel(), S.numel(), ms, st)
 
+    # R's tuple exchange (xGMI) runs while S is shard-partitioned (HBM): RCCL works on
+    # its own stream, the partition kernels on the current one.
     pR, cR = partition_fn(R, R.numel(), dest_bits)
+    rR, nR, wR = _exchange(pR, cR, group, async_op=True)
     pS, cS = partition_fn(S, S.numel(), dest_bits)
-    sync()
     t1 = time.perf_counter()
     ms["shard_partition"] = (t1 - t0) * 1e3
-    rR, nR = _exchange(pR, cR, group)
-    rS, nS = _exchange(pS, cS, group)
+    rS, nS, wS = _exchange(pS, cS, group, async_op=True)
+    wR.wait()
+    wS.wait()
     sync()
     t2 = time.perf_counter()
     ms["exchange"] = (t2 - t1) * 1e3

@@ -160,12 +160,16 @@ def test_full_size_config2_property(sgx, gpu):
     torch.cuda.empty_cache()
 
 
-def test_native_driver_binary(gpu):
+@pytest.mark.parametrize("alg,extra", [("RHO", []), ("RHT", []), ("RHO", ["-m"]), ("RHT", ["-m", "-l", "50"])])
+def test_native_driver_binary(gpu, alg, extra):
     exe = os.path.join(PKG, "bin", "native_mi355")
-    out = subprocess.run([exe, "-a", "RHO", "-r", str(1 << 20), "-s", str(1 << 20), "-n", "2"],
+    out = subprocess.run([exe, "-a", alg, "-r", str(1 << 20), "-s", str(1 << 20), "-n", "2"] + extra,
                          capture_output=True, text=True, timeout=300, check=True).stdout
-    assert "Matches = 1048576" in out
-    assert "Throughput (M rec/sec)" in out
+    m = (1 << 19) if "50" in extra else (1 << 20)
+    assert f"Matches = {m}" in out
+    assert "Throughput (M rec/sec)" in out and f"Running {alg}" in out
+    if "-m" in extra:
+        assert f"Materialized {m} tuples" in out
 
 
 # ---------------------------------------------------------------- materialisation
