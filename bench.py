@@ -59,6 +59,8 @@ def main():
                          "global (strong), c5 = Zipf 0.75 |R| = |S| = 2^28 global (strong)")
     ap.add_argument("--algorithm", choices=["RHO", "RHT"], default="RHO",
                     help="build/probe: RHO bucket chaining (headline) or RHT histogram join")
+    ap.add_argument("--partition-overlap", type=int, choices=[0, 1], default=1,
+                    help="1: R/S partition chains on two streams (timed region); 0: one stream")
     ap.add_argument("--no-scan", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -125,6 +127,7 @@ def main():
     def step():
         return sharded_rho_join(R, S, algorithm=args.algorithm)
 
+    sgxamd.set_partition_overlap(bool(args.partition_overlap))
     for _ in range(args.warmup):
         res = step()
         assert res.matches == N_glob, (res.matches, N_glob)
@@ -142,6 +145,22 @@ def main():
     ok = all(r.matches == N_glob for r in results)
     value = N_glob * args.steps / elapsed / 1e6  # M probed tuples/s, all ranks
     ms_per_step = elapsed / args.steps * 1e3
+    kernel_times = "timed region (one stream)"
+    if args.partition_overlap:
+        # With two streams a kernel's event span includes the concurrent chain's
+        # kernels; per-kernel durations for the roofline come from an untimed
+        # pass with the chains serialised (same kernels, same inputs).
+        iso_steps = max(3, min(args.steps, 5))
+        sgxamd.set_partition_overlap(False)
+        step()
+        per_kernel = {}
+        for _ in range(iso_steps):
+            r_iso = step()
+            ok = ok and r_iso.matches == N_glob
+            for name, ms in sgxamd.timings():
+                per_kernel.setdefault(name, []).append(ms)
+        sgxamd.set_partition_overlap(True)
+        kernel_times = f"isolation pass after the timed region: {iso_steps} steps, partition chains on one stream"
 
     # roofline of the dominant kernel (this rank's event times; rank 0 reports)
     nR = results[-1].recv_r
@@ -171,7 +190,8 @@ def main():
         "probe_phase_M_probed_tuples_per_s": round(nS / (avg["join_build_probe"] * 1e-3) / 1e6, 1),
         "probe_roofline": {"achieved": round(probe_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                            "frac": round(probe_gbs / HBM_PEAK_GBS, 4)},
-        "kernel_ms_avg": phase,
+        "kernel_ms_avg": phase, "kernel_times_from": kernel_times,
+        "partition_overlap": bool(args.partition_overlap),
         "radix_bits": ls.get("radix_bits"), "passes": ls.get("passes"),
         "step_ms_breakdown": {k: round(v, 3) for k, v in results[-1].ms.items()},
     }

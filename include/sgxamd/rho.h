@@ -129,6 +129,14 @@ int mi355_rho_shard_partition(const struct row_t *in, uint64_t n, uint32_t key_s
 void mi355_timing_enable(int on);
 int mi355_timing_get(const char **names, double *ms, int cap);
 
+/*
+ * Partition-chain overlap of this thread's joins (default 1): R's and S's
+ * partition passes run on two HIP streams, joined before build/probe.  0 runs
+ * them back to back on one stream, so each kernel's event time is its own
+ * (per-kernel roofline measurements).  Results are identical either way.
+ */
+void mi355_set_partition_overlap(int on);
+
 /* Stream used by calls that take no explicit stream (NULL = library stream). */
 void mi355_set_stream(void *stream);
 

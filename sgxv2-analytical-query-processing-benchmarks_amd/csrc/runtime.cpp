@@ -14,6 +14,7 @@ thread_local std::string t_last_error;
 thread_local bool t_timing = false;
 thread_local void *t_stream = nullptr;
 thread_local Timer t_timer;
+thread_local bool t_overlap = true;
 std::mutex g_ctx_mu;
 std::map<int, std::unique_ptr<Context>> g_ctx;
 }  // namespace
@@ -96,7 +97,23 @@ double Timer::ms_of_prefix(const std::string &prefix) const {
 }
 
 Timer &thread_timer() { return t_timer; }
+Timer &thread_side_timer() {
+    static thread_local Timer t;
+    return t;
+}
+
+hipStream_t side_stream(Context *ctx) {
+    if (!ctx->side) {
+        if (hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) != hipSuccess) return nullptr;
+        for (hipEvent_t *e : {&ctx->ev_fork, &ctx->ev_join})
+            if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return nullptr;
+        for (hipEvent_t *e : {&ctx->ev_t0, &ctx->ev_t1})
+            if (hipEventCreate(e) != hipSuccess) return nullptr;
+    }
+    return ctx->side;
+}
 bool thread_timing_enabled() { return t_timing; }
+bool thread_partition_overlap() { return t_overlap; }
 
 Context *current_context(int *status) {
     int ndev = 0;
@@ -162,6 +179,8 @@ int mi355_device_count(void) {
 }
 
 void mi355_timing_enable(int on) { sgxamd::t_timing = on != 0; }
+
+void mi355_set_partition_overlap(int on) { sgxamd::t_overlap = on != 0; }
 
 int mi355_timing_get(const char **names, double *ms, int cap) {
     const auto &rec = sgxamd::t_timer.records();

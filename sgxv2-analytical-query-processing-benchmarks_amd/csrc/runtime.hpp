@@ -48,6 +48,10 @@ class Timer {
     void collect();
     const std::vector<std::pair<std::string, double>> &records() const { return records_; }
     double ms_of_prefix(const std::string &prefix) const;
+    // after collect(): take over another timer's records (a second stream of the same call)
+    void append(const Timer &other) {
+        records_.insert(records_.end(), other.records_.begin(), other.records_.end());
+    }
     bool enabled() const { return enabled_; }
 
    private:
@@ -65,6 +69,8 @@ class Timer {
 struct Context {
     int device = -1;
     hipStream_t stream = nullptr;  // library stream (non-blocking)
+    hipStream_t side = nullptr;    // second stream: the S partition chain runs beside R's
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_t0 = nullptr, ev_t1 = nullptr;
     std::mutex mu;                 // one call at a time per device context
     // join workspace
     DeviceBuffer inR, inS;         // staging of host relations
@@ -81,7 +87,11 @@ struct Context {
 Context *current_context(int *status);
 
 Timer &thread_timer();
+Timer &thread_side_timer();
+// Lazily created side stream and fork/join/total events of ctx (nullptr on failure).
+hipStream_t side_stream(Context *ctx);
 bool thread_timing_enabled();
+bool thread_partition_overlap();
 hipStream_t thread_stream(Context *ctx, void *explicit_stream);
 
 bool is_device_pointer(const void *p);

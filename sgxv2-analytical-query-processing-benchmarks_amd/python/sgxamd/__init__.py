@@ -128,6 +128,7 @@ SIGNATURES = {
     "mi355_last_join_stats": (C.c_int, [C.POINTER(rho_stats)]),
     "mi355_rho_shard_partition": (C.c_int, [_P, C.c_uint64, C.c_uint32, C.c_uint32, _P, _U64P, _P]),
     "mi355_timing_enable": (None, [C.c_int]),
+    "mi355_set_partition_overlap": (None, [C.c_int]),
     "mi355_timing_get": (C.c_int, [C.POINTER(C.c_char_p), C.POINTER(C.c_double), C.c_int]),
     "mi355_set_stream": (None, [_P]),
     # scan.h
@@ -292,6 +293,11 @@ def shard_partition(inp, n: int, key_shift: int, dest_bits: int, out, stream: in
 
 def timing_enable(on: bool = True) -> None:
     lib.mi355_timing_enable(1 if on else 0)
+
+
+def set_partition_overlap(on: bool = True) -> None:
+    """R/S partition chains on two streams (default) or back to back on one."""
+    lib.mi355_set_partition_overlap(1 if on else 0)
 
 
 def timings() -> list[tuple[str, float]]:

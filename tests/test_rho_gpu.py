@@ -302,3 +302,24 @@ def test_rht_dropin_and_full_size(sgx, gpu):
     assert sgx.rho_join(dR, n, dS, n, algorithm="RHT").matches == n
     del dR, dS
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("case", ["pk_fk", "dups"])
+def test_partition_overlap_same_result(sgx, orc, gpu, case):
+    """Two-stream partition chains (default) and one stream give the same join."""
+    rng = np.random.default_rng(5)
+    if case == "pk_fk":
+        R, S = sgx.reference_relations(1 << 18, 1 << 19)
+    else:
+        R = rel(rng.integers(0, 5000, 60_000).astype(np.uint32))
+        S = rel(rng.integers(0, 5000, 90_000).astype(np.uint32))
+    exp = orc.rho_join_triples(R, S, 4)
+    got = {}
+    try:
+        for on in (True, False):
+            sgx.set_partition_overlap(on)
+            for bits, passes in [(8, 1), (14, 2)]:
+                got[(on, bits)] = gpu_triples(sgx, R, S, radix_bits=bits, passes=passes)
+                assert np.array_equal(sorted_triples(got[(on, bits)]), sorted_triples(exp)), (case, on, bits)
+    finally:
+        sgx.set_partition_overlap(True)
