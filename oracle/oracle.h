@@ -90,6 +90,27 @@ uint64_t oracle_dict_scan(int64_t lo, int64_t hi, const int64_t *dict, uint64_t 
                           int code_bytes, size_t n, int64_t *out);
 uint64_t oracle_scan_count_i32_mt(int32_t lo, int32_t hi, const int32_t *in, size_t n, int nthreads);
 
+/* TPC-H callers (tpch_oracle.c; tables as in sgxamd/tpch.h).  oracle_tpch_filter:
+ * filter_table of selection `which` of `query` into out (rows in input order),
+ * returns the row count.  The queries return the reference's result (Q19: the
+ * final predicate's count) and fill info[0..2] = rows after selection 1..3,
+ * info[3..5] = cardinality of join 1..3. */
+struct CustomerTable;
+struct OrdersTable;
+struct LineItemTable;
+struct PartTable;
+struct NationTable;
+uint64_t oracle_tpch_filter(int query, int which, const struct CustomerTable *c, const struct OrdersTable *o,
+                            const struct LineItemTable *l, const struct PartTable *p, struct row_t *out);
+int64_t oracle_tpch_q3(const struct CustomerTable *c, const struct OrdersTable *o, const struct LineItemTable *l,
+                       int nthreads, int rht, uint64_t *info);
+int64_t oracle_tpch_q10(const struct CustomerTable *c, const struct OrdersTable *o, const struct LineItemTable *l,
+                        const struct NationTable *n, int nthreads, int rht, uint64_t *info);
+int64_t oracle_tpch_q12(const struct LineItemTable *l, const struct OrdersTable *o, int nthreads, int rht,
+                        uint64_t *info);
+int64_t oracle_tpch_q19(const struct LineItemTable *l, const struct PartTable *p, int nthreads, int rht,
+                        uint64_t *info);
+
 #ifdef __cplusplus
 }
 #endif

@@ -54,6 +54,11 @@ def _load() -> C.CDLL:
         "oracle_scan_count_i32_mt": (C.c_uint64, [C.c_int32, C.c_int32, P, C.c_size_t, C.c_int]),
         "oracle_scan_sum_u8": (C.c_uint64, [C.c_uint8, C.c_uint8, P, C.c_size_t]),
         "oracle_dict_scan": (C.c_uint64, [C.c_int64, C.c_int64, P, C.c_uint64, P, C.c_int, C.c_size_t, P]),
+        "oracle_tpch_filter": (C.c_uint64, [C.c_int, C.c_int, P, P, P, P, P]),
+        "oracle_tpch_q3": (C.c_int64, [P, P, P, C.c_int, C.c_int, U64P]),
+        "oracle_tpch_q10": (C.c_int64, [P, P, P, P, C.c_int, C.c_int, U64P]),
+        "oracle_tpch_q12": (C.c_int64, [P, P, C.c_int, C.c_int, U64P]),
+        "oracle_tpch_q19": (C.c_int64, [P, P, C.c_int, C.c_int, U64P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -160,3 +165,34 @@ def dict_scan(lo: int, hi: int, dictionary, codes):
     out = np.zeros(max(k, 1), dtype=np.int64)
     lib.oracle_dict_scan(lo, hi, _p(d), len(d), _p(c), c.dtype.itemsize, len(c), _p(out))
     return out[:k]
+
+
+# ---------------------------------------------------------------- TPC-H ---
+# `tables` is any object with .struct(name) -> ctypes table struct (host columns),
+# e.g. sgxamd.tpch.Tables; the structs follow sgxamd/tpch.h.
+_ROW = np.dtype([("key", "<u4"), ("payload", "<u4")])
+
+
+def _sp(tables, name):
+    s = tables.struct(name)
+    return C.addressof(s) if s is not None else None, s
+
+
+def tpch_filter(query: int, which: int, tables) -> np.ndarray:
+    """filter_table (filters.hpp:118-138) of one selection: rows in input order."""
+    refs = [_sp(tables, t) for t in ("customer", "orders", "lineitem", "part")]
+    cap = max(tables.n(t) for t in ("customer", "orders", "lineitem", "part")) + 1
+    out = np.zeros(cap, dtype=_ROW)
+    k = lib.oracle_tpch_filter(query, which, *[r[0] for r in refs], out.ctypes.data)
+    return out[:k]
+
+
+def tpch_query(query: int, tables, nthreads: int = 4, rht: bool = False) -> dict:
+    """tpch.cpp's query `query` on the CPU restatement: result + per-step sizes."""
+    info = (C.c_uint64 * 6)()
+    names = {3: ("customer", "orders", "lineitem"), 10: ("customer", "orders", "lineitem", "nation"),
+             12: ("lineitem", "orders"), 19: ("lineitem", "part")}[query]
+    refs = [_sp(tables, t) for t in names]
+    fn = getattr(lib, f"oracle_tpch_q{query}")
+    res = fn(*[r[0] for r in refs], nthreads, 1 if rht else 0, info)
+    return {"result": int(res), "filtered": [int(x) for x in info[0:3]], "join_matches": [int(x) for x in info[3:6]]}

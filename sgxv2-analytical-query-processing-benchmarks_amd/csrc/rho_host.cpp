@@ -13,6 +13,7 @@
 #include <string>
 
 #include "common.hpp"
+#include "rho_device.hpp"
 #include "rho_internal.hpp"
 #include "runtime.hpp"
 #include "sgxamd/rho.h"
@@ -156,7 +157,8 @@ void plan_relation(Arena &A, RelPlan &rp, uint64_t n, const Policy &pol) {
 // the task counts into output offsets, then a write pass; `out` must be device
 // memory with room for out_cap triples (MI355_ERR_CAPACITY otherwise).
 int join_device(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const row_t *dS, uint64_t nS,
-                const mi355_rho_opts *opts, mi355_rho_stats *st, output_triple_t *out, uint64_t out_cap) {
+                const mi355_rho_opts *opts, mi355_rho_stats *st, output_triple_t *out, uint64_t out_cap,
+                DeviceBuffer *grow) {
     const uint32_t key_shift = opts ? opts->key_shift : 0;
     const bool materialize = opts && opts->materialize;
     const int algo = (opts && opts->algorithm == MI355_ALGO_RHT) ? kAlgoHistogram : kAlgoChaining;
@@ -241,6 +243,11 @@ int join_device(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const
         RHO_HIP(hipMemcpyAsync(ctx->host_result, result, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
         RHO_HIP(hipStreamSynchronize(s));
         const uint64_t total = ctx->host_result[0];
+        if (grow && total > out_cap) {  // caller-owned growable output (device pipelines)
+            RHO_HIP(grow->ensure(std::max<uint64_t>(total, 1) * sizeof(output_triple_t)));
+            out = grow->as<output_triple_t>();
+            out_cap = total;
+        }
         if (total > out_cap || (total > 0 && out == nullptr)) {
             tm.end_call();
             tm.collect();
@@ -389,8 +396,10 @@ int mi355_rho_join_ex(const row_t *R, uint64_t nR, const row_t *S, uint64_t nS, 
     return MI355_OK;
 }
 
+}  // extern "C"
+
 // Host chunked table of n triples (ChunkedTable.cpp layout: TUPLES_PER_CHUNK per chunk).
-static chunked_table_t *make_chunked_table(const output_triple_t *src, uint64_t n) {
+chunked_table_t *rho::make_chunked_table(const output_triple_t *src, uint64_t n) {
     auto *t = static_cast<chunked_table_t *>(std::calloc(1, sizeof(chunked_table_t)));
     if (!t) return nullptr;
     const uint64_t per = SGXAMD_TUPLES_PER_CHUNK;
@@ -418,6 +427,8 @@ static chunked_table_t *make_chunked_table(const output_triple_t *src, uint64_t 
     t->num_tuples = n;
     return t;
 }
+
+extern "C" {
 
 void mi355_free_chunked_table(chunked_table_t *table) {
     if (!table) return;
@@ -470,7 +481,7 @@ static int table_join(const table_t *relR, const table_t *relS, const joinconfig
     out->result = nullptr;
     out->result_type = 0;
     if (materialize) {
-        chunked_table_t *t = make_chunked_table(host, st.matches);
+        chunked_table_t *t = rho::make_chunked_table(host, st.matches);
         std::free(host);
         if (!t) {
             set_last_error("host allocation of the chunked table failed");

@@ -77,6 +77,9 @@ struct Context {
     DeviceBuffer t1R, t1S, t2R, t2S;
     Arena scratch;
     DeviceBuffer mat;              // materialised output_triple_t (when the caller's buffer is host memory)
+    // TPC-H workspace: staged host columns, selection bits/offsets, intermediate
+    // relations and join-result triples
+    DeviceBuffer tp_cols[12], tp_mask, tp_blk, tp_rel[3], tp_trip;
     // scan workspace
     DeviceBuffer scan_in, scan_out, scan_aux, scan_dict;
     uint64_t *host_result = nullptr;  // pinned 64 x u64

@@ -113,6 +113,47 @@ class rho_stats(C.Structure):
         return {f: getattr(self, f) for f, _ in self._fields_}
 
 
+# TPC-H tables (sgxamd/tpch.h = TpcHTypes.hpp:53-87): column pointers, host or device.
+class LineItemTable(C.Structure):
+    _fields_ = [("numTuples", C.c_uint64), ("l_orderkey", C.c_void_p), ("l_shipdate", C.c_void_p),
+                ("l_commitdate", C.c_void_p), ("l_receiptdate", C.c_void_p), ("l_shipmode", C.c_void_p),
+                ("l_partkey", C.c_void_p), ("l_quantity", C.c_void_p), ("l_shipinstruct", C.c_void_p),
+                ("l_returnflag", C.c_void_p)]
+
+
+class OrdersTable(C.Structure):
+    _fields_ = [("numTuples", C.c_uint64), ("o_orderkey", C.c_void_p), ("o_orderdate", C.c_void_p),
+                ("o_custkey", C.c_void_p)]
+
+
+class CustomerTable(C.Structure):
+    _fields_ = [("numTuples", C.c_uint64), ("c_custkey", C.c_void_p), ("c_mktsegment", C.c_void_p),
+                ("c_nationkey", C.c_void_p)]
+
+
+class PartTable(C.Structure):
+    _fields_ = [("numTuples", C.c_uint64), ("p_partkey", C.c_void_p), ("p_brand", C.c_void_p),
+                ("p_size", C.c_void_p), ("p_container", C.c_void_p)]
+
+
+class NationTable(C.Structure):
+    _fields_ = [("numTuples", C.c_uint64), ("n_nationkey", C.c_void_p)]
+
+
+class tpch_stats(C.Structure):
+    _fields_ = [("result", C.c_uint64), ("join_matches", C.c_uint64 * 3), ("filtered", C.c_uint64 * 3),
+                ("ms_selection", C.c_double * 3), ("ms_join", C.c_double * 3), ("ms_copy", C.c_double),
+                ("ms_total", C.c_double), ("ms_h2d", C.c_double), ("input_tuples", C.c_uint64),
+                ("column_bytes", C.c_uint64)]
+
+    def as_dict(self) -> dict:
+        out = {}
+        for f, _ in self._fields_:
+            v = getattr(self, f)
+            out[f] = list(v) if hasattr(v, "__len__") else v
+        return out
+
+
 # Every symbol declared in include/sgxamd/*.h with its (restype, argtypes).
 _P = C.c_void_p
 _U64P = C.POINTER(C.c_uint64)
@@ -159,6 +200,34 @@ SIGNATURES = {
     "mi355_gen_zipf_dev": (C.c_int, [_P, C.c_uint64, C.c_uint64, C.c_uint32, C.c_double, C.c_uint64, _P]),
     "mi355_gen_scan_u8_dev": (C.c_int, [_P, C.c_size_t, C.c_int, C.c_uint64, _P]),
     "mi355_gen_scan_i32_dev": (C.c_int, [_P, C.c_size_t, C.c_int, C.c_uint64, _P]),
+    # tpch.h
+    "mi355_tpch_q3": (C.c_int, [C.POINTER(CustomerTable), C.POINTER(OrdersTable), C.POINTER(LineItemTable), C.c_int,
+                                C.POINTER(tpch_stats)]),
+    "mi355_tpch_q10": (C.c_int, [C.POINTER(CustomerTable), C.POINTER(OrdersTable), C.POINTER(LineItemTable),
+                                 C.POINTER(NationTable), C.c_int, C.POINTER(tpch_stats)]),
+    "mi355_tpch_q12": (C.c_int, [C.POINTER(LineItemTable), C.POINTER(OrdersTable), C.c_int, C.POINTER(tpch_stats)]),
+    "mi355_tpch_q19": (C.c_int, [C.POINTER(LineItemTable), C.POINTER(PartTable), C.c_int, C.POINTER(tpch_stats),
+                                 C.c_int, C.POINTER(C.c_void_p)]),
+    "mi355_tpch_filter": (C.c_int, [C.c_int, C.c_int, C.POINTER(CustomerTable), C.POINTER(OrdersTable),
+                                    C.POINTER(LineItemTable), C.POINTER(PartTable), _P, C.c_uint64, _U64P]),
+    "mi355_tpch_load_lineitem": (C.c_int, [C.POINTER(LineItemTable), C.c_char_p, C.c_int, C.c_int, C.c_int]),
+    "mi355_tpch_load_orders": (C.c_int, [C.POINTER(OrdersTable), C.c_char_p, C.c_int, C.c_int, C.c_int]),
+    "mi355_tpch_load_customer": (C.c_int, [C.POINTER(CustomerTable), C.c_char_p, C.c_int, C.c_int, C.c_int]),
+    "mi355_tpch_load_part": (C.c_int, [C.POINTER(PartTable), C.c_char_p, C.c_int, C.c_int, C.c_int]),
+    "mi355_tpch_load_nation": (C.c_int, [C.POINTER(NationTable), C.c_char_p, C.c_int, C.c_int, C.c_int]),
+    "mi355_tpch_store": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(LineItemTable), C.POINTER(OrdersTable),
+                                   C.POINTER(CustomerTable), C.POINTER(PartTable), C.POINTER(NationTable)]),
+    "mi355_tpch_free_lineitem": (None, [C.POINTER(LineItemTable)]),
+    "mi355_tpch_free_orders": (None, [C.POINTER(OrdersTable)]),
+    "mi355_tpch_free_customer": (None, [C.POINTER(CustomerTable)]),
+    "mi355_tpch_free_part": (None, [C.POINTER(PartTable)]),
+    "mi355_tpch_free_nation": (None, [C.POINTER(NationTable)]),
+    "mi355_tpch_generate": (C.c_int, [C.c_uint32, C.c_uint64, C.POINTER(LineItemTable), C.POINTER(OrdersTable),
+                                      C.POINTER(CustomerTable), C.POINTER(PartTable), C.POINTER(NationTable)]),
+    "mi355_tpch_sizes": (C.c_int, [C.c_uint32, C.c_uint64, _U64P, _U64P, _U64P, _U64P, _U64P]),
+    "mi355_tpch_generate_dev": (C.c_int, [C.c_uint32, C.c_uint64, C.POINTER(LineItemTable), C.POINTER(OrdersTable),
+                                          C.POINTER(CustomerTable), C.POINTER(PartTable), C.POINTER(NationTable),
+                                          _P]),
 }
 
 
@@ -269,7 +338,16 @@ def chunked_table_triples(res: result_t):
 
     if not res.materialized or res.result_type != 1 or not res.result:
         return np.zeros((0, 3), dtype=np.uint32)
-    t = C.cast(res.result, C.POINTER(chunked_table_t)).contents
+    return chunked_table_triples_ptr(res.result)
+
+
+def chunked_table_triples_ptr(table_ptr: int):
+    """The triples of the chunked_table_t at table_ptr, as chunked_table_triples."""
+    import numpy as np
+
+    if not table_ptr:
+        return np.zeros((0, 3), dtype=np.uint32)
+    t = C.cast(table_ptr, C.POINTER(chunked_table_t)).contents
     parts = []
     for c in range(t.num_chunks):
         base = t.chunks[c]

@@ -15,12 +15,18 @@ LIB = os.path.join(PKG, "libsgxamd.so")
 CXX_SYMBOLS = {
     "RHO": "_Z3RHOPK7table_tS1_PK12joinconfig_t",
     "run_join": "_Z8run_joinP8result_tPK7table_tS3_PKcPK12joinconfig_t",
+    # TPC-H callers, tpch.hpp:7-21, and a loader, TpcHCommons.hpp:33
+    "tpch_q3": "_Z7tpch_q3P8result_tPK13CustomerTablePK11OrdersTablePK13LineItemTablePKcP12joinconfig_t",
+    "tpch_q10": "_Z8tpch_q10P8result_tPK13CustomerTablePK11OrdersTablePK13LineItemTablePK11NationTablePKcP12joinconfig_t",
+    "tpch_q12": "_Z8tpch_q12P8result_tPK13LineItemTablePK11OrdersTablePKcP12joinconfig_t",
+    "tpch_q19": "_Z8tpch_q19P8result_tPK13LineItemTablePK9PartTablePKcP12joinconfig_t",
+    "load_lineitems_from_binary": "_Z26load_lineitems_from_binaryP13LineItemTablehh",
 }
 
 
 def declared_c_functions():
     names = set()
-    for h in ("rho.h", "scan.h", "generator.h"):
+    for h in ("rho.h", "scan.h", "generator.h", "tpch.h"):
         text = open(os.path.join(INCLUDE, h)).read()
         text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
         names |= set(re.findall(r"\b(mi355_\w+)\s*\(", text))
