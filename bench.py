@@ -62,6 +62,8 @@ def main():
     ap.add_argument("--partition-overlap", type=int, choices=[0, 1], default=1,
                     help="1: R/S partition chains on two streams (timed region); 0: one stream")
     ap.add_argument("--no-scan", action="store_true")
+    ap.add_argument("--no-tpch", action="store_true")
+    ap.add_argument("--tpch-scale-milli", type=int, default=10000, help="TPC-H scale factor x 1000 (10000 = SF10)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -257,6 +259,55 @@ def main():
         del col, bv, idx
         torch.cuda.empty_cache()
 
+    # ---------------- TPC-H callers: Q3/Q10/Q12/Q19 on device-resident
+    # synthetic tables, one GPU (the pipelines are single-device; skipped for N > 1)
+    tpch_info = None
+    if not args.no_tpch and world == 1 and args.workload == "c2":
+        import sgxamd.tpch as T
+
+        sm = args.tpch_scale_milli
+        tb = T.generate_dev(sm, 42, device=dev, stream=stream)
+        torch.cuda.synchronize()
+        tpch_info = {"scale_factor": sm / 1000, "rows": dict(tb.sizes), "algorithm": args.algorithm,
+                     "data": "synthetic TPC-H-shaped tables (tpch_gen.hpp, spec distributions), device-generated"}
+        for q in (3, 10, 12, 19):
+            fn = T.QUERIES[q]
+            for _ in range(max(1, args.warmup)):
+                fn(tb, args.algorithm)
+            runs = []
+            t1 = time.perf_counter()
+            for _ in range(args.steps):
+                runs.append(fn(tb, args.algorithm))
+            el = (time.perf_counter() - t1) / args.steps
+            ms = statistics.median(r["ms_total"] for r in runs)
+            r = runs[-1]
+            tpch_info[f"Q{q}"] = {
+                "result": r["result"], "join_matches": r["join_matches"], "filtered": r["filtered"],
+                "ms_total_device": round(ms, 4), "ms_wall_per_query": round(el * 1e3, 4),
+                "ms_selection": [round(x, 4) for x in r["ms_selection"]],
+                "ms_join": [round(x, 4) for x in r["ms_join"]], "ms_copy": round(r["ms_copy"], 4),
+                "M_rec_per_s": round(r["input_tuples"] / (ms * 1e3), 1),
+                "column_GB_per_s": round(r["column_bytes"] / (ms * 1e-3) / 1e9, 1),
+            }
+        if rank == 0 and not args.no_cpu_baseline:  # the oracle's tpch.cpp restatement, SF 1 host copy
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import oracle
+
+            host = T.to_numpy(T.generate_dev(1000, 42, device=dev, stream=stream))
+            cpu_t = {}
+            for q in (3, 10, 12, 19):
+                t1 = time.perf_counter()
+                oracle.tpch_query(q, host, nthreads=args.cpu_threads)
+                el = time.perf_counter() - t1
+                n_in = sum(host.n(t) for t in T.QUERY_TABLES[q])
+                cpu_t[f"Q{q}"] = {"ms": round(el * 1e3, 2), "M_rec_per_s": round(n_in / el / 1e6, 1)}
+            tpch_info["cpu_baseline"] = {"kind": "port", "cores": args.cpu_threads, "scale_factor": 1.0,
+                                         "sample": "oracle tpch.cpp restatement (scalar filter_table, pthreads "
+                                                   "RHO joins), one run per query", **cpu_t}
+            del host
+        del tb
+        torch.cuda.empty_cache()
+
     # ---------------- CPU baseline: restated reference RHO on this host, rank 0 at N=1
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -290,7 +341,7 @@ def main():
                     + " relations, 8-byte {key, payload} tuples",
             "config": {"workload": workload, "algorithm": args.algorithm, "global_R": gR, "global_S": gS,
                        "parallelism": f"radix-shard{world}"},
-            "roofline": roofline, "cpu_baseline": cpu, "rho": rho_info, "scan": scan_info,
+            "roofline": roofline, "cpu_baseline": cpu, "rho": rho_info, "scan": scan_info, "tpch": tpch_info,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -19,5 +19,7 @@ d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 print("value", d["value"], "ms/step", d["ms_per_step"], "roofline", d["roofline"]["kernel"], d["roofline"]["frac"])
 print(json.dumps(d["rho"]["kernel_ms_avg"]))
 sc=d.get("scan")
+tp=d.get("tpch")
+if tp: print("tpch SF", tp["scale_factor"], json.dumps({q: (tp[q]["ms_total_device"], tp[q]["M_rec_per_s"], tp[q]["column_GB_per_s"], tp[q]["result"]) for q in ("Q3","Q10","Q12","Q19")}))
 if sc: print("scan count GB/s", sc["count"]["input_GB_per_s"], "bv", sc["bitvector"]["total_GB_per_s"], "index", sc["index"]["total_GB_per_s"], json.dumps(sc["index"]["kernel_ms_avg"]))
 PY

@@ -182,8 +182,10 @@ int join_device(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const
     plan_relation(A, pr, nR, pol);
     plan_relation(A, ps, nS, pol);
     const uint64_t P = 1ull << pol.bits;
-    const uint32_t join_grid = (uint32_t)std::min<uint64_t>(P, 2048);
     const uint32_t over_cap = (uint32_t)(nS / kSChunk + 1);
+    // one workgroup per task up to 2048 (few partitions with a large S — a tiny build
+    // side — still spread their S chunks over the chip)
+    const uint32_t join_grid = (uint32_t)std::min<uint64_t>(P + over_cap - 1, 2048);
     const size_t off_over = A.reserve(sizeof(uint64_t) * over_cap);
     const size_t off_nover = A.reserve(sizeof(uint32_t));
     const size_t off_counts = A.reserve(sizeof(uint64_t) * (materialize ? P + over_cap : join_grid));
