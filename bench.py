@@ -59,7 +59,7 @@ def main():
                          "global (strong), c5 = Zipf 0.75 |R| = |S| = 2^28 global (strong)")
     ap.add_argument("--algorithm", choices=["RHO", "RHT"], default="RHO",
                     help="build/probe: RHO bucket chaining (headline) or RHT histogram join")
-    ap.add_argument("--partition-overlap", type=int, choices=[0, 1], default=1,
+    ap.add_argument("--partition-overlap", type=int, choices=[0, 1], default=0,
                     help="1: R/S partition chains on two streams (timed region); 0: one stream")
     ap.add_argument("--no-scan", action="store_true")
     ap.add_argument("--no-tpch", action="store_true")

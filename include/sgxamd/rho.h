@@ -130,10 +130,10 @@ void mi355_timing_enable(int on);
 int mi355_timing_get(const char **names, double *ms, int cap);
 
 /*
- * Partition-chain overlap of this thread's joins (default 1): R's and S's
- * partition passes run on two HIP streams, joined before build/probe.  0 runs
- * them back to back on one stream, so each kernel's event time is its own
- * (per-kernel roofline measurements).  Results are identical either way.
+ * Partition-chain overlap of this thread's joins (default 0): 1 runs R's and S's
+ * partition passes on two HIP streams, joined before build/probe; 0 runs them back
+ * to back on one stream, so each kernel's event time is its own.  Results are
+ * identical either way (DESIGN.md §7 has the measurements behind the default).
  */
 void mi355_set_partition_overlap(int on);
 

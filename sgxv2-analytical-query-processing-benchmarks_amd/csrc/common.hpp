@@ -21,6 +21,29 @@ __device__ __forceinline__ uint4 ld_nt(const uint4 *p) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 __device__ __forceinline__ uint64_t ld_nt(const uint64_t *p) { return __builtin_nontemporal_load(p); }
+
+// Bijection blockIdx -> work item that gives each of the 8 XCDs (blocks are dealt to
+// XCDs round-robin by blockIdx) one contiguous run of the n items, so neighbouring
+// segments — which share partially written output lines — meet in the same L2.
+__device__ __forceinline__ uint32_t xcd_contiguous(uint32_t b, uint32_t n) {
+    constexpr uint32_t X = 8;
+    const uint32_t q = n / X, r = n % X, x = b % X, i = b / X;
+    return x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
+}
+
+// Raw buffer resource over [base, base + bytes) (gfx9 dword3 for untyped dword access).
+// Loads through it take a 32-bit per-lane offset and a uniform SGPR offset, so a
+// streaming loop keeps no 64-bit per-lane addresses live, and out-of-range lanes
+// read 0 (the hardware bounds check) instead of needing a tail path.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, (int)bytes, 0x00020000);
+}
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+// non-temporal 8-byte buffer load (aux bit 1 = nt)
+__device__ __forceinline__ uint64_t buf_ld_nt_u64(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    const u32x2_t v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, (int)soff, 2);
+    return ((uint64_t)v.y << 32) | v.x;
+}
 __device__ __forceinline__ void st_nt(uint64_t *p, uint64_t v) { __builtin_nontemporal_store(v, p); }
 __device__ __forceinline__ void st_nt(uint32_t *p, uint32_t v) { __builtin_nontemporal_store(v, p); }
 

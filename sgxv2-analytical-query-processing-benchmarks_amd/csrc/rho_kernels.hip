@@ -56,7 +56,9 @@ __global__ __launch_bounds__(kBlock) void k_hist(const uint32_t *__restrict__ in
                                                  uint32_t nseg_stride) {
     __shared__ uint32_t h[kMaxF];
     __shared__ uint32_t sbase[kMaxF + 1];
-    const uint32_t g = blockIdx.x;
+    // XCD-contiguous segments for one-region passes (measured faster there, slower
+    // over pass 2's many regions)
+    const uint32_t g = layout == kDigitMajor ? xcd_contiguous(blockIdx.x, gridDim.x) : blockIdx.x;
     uint32_t r;
     uint64_t b, e;
     if (!seg_lookup(m, g, sbase, r, b, e)) return;
@@ -241,24 +243,17 @@ template <int BITS, int ITEMS, int NT>
 constexpr int scatter_waves_per_simd() {
     constexpr int k = (160 * 1024) / (int)sizeof(ScatterLds<BITS, ITEMS, NT>);
     constexpr int w = (k < 1 ? 1 : k) * NT / 256;
-    return w < 1 ? 1 : (w > 8 ? 8 : w);
+    // at most 4 waves/SIMD (128 VGPRs): fewer registers spill, and a scratch reload is
+    // a vector-memory op whose wait would also wait for every store in flight
+    return w < 1 ? 1 : (w > 4 ? 4 : w);
 }
 
+// One tile of the segment behind rsrc (byte offset soff of the tile); lanes past the
+// segment end read 0 through the buffer bounds check.
 template <int ITEMS, int NT>
-__device__ __forceinline__ void load_tile(const uint64_t *__restrict__ in, uint64_t tb, uint64_t e,
-                                          uint64_t (&dst)[ITEMS]) {
-    constexpr uint32_t TILE = NT * ITEMS;
-    if (tb + TILE <= e) {
+__device__ __forceinline__ void load_tile(__amdgpu_buffer_rsrc_t rs, uint32_t soff, uint64_t (&dst)[ITEMS]) {
 #pragma unroll
-        for (int k = 0; k < ITEMS; ++k) dst[k] = ld_nt(in + tb + threadIdx.x + k * NT);
-    } else {
-        const uint32_t tn = (uint32_t)(e - tb);
-#pragma unroll
-        for (int k = 0; k < ITEMS; ++k) {
-            const uint32_t li = threadIdx.x + k * NT;
-            dst[k] = li < tn ? in[tb + li] : 0ull;
-        }
-    }
+    for (int k = 0; k < ITEMS; ++k) dst[k] = buf_ld_nt_u64(rs, threadIdx.x * 8u, soff + (uint32_t)(k * NT * 8));
 }
 
 // Block-wide exclusive scan of two u32 counters at once (one __syncthreads).
@@ -289,18 +284,19 @@ __device__ __forceinline__ void block_scan2(uint32_t a, uint32_t b, uint32_t (&w
     eb = pb + ib - b;
 }
 
+// Phases A-C of one tile: the tile ends up digit-sorted in L.tile (v is dead after).
 template <int BITS, int ITEMS, int NT>
-__device__ __forceinline__ void scatter_tile(ScatterLds<BITS, ITEMS, NT> &L, uint64_t &pend, uint32_t &carried,
-                                             const uint64_t (&v)[ITEMS], uint64_t *__restrict__ out, uint32_t tn,
-                                             uint32_t shift, uint64_t tbase_global) {
-    constexpr uint32_t F = 1u << BITS, mask = F - 1, NG = NT / kGran, NW = NT / kWave;
-    constexpr uint32_t CS = kGran - 1;
+__device__ __forceinline__ uint32_t scatter_tile_sort(ScatterLds<BITS, ITEMS, NT> &L, uint64_t &pend,
+                                                      uint32_t &carried, const uint64_t (&v)[ITEMS],
+                                                      uint64_t *__restrict__ out, uint32_t tn, uint32_t shift,
+                                                      uint64_t tbase_global) {
+    constexpr uint32_t F = 1u << BITS, mask = F - 1, NW = NT / kWave;
     const uint32_t tid = threadIdx.x;
 #ifdef SGXAMD_ABLATE_NOSORT  // development ablation (tools/part_bench): the memory pipeline alone
 #pragma unroll
     for (int k = 0; k < ITEMS; ++k)
         if (tid + k * NT < tn) st_nt(out + tbase_global + tid + k * NT, v[k]);
-    return;
+    return 0;
 #endif
     (void)tbase_global;
     // A. slot of every tuple inside its digit
@@ -346,6 +342,19 @@ __device__ __forceinline__ void scatter_tile(ScatterLds<BITS, ITEMS, NT> &L, uin
         }
     }
     __syncthreads();
+    return gtot;
+}
+
+// Phases D-E of the tile sorted by scatter_tile_sort (gtot = its granule count).
+template <int BITS, int ITEMS, int NT>
+__device__ __forceinline__ void scatter_tile_write(ScatterLds<BITS, ITEMS, NT> &L, uint64_t *__restrict__ out,
+                                                   uint32_t gtot) {
+    constexpr uint32_t F = 1u << BITS, NG = NT / kGran;
+    constexpr uint32_t CS = kGran - 1;
+#ifdef SGXAMD_ABLATE_NOSORT
+    return;
+#endif
+    const uint32_t tid = threadIdx.x;
     // D. whole granules, 16 lanes (one 128-B line) per granule
     const uint32_t lane = tid & (kGran - 1), grp = tid / kGran;
     for (uint32_t j = grp; j < gtot; j += NG) {
@@ -388,7 +397,7 @@ __global__ __launch_bounds__(NT, (scatter_waves_per_simd<BITS, ITEMS, NT>())) vo
     constexpr uint32_t F = 1u << BITS, NG = NT / kGran, CS = kGran - 1;
     static_assert(F <= NT, "one owner thread per digit");
     __shared__ ScatterLds<BITS, ITEMS, NT> L;
-    const uint32_t g = blockIdx.x;
+    const uint32_t g = xcd_contiguous(blockIdx.x, gridDim.x);
     uint32_t r;
     uint64_t b, e;
     if (!seg_lookup(m, g, L.sbase, r, b, e)) return;
@@ -401,15 +410,41 @@ __global__ __launch_bounds__(NT, (scatter_waves_per_simd<BITS, ITEMS, NT>())) vo
         L.cnt[tid] = 0;
     }
     __syncthreads();  // sbase (aliased with tile) is dead from here on
+    // segments hold far fewer than 2^29 tuples (seg_size_for), so byte offsets fit 32 bits
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(in + b, (uint32_t)((e - b) * sizeof(uint64_t)));
+    // Two tiles in flight: tile T+2 loads into T's registers as soon as T is sorted into
+    // LDS, and T+1's registers are waited for right after that — before T's stores are
+    // issued.  gfx950 retires loads and stores through one in-order vmcnt, so a wait for
+    // a load also waits for every older store; placed here, the older stores are those of
+    // tile T-1, issued a whole sort phase earlier, instead of the ones just issued.
+    // Loads past the segment end read 0 (buffer bounds), so every load is unconditional
+    // and the compiler sees a fixed count of loads between a load and its use.
     uint64_t va[ITEMS], vb[ITEMS];
-    load_tile<ITEMS, NT>(in, b, e, va);
-    for (uint64_t tb = b; tb < e; tb += 2 * TILE) {
-        if (tb + TILE < e) load_tile<ITEMS, NT>(in, tb + TILE, e, vb);
-        scatter_tile<BITS, ITEMS, NT>(L, pend, carried, va, out, (uint32_t)min<uint64_t>(TILE, e - tb), shift, tb);
+    load_tile<ITEMS, NT>(rs, 0u, va);
+    load_tile<ITEMS, NT>(rs, TILE * 8u, vb);
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) asm volatile("" ::"v"(va[k]));
+    // Each sort reads registers that were waited for earlier in straight-line code, so
+    // the compiler's wait analysis never merges a loop back-edge into a first use.
+    uint32_t gt = scatter_tile_sort<BITS, ITEMS, NT>(L, pend, carried, va, out, (uint32_t)min<uint64_t>(TILE, e - b),
+                                                     shift, b);
+    for (uint64_t tb = b;; tb += 2 * TILE) {
+        const uint32_t off = (uint32_t)((tb - b) * 8);
+        // tile tb is sorted in LDS; vb holds (in flight) tile tb + TILE
+        load_tile<ITEMS, NT>(rs, off + 2 * TILE * 8u, va);
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) asm volatile("" ::"v"(vb[k]));
+        scatter_tile_write<BITS, ITEMS, NT>(L, out, gt);
         if (tb + TILE >= e) break;
-        const uint64_t t2 = tb + TILE;
-        if (t2 + TILE < e) load_tile<ITEMS, NT>(in, t2 + TILE, e, va);
-        scatter_tile<BITS, ITEMS, NT>(L, pend, carried, vb, out, (uint32_t)min<uint64_t>(TILE, e - t2), shift, t2);
+        gt = scatter_tile_sort<BITS, ITEMS, NT>(L, pend, carried, vb, out, (uint32_t)min<uint64_t>(TILE, e - tb - TILE),
+                                                shift, tb + TILE);
+        load_tile<ITEMS, NT>(rs, off + 3 * TILE * 8u, vb);
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) asm volatile("" ::"v"(va[k]));
+        scatter_tile_write<BITS, ITEMS, NT>(L, out, gt);
+        if (tb + 2 * TILE >= e) break;
+        gt = scatter_tile_sort<BITS, ITEMS, NT>(L, pend, carried, va, out,
+                                                (uint32_t)min<uint64_t>(TILE, e - tb - 2 * TILE), shift, tb + 2 * TILE);
     }
     // flush the carried (partial) granules
     __syncthreads();

@@ -14,7 +14,7 @@ thread_local std::string t_last_error;
 thread_local bool t_timing = false;
 thread_local void *t_stream = nullptr;
 thread_local Timer t_timer;
-thread_local bool t_overlap = true;
+thread_local bool t_overlap = false;
 std::mutex g_ctx_mu;
 std::map<int, std::unique_ptr<Context>> g_ctx;
 }  // namespace
