@@ -229,7 +229,7 @@ int join_device(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const
     uint64_t *result = A.at<uint64_t>(off_result);
     const uint32_t hash_shift = key_shift + pol.bits;
     tm.mark("join_tasks");
-    RHO_HIP(launch_make_tasks(pcR, pcS, P, over, over_cap, n_over, s));
+    RHO_HIP(launch_make_tasks(pcR, pcS, P, over, over_cap, n_over, result + 1, s));
     if (!materialize) {
         tm.mark("join_build_probe");
         RHO_HIP(launch_join(fR, fS, psR, pcR, psS, pcS, P, over, n_over, hash_shift, pol.rcap, join_grid, kJoinCount,
@@ -263,8 +263,6 @@ int join_device(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const
     }
     tm.end_call();
     if (s2) RHO_HIP(hipEventRecord(ctx->ev_t1, s));
-    RHO_HIP(launch_max(pcR, P, result + 1, s));
-    RHO_HIP(launch_max(pcS, P, result + 2, s));
     RHO_HIP(hipMemcpyAsync(ctx->host_result, result, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     RHO_HIP(hipMemcpyAsync(ctx->host_result + 3, n_over, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     RHO_HIP(hipStreamSynchronize(s));

@@ -618,12 +618,20 @@ __global__ __launch_bounds__(kBlock) void k_join(const uint64_t *__restrict__ R,
                 for (uint64_t s0 = 0; s0 < nS; s0 += RCAP) {  // PROBE-LOOP (:429-436)
                     uint32_t ks[U], cur[U];
                     uint32_t sv[MODE == kJoinWrite ? U : 1];
+                    if constexpr (MODE == kJoinWrite) {
 #pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        const uint64_t i = s0 + tid + u * kBlock;
-                        const uint64_t x = i < nS ? ld_nt(sp + i) : 0ull;
-                        ks[u] = (uint32_t)x;
-                        if constexpr (MODE == kJoinWrite) sv[u] = (uint32_t)(x >> 32);
+                        for (int u = 0; u < U; ++u) {
+                            const uint64_t i = s0 + tid + u * kBlock;
+                            const uint64_t x = i < nS ? ld_nt(sp + i) : 0ull;
+                            ks[u] = (uint32_t)x;
+                            sv[u] = (uint32_t)(x >> 32);
+                        }
+                    } else {
+#pragma unroll
+                        for (int u = 0; u < U; ++u) {
+                            const uint64_t i = s0 + tid + u * kBlock;
+                            ks[u] = i < nS ? __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(sp + i)) : 0u;
+                        }
                     }
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
@@ -929,24 +937,47 @@ hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, 
 __global__ __launch_bounds__(kBlock) void k_make_tasks(const uint64_t *__restrict__ r_count,
                                                        const uint64_t *__restrict__ s_count, uint64_t P,
                                                        uint64_t *__restrict__ over, uint32_t over_cap,
-                                                       uint32_t *__restrict__ n_over) {
+                                                       uint32_t *__restrict__ n_over, uint64_t *__restrict__ max_rs) {
+    uint64_t mr = 0, ms = 0;  // largest partitions (diagnostics), folded into this pass over the counts
     for (uint64_t p = blockIdx.x * (uint64_t)kBlock + threadIdx.x; p < P; p += (uint64_t)gridDim.x * kBlock) {
-        const uint64_t nS = s_count[p];
-        if (r_count[p] == 0 || nS <= kSChunk) continue;
+        const uint64_t nS = s_count[p], nR = r_count[p];
+        mr = nR > mr ? nR : mr;
+        ms = nS > ms ? nS : ms;
+        if (nR == 0 || nS <= kSChunk) continue;
         const uint32_t k = (uint32_t)((nS + kSChunk - 1) / kSChunk) - 1;
         const uint32_t base = atomicAdd(n_over, k);
         for (uint32_t j = 0; j < k && base + j < over_cap; ++j) over[base + j] = p | ((uint64_t)(j + 1) << 32);
     }
+    if (max_rs) {  // one pair of device atomics per workgroup
+        __shared__ uint64_t red[2][kWaves];
+#pragma unroll
+        for (int off = kWave / 2; off > 0; off >>= 1) {
+            const uint64_t a = __shfl_xor(mr, off, kWave), b = __shfl_xor(ms, off, kWave);
+            mr = a > mr ? a : mr;
+            ms = b > ms ? b : ms;
+        }
+        if (__lane_id() == 0) {
+            red[0][threadIdx.x / kWave] = mr;
+            red[1][threadIdx.x / kWave] = ms;
+        }
+        __syncthreads();
+        if (threadIdx.x < 2) {
+            uint64_t m = 0;
+            for (int w = 0; w < kWaves; ++w) m = red[threadIdx.x][w] > m ? red[threadIdx.x][w] : m;
+            if (m) atomicMax((unsigned long long *)&max_rs[threadIdx.x], (unsigned long long)m);
+        }
+    }
 }
 
 hipError_t launch_make_tasks(const uint64_t *r_count, const uint64_t *s_count, uint64_t P, uint64_t *over,
-                             uint32_t over_cap, uint32_t *n_over, hipStream_t s) {
+                             uint32_t over_cap, uint32_t *n_over, uint64_t *max_rs, hipStream_t s) {
     hipError_t e = hipMemsetAsync(n_over, 0, sizeof(uint32_t), s);
+    if (e == hipSuccess && max_rs) e = hipMemsetAsync(max_rs, 0, 2 * sizeof(uint64_t), s);
     if (e != hipSuccess) return e;
     uint64_t blocks = (P + kBlock - 1) / kBlock;
     if (blocks > 1024) blocks = 1024;
     hipLaunchKernelGGL(k_make_tasks, dim3((uint32_t)blocks), dim3(kBlock), 0, s, r_count, s_count, P, over, over_cap,
-                       n_over);
+                       n_over, max_rs);
     return hipGetLastError();
 }
 
@@ -992,30 +1023,6 @@ __global__ __launch_bounds__(kBlock) void k_reduce(const uint64_t *__restrict__ 
 
 hipError_t launch_reduce(const uint64_t *partials, uint32_t n, uint64_t *result, hipStream_t s) {
     hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kBlock), 0, s, partials, n, result);
-    return hipGetLastError();
-}
-
-__global__ __launch_bounds__(kBlock) void k_max(const uint64_t *__restrict__ v, uint64_t n,
-                                                uint64_t *__restrict__ out) {
-    __shared__ uint64_t red[kWaves];
-    uint64_t acc = 0;
-    for (uint64_t i = threadIdx.x; i < n; i += kBlock) acc = v[i] > acc ? v[i] : acc;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        const uint64_t t = __shfl_xor(acc, off, kWave);
-        acc = t > acc ? t : acc;
-    }
-    if (__lane_id() == 0) red[threadIdx.x / kWave] = acc;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint64_t t = 0;
-        for (int w = 0; w < kWaves; ++w) t = red[w] > t ? red[w] : t;
-        *out = t;
-    }
-}
-
-hipError_t launch_max(const uint64_t *v, uint64_t n, uint64_t *result, hipStream_t s) {
-    hipLaunchKernelGGL(k_max, dim3(1), dim3(kBlock), 0, s, v, n, result);
     return hipGetLastError();
 }
 
