@@ -37,13 +37,21 @@ struct Policy {
     uint32_t bits, passes, b1, b2, rcap;
 };
 
-Policy choose_policy(uint64_t nR, const mi355_rho_opts *o) {
+Policy choose_policy(uint64_t nR, uint64_t nS, const mi355_rho_opts *o) {
     Policy p{};
     if (o && o->radix_bits > 0) {
         p.bits = std::min<uint32_t>((uint32_t)o->radix_bits, kMaxBits);
     } else {
-        const uint64_t need = (nR + kTargetPartition - 1) / kTargetPartition;
-        p.bits = std::min(ceil_log2(std::max<uint64_t>(need, 1)), kMaxBits);
+        // R partitions fit one LDS chain table; and when S is much larger than R, enough
+        // partitions that an average S partition is one build/probe task (kSChunk):
+        // every further S chunk of a partition rebuilds its R table.
+        // The S-driven bits stop at 16 (two passes of <= 8 bits: a 9-bit pass-1 scatter
+        // holds 512 digits in LDS and runs at half speed).
+        const uint64_t need_r = (nR + kTargetPartition - 1) / kTargetPartition;
+        const uint64_t need_s = (nS + kSChunk - 1) / kSChunk;
+        const uint32_t bits_r = ceil_log2(std::max<uint64_t>(need_r, 1));
+        const uint32_t bits_s = std::min<uint32_t>(ceil_log2(std::max<uint64_t>(need_s, 1)), 16);
+        p.bits = std::min(std::max(bits_r, bits_s), kMaxBits);
     }
     p.passes = (o && o->passes > 0) ? (uint32_t)o->passes : (p.bits <= 8 ? 1u : 2u);
     if (p.passes > 2) p.passes = 2;
@@ -162,7 +170,7 @@ int join_device(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const
     const uint32_t key_shift = opts ? opts->key_shift : 0;
     const bool materialize = opts && opts->materialize;
     const int algo = (opts && opts->algorithm == MI355_ALGO_RHT) ? kAlgoHistogram : kAlgoChaining;
-    const Policy pol = choose_policy(nR, opts);
+    const Policy pol = choose_policy(nR, nS, opts);
     if (key_shift + pol.bits > 31) {
         set_last_error("key_shift + radix bits must stay below 32");
         return MI355_ERR_INVALID;

@@ -159,38 +159,55 @@ hipError_t launch_scan_single(uint64_t *hist, uint32_t nseg, uint32_t bits, uint
     return hipGetLastError();
 }
 
-// One block per region, one thread per digit: cursors for [g][d] and the partition table.
+// One block per region.  Cursors for [g][d] and the partition table.  The region's
+// segments are split among S = 512 / F threads per digit (tid = j * F + d), so the
+// reads of one digit's column run in parallel instead of as one dependent chain.
 __global__ __launch_bounds__(kMaxF) void k_scan_regions(uint64_t *__restrict__ hist,
                                                         const uint32_t *__restrict__ seg_base,
                                                         const uint64_t *__restrict__ reg_start, uint32_t F,
                                                         uint64_t *__restrict__ part_start,
                                                         uint64_t *__restrict__ part_count) {
     __shared__ uint64_t scratch[kMaxF / kWave + 1];
-    const uint32_t r = blockIdx.x, d = threadIdx.x;
+    __shared__ uint64_t part[kMaxF];   // [j][d]: sum of thread j's chunk, then its prefix inside d
+    __shared__ uint64_t startd[kMaxF];
+    const uint32_t r = blockIdx.x, tid = threadIdx.x;
+    const uint32_t S = kMaxF / F, d = tid % F, j = tid / F;
     const uint32_t sb = seg_base[r], se = seg_base[r + 1];
-    uint64_t run = 0;
-    if (d < F) {
-        for (uint32_t g = sb; g < se; ++g) {
-            const uint64_t c = hist[(uint64_t)g * F + d];
-            hist[(uint64_t)g * F + d] = run;
-            run += c;
+    const uint32_t per = (se - sb + S - 1) / S;
+    const uint32_t g0 = min(se, sb + j * per), g1 = min(se, g0 + per);
+    uint64_t sum = 0;
+    for (uint32_t g = g0; g < g1; ++g) sum += hist[(uint64_t)g * F + d];
+    part[tid] = sum;
+    __syncthreads();
+    uint64_t total = 0;
+    if (j == 0) {
+        for (uint32_t jj = 0; jj < S; ++jj) {
+            const uint64_t t = part[jj * F + d];
+            part[jj * F + d] = total;
+            total += t;
         }
     }
     uint64_t tot;
-    const uint64_t ex = block_excl_scan_u64(d < F ? run : 0, scratch, &tot);
-    if (d < F) {
+    const uint64_t ex = block_excl_scan_u64(j == 0 ? total : 0, scratch, &tot);  // digits are tids 0..F-1
+    if (j == 0) {
         const uint64_t start = reg_start[r] + ex;
-        for (uint32_t g = sb; g < se; ++g) hist[(uint64_t)g * F + d] += start;
+        startd[d] = start;
         part_start[(uint64_t)r * F + d] = start;
-        part_count[(uint64_t)r * F + d] = run;
+        part_count[(uint64_t)r * F + d] = total;
+    }
+    __syncthreads();
+    uint64_t run = startd[d] + part[tid];
+    for (uint32_t g = g0; g < g1; ++g) {
+        const uint64_t c = hist[(uint64_t)g * F + d];
+        hist[(uint64_t)g * F + d] = run;
+        run += c;
     }
 }
 
 hipError_t launch_scan_regions(uint64_t *hist, const uint32_t *seg_base, const uint64_t *reg_start, uint32_t nreg,
                                uint32_t bits, uint64_t *part_start, uint64_t *part_count, hipStream_t s) {
     const uint32_t F = 1u << bits;
-    const uint32_t threads = F < 64 ? 64 : F;
-    hipLaunchKernelGGL(k_scan_regions, dim3(nreg), dim3(threads), 0, s, hist, seg_base, reg_start, F, part_start,
+    hipLaunchKernelGGL(k_scan_regions, dim3(nreg), dim3(kMaxF), 0, s, hist, seg_base, reg_start, F, part_start,
                        part_count);
     return hipGetLastError();
 }

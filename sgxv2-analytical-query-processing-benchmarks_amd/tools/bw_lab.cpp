@@ -75,6 +75,31 @@ __global__ __launch_bounds__(256) void k_gscatter(const v4u *__restrict__ a, v4u
     }
 }
 
+// Half-line granules written by one workgroup: the block owns NS output streams and
+// writes its data as 64-B halves, all lower halves first (one per stream), then, a
+// phase later, the upper halves — the write pattern of a key/payload-split scatter
+// whose 16-tuple granules fill 128-B lines in two steps.  NTS: non-temporal stores.
+template <bool NTS>
+__global__ __launch_bounds__(256) void k_halfpair(const v4u *__restrict__ a, v4u *__restrict__ b, uint64_t n16) {
+    constexpr int NS = 256;               // streams (lines in flight) per block
+    const uint64_t per_block = NS * 8;    // 16-B words per block step: NS lines of 128 B
+    for (uint64_t base = (uint64_t)blockIdx.x * per_block; base < n16; base += (uint64_t)gridDim.x * per_block) {
+        for (int half = 0; half < 2; ++half) {
+            for (int w = threadIdx.x; w < NS * 4; w += 256) {   // 4 words = one 64-B half per stream
+                const int line = w / 4, q = w % 4;
+                // stream `line` of this block: lines spaced NS apart in the output (strided streams)
+                const uint64_t dst = (base / 8 + (uint64_t)line) * 8 + half * 4 + q;
+                const uint64_t src = base + half * NS * 4 + w;
+                if (dst < n16 && src < n16) {
+                    const v4u v = __builtin_nontemporal_load(a + src);
+                    if (NTS) __builtin_nontemporal_store(v, b + dst); else b[dst] = v;
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
 // Read only the first H bytes of every 128-B line (blocked-SoA key column probe).
 template <int H, bool NT>
 __global__ __launch_bounds__(256) void k_read_half(const uint32_t *__restrict__ a, uint64_t nlines, uint32_t *out) {
@@ -121,6 +146,8 @@ int main(int argc, char **argv) {
     GS(64, 256, false) GS(128, 256, false) GS(256, 256, false) GS(512, 256, false) GS(1024, 256, false)
     GS(128, 256, true) GS(256, 256, true) GS(512, 256, true)
     GS(128, 64, false) GS(128, 1024, false) GS(256, 1024, false) GS(256, 64, false)
+    t("halfpair 64B plain", 2.0 * bytes, [&] { hipLaunchKernelGGL((k_halfpair<false>), dim3(4096), dim3(256), 0, 0, a, b, n16); });
+    t("halfpair 64B nts", 2.0 * bytes, [&] { hipLaunchKernelGGL((k_halfpair<true>), dim3(4096), dim3(256), 0, 0, a, b, n16); });
     printf("-- partial-line reads, grid 4096 (GB/s counts the bytes of whole lines)\n");
     t("read full 128B/line nt", bytes, [&] { hipLaunchKernelGGL((k_read_half<128, true>), dim3(4096), dim3(256), 0, 0, (const uint32_t *)a, bytes / 128, o); });
     t("read 64B/line nt", bytes, [&] { hipLaunchKernelGGL((k_read_half<64, true>), dim3(4096), dim3(256), 0, 0, (const uint32_t *)a, bytes / 128, o); });
