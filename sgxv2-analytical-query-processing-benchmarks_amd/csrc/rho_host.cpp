@@ -195,9 +195,10 @@ int join_device(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const
     // side — still spread their S chunks over the chip)
     const uint32_t join_grid = (uint32_t)std::min<uint64_t>(P + over_cap - 1, 2048);
     const size_t off_over = A.reserve(sizeof(uint64_t) * over_cap);
-    const size_t off_nover = A.reserve(sizeof(uint32_t));
     const size_t off_counts = A.reserve(sizeof(uint64_t) * (materialize ? P + over_cap : join_grid));
     const size_t off_toff = A.reserve(sizeof(uint64_t) * (materialize ? P + over_cap : 1));
+    // result[0] = matches, [1] / [2] = largest R / S partition, [3] = extra S-chunk tasks
+    // (u32): one zeroing and one read-back for all four
     const size_t off_result = A.reserve(sizeof(uint64_t) * 4);
     RHO_HIP(A.buf.ensure(A.used));
 
@@ -231,13 +232,13 @@ int join_device(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const
         RHO_HIP(hipStreamWaitEvent(s, ctx->ev_join, 0));
     }
     uint64_t *over = A.at<uint64_t>(off_over);
-    uint32_t *n_over = A.at<uint32_t>(off_nover);
     uint64_t *counts = A.at<uint64_t>(off_counts);
     uint64_t *task_off = A.at<uint64_t>(off_toff);
     uint64_t *result = A.at<uint64_t>(off_result);
+    uint32_t *n_over = reinterpret_cast<uint32_t *>(result + 3);
     const uint32_t hash_shift = key_shift + pol.bits;
     tm.mark("join_tasks");
-    RHO_HIP(launch_make_tasks(pcR, pcS, P, over, over_cap, n_over, result + 1, s));
+    RHO_HIP(launch_make_tasks(pcR, pcS, P, over, over_cap, result + 1, s));
     if (!materialize) {
         tm.mark("join_build_probe");
         RHO_HIP(launch_join(fR, fS, psR, pcR, psS, pcS, P, over, n_over, hash_shift, pol.rcap, join_grid, kJoinCount,
@@ -271,8 +272,7 @@ int join_device(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const
     }
     tm.end_call();
     if (s2) RHO_HIP(hipEventRecord(ctx->ev_t1, s));
-    RHO_HIP(hipMemcpyAsync(ctx->host_result, result, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-    RHO_HIP(hipMemcpyAsync(ctx->host_result + 3, n_over, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    RHO_HIP(hipMemcpyAsync(ctx->host_result, result, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     RHO_HIP(hipStreamSynchronize(s));
     tm.collect();
     float wall = -1.f;

@@ -65,9 +65,10 @@ constexpr uint64_t kSChunk = 8192;
 enum JoinMode : int { kJoinCount = 0, kJoinTaskCount = 1, kJoinWrite = 2 };
 // Build/probe algorithm of one task: RHO's bucket chaining or RHT's histogram join.
 enum JoinAlgo : int { kAlgoChaining = 0, kAlgoHistogram = 1 };
-// max_rs (nullable): [0] = largest R partition, [1] = largest S partition.
+// meta (zeroed here): [0] = largest R partition, [1] = largest S partition,
+// [2] = the number of extra tasks (u32 n_over, read by launch_join / launch_excl_scan).
 hipError_t launch_make_tasks(const uint64_t *r_count, const uint64_t *s_count, uint64_t P, uint64_t *over,
-                             uint32_t over_cap, uint32_t *n_over, uint64_t *max_rs, hipStream_t s);
+                             uint32_t over_cap, uint64_t *meta, hipStream_t s);
 hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, const uint64_t *r_count,
                        const uint64_t *s_start, const uint64_t *s_count, uint64_t P, const uint64_t *over,
                        const uint32_t *n_over, uint32_t hash_shift, uint32_t rcap, uint32_t grid, int mode,

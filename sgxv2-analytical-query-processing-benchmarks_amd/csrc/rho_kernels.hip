@@ -965,7 +965,7 @@ __global__ __launch_bounds__(kBlock) void k_make_tasks(const uint64_t *__restric
         const uint32_t base = atomicAdd(n_over, k);
         for (uint32_t j = 0; j < k && base + j < over_cap; ++j) over[base + j] = p | ((uint64_t)(j + 1) << 32);
     }
-    if (max_rs) {  // one pair of device atomics per workgroup
+    {  // one pair of device atomics per workgroup
         __shared__ uint64_t red[2][kWaves];
 #pragma unroll
         for (int off = kWave / 2; off > 0; off >>= 1) {
@@ -987,14 +987,14 @@ __global__ __launch_bounds__(kBlock) void k_make_tasks(const uint64_t *__restric
 }
 
 hipError_t launch_make_tasks(const uint64_t *r_count, const uint64_t *s_count, uint64_t P, uint64_t *over,
-                             uint32_t over_cap, uint32_t *n_over, uint64_t *max_rs, hipStream_t s) {
-    hipError_t e = hipMemsetAsync(n_over, 0, sizeof(uint32_t), s);
-    if (e == hipSuccess && max_rs) e = hipMemsetAsync(max_rs, 0, 2 * sizeof(uint64_t), s);
+                             uint32_t over_cap, uint64_t *meta, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(meta, 0, 3 * sizeof(uint64_t), s);
     if (e != hipSuccess) return e;
+    uint32_t *n_over = reinterpret_cast<uint32_t *>(meta + 2);
     uint64_t blocks = (P + kBlock - 1) / kBlock;
     if (blocks > 1024) blocks = 1024;
     hipLaunchKernelGGL(k_make_tasks, dim3((uint32_t)blocks), dim3(kBlock), 0, s, r_count, s_count, P, over, over_cap,
-                       n_over, max_rs);
+                       n_over, meta);
     return hipGetLastError();
 }
 
