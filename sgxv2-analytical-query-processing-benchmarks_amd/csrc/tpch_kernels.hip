@@ -3,8 +3,8 @@
 // table generator.
 //
 // Selections (filters.hpp:118-138 + Q*Predicates.hpp): pass 1 reads only the
-// predicate columns (coalesced, one row per lane per step) and keeps one bit per
-// row (a u16 per lane for its 16 rows) plus a count per workgroup; an exclusive
+// predicate columns (16 consecutive rows per lane, 16-B vector loads) and keeps one
+// bit per row (a u16 per lane) plus a count per workgroup; an exclusive
 // scan of the counts gives each workgroup its output offset; pass 2 reads the
 // bits and gathers the emitted columns of the matching rows only, writing them in
 // input order — exactly the rows, in the order, the reference's scalar
@@ -19,36 +19,76 @@ namespace sgxamd {
 namespace tpch {
 
 // ------------------------------------------------------------ predicates ---
-// pred(i): does row i survive; emit(i): the row_t the reference's copy function writes.
+// 16 consecutive elements of a column from row i0 (16-B non-temporal vector loads when
+// the run is whole and aligned; element loads at the column's end).
+template <typename T>
+__device__ __forceinline__ void load16(const T *__restrict__ p, uint64_t i0, uint64_t n, T (&v)[16]) {
+    constexpr int PER = 16 / (int)sizeof(T);
+    static_assert(16 % sizeof(T) == 0, "element size divides 16 bytes");
+    if (i0 + 16 <= n && (reinterpret_cast<uintptr_t>(p + i0) & 15) == 0) {
+        const u32x4_t *q = reinterpret_cast<const u32x4_t *>(p + i0);
+#pragma unroll
+        for (int j = 0; j < 16 / PER; ++j) {
+            const u32x4_t w = __builtin_nontemporal_load(q + j);
+            __builtin_memcpy(&v[j * PER], &w, 16);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] = i0 + k < n ? p[i0 + k] : T{};
+    }
+}
+
+// Two row layouts per workgroup of 4096 rows.  kConsecutive (1- and 4-byte columns):
+// lane t owns rows 16 t .. 16 t + 15, one 16-B load per 16 rows of a byte column, and
+// mask16(i0, n) gives bit k = row i0 + k survives.  Otherwise (8-byte columns): lane t
+// owns rows t + 256 k, each load instruction of a wave covers 512 contiguous bytes,
+// and pred(i) tests one row.  emit(i): the row_t the reference's copy function writes.
 struct Q3Customer {  // Q3Predicates.hpp:166-174
+    static constexpr bool kConsecutive = true;  // narrow columns: 16 rows per lane
     FilterCols c;
-    __device__ bool pred(uint64_t i) const { return c.b0[i] == TPCH_MKT_BUILDING; }
+    __device__ uint32_t mask16(uint64_t i0, uint64_t n) const {
+        uint8_t m[16];
+        load16(c.b0, i0, n, m);
+        uint32_t bits = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) bits |= (uint32_t)(m[k] == TPCH_MKT_BUILDING) << k;
+        return bits;
+    }
     __device__ row_t emit(uint64_t i) const { return c.rows[i]; }
 };
-struct Q3Orders {  // :176-185  key = o_custkey, payload = o_orderkey.key
+struct DateFilter {  // orders / lineitem date selections: lo <= d0 < hi (open ends as 0 / ~0)
+    static constexpr bool kConsecutive = false;  // 8-byte column: row per lane
     FilterCols c;
-    __device__ bool pred(uint64_t i) const { return c.d0[i] < TPCH_TIMESTAMP_1995_03_15_SECONDS; }
-    __device__ row_t emit(uint64_t i) const { return row_t{c.keys[i], c.rows[i].key}; }
-};
-struct Q3Lineitem {  // :187-195
-    FilterCols c;
-    __device__ bool pred(uint64_t i) const { return c.d0[i] >= TPCH_TIMESTAMP_1995_03_16_SECONDS; }
-    __device__ row_t emit(uint64_t i) const { return c.rows[i]; }
-};
-struct Q10Orders {  // Q10Predicates.hpp:26-35  key = o_custkey, payload = o_orderkey.payload
-    FilterCols c;
+    uint64_t lo, hi;
     __device__ bool pred(uint64_t i) const {
         const uint64_t d = c.d0[i];
-        return d >= TPCH_TIMESTAMP_1993_10_01_SECONDS && d < TPCH_TIMESTAMP_1994_01_01_SECONDS;
+        return d >= lo && d < hi;
     }
+};
+struct Q3Orders : DateFilter {  // :176-185  o_orderdate < 1995-03-15 -> {o_custkey, o_orderkey}
+    __device__ row_t emit(uint64_t i) const { return row_t{c.keys[i], c.rows[i].key}; }
+};
+struct Q3Lineitem : DateFilter {  // :187-195  l_shipdate >= 1995-03-16 -> l_orderkey
+    __device__ row_t emit(uint64_t i) const { return c.rows[i]; }
+};
+struct Q10Orders : DateFilter {  // Q10Predicates.hpp:26-35 -> {o_custkey, o_orderkey.payload}
     __device__ row_t emit(uint64_t i) const { return row_t{c.keys[i], c.rows[i].payload}; }
 };
 struct Q10Lineitem {  // :37-45
+    static constexpr bool kConsecutive = true;  // narrow columns: 16 rows per lane
     FilterCols c;
-    __device__ bool pred(uint64_t i) const { return c.c0[i] == TPCH_L_RETURNFLAG_R; }
+    __device__ uint32_t mask16(uint64_t i0, uint64_t n) const {
+        char f[16];
+        load16(c.c0, i0, n, f);
+        uint32_t bits = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) bits |= (uint32_t)(f[k] == TPCH_L_RETURNFLAG_R) << k;
+        return bits;
+    }
     __device__ row_t emit(uint64_t i) const { return c.rows[i]; }
 };
 struct Q12Lineitem {  // Q12Predicates.hpp:22-37  d0 = shipdate, d1 = commitdate, d2 = receiptdate
+    static constexpr bool kConsecutive = false;  // three 8-byte columns: row per lane
     FilterCols c;
     __device__ bool pred(uint64_t i) const {
         const uint8_t m = c.b0[i];
@@ -60,38 +100,70 @@ struct Q12Lineitem {  // Q12Predicates.hpp:22-37  d0 = shipdate, d1 = commitdate
     __device__ row_t emit(uint64_t i) const { return c.rows[i]; }
 };
 struct Q19Part {  // Q19Predicates.hpp:40-55  b0 = brand, b1 = container, u0 = size
+    static constexpr bool kConsecutive = true;  // narrow columns: 16 rows per lane
     FilterCols c;
-    __device__ bool pred(uint64_t i) const {
-        const uint8_t b = c.b0[i], k = c.b1[i];
-        const uint32_t sz = c.u0[i];
-        return b >= TPCH_P_BRAND_12 && b <= TPCH_P_BRAND_34 && k >= TPCH_P_CONTAINER_SM_CASE &&
-               k <= TPCH_P_CONTAINER_LG_PKG && sz >= 1 && sz <= 15;
+    __device__ uint32_t mask16(uint64_t i0, uint64_t n) const {
+        uint8_t b[16], k8[16];
+        uint32_t sz[16];
+        load16(c.b0, i0, n, b);
+        load16(c.b1, i0, n, k8);
+        load16(c.u0, i0, n, sz);
+        uint32_t bits = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const bool ok = b[k] >= TPCH_P_BRAND_12 && b[k] <= TPCH_P_BRAND_34 && k8[k] >= TPCH_P_CONTAINER_SM_CASE &&
+                            k8[k] <= TPCH_P_CONTAINER_LG_PKG && sz[k] >= 1 && sz[k] <= 15;
+            bits |= (uint32_t)ok << k;
+        }
+        return bits;
     }
     __device__ row_t emit(uint64_t i) const { return c.rows[i]; }
 };
-struct Q19Lineitem {  // :27-38  key = l_partkey, payload = l_orderkey.payload; b0 = shipmode, b1 = shipinstruct
+struct Q19Lineitem {  // :27-38  -> {l_partkey, l_orderkey.payload}; b0 = shipmode, b1 = shipinstruct
+    static constexpr bool kConsecutive = true;  // narrow columns: 16 rows per lane
     FilterCols c;
-    __device__ bool pred(uint64_t i) const {
-        const float q = c.f0[i];
-        const uint8_t m = c.b0[i];
-        return q >= 1.f && q <= 30.f && (m == TPCH_L_SHIPMODE_AIR || m == TPCH_L_SHIPMODE_AIR_REG) &&
-               c.b1[i] == TPCH_L_SHIPINSTRUCT_DELIVER_IN_PERSON;
+    __device__ uint32_t mask16(uint64_t i0, uint64_t n) const {
+        float q[16];
+        uint8_t m[16], ins[16];
+        load16(c.f0, i0, n, q);
+        load16(c.b0, i0, n, m);
+        load16(c.b1, i0, n, ins);
+        uint32_t bits = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const bool ok = q[k] >= 1.f && q[k] <= 30.f &&
+                            (m[k] == TPCH_L_SHIPMODE_AIR || m[k] == TPCH_L_SHIPMODE_AIR_REG) &&
+                            ins[k] == TPCH_L_SHIPINSTRUCT_DELIVER_IN_PERSON;
+            bits |= (uint32_t)ok << k;
+        }
+        return bits;
     }
     __device__ row_t emit(uint64_t i) const { return row_t{c.keys[i], c.rows[i].payload}; }
 };
 
 // --------------------------------------------------------------- filters ---
 template <class P>
+__device__ __forceinline__ uint32_t lane_bits(const P &p, uint64_t n) {
+    uint32_t bits = 0;
+    if constexpr (P::kConsecutive) {
+        const uint64_t i0 = (uint64_t)blockIdx.x * kFilterSeg + (uint64_t)threadIdx.x * kFilterItems;
+        if (i0 < n) bits = p.mask16(i0, n);
+    } else {
+        const uint64_t base = (uint64_t)blockIdx.x * kFilterSeg + threadIdx.x;
+#pragma unroll
+        for (int k = 0; k < kFilterItems; ++k) {
+            const uint64_t i = base + (uint64_t)k * kFilterThreads;
+            if (i < n && p.pred(i)) bits |= 1u << k;
+        }
+    }
+    return bits;
+}
+
+template <class P>
 __global__ __launch_bounds__(kFilterThreads) void k_filter_mark(P p, uint64_t n, uint16_t *__restrict__ mask,
                                                                 uint64_t *__restrict__ blk_count) {
     __shared__ uint32_t red[kFilterThreads / kWave];
-    const uint64_t base = (uint64_t)blockIdx.x * kFilterSeg + threadIdx.x;
-    uint32_t bits = 0;
-#pragma unroll
-    for (int k = 0; k < kFilterItems; ++k) {
-        const uint64_t i = base + (uint64_t)k * kFilterThreads;
-        if (i < n && p.pred(i)) bits |= 1u << k;
-    }
+    const uint32_t bits = lane_bits(p, n);
     mask[(uint64_t)blockIdx.x * kFilterThreads + threadIdx.x] = (uint16_t)bits;
     uint32_t c = __popc(bits);
     for (int o = kWave / 2; o > 0; o >>= 1) c += __shfl_xor(c, o);
@@ -109,83 +181,88 @@ __global__ __launch_bounds__(kFilterThreads) void k_filter_emit(P p, uint64_t n,
                                                                 const uint64_t *__restrict__ blk_off,
                                                                 row_t *__restrict__ out) {
     constexpr int W = kFilterThreads / kWave;
-    __shared__ uint32_t pre[kFilterItems * W];
-    const uint32_t lane = __lane_id(), w = threadIdx.x / kWave;
-    const uint32_t bits = mask[(uint64_t)blockIdx.x * kFilterThreads + threadIdx.x];
-    // rows of (item k, wave w) come in row order k-major, w-minor
-#pragma unroll
-    for (int k = 0; k < kFilterItems; ++k) {
-        const uint64_t bal = __ballot((bits >> k) & 1u);
-        if (lane == 0) pre[k * W + w] = (uint32_t)__popcll(bal);
-    }
-    __syncthreads();
-    if (threadIdx.x < kWave) {  // kFilterItems * W == 64 entries: one wave scans them
-        const uint64_t v = pre[threadIdx.x];
-        const uint64_t incl = wave_incl_scan_u64(v);
-        pre[threadIdx.x] = (uint32_t)(incl - v);
-    }
-    __syncthreads();
-    if (bits == 0) return;
+    static_assert(kFilterItems * W == kWave, "one wave scans the (item, wave) counts");
+    uint32_t bits = mask[(uint64_t)blockIdx.x * kFilterThreads + threadIdx.x];
     const uint64_t obase = blk_off[blockIdx.x];
-    const uint64_t lt = (1ull << lane) - 1;
-    const uint64_t base = (uint64_t)blockIdx.x * kFilterSeg + threadIdx.x;
+    if constexpr (P::kConsecutive) {
+        // lanes own consecutive row runs: the lane order is the row order
+        __shared__ uint64_t scratch[W + 1];
+        uint64_t tot;
+        uint64_t o = obase + block_excl_scan_u64(__popc(bits), scratch, &tot);
+        const uint64_t i0 = (uint64_t)blockIdx.x * kFilterSeg + (uint64_t)threadIdx.x * kFilterItems;
+        while (bits) {
+            const int k = __ffs(bits) - 1;
+            bits &= bits - 1;
+            out[o++] = p.emit(i0 + k);
+        }
+    } else {
+        // rows of (item k, wave w) come in row order k-major, w-minor
+        __shared__ uint32_t pre[kFilterItems * W];
+        const uint32_t lane = __lane_id(), w = threadIdx.x / kWave;
 #pragma unroll
-    for (int k = 0; k < kFilterItems; ++k) {
-        const bool b = (bits >> k) & 1u;
-        const uint64_t bal = __ballot(b);
-        if (b) {
-            const uint64_t i = base + (uint64_t)k * kFilterThreads;
-            out[obase + pre[k * W + w] + __popcll(bal & lt)] = p.emit(i);
+        for (int k = 0; k < kFilterItems; ++k) {
+            const uint64_t bal = __ballot((bits >> k) & 1u);
+            if (lane == 0) pre[k * W + w] = (uint32_t)__popcll(bal);
+        }
+        __syncthreads();
+        if (threadIdx.x < kWave) {
+            const uint64_t v = pre[threadIdx.x];
+            const uint64_t incl = wave_incl_scan_u64(v);
+            pre[threadIdx.x] = (uint32_t)(incl - v);
+        }
+        __syncthreads();
+        if (bits == 0) return;
+        const uint64_t lt = (1ull << lane) - 1;
+        const uint64_t base = (uint64_t)blockIdx.x * kFilterSeg + threadIdx.x;
+#pragma unroll
+        for (int k = 0; k < kFilterItems; ++k) {
+            const bool b = (bits >> k) & 1u;
+            const uint64_t bal = __ballot(b);
+            if (b) out[obase + pre[k * W + w] + __popcll(bal & lt)] = p.emit(base + (uint64_t)k * kFilterThreads);
         }
     }
 }
 
-static_assert(kFilterItems * (kFilterThreads / kWave) == kWave, "emit scan assumes one wave of (item, wave) counts");
-
 template <class P>
-hipError_t mark_as(const FilterCols &c, uint64_t n, uint16_t *mask, uint64_t *blk, hipStream_t s) {
+hipError_t mark_as(const P &pr, uint64_t n, uint16_t *mask, uint64_t *blk, hipStream_t s) {
     const uint64_t g = filter_blocks(n);
     if (g == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_filter_mark<P>, dim3((uint32_t)g), dim3(kFilterThreads), 0, s, P{c}, n, mask, blk);
+    hipLaunchKernelGGL(k_filter_mark<P>, dim3((uint32_t)g), dim3(kFilterThreads), 0, s, pr, n, mask, blk);
     return hipGetLastError();
 }
 template <class P>
-hipError_t emit_as(const FilterCols &c, uint64_t n, const uint16_t *mask, const uint64_t *off, row_t *out,
-                   hipStream_t s) {
+hipError_t emit_as(const P &pr, uint64_t n, const uint16_t *mask, const uint64_t *off, row_t *out, hipStream_t s) {
     const uint64_t g = filter_blocks(n);
     if (g == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_filter_emit<P>, dim3((uint32_t)g), dim3(kFilterThreads), 0, s, P{c}, n, mask, off, out);
+    hipLaunchKernelGGL(k_filter_emit<P>, dim3((uint32_t)g), dim3(kFilterThreads), 0, s, pr, n, mask, off, out);
     return hipGetLastError();
+}
+
+// The predicate object of selection id (date bounds of DateFilter as in the reference).
+template <class F>
+hipError_t with_filter(FilterId id, const FilterCols &c, F &&f) {
+    constexpr uint64_t NONE = ~0ull;
+    switch (id) {
+        case kQ3Customer: return f(Q3Customer{c});
+        case kQ3Orders: return f(Q3Orders{{c, 0, TPCH_TIMESTAMP_1995_03_15_SECONDS}});
+        case kQ3Lineitem: return f(Q3Lineitem{{c, TPCH_TIMESTAMP_1995_03_16_SECONDS, NONE}});
+        case kQ10Orders: return f(Q10Orders{{c, TPCH_TIMESTAMP_1993_10_01_SECONDS, TPCH_TIMESTAMP_1994_01_01_SECONDS}});
+        case kQ10Lineitem: return f(Q10Lineitem{c});
+        case kQ12Lineitem: return f(Q12Lineitem{c});
+        case kQ19Part: return f(Q19Part{c});
+        case kQ19Lineitem: return f(Q19Lineitem{c});
+        default: return hipErrorInvalidValue;
+    }
 }
 
 hipError_t launch_filter_mark(FilterId id, const FilterCols &c, uint64_t n, uint16_t *mask, uint64_t *blk,
                               hipStream_t s) {
-    switch (id) {
-        case kQ3Customer: return mark_as<Q3Customer>(c, n, mask, blk, s);
-        case kQ3Orders: return mark_as<Q3Orders>(c, n, mask, blk, s);
-        case kQ3Lineitem: return mark_as<Q3Lineitem>(c, n, mask, blk, s);
-        case kQ10Orders: return mark_as<Q10Orders>(c, n, mask, blk, s);
-        case kQ10Lineitem: return mark_as<Q10Lineitem>(c, n, mask, blk, s);
-        case kQ12Lineitem: return mark_as<Q12Lineitem>(c, n, mask, blk, s);
-        case kQ19Part: return mark_as<Q19Part>(c, n, mask, blk, s);
-        case kQ19Lineitem: return mark_as<Q19Lineitem>(c, n, mask, blk, s);
-        default: return hipErrorInvalidValue;
-    }
+    return with_filter(id, c, [&](const auto &pr) { return mark_as(pr, n, mask, blk, s); });
 }
 
 hipError_t launch_filter_emit(FilterId id, const FilterCols &c, uint64_t n, const uint16_t *mask,
                               const uint64_t *off, row_t *out, hipStream_t s) {
-    switch (id) {
-        case kQ3Customer: return emit_as<Q3Customer>(c, n, mask, off, out, s);
-        case kQ3Orders: return emit_as<Q3Orders>(c, n, mask, off, out, s);
-        case kQ3Lineitem: return emit_as<Q3Lineitem>(c, n, mask, off, out, s);
-        case kQ10Orders: return emit_as<Q10Orders>(c, n, mask, off, out, s);
-        case kQ10Lineitem: return emit_as<Q10Lineitem>(c, n, mask, off, out, s);
-        case kQ12Lineitem: return emit_as<Q12Lineitem>(c, n, mask, off, out, s);
-        case kQ19Part: return emit_as<Q19Part>(c, n, mask, off, out, s);
-        case kQ19Lineitem: return emit_as<Q19Lineitem>(c, n, mask, off, out, s);
-        default: return hipErrorInvalidValue;
-    }
+    return with_filter(id, c, [&](const auto &pr) { return emit_as(pr, n, mask, off, out, s); });
 }
 
 // ------------------------------------------------------------ transforms ---
