@@ -61,6 +61,9 @@ def main():
                     help="build/probe: RHO bucket chaining (headline) or RHT histogram join")
     ap.add_argument("--partition-overlap", type=int, choices=[0, 1], default=0,
                     help="1: R/S partition chains on two streams (timed region); 0: one stream")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="nccl = RCCL over xGMI (one GPU per rank); gloo = single-GPU rehearsal of the "
+                         "multi-rank path (ranks share the visible GPUs, tuples staged through host memory)")
     ap.add_argument("--no-scan", action="store_true")
     ap.add_argument("--no-tpch", action="store_true")
     ap.add_argument("--tpch-scale-milli", type=int, default=10000, help="TPC-H scale factor x 1000 (10000 = SF10)")
@@ -81,10 +84,19 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    if args.dist_backend == "gloo":  # rehearsal: ranks may share a device
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            from sgxamd.dist import stdout_to_stderr
+
+            with stdout_to_stderr():
+                dist.init_process_group("gloo")
+    coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")  # bench-side collectives
 
     def barrier():
         if world > 1:
@@ -94,7 +106,7 @@ def main():
     def max_over_ranks(x: float) -> float:
         if world == 1:
             return x
-        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        t = torch.tensor([x], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
@@ -198,7 +210,7 @@ def main():
         "step_ms_breakdown": {k: round(v, 3) for k, v in results[-1].ms.items()},
     }
     if args.workload == "c5":  # per-partition / per-GPU load report (skew)
-        rs = torch.tensor([float(nS)], dtype=torch.float64, device=dev)
+        rs = torch.tensor([float(nS)], dtype=torch.float64, device=coll_dev)
         if world > 1:
             allr = [torch.zeros_like(rs) for _ in range(world)]
             dist.all_gather(allr, rs)
@@ -340,7 +352,9 @@ def main():
                     + ("Zipf(0.75) over 1..|R|" if args.workload == "c5" else "fk (shuffled copies of 1..|R|)")
                     + " relations, 8-byte {key, payload} tuples",
             "config": {"workload": workload, "algorithm": args.algorithm, "global_R": gR, "global_S": gS,
-                       "parallelism": f"radix-shard{world}"},
+                       "parallelism": f"radix-shard{world}",
+                       **({"dist_backend": "gloo (single-GPU rehearsal, not a scaling number)"}
+                          if world > 1 and args.dist_backend == "gloo" else {})},
             "roofline": roofline, "cpu_baseline": cpu, "rho": rho_info, "scan": scan_info, "tpch": tpch_info,
         }
         print(json.dumps(line), flush=True)

@@ -121,6 +121,23 @@ int mi355_rho_shard_partition(const struct row_t *in, uint64_t n, uint32_t key_s
                               void *stream);
 
 /*
+ * Pipelined join in two calls, for callers whose S arrives later in the stream
+ * order than R (the multi-GPU exchange: R's local partition passes run while S is
+ * still on the wire).  begin plans both relations (|S| = nS), enqueues R's partition
+ * passes on opts->stream (or the library stream) and returns without waiting;
+ * finish enqueues S's passes and the build/probe on the same stream, waits, and
+ * fills stats.  Both relations must be device-resident; S only has to be valid in
+ * the stream order when finish is called (e.g. after a hipStreamWaitEvent on the
+ * exchange).  opts (key_shift, algorithm, materialize with a device out) must be the
+ * same in both calls.  One pending join per device; other join or shard calls on
+ * that device fail with MI355_ERR_INVALID until finish.  begin + finish computes
+ * exactly what mi355_rho_join_ex computes.
+ */
+int mi355_rho_join_begin(const struct row_t *R, uint64_t nR, uint64_t nS, const mi355_rho_opts *opts);
+int mi355_rho_join_finish(const struct row_t *S, uint64_t nS, const mi355_rho_opts *opts,
+                          mi355_rho_stats *stats);
+
+/*
  * Per-kernel timing of the last call on this thread that ran with timing
  * enabled (opts->timing or mi355_timing_enable(1)): names and milliseconds
  * of every recorded kernel, in launch order.  Returns the number of records

@@ -44,6 +44,11 @@ __device__ __forceinline__ uint64_t buf_ld_nt_u64(__amdgpu_buffer_rsrc_t r, uint
     const u32x2_t v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, (int)soff, 2);
     return ((uint64_t)v.y << 32) | v.x;
 }
+// non-temporal 16-byte buffer load
+__device__ __forceinline__ uint4 buf_ld_nt_u128(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 2);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
 __device__ __forceinline__ void st_nt(uint64_t *p, uint64_t v) { __builtin_nontemporal_store(v, p); }
 __device__ __forceinline__ void st_nt(uint32_t *p, uint32_t v) { __builtin_nontemporal_store(v, p); }
 

@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <unordered_map>
 
 #include "common.hpp"
 #include "rho_device.hpp"
@@ -160,18 +161,50 @@ void plan_relation(Arena &A, RelPlan &rp, uint64_t n, const Policy &pol) {
 
 }  // namespace
 
-// The whole join on device-resident inputs.  Caller holds ctx->mu.
-// Materialisation (opts->materialize): a per-task count pass, an exclusive scan of
-// the task counts into output offsets, then a write pass; `out` must be device
-// memory with room for out_cap triples (MI355_ERR_CAPACITY otherwise).
-int join_device(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const row_t *dS, uint64_t nS,
-                const mi355_rho_opts *opts, mi355_rho_stats *st, output_triple_t *out, uint64_t out_cap,
-                DeviceBuffer *grow) {
-    const uint32_t key_shift = opts ? opts->key_shift : 0;
-    const bool materialize = opts && opts->materialize;
-    const int algo = (opts && opts->algorithm == MI355_ALGO_RHT) ? kAlgoHistogram : kAlgoChaining;
-    const Policy pol = choose_policy(nR, nS, opts);
-    if (key_shift + pol.bits > 31) {
+// One join between its two halves (join_begin / join_finish): the policy and plans of
+// both relations, R's partitioned result and the scratch offsets of the join.
+struct PendingJoin {
+    bool active = false;
+    hipStream_t s = nullptr;
+    Policy pol{};
+    RelPlan pr{}, ps{};
+    uint64_t nR = 0, nS = 0;
+    uint32_t key_shift = 0;
+    bool materialize = false;
+    int algo = kAlgoChaining;
+    hipStream_t s2 = nullptr;
+    const row_t *fR = nullptr;
+    const uint64_t *psR = nullptr, *pcR = nullptr;
+    size_t off_over = 0, off_counts = 0, off_toff = 0, off_result = 0;
+    uint32_t over_cap = 0, join_grid = 0;
+};
+
+namespace {
+std::mutex g_pending_mu;
+std::unordered_map<const Context *, PendingJoin> g_pending;
+
+PendingJoin &pending_of(const Context *ctx) {
+    std::lock_guard<std::mutex> lk(g_pending_mu);
+    return g_pending[ctx];
+}
+}  // namespace
+
+// First half: plans both relations (|S| = nS, its tuples are not read yet), then
+// enqueues R's partition passes on s and returns without waiting.  The second half
+// may start after S has been produced later in the stream order of s (multi-GPU:
+// R's local passes run while S is still being exchanged).  Caller holds ctx->mu.
+int join_begin(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, uint64_t nS, const mi355_rho_opts *opts,
+               PendingJoin &pj) {
+    pj = PendingJoin{};
+    pj.s = s;
+    pj.nR = nR;
+    pj.nS = nS;
+    pj.key_shift = opts ? opts->key_shift : 0;
+    pj.materialize = opts && opts->materialize;
+    pj.algo = (opts && opts->algorithm == MI355_ALGO_RHT) ? kAlgoHistogram : kAlgoChaining;
+    pj.pol = choose_policy(nR, nS, opts);
+    const Policy &pol = pj.pol;
+    if (pj.key_shift + pol.bits > 31) {
         set_last_error("key_shift + radix bits must stay below 32");
         return MI355_ERR_INVALID;
     }
@@ -186,60 +219,91 @@ int join_device(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const
     }
     Arena &A = ctx->scratch;
     A.reset();
-    RelPlan pr{}, ps{};
-    plan_relation(A, pr, nR, pol);
-    plan_relation(A, ps, nS, pol);
+    plan_relation(A, pj.pr, nR, pol);
+    plan_relation(A, pj.ps, nS, pol);
     const uint64_t P = 1ull << pol.bits;
-    const uint32_t over_cap = (uint32_t)(nS / kSChunk + 1);
+    pj.over_cap = (uint32_t)(nS / kSChunk + 1);
     // one workgroup per task up to 2048 (few partitions with a large S — a tiny build
     // side — still spread their S chunks over the chip)
-    const uint32_t join_grid = (uint32_t)std::min<uint64_t>(P + over_cap - 1, 2048);
-    const size_t off_over = A.reserve(sizeof(uint64_t) * over_cap);
-    const size_t off_counts = A.reserve(sizeof(uint64_t) * (materialize ? P + over_cap : join_grid));
-    const size_t off_toff = A.reserve(sizeof(uint64_t) * (materialize ? P + over_cap : 1));
+    pj.join_grid = (uint32_t)std::min<uint64_t>(P + pj.over_cap - 1, 2048);
+    pj.off_over = A.reserve(sizeof(uint64_t) * pj.over_cap);
+    pj.off_counts = A.reserve(sizeof(uint64_t) * (pj.materialize ? P + pj.over_cap : pj.join_grid));
+    pj.off_toff = A.reserve(sizeof(uint64_t) * (pj.materialize ? P + pj.over_cap : 1));
     // result[0] = matches, [1] / [2] = largest R / S partition, [3] = extra S-chunk tasks
     // (u32): one zeroing and one read-back for all four
-    const size_t off_result = A.reserve(sizeof(uint64_t) * 4);
+    pj.off_result = A.reserve(sizeof(uint64_t) * 4);
     RHO_HIP(A.buf.ensure(A.used));
 
-    const row_t *fR = nullptr, *fS = nullptr;
-    const uint64_t *psR = nullptr, *pcR = nullptr, *psS = nullptr, *pcS = nullptr;
-    int rc;
-    // R's and S's partition chains are independent: S's runs on the side stream so
-    // that one relation's latency-bound scatter shares the chip with the other's
+    // R's and S's partition chains are independent: with overlap on, S's runs on the
+    // side stream so that one relation's scatter shares the chip with the other's
     // kernels (fork/join events around it).
-    hipStream_t s2 = thread_partition_overlap() ? side_stream(ctx) : nullptr;
-    Timer &tm2 = thread_side_timer();
-    if (s2) RHO_HIP(hipEventRecord(ctx->ev_t0, s));
-    if (s2) {
+    pj.s2 = thread_partition_overlap() ? side_stream(ctx) : nullptr;
+    if (pj.s2) {
+        RHO_HIP(hipEventRecord(ctx->ev_t0, s));
         RHO_HIP(hipEventRecord(ctx->ev_fork, s));
+    }
+    int rc;
+    for (int pass = 0; pass < (int)pol.passes; ++pass)
+        if ((rc = partition_relation(ctx, s, tm, "R_", dR, ctx->t1R.as<row_t>(), ctx->t2R.as<row_t>(), pj.pr, pol,
+                                     pj.key_shift, &pj.fR, &pj.psR, &pj.pcR, pass == 1)))
+            return rc;
+    pj.active = true;
+    return MI355_OK;
+}
+
+// Second half: S's partition passes, build/probe (and materialisation), then the
+// result read-back.  fork_now: the side stream (overlap on) forks from s here instead
+// of at join_begin, because S only became valid in between.
+int join_finish(Context *ctx, PendingJoin &pj, const row_t *dS, uint64_t nS, mi355_rho_stats *st,
+                output_triple_t *out, uint64_t out_cap, DeviceBuffer *grow, bool fork_now) {
+    if (!pj.active) {
+        set_last_error("join_finish without join_begin");
+        return MI355_ERR_INVALID;
+    }
+    pj.active = false;
+    if (nS != pj.nS) {
+        set_last_error("join_finish: |S| differs from the one given to join_begin");
+        return MI355_ERR_INVALID;
+    }
+    hipStream_t s = pj.s;
+    const Policy &pol = pj.pol;
+    Arena &A = ctx->scratch;
+    Timer &tm = thread_timer();
+    Timer &tm2 = thread_side_timer();
+    hipStream_t s2 = pj.s2;
+    if (s2) {
+        if (fork_now) RHO_HIP(hipEventRecord(ctx->ev_fork, s));
         RHO_HIP(hipStreamWaitEvent(s2, ctx->ev_fork, 0));
         tm2.begin_call(s2, true);
     }
     hipStream_t sS = s2 ? s2 : s;
     Timer &tmS = s2 ? tm2 : tm;
-    for (int pass = 0; pass < pol.passes; ++pass) {
-        if ((rc = partition_relation(ctx, s, tm, "R_", dR, ctx->t1R.as<row_t>(), ctx->t2R.as<row_t>(), pr, pol,
-                                     key_shift, &fR, &psR, &pcR, pass == 1)))
+    const row_t *fS = nullptr;
+    const uint64_t *psS = nullptr, *pcS = nullptr;
+    int rc;
+    for (int pass = 0; pass < (int)pol.passes; ++pass)
+        if ((rc = partition_relation(ctx, sS, tmS, "S_", dS, ctx->t1S.as<row_t>(), ctx->t2S.as<row_t>(), pj.ps, pol,
+                                     pj.key_shift, &fS, &psS, &pcS, pass == 1)))
             return rc;
-        if ((rc = partition_relation(ctx, sS, tmS, "S_", dS, ctx->t1S.as<row_t>(), ctx->t2S.as<row_t>(), ps, pol,
-                                     key_shift, &fS, &psS, &pcS, pass == 1)))
-            return rc;
-    }
     if (s2) {
         tm2.end_call();
         RHO_HIP(hipEventRecord(ctx->ev_join, s2));
         RHO_HIP(hipStreamWaitEvent(s, ctx->ev_join, 0));
     }
-    uint64_t *over = A.at<uint64_t>(off_over);
-    uint64_t *counts = A.at<uint64_t>(off_counts);
-    uint64_t *task_off = A.at<uint64_t>(off_toff);
-    uint64_t *result = A.at<uint64_t>(off_result);
+    const row_t *fR = pj.fR;
+    const uint64_t *psR = pj.psR, *pcR = pj.pcR;
+    const uint64_t P = 1ull << pol.bits;
+    const uint32_t join_grid = pj.join_grid;
+    const int algo = pj.algo;
+    uint64_t *over = A.at<uint64_t>(pj.off_over);
+    uint64_t *counts = A.at<uint64_t>(pj.off_counts);
+    uint64_t *task_off = A.at<uint64_t>(pj.off_toff);
+    uint64_t *result = A.at<uint64_t>(pj.off_result);
     uint32_t *n_over = reinterpret_cast<uint32_t *>(result + 3);
-    const uint32_t hash_shift = key_shift + pol.bits;
+    const uint32_t hash_shift = pj.key_shift + pol.bits;
     tm.mark("join_tasks");
-    RHO_HIP(launch_make_tasks(pcR, pcS, P, over, over_cap, result + 1, s));
-    if (!materialize) {
+    RHO_HIP(launch_make_tasks(pcR, pcS, P, over, pj.over_cap, result + 1, s));
+    if (!pj.materialize) {
         tm.mark("join_build_probe");
         RHO_HIP(launch_join(fR, fS, psR, pcR, psS, pcS, P, over, n_over, hash_shift, pol.rcap, join_grid, kJoinCount,
                             algo, counts, nullptr, nullptr, s));
@@ -302,9 +366,33 @@ int join_device(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const
     return MI355_OK;
 }
 
+// The whole join on device-resident inputs.  Caller holds ctx->mu.
+// Materialisation (opts->materialize): a per-task count pass, an exclusive scan of
+// the task counts into output offsets, then a write pass; `out` must be device
+// memory with room for out_cap triples (MI355_ERR_CAPACITY otherwise).
+int join_device(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const row_t *dS, uint64_t nS,
+                const mi355_rho_opts *opts, mi355_rho_stats *st, output_triple_t *out, uint64_t out_cap,
+                DeviceBuffer *grow) {
+    PendingJoin &pj = pending_of(ctx);
+    if (pj.active) {
+        set_last_error("a pipelined join (mi355_rho_join_begin) is pending on this device");
+        return MI355_ERR_INVALID;
+    }
+    int rc = join_begin(ctx, s, dR, nR, nS, opts, pj);
+    if (rc) {
+        pj.active = false;
+        return rc;
+    }
+    return join_finish(ctx, pj, dS, nS, st, out, out_cap, grow, false);
+}
+
 // Stable partition by destination shard (multi-GPU exchange step).
 int shard_partition_device(Context *ctx, hipStream_t s, const row_t *in, uint64_t n, uint32_t key_shift,
                            uint32_t dest_bits, row_t *out, uint64_t *dest_counts) {
+    if (pending_of(ctx).active) {  // the arena holds the pending join's R partitions
+        set_last_error("shard_partition while a pipelined join is pending on this device");
+        return MI355_ERR_INVALID;
+    }
     Policy pol{};
     pol.bits = pol.b1 = dest_bits;
     pol.passes = 1;
@@ -507,6 +595,62 @@ int mi355_rho_join(const table_t *relR, const table_t *relS, const joinconfig_t 
 
 int mi355_rht_join(const table_t *relR, const table_t *relS, const joinconfig_t *config, result_t *out) {
     return table_join(relR, relS, config, out, MI355_ALGO_RHT);
+}
+
+// Pipelined join (multi-GPU exchange): begin enqueues R's partition passes and returns;
+// finish runs S's passes and build/probe once S is valid in the stream order.
+int mi355_rho_join_begin(const row_t *R, uint64_t nR, uint64_t nS, const mi355_rho_opts *opts) {
+    if ((!R && nR) || nR == 0 || nS == 0) {
+        set_last_error("join_begin needs non-empty relations");
+        return MI355_ERR_INVALID;
+    }
+    if (!is_device_pointer(R)) {
+        set_last_error("join_begin needs a device-resident R");
+        return MI355_ERR_INVALID;
+    }
+    if (opts && opts->materialize && opts->out && !is_device_pointer(opts->out)) {
+        set_last_error("join_begin: materialisation output must be device memory");
+        return MI355_ERR_INVALID;
+    }
+    int status = MI355_OK;
+    Context *ctx = current_context(&status);
+    if (!ctx) return status;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    rho::PendingJoin &pj = rho::pending_of(ctx);
+    if (pj.active) {
+        set_last_error("a pipelined join is already pending on this device");
+        return MI355_ERR_INVALID;
+    }
+    const int rc = rho::join_begin(ctx, thread_stream(ctx, opts ? opts->stream : nullptr), R, nR, nS, opts, pj);
+    if (rc) pj.active = false;
+    return rc;
+}
+
+int mi355_rho_join_finish(const row_t *S, uint64_t nS, const mi355_rho_opts *opts, mi355_rho_stats *stats) {
+    int status = MI355_OK;
+    Context *ctx = current_context(&status);
+    if (!ctx) return status;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    rho::PendingJoin &pj = rho::pending_of(ctx);
+    mi355_rho_stats local{};
+    mi355_rho_stats *st = stats ? stats : &local;
+    std::memset(st, 0, sizeof(*st));
+    if (!pj.active) {
+        set_last_error("mi355_rho_join_finish without mi355_rho_join_begin");
+        return MI355_ERR_INVALID;
+    }
+    if ((!S && nS) || !is_device_pointer(S)) {
+        pj.active = false;
+        set_last_error("join_finish needs a device-resident S");
+        return MI355_ERR_INVALID;
+    }
+    struct Remember {
+        mi355_rho_stats *st;
+        ~Remember() { g_last_stats = *st; }
+    } remember{st};
+    const bool materialize = opts && opts->materialize;
+    return rho::join_finish(ctx, pj, S, nS, st, materialize ? opts->out : nullptr,
+                            materialize ? opts->out_capacity : 0, nullptr, true);
 }
 
 int mi355_rho_shard_partition(const row_t *in, uint64_t n, uint32_t key_shift, uint32_t dest_bits, row_t *out,

@@ -83,24 +83,140 @@ __device__ __forceinline__ uint64_t match_sum(const uint4 &q, uint32_t m) {
     return acc;
 }
 
+// OR of x over each group of LPW consecutive lanes (LPW = 4, 8 or 16; the groups'
+// bit fields do not overlap, so OR = sum) with DPP row operations on the VALU (no LDS
+// round trips): quad_perm [1,0,3,2] and [2,3,0,1], then inside each 16-lane row
+// row_ror:4 + row_ror:8 (LPW 16), or the neighbouring quad of the same 8-lane group
+// (row_ror:4 reads lane i-4, row_ror:12 lane i+4; LPW 8).  Every lane of a group
+// ends with the group's full word.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, true);
+}
+template <uint32_t LPW>
+__device__ __forceinline__ uint64_t group_or(uint64_t x) {
+    static_assert(LPW == 4 || LPW == 8 || LPW == 16, "lanes per 64-row word");
+    uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    lo |= dpp_u32<0xB1>(lo);
+    hi |= dpp_u32<0xB1>(hi);
+    lo |= dpp_u32<0x4E>(lo);
+    hi |= dpp_u32<0x4E>(hi);
+    if (LPW == 8) {
+        const bool upper = (__lane_id() & 4u) != 0;  // quad 1 or 3 of the row: partner is i-4
+        const uint32_t plo_a = dpp_u32<0x124>(lo), phi_a = dpp_u32<0x124>(hi);
+        const uint32_t plo_b = dpp_u32<0x12C>(lo), phi_b = dpp_u32<0x12C>(hi);
+        lo |= upper ? plo_a : plo_b;
+        hi |= upper ? phi_a : phi_b;
+    }
+    if (LPW == 16) {
+        lo |= dpp_u32<0x124>(lo);
+        hi |= dpp_u32<0x124>(hi);
+        lo |= dpp_u32<0x128>(lo);
+        hi |= dpp_u32<0x128>(hi);
+    }
+    return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+
 // Count (WRITE=false) or bitvector + count (WRITE=true) of one chunk per workgroup.
 // rows_per_chunk is a multiple of kWaves * 64 * V * kUnroll.
 // SUM=true accumulates the matching values instead of counting them (SIMD512::sum).
+//
+// The block iterations that lie wholly inside the chunk run software-pipelined over
+// two register sets: iteration i+1's loads are issued before iteration i's bitvector
+// stores.  gfx950 retires loads and stores through one in-order vmcnt, so a wait for a
+// load also waits for every older store; issued in this order, the wait for i+1's
+// loads never waits for i's stores.  Loads are raw buffer loads over the chunk (one
+// 32-bit lane offset + a uniform offset; the prefetch past the last iteration reads
+// 0 from the bounds check and is not used).  A ragged chunk end (only the last chunk
+// of a column) takes the element-wise tail path.
+template <typename T, bool WRITE, bool SUM>
+struct PredicateTile {
+    static constexpr uint32_t V = 16 / sizeof(T);  // rows per lane per load
+    static constexpr uint32_t LPW = 64 / V;        // lanes per 64-row word
+    static constexpr uint32_t FULL = (1u << V) - 1u;
+    static constexpr uint64_t STEP = (uint64_t)kWaves * 64 * V;  // rows per block per load round
+
+    // masks, counts (or sums) and bitvector words of kUnroll loads starting at row `base`.
+    // FULL_TILE: every row is inside the column, and all LPW lanes of a group store
+    // their (identical) word — no branch around the store, so the compiler's vmcnt
+    // accounting sees a fixed number of stores between the prefetch and its wait.
+    template <bool FULL_TILE>
+    static __device__ __forceinline__ void process(const uint4 (&q)[kUnroll], const uint32_t (&valid)[kUnroll],
+                                                   uint64_t base, uint64_t r1, uint64_t nwords, T lo, T hi,
+                                                   uint64_t *__restrict__ bv, uint64_t &count) {
+        const uint32_t lane = __lane_id();
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const uint32_t m = match_mask<T>(q[u], lo, hi, valid[u]);
+            if (SUM) count += match_sum<T>(q[u], m);
+            else count += __popc(m);
+            if (WRITE) {
+                const uint64_t x = group_or<LPW>((uint64_t)m << (V * (lane % LPW)));
+                const uint64_t word = (base + u * STEP) / 64 + lane / LPW;
+                if (FULL_TILE) bv[word] = x;
+                else if ((lane % LPW) == 0 && word < nwords && (base + u * STEP) < r1) bv[word] = x;
+            }
+        }
+    }
+};
+
 template <typename T, bool WRITE, bool SUM = false>
 __global__ __launch_bounds__(kBlock) void k_predicate(const T *__restrict__ in, uint64_t n, T lo, T hi,
                                                       uint64_t rows_per_chunk, uint64_t *__restrict__ bv,
                                                       uint64_t *__restrict__ chunk_counts) {
-    constexpr uint32_t V = 16 / sizeof(T);  // rows per lane per load
-    constexpr uint32_t LPW = 64 / V;        // lanes per 64-row word
-    constexpr uint32_t FULL = (1u << V) - 1u;
+    using PT = PredicateTile<T, WRITE, SUM>;
+    constexpr uint32_t V = PT::V, FULL = PT::FULL;
+    constexpr uint64_t STEP = PT::STEP;
+    constexpr uint64_t ITER = STEP * kUnroll;  // rows per block iteration
     __shared__ uint64_t red[kWaves];
     const uint32_t lane = __lane_id(), wave = threadIdx.x / kWave;
     const uint64_t r0 = (uint64_t)blockIdx.x * rows_per_chunk;
     const uint64_t r1 = (r0 + rows_per_chunk < n) ? r0 + rows_per_chunk : n;
     const uint64_t nwords = (n + 63) / 64;
-    constexpr uint64_t STEP = (uint64_t)kWaves * 64 * V;  // rows per block per load round
+    const uint64_t nfull = (r1 - r0) / ITER;
+    const uint64_t full_end = r0 + nfull * ITER;
     uint64_t count = 0;
-    for (uint64_t base = r0 + (uint64_t)wave * 64 * V; base < r1; base += STEP * kUnroll) {
+    if (nfull > 0) {
+        // chunks hold far fewer than 2^32 bytes (geometry(): n / 2048 rows)
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(in + r0, (uint32_t)((full_end - r0) * sizeof(T)));
+        const uint32_t voff = (uint32_t)(((uint64_t)wave * 64 * V + (uint64_t)lane * V) * sizeof(T));
+        uint32_t valid[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) valid[u] = FULL;
+        uint4 qa[kUnroll], qb[kUnroll];
+        auto load = [&](uint4(&q)[kUnroll], uint64_t it) {
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u)
+                q[u] = buf_ld_nt_u128(rs, voff, (uint32_t)((it * ITER + u * STEP) * sizeof(T)));
+            __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the stores that follow
+        };
+        // an empty asm that reads a register set forces its wait at that point, in
+        // straight-line code right after the other set's prefetch (otherwise the
+        // compiler's wait analysis merges the loop back-edge into a vmcnt(0))
+        auto wait_for = [](const uint4(&q)[kUnroll]) {
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) asm volatile("" ::"v"(q[u].x), "v"(q[u].y), "v"(q[u].z), "v"(q[u].w));
+        };
+        const uint64_t wbase = r0 + (uint64_t)wave * 64 * V;
+        // iterations in pairs, no branch between a prefetch and its wait (LLVM would sink
+        // a prefetch whose result is dead on an early-exit path below the next stores)
+        load(qa, 0);
+        load(qb, 1);
+        wait_for(qa);
+        const uint64_t npairs = nfull / 2;
+        for (uint64_t p = 0; p < npairs; ++p) {
+            const uint64_t it = 2 * p;
+            PT::template process<true>(qa, valid, wbase + it * ITER, r1, nwords, lo, hi, bv, count);
+            load(qa, it + 2);
+            wait_for(qb);
+            PT::template process<true>(qb, valid, wbase + (it + 1) * ITER, r1, nwords, lo, hi, bv, count);
+            load(qb, it + 3);
+            wait_for(qa);
+        }
+        if (nfull & 1) PT::template process<true>(qa, valid, wbase + (nfull - 1) * ITER, r1, nwords, lo, hi, bv, count);
+    }
+    // ragged end of the last chunk: fewer than ITER rows, element loads at the very end
+    for (uint64_t base = full_end + (uint64_t)wave * 64 * V; base < r1; base += ITER) {
         uint4 q[kUnroll];
         uint32_t valid[kUnroll];
 #pragma unroll
@@ -109,7 +225,7 @@ __global__ __launch_bounds__(kBlock) void k_predicate(const T *__restrict__ in, 
             if (row + V <= r1) {
                 q[u] = ld_nt(reinterpret_cast<const uint4 *>(in + row));
                 valid[u] = FULL;
-            } else if (row < r1) {  // ragged tail: element loads packed like a uint4
+            } else if (row < r1) {  // element loads packed like a uint4
                 uint32_t w[4] = {0, 0, 0, 0};
 #pragma unroll
                 for (uint32_t j = 0; j < V; ++j) {
@@ -125,19 +241,7 @@ __global__ __launch_bounds__(kBlock) void k_predicate(const T *__restrict__ in, 
                 valid[u] = 0;
             }
         }
-#pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
-            const uint32_t m = match_mask<T>(q[u], lo, hi, valid[u]);
-            if (SUM) count += match_sum<T>(q[u], m);
-            else count += __popc(m);
-            if (WRITE) {
-                uint64_t x = (uint64_t)m << (V * (lane % LPW));
-#pragma unroll
-                for (uint32_t off = 1; off < LPW; off <<= 1) x |= __shfl_xor(x, off, kWave);
-                const uint64_t word = (base + u * STEP) / 64 + lane / LPW;
-                if ((lane % LPW) == 0 && word < nwords && (base + u * STEP) < r1) bv[word] = x;
-            }
-        }
+        PT::template process<false>(q, valid, base, r1, nwords, lo, hi, bv, count);
     }
     count = wave_sum_u64(count);
     if (lane == 0) red[wave] = count;

@@ -168,6 +168,8 @@ SIGNATURES = {
     "mi355_rht_join": (C.c_int, [C.POINTER(table_t), C.POINTER(table_t), C.POINTER(joinconfig_t), C.POINTER(result_t)]),
     "mi355_last_join_stats": (C.c_int, [C.POINTER(rho_stats)]),
     "mi355_rho_shard_partition": (C.c_int, [_P, C.c_uint64, C.c_uint32, C.c_uint32, _P, _U64P, _P]),
+    "mi355_rho_join_begin": (C.c_int, [_P, C.c_uint64, C.c_uint64, C.POINTER(rho_opts)]),
+    "mi355_rho_join_finish": (C.c_int, [_P, C.c_uint64, C.POINTER(rho_opts), C.POINTER(rho_stats)]),
     "mi355_timing_enable": (None, [C.c_int]),
     "mi355_set_partition_overlap": (None, [C.c_int]),
     "mi355_timing_get": (C.c_int, [C.POINTER(C.c_char_p), C.POINTER(C.c_double), C.c_int]),
@@ -311,6 +313,24 @@ def rho_join(R, nR: int, S, nS: int, *, radix_bits: int = 0, passes: int = 0, ke
     if rc == -5:
         raise Mi355Error(rc, f"capacity: {int(st.matches)} triples needed")
     _check(rc)
+    return JoinResult(int(st.matches), st.as_dict())
+
+
+def rho_join_begin(R, nR: int, nS: int, *, key_shift: int = 0, stream: int | None = None,
+                   algorithm: str = "RHO") -> None:
+    """First half of a pipelined count join (mi355_rho_join_begin): plans both
+    relations and enqueues R's partition passes on `stream`; returns at once."""
+    o = rho_opts(0, 0, key_shift, 0, 0, ALGORITHMS[algorithm], stream or None, None, 0)
+    _check(lib.mi355_rho_join_begin(ptr(R), nR, nS, C.byref(o)))
+
+
+def rho_join_finish(S, nS: int, *, key_shift: int = 0, stream: int | None = None,
+                    algorithm: str = "RHO") -> JoinResult:
+    """Second half (mi355_rho_join_finish): S's passes and build/probe, after S became
+    valid in the stream order; blocks and returns the count."""
+    o = rho_opts(0, 0, key_shift, 0, 0, ALGORITHMS[algorithm], stream or None, None, 0)
+    st = rho_stats()
+    _check(lib.mi355_rho_join_finish(ptr(S), nS, C.byref(o), C.byref(st)))
     return JoinResult(int(st.matches), st.as_dict())
 
 

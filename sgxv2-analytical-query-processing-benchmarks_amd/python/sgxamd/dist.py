@@ -1,4 +1,4 @@
-"""Multi-GPU RHO: radix-partition sharding with one all-to-all exchange.
+"""Multi-GPU RHO: radix-partition sharding with one all-to-all exchange per relation.
 
 One process per GPU (torch.distributed; backend "nccl" is RCCL over xGMI on
 ROCm, "gloo" runs the same code on CPU tensors in tests).  Every rank holds a
@@ -9,25 +9,38 @@ tmpR/tmpS arrays (:1421-1433) across sockets:
   1. shard partition: stable radix partition of the local slice by destination
      d = key & (G - 1) (the low log2(G) key bits, i.e. pass-1 radix bits of
      radix_join.cpp:1118-1119 taken by the shard level);
-  2. split exchange: all_to_all of the G per-destination counts;
-  3. tuple exchange: all_to_all_single of the 8-byte tuples (viewed as int64); R's
-     exchange is left in flight while S is shard-partitioned;
+  2. split exchange: all_to_all of the G per-destination counts (host integers, on
+     a gloo side group so they never queue behind a tuple exchange on the RCCL
+     stream);
+  3. tuple exchange: all_to_all_single of the 8-byte tuples (viewed as int64);
   4. local join of the received R' and S' with key_shift = log2(G) (all their keys
      agree on the low bits, so the local radix bits start above them);
   5. all_reduce(sum) of the match counts (exact: integer sum).
+
+Pipelining (one timeline per rank; RCCL runs on its own stream):
+
+    compute:  shard R | shard S | .... R' local passes | S' local passes, build/probe
+    xGMI:             | R exchange ......| S exchange ........|
+
+S is shard-partitioned while R is on the wire, and R's local partition passes
+(mi355_rho_join_begin) run while S is on the wire; S's passes and the build/probe
+(mi355_rho_join_finish) follow S's arrival in stream order.
 
 G must be a power of two.  The local compute (steps 1 and 4) defaults to the
 HIP library; tests inject CPU restatements to run the exchange logic on gloo.
 """
 from __future__ import annotations
 
+import contextlib
+import os
+import sys
 import time
 from dataclasses import dataclass, field
 
 import torch
 import torch.distributed as dist
 
-from . import rho_join, shard_partition
+from . import rho_join, rho_join_begin, rho_join_finish, shard_partition
 
 
 def _log2_exact(g: int) -> int:
@@ -47,35 +60,114 @@ class ShardedJoinResult:
     local_stats: dict = field(default_factory=dict)
 
 
+class _Done:
+    """Completed exchange (gloo staging is synchronous)."""
+
+    def wait(self):
+        return None
+
+
+def _stream_of(t: torch.Tensor):
+    return torch.cuda.current_stream(t.device).cuda_stream if t.is_cuda else None
+
+
 def _default_partition(t: torch.Tensor, n: int, dest_bits: int):
     out = torch.empty_like(t)
-    stream = torch.cuda.current_stream().cuda_stream if t.is_cuda else None
-    counts = shard_partition(t, n, 0, dest_bits, out, stream)
+    counts = shard_partition(t, n, 0, dest_bits, out, _stream_of(t))
     return out, counts
 
 
-def _default_local_join(R: torch.Tensor, nR: int, S: torch.Tensor, nS: int, key_shift: int,
-                        algorithm: str = "RHO"):
-    stream = torch.cuda.current_stream().cuda_stream if R.is_cuda else None
-    res = rho_join(R, nR, S, nS, key_shift=key_shift, stream=stream, algorithm=algorithm)
-    return res.matches, res.stats
+class _LibraryLocalJoin:
+    """Local join through the pipelined C-ABI: begin (R's passes, asynchronous) and
+    finish (S's passes + build/probe, blocking)."""
+
+    def __init__(self, algorithm: str):
+        self.algorithm = algorithm
+        self.shift = 0
+
+    def begin(self, R, nR, nS, shift):
+        self.shift = shift
+        if R.is_cuda:
+            rho_join_begin(R, nR, nS, key_shift=shift, stream=_stream_of(R), algorithm=self.algorithm)
+        else:  # host tensors: one blocking call in finish
+            self.R, self.nR = R, nR
+
+    def finish(self, S, nS):
+        if S.is_cuda:
+            res = rho_join_finish(S, nS, key_shift=self.shift, stream=_stream_of(S), algorithm=self.algorithm)
+        else:
+            res = rho_join(self.R, self.nR, S, nS, key_shift=self.shift, algorithm=self.algorithm)
+        return res.matches, res.stats
 
 
-def _exchange(t: torch.Tensor, send_counts: list[int], group, async_op: bool = False):
-    """all_to_all of the per-destination counts (blocking, tiny), then of the tuples.
-    With async_op the tuple exchange is left in flight: (out, total, work)."""
-    world = dist.get_world_size(group)
-    dev = t.device
-    sc = torch.tensor(send_counts, dtype=torch.int64, device=dev)
-    rc = torch.empty(world, dtype=torch.int64, device=dev)
-    dist.all_to_all_single(rc, sc, group=group)
-    recv_counts = [int(x) for x in rc.tolist()]
+class _InjectedLocalJoin:
+    """A caller-supplied local_join_fn(R, nR, S, nS, shift) seen through begin/finish."""
+
+    def __init__(self, fn):
+        self.fn = fn
+
+    def begin(self, R, nR, nS, shift):
+        self.args = (R, nR, shift)
+
+    def finish(self, S, nS):
+        R, nR, shift = self.args
+        return self.fn(R, nR, S, nS, shift)
+
+
+@contextlib.contextmanager
+def stdout_to_stderr():
+    """Route file descriptor 1 to 2 for the duration (gloo's connection banner is
+    printed to stdout by native code; bench.py's stdout carries exactly one JSON line)."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
+_count_groups: dict = {}
+
+
+def _count_group(group):
+    """A gloo group over the same ranks for the host-side count exchanges (created
+    collectively on first use, cached)."""
+    backend = dist.get_backend(group)
+    if backend == "gloo":
+        return group
+    key = id(group)
+    if key not in _count_groups:
+        ranks = None if group is None else dist.get_process_group_ranks(group)
+        with stdout_to_stderr():
+            _count_groups[key] = dist.new_group(ranks=ranks, backend="gloo")
+    return _count_groups[key]
+
+
+def _exchange_counts(send_counts: list[int], cgroup) -> list[int]:
+    world = dist.get_world_size(cgroup)
+    sc = torch.tensor(send_counts, dtype=torch.int64)
+    rc = torch.empty(world, dtype=torch.int64)
+    dist.all_to_all_single(rc, sc, group=cgroup)
+    return [int(x) for x in rc.tolist()]
+
+
+def _exchange_tuples(t: torch.Tensor, send_counts: list[int], recv_counts: list[int], group):
+    """all_to_all_single of the tuples, left in flight: (out, total, work).  A gloo
+    group with device tensors (single-GPU rehearsal of the multi-rank path) stages
+    through host memory synchronously."""
     total = sum(recv_counts)
-    out = torch.empty(max(total, 1), dtype=torch.int64, device=dev)
-    work = dist.all_to_all_single(out[:total], t, recv_counts, send_counts, group=group, async_op=async_op)
-    if async_op:
-        return out, total, work
-    return out, total
+    out = torch.empty(max(total, 1), dtype=torch.int64, device=t.device)
+    if t.is_cuda and dist.get_backend(group) == "gloo":
+        host_out = torch.empty(max(total, 1), dtype=torch.int64)
+        dist.all_to_all_single(host_out[:total], t[:sum(send_counts)].cpu(), recv_counts, send_counts, group=group)
+        out[:total].copy_(host_out[:total])
+        return out, total, _Done()
+    work = dist.all_to_all_single(out[:total], t[:sum(send_counts)], recv_counts, send_counts, group=group,
+                                  async_op=True)
+    return out, total, work
 
 
 def sharded_rho_join(R: torch.Tensor, S: torch.Tensor, *, group=None, partition_fn=None,
@@ -86,38 +178,45 @@ def sharded_rho_join(R: torch.Tensor, S: torch.Tensor, *, group=None, partition_
     on every rank.
     """
     partition_fn = partition_fn or _default_partition
-    if local_join_fn is None:
-        def local_join_fn(R_, nR_, S_, nS_, shift_):
-            return _default_local_join(R_, nR_, S_, nS_, shift_, algorithm)
+    local = _InjectedLocalJoin(local_join_fn) if local_join_fn is not None else _LibraryLocalJoin(algorithm)
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     dest_bits = _log2_exact(world)
     ms = {}
     sync = (lambda: torch.cuda.synchronize()) if R.is_cuda else (lambda: None)
     t0 = time.perf_counter()
     if world == 1:
-        local, st = local_join_fn(R, R.numel(), S, S.numel(), 0)
+        local.begin(R, R.numel(), S.numel(), 0)
+        m, st = local.finish(S, S.numel())
         sync()
         ms["local_join"] = (time.perf_counter() - t0) * 1e3
-        return ShardedJoinResult(int(local), int(local), R.numel(), S.numel(), ms, st)
+        return ShardedJoinResult(int(m), int(m), R.numel(), S.numel(), ms, st)
 
-    # R's tuple exchange (xGMI) runs while S is shard-partitioned (HBM): RCCL works on
-    # its own stream, the partition kernels on the current one.
+    cgroup = _count_group(group)
+    # R: shard partition, counts, tuple exchange left in flight on the RCCL stream
     pR, cR = partition_fn(R, R.numel(), dest_bits)
-    rR, nR, wR = _exchange(pR, cR, group, async_op=True)
+    rcR = _exchange_counts(cR, cgroup)
+    rR, nR, wR = _exchange_tuples(pR, cR, rcR, group)
+    # S: shard partition on the compute stream while R is on the wire
     pS, cS = partition_fn(S, S.numel(), dest_bits)
+    rcS = _exchange_counts(cS, cgroup)
     t1 = time.perf_counter()
     ms["shard_partition"] = (t1 - t0) * 1e3
-    rS, nS, wS = _exchange(pS, cS, group, async_op=True)
+    rS, nS, wS = _exchange_tuples(pS, cS, rcS, group)
+    # R's local passes once R has arrived (stream order), while S is on the wire
     wR.wait()
-    wS.wait()
+    if nR and nS:
+        local.begin(rR, nR, nS, dest_bits)
+        wS.wait()
+        m, st = local.finish(rS, nS)
+    else:
+        wS.wait()
+        m, st = 0, {}
     sync()
     t2 = time.perf_counter()
-    ms["exchange"] = (t2 - t1) * 1e3
-    local, st = local_join_fn(rR, nR, rS, nS, dest_bits)
-    sync()
-    t3 = time.perf_counter()
-    ms["local_join"] = (t3 - t2) * 1e3
-    tot = torch.tensor([int(local)], dtype=torch.int64, device=R.device)
-    dist.all_reduce(tot, op=dist.ReduceOp.SUM, group=group)
-    ms["all_reduce"] = (time.perf_counter() - t3) * 1e3
-    return ShardedJoinResult(int(tot.item()), int(local), nR, nS, ms, st)
+    ms["exchange_and_local_join"] = (t2 - t1) * 1e3
+    tot = torch.tensor([int(m)], dtype=torch.int64)
+    dist.all_reduce(tot, op=dist.ReduceOp.SUM, group=cgroup)
+    ms["all_reduce"] = (time.perf_counter() - t2) * 1e3
+    # keep the send buffers alive until both exchanges completed
+    del pR, pS
+    return ShardedJoinResult(int(tot.item()), int(m), nR, nS, ms, st)

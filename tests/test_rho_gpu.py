@@ -323,3 +323,51 @@ def test_partition_overlap_same_result(sgx, orc, gpu, case):
                 assert np.array_equal(sorted_triples(got[(on, bits)]), sorted_triples(exp)), (case, on, bits)
     finally:
         sgx.set_partition_overlap(True)
+
+
+@pytest.mark.parametrize("case", ["pk_fk_shift", "dups", "rht"])
+def test_pipelined_begin_finish(sgx, orc, gpu, case):
+    """mi355_rho_join_begin + mi355_rho_join_finish == one mi355_rho_join_ex call (the
+    multi-GPU path's local join, with S written to HBM only between the two calls)."""
+    import torch
+
+    rng = np.random.default_rng(9)
+    shift, algo = 0, "RHO"
+    if case == "pk_fk_shift":  # a shard's view: every key has the same low 2 bits
+        R, S = sgx.reference_relations(1 << 18, 3 << 17)
+        R = R[(R["key"] & 3) == 1]
+        S = S[(S["key"] & 3) == 1]
+        shift = 2
+    else:
+        R = rel(rng.integers(0, 7000, 70_001).astype(np.uint32))
+        S = rel(rng.integers(0, 7000, 50_003).astype(np.uint32))
+        algo = "RHT" if case == "rht" else "RHO"
+    exp = orc.count_join_sort(R, S)
+    dR = torch.from_numpy(R.view(np.int64).copy()).to(gpu)
+    dS = torch.empty(len(S), dtype=torch.int64, device=gpu)
+    stream = torch.cuda.current_stream().cuda_stream
+    sgx.rho_join_begin(dR, len(R), len(S), key_shift=shift, stream=stream, algorithm=algo)
+    dS.copy_(torch.from_numpy(S.view(np.int64).copy()))  # S lands after begin, in stream order
+    res = sgx.rho_join_finish(dS, len(S), key_shift=shift, stream=stream, algorithm=algo)
+    assert res.matches == exp
+    assert sgx.rho_join(dR, len(R), dS, len(S), key_shift=shift, algorithm=algo).matches == exp
+
+
+def test_pipelined_guards(sgx, gpu):
+    import torch
+
+    R, S = sgx.reference_relations(1 << 14, 1 << 14)
+    dR = torch.from_numpy(R.view(np.int64).copy()).to(gpu)
+    dS = torch.from_numpy(S.view(np.int64).copy()).to(gpu)
+    with pytest.raises(sgx.Mi355Error):  # finish without begin
+        sgx.rho_join_finish(dS, len(S))
+    sgx.rho_join_begin(dR, len(R), len(S))
+    with pytest.raises(sgx.Mi355Error):  # another join while one is pending
+        sgx.rho_join(dR, len(R), dS, len(S))
+    with pytest.raises(sgx.Mi355Error):  # the shard step would reuse the pending join's scratch
+        sgx.shard_partition(dR, len(R), 0, 2, torch.empty_like(dR))
+    with pytest.raises(sgx.Mi355Error):  # |S| differs from begin's
+        sgx.rho_join_finish(dS, len(S) - 1)
+    sgx.rho_join_begin(dR, len(R), len(S))
+    assert sgx.rho_join_finish(dS, len(S)).matches == len(S)
+    assert sgx.rho_join(dR, len(R), dS, len(S)).matches == len(S)
