@@ -11,7 +11,7 @@ OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 
 if [ -z "$SKIP_TESTS" ]; then
-  timeout -k 10 600 python -m pytest tests -m gpu -q -p no:cacheprovider > "$OUT/gpu_tests.log" 2>&1 \
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > "$OUT/gpu_tests.log" 2>&1 \
     || { echo "gpu tests failed"; tail -40 "$OUT/gpu_tests.log"; exit 1; }
   tail -2 "$OUT/gpu_tests.log"
 fi
