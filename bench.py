@@ -29,18 +29,26 @@ sys.path.insert(0, os.path.join(PKG, "python"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 METRIC = "M probed tuples/sec (RHO join) + scan GB/s vs HBM roofline, 1/2/4/8 MI355X"
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic_r01e.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic_r01h.json")
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def algorithmic_bytes(kernel: str, nR: int, nS: int) -> int:
-    """Bytes a kernel must move per launch (DESIGN.md 'Kernels and their rooflines')."""
+def algorithmic_bytes(kernel: str, nR: int, nS: int, passes: int = 2, pass2_bits: int = 8) -> int:
+    """Bytes a kernel must move per launch (DESIGN.md 'Kernels and their rooflines').
+
+    Two-pass plans: the pass-1 scatter also writes one pass-2 digit byte per tuple (the
+    digit side stream) and the pass-2 histogram reads those bytes, not the tuples."""
     n = nR if kernel.startswith("R_") else nS
+    side = passes == 2 and pass2_bits <= 8 and os.environ.get("SGXAMD_DIGIT_SIDE", "1") != "0"  # uses_digit_side()
+    if kernel.endswith("pass2_hist") and side:
+        return n              # one digit byte per tuple
     if kernel.endswith("_hist"):
         return 8 * n          # read every tuple once (key only used, AoS line read)
+    if kernel.endswith("pass1_scatter") and side:
+        return 17 * n         # read + write every tuple, + its pass-2 digit byte
     if kernel.endswith("_scatter"):
         return 16 * n         # read + write every tuple
     if kernel == "join_build_probe":
@@ -180,9 +188,10 @@ def main():
     nR = results[-1].recv_r
     nS = results[-1].recv_s
     avg = {k: statistics.mean(v) for k, v in per_kernel.items()}
-    byte_kernels = {k: v for k, v in avg.items() if algorithmic_bytes(k, nR, nS) > 0}
+    plan = (results[-1].local_stats.get("passes") or 2, results[-1].local_stats.get("pass2_bits") or 0)
+    byte_kernels = {k: v for k, v in avg.items() if algorithmic_bytes(k, nR, nS, *plan) > 0}
     dom = max(byte_kernels, key=byte_kernels.get)
-    achieved = algorithmic_bytes(dom, nR, nS) / (avg[dom] * 1e-3) / 1e9
+    achieved = algorithmic_bytes(dom, nR, nS, *plan) / (avg[dom] * 1e-3) / 1e9
     traffic = None
     if os.path.exists(TRAFFIC_FILE):
         try:
@@ -194,7 +203,7 @@ def main():
             traffic = None
     roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "avg_ms": round(avg[dom], 4), "algorithmic_bytes": algorithmic_bytes(dom, nR, nS)}
+                "avg_ms": round(avg[dom], 4), "algorithmic_bytes": algorithmic_bytes(dom, nR, nS, *plan)}
     probe_gbs = algorithmic_bytes("join_build_probe", nR, nS) / (avg["join_build_probe"] * 1e-3) / 1e9
     phase = {k: round(v, 4) for k, v in sorted(avg.items())}
     ls = results[-1].local_stats

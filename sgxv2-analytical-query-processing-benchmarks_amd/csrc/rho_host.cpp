@@ -71,6 +71,19 @@ Policy choose_policy(uint64_t nR, uint64_t nS, const mi355_rho_opts *o) {
     return p;
 }
 
+// Two-pass plans carry the pass-2 digit of every pass-1 output tuple in a byte side
+// stream (launch_hist_side); a 9-bit pass-2 digit does not fit and takes the tuple
+// histogram instead.
+// SGXAMD_DIGIT_SIDE=0 turns it off (development A/B switch; results are identical).
+inline bool digit_side_enabled() {
+    static const bool on = [] {
+        const char *e = std::getenv("SGXAMD_DIGIT_SIDE");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return on;
+}
+inline bool uses_digit_side(const Policy &p) { return p.passes == 2 && p.b2 <= 8 && digit_side_enabled(); }
+
 inline uint64_t seg_size_for(uint64_t n) {
     uint64_t s = (n + kSegTarget - 1) / kSegTarget;
     s = (s + kTile - 1) / kTile * kTile;
@@ -97,10 +110,12 @@ struct RelPlan {
     } while (0)
 
 // One relation through pass 1 (and pass 2).  Returns the final buffer and
-// partition table pointers through *final / *pstart / *pcnt.
+// partition table pointers through *final / *pstart / *pcnt.  side (n bytes, two-pass
+// plans whose pass-2 digit fits a byte): the pass-1 scatter writes every tuple's pass-2
+// digit there, and pass 2's histogram reads those bytes instead of the tuples.
 int partition_relation(Context *ctx, hipStream_t s, Timer &tm, const char *tag, const row_t *in, row_t *t1,
-                       row_t *t2, RelPlan &rp, const Policy &pol, uint32_t key_shift, const row_t **final_rel,
-                       const uint64_t **pstart, const uint64_t **pcnt, bool pass2_now) {
+                       row_t *t2, uint8_t *side, RelPlan &rp, const Policy &pol, uint32_t key_shift,
+                       const row_t **final_rel, const uint64_t **pstart, const uint64_t **pcnt, bool pass2_now) {
     Arena &A = ctx->scratch;
     uint64_t *hist1 = A.at<uint64_t>(rp.hist1);
     uint64_t *tot1 = A.at<uint64_t>(rp.tot1);
@@ -108,6 +123,7 @@ int partition_relation(Context *ctx, hipStream_t s, Timer &tm, const char *tag, 
     uint64_t *cnt1 = A.at<uint64_t>(rp.cnt1);
     uint32_t *segbase2 = A.at<uint32_t>(rp.segbase2);
     std::string t(tag);
+    const bool use_side = side != nullptr && uses_digit_side(pol);
     if (!pass2_now) {
         SegMap m1{nullptr, nullptr, nullptr, 1, rp.seg1, rp.n};
         tm.mark((t + "pass1_hist").c_str());
@@ -116,7 +132,9 @@ int partition_relation(Context *ctx, hipStream_t s, Timer &tm, const char *tag, 
         RHO_HIP(launch_scan_single(hist1, rp.nseg1, pol.b1, tot1, start1, cnt1, 0,
                                    pol.passes == 2 ? segbase2 : nullptr, rp.seg2, s));
         tm.mark((t + "pass1_scatter").c_str());
-        RHO_HIP(launch_scatter(in, t1, m1, rp.nseg1, key_shift, pol.b1, hist1, kDigitMajor, rp.nseg1, start1, s));
+        const DigitSide ds{side, key_shift + pol.b1, pol.b2};
+        RHO_HIP(launch_scatter(in, t1, m1, rp.nseg1, key_shift, pol.b1, hist1, kDigitMajor, rp.nseg1, start1,
+                               use_side ? &ds : nullptr, s));
         *final_rel = t1;
         *pstart = start1;
         *pcnt = cnt1;
@@ -129,11 +147,14 @@ int partition_relation(Context *ctx, hipStream_t s, Timer &tm, const char *tag, 
     SegMap m2{start1, cnt1, segbase2, F1, rp.seg2, rp.n};
     const uint32_t shift2 = key_shift + pol.b1;
     tm.mark((t + "pass2_hist").c_str());
-    RHO_HIP(launch_hist(t1, m2, rp.grid2, shift2, pol.b2, hist2, kSegMajor, 0, s));
+    if (use_side)
+        RHO_HIP(launch_hist_side(side, m2, rp.grid2, pol.b2, hist2, s));
+    else
+        RHO_HIP(launch_hist(t1, m2, rp.grid2, shift2, pol.b2, hist2, kSegMajor, 0, s));
     tm.mark((t + "pass2_scan").c_str());
     RHO_HIP(launch_scan_regions(hist2, segbase2, start1, F1, pol.b2, ps, pc, s));
     tm.mark((t + "pass2_scatter").c_str());
-    RHO_HIP(launch_scatter(t1, t2, m2, rp.grid2, shift2, pol.b2, hist2, kSegMajor, 0, nullptr, s));
+    RHO_HIP(launch_scatter(t1, t2, m2, rp.grid2, shift2, pol.b2, hist2, kSegMajor, 0, nullptr, nullptr, s));
     *final_rel = t2;
     *pstart = ps;
     *pcnt = pc;
@@ -217,6 +238,10 @@ int join_begin(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, uint64
         RHO_HIP(ctx->t2R.ensure(std::max<uint64_t>(nR, 1) * sizeof(row_t)));
         RHO_HIP(ctx->t2S.ensure(std::max<uint64_t>(nS, 1) * sizeof(row_t)));
     }
+    if (uses_digit_side(pol)) {
+        RHO_HIP(ctx->sideR.ensure(std::max<uint64_t>(nR, 16)));
+        RHO_HIP(ctx->sideS.ensure(std::max<uint64_t>(nS, 16)));
+    }
     Arena &A = ctx->scratch;
     A.reset();
     plan_relation(A, pj.pr, nR, pol);
@@ -244,8 +269,9 @@ int join_begin(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, uint64
     }
     int rc;
     for (int pass = 0; pass < (int)pol.passes; ++pass)
-        if ((rc = partition_relation(ctx, s, tm, "R_", dR, ctx->t1R.as<row_t>(), ctx->t2R.as<row_t>(), pj.pr, pol,
-                                     pj.key_shift, &pj.fR, &pj.psR, &pj.pcR, pass == 1)))
+        if ((rc = partition_relation(ctx, s, tm, "R_", dR, ctx->t1R.as<row_t>(), ctx->t2R.as<row_t>(),
+                                     ctx->sideR.as<uint8_t>(), pj.pr, pol, pj.key_shift, &pj.fR, &pj.psR, &pj.pcR,
+                                     pass == 1)))
             return rc;
     pj.active = true;
     return MI355_OK;
@@ -282,8 +308,9 @@ int join_finish(Context *ctx, PendingJoin &pj, const row_t *dS, uint64_t nS, mi3
     const uint64_t *psS = nullptr, *pcS = nullptr;
     int rc;
     for (int pass = 0; pass < (int)pol.passes; ++pass)
-        if ((rc = partition_relation(ctx, sS, tmS, "S_", dS, ctx->t1S.as<row_t>(), ctx->t2S.as<row_t>(), pj.ps, pol,
-                                     pj.key_shift, &fS, &psS, &pcS, pass == 1)))
+        if ((rc = partition_relation(ctx, sS, tmS, "S_", dS, ctx->t1S.as<row_t>(), ctx->t2S.as<row_t>(),
+                                     ctx->sideS.as<uint8_t>(), pj.ps, pol, pj.key_shift, &fS, &psS, &pcS,
+                                     pass == 1)))
             return rc;
     if (s2) {
         tm2.end_call();
@@ -405,7 +432,8 @@ int shard_partition_device(Context *ctx, hipStream_t s, const row_t *in, uint64_
     tm.begin_call(s, thread_timing_enabled());
     const row_t *f;
     const uint64_t *pst, *pcn;
-    int rc = partition_relation(ctx, s, tm, "shard_", in, out, nullptr, rp, pol, key_shift, &f, &pst, &pcn, false);
+    int rc = partition_relation(ctx, s, tm, "shard_", in, out, nullptr, nullptr, rp, pol, key_shift, &f, &pst, &pcn,
+                                false);
     if (rc) return rc;
     tm.end_call();
     const uint32_t F = 1u << dest_bits;

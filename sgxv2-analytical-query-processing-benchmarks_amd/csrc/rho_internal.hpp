@@ -48,11 +48,26 @@ hipError_t launch_scan_regions(uint64_t *hist, const uint32_t *seg_base, const u
                                uint32_t nreg, uint32_t bits, uint64_t *part_start, uint64_t *part_count,
                                hipStream_t s);
 
+// Digit side stream of a two-pass partition: the pass-1 scatter also writes, for the
+// tuple it stores at position a of its output, the tuple's pass-2 digit
+// (key >> shift2) & (2^bits2 - 1) to side[a].  Pass 2's histogram then reads one byte
+// per tuple (launch_hist_side) instead of the 8-byte tuple.
+struct DigitSide {
+    uint8_t *side;
+    uint32_t shift2;
+    uint32_t bits2;
+};
+
+// Pass-2 histogram from the digit side stream (segment-major [g][F]; segments as m).
+hipError_t launch_hist_side(const uint8_t *side, const SegMap &m, uint32_t grid, uint32_t bits, uint64_t *hist,
+                            hipStream_t s);
+
 // Stable scatter of every segment into `out` at the cursors of the scan.
 // digit_base (nullable) is added to the cursors: base[r * F + d].
+// ds (nullable): also write the digit side stream for the next pass.
 hipError_t launch_scatter(const row_t *in, row_t *out, const SegMap &m, uint32_t grid, uint32_t shift,
                           uint32_t bits, const uint64_t *cursors, HistLayout layout, uint32_t nseg_stride,
-                          const uint64_t *digit_base, hipStream_t s);
+                          const uint64_t *digit_base, const DigitSide *ds, hipStream_t s);
 
 // Build + probe over tasks (partition x S chunk of at most kSChunk tuples).
 // Tasks 0..P-1 are the partitions' first chunks; over[0 .. *n_over) holds the

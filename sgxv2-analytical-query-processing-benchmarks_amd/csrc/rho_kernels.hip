@@ -104,6 +104,54 @@ hipError_t launch_hist(const row_t *in, const SegMap &m, uint32_t grid, uint32_t
     return hipGetLastError();
 }
 
+// Pass-2 histogram over the digit side stream written by the pass-1 scatter: the same
+// segments as the pass-2 scatter, one byte (the digit itself) per tuple instead of the
+// 8-byte tuple.  16-B non-temporal loads (16 digits per lane, 4 in flight), an
+// unaligned head and tail byte by byte; segment-major [g][F] output.
+__global__ __launch_bounds__(kBlock) void k_hist_side(const uint8_t *__restrict__ side, SegMap m, uint32_t bits,
+                                                      uint64_t *__restrict__ hist) {
+    __shared__ uint32_t h[kMaxF];
+    __shared__ uint32_t sbase[kMaxF + 1];
+    const uint32_t g = blockIdx.x;
+    uint32_t r;
+    uint64_t b, e;
+    if (!seg_lookup(m, g, sbase, r, b, e)) return;
+    const uint32_t F = 1u << bits;
+    for (uint32_t d = threadIdx.x; d < F; d += kBlock) h[d] = 0;
+    __syncthreads();
+    uint64_t a0 = (b + 15) & ~uint64_t(15);
+    if (a0 > e) a0 = e;
+    const uint64_t a1 = a0 + ((e - a0) & ~uint64_t(15));
+    if (threadIdx.x < a0 - b) atomicAdd(&h[side[b + threadIdx.x]], 1u);
+    if (threadIdx.x < e - a1) atomicAdd(&h[side[a1 + threadIdx.x]], 1u);
+    const uint4 *v = reinterpret_cast<const uint4 *>(side + a0);
+    const uint64_t nv = (a1 - a0) / 16;
+    auto count16 = [&](const uint4 &q) {
+        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int j = 0; j < 16; ++j) atomicAdd(&h[__builtin_amdgcn_ubfe(w[j >> 2], (j & 3) * 8, 8)], 1u);
+    };
+    constexpr int U = 4;
+    uint64_t i = threadIdx.x;
+    for (; i + (U - 1) * kBlock < nv; i += U * kBlock) {
+        uint4 q[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) q[u] = ld_nt(v + i + u * kBlock);
+#pragma unroll
+        for (int u = 0; u < U; ++u) count16(q[u]);
+    }
+    for (; i < nv; i += kBlock) count16(ld_nt(v + i));
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < F; d += kBlock) hist[(uint64_t)g * F + d] = h[d];
+}
+
+hipError_t launch_hist_side(const uint8_t *side, const SegMap &m, uint32_t grid, uint32_t bits, uint64_t *hist,
+                            hipStream_t s) {
+    if (grid == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_hist_side, dim3(grid), dim3(kBlock), 0, s, side, m, bits, hist);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------------ scans ---
 // One block per digit column: exclusive prefix over the segments (in place).
 __global__ __launch_bounds__(kBlock) void k_scan_cols(uint64_t *__restrict__ hist, uint32_t nseg,
@@ -363,9 +411,12 @@ __device__ __forceinline__ uint32_t scatter_tile_sort(ScatterLds<BITS, ITEMS, NT
 }
 
 // Phases D-E of the tile sorted by scatter_tile_sort (gtot = its granule count).
-template <int BITS, int ITEMS, int NT>
+// SIDE: every stored tuple's next-pass digit also goes to side[a] (a 16-lane group
+// writes 16 consecutive bytes next to its 128-B granule).
+template <int BITS, int ITEMS, int NT, bool SIDE>
 __device__ __forceinline__ void scatter_tile_write(ScatterLds<BITS, ITEMS, NT> &L, uint64_t *__restrict__ out,
-                                                   uint32_t gtot) {
+                                                   uint32_t gtot, uint8_t *__restrict__ side, uint32_t shift2,
+                                                   uint32_t mask2) {
     constexpr uint32_t F = 1u << BITS, NG = NT / kGran;
     constexpr uint32_t CS = kGran - 1;
 #ifdef SGXAMD_ABLATE_NOSORT
@@ -381,8 +432,10 @@ __device__ __forceinline__ void scatter_tile_write(ScatterLds<BITS, ITEMS, NT> &
         const uint32_t cd = m.y & 0xFFu, wd = m.y >> 16;
         const uint64_t a = (pd / kGran + (j - L.gbase[d])) * kGran + lane;
         const uint64_t q = a - pd;  // sequence position inside d (wraps when a < pd)
-        if (a >= pd && q < wd) {
-            const uint64_t x = q < cd ? L.carry[d * CS + q] : L.tile[m.x + q - cd];
+        const bool valid = a >= pd && q < wd;
+        uint64_t x = 0;
+        if (valid) {
+            x = q < cd ? L.carry[d * CS + q] : L.tile[m.x + q - cd];
 #ifdef SGXAMD_ABLATE_NOSTORE  // development ablation: everything but the global stores
             if (x == ~0ull) out[0] = x;
 #elif defined(SGXAMD_PLAIN_STORE)
@@ -391,6 +444,10 @@ __device__ __forceinline__ void scatter_tile_write(ScatterLds<BITS, ITEMS, NT> &
             st_nt(out + a, x);
 #endif
         }
+        // next-pass digit beside the tuple: the 16 lanes of a granule write 16
+        // consecutive bytes (measured faster than gathering them into one 16-B store
+        // per granule with DPP)
+        if (SIDE && valid) side[a] = (uint8_t)(((uint32_t)x >> shift2) & mask2);
     }
     __syncthreads();
     // E. new carries (the next tile's phase A touches only cnt; C/D come after barriers)
@@ -405,11 +462,12 @@ __device__ __forceinline__ void scatter_tile_write(ScatterLds<BITS, ITEMS, NT> &
     }
 }
 
-template <int BITS, int ITEMS, int NT>
+template <int BITS, int ITEMS, int NT, bool SIDE>
 __global__ __launch_bounds__(NT, (scatter_waves_per_simd<BITS, ITEMS, NT>())) void k_scatter(const uint64_t *__restrict__ in, uint64_t *__restrict__ out,
                                                 SegMap m, uint32_t shift, const uint64_t *__restrict__ cur_init,
                                                 HistLayout layout, uint32_t nseg_stride,
-                                                const uint64_t *__restrict__ digit_base) {
+                                                const uint64_t *__restrict__ digit_base,
+                                                uint8_t *__restrict__ side, uint32_t shift2, uint32_t mask2) {
     constexpr uint32_t TILE = NT * ITEMS;
     constexpr uint32_t F = 1u << BITS, NG = NT / kGran, CS = kGran - 1;
     static_assert(F <= NT, "one owner thread per digit");
@@ -451,14 +509,14 @@ __global__ __launch_bounds__(NT, (scatter_waves_per_simd<BITS, ITEMS, NT>())) vo
         load_tile<ITEMS, NT>(rs, off + 2 * TILE * 8u, va);
 #pragma unroll
         for (int k = 0; k < ITEMS; ++k) asm volatile("" ::"v"(vb[k]));
-        scatter_tile_write<BITS, ITEMS, NT>(L, out, gt);
+        scatter_tile_write<BITS, ITEMS, NT, SIDE>(L, out, gt, side, shift2, mask2);
         if (tb + TILE >= e) break;
         gt = scatter_tile_sort<BITS, ITEMS, NT>(L, pend, carried, vb, out, (uint32_t)min<uint64_t>(TILE, e - tb - TILE),
                                                 shift, tb + TILE);
         load_tile<ITEMS, NT>(rs, off + 3 * TILE * 8u, vb);
 #pragma unroll
         for (int k = 0; k < ITEMS; ++k) asm volatile("" ::"v"(va[k]));
-        scatter_tile_write<BITS, ITEMS, NT>(L, out, gt);
+        scatter_tile_write<BITS, ITEMS, NT, SIDE>(L, out, gt, side, shift2, mask2);
         if (tb + 2 * TILE >= e) break;
         gt = scatter_tile_sort<BITS, ITEMS, NT>(L, pend, carried, va, out,
                                                 (uint32_t)min<uint64_t>(TILE, e - tb - 2 * TILE), shift, tb + 2 * TILE);
@@ -471,19 +529,30 @@ __global__ __launch_bounds__(NT, (scatter_waves_per_simd<BITS, ITEMS, NT>())) vo
     }
     __syncthreads();
     const uint32_t lane = tid & (kGran - 1);
-    for (uint32_t d = tid / kGran; d < F; d += NG)
-        if (lane < L.cnt[d]) out[L.pend[d] + lane] = L.carry[d * CS + lane];
+    for (uint32_t d = tid / kGran; d < F; d += NG) {
+        if (lane < L.cnt[d]) {
+            const uint64_t x = L.carry[d * CS + lane];
+            out[L.pend[d] + lane] = x;
+            if (SIDE) side[L.pend[d] + lane] = (uint8_t)(((uint32_t)x >> shift2) & mask2);
+        }
+    }
 }
 
 template <int ITEMS, int NT>
 hipError_t launch_scatter_items(const uint64_t *in, uint64_t *out, const SegMap &m, uint32_t grid, uint32_t shift,
                                 uint32_t bits, const uint64_t *cursors, HistLayout layout, uint32_t nseg_stride,
-                                const uint64_t *digit_base, hipStream_t s) {
+                                const uint64_t *digit_base, hipStream_t s, const DigitSide *ds = nullptr) {
+    uint8_t *side = ds ? ds->side : nullptr;
+    const uint32_t shift2 = ds ? ds->shift2 : 0, mask2 = ds ? (1u << ds->bits2) - 1u : 0;
 #define SCATTER_CASE(B)                                                                                  \
     case B:                                                                                              \
         if constexpr (sizeof(ScatterLds<B, ITEMS, NT>) <= 160 * 1024 && (1 << B) <= NT) {                  \
-            hipLaunchKernelGGL((k_scatter<B, ITEMS, NT>), dim3(grid), dim3(NT), 0, s, in, out, m, shift,   \
-                               cursors, layout, nseg_stride, digit_base);                                \
+            if (side)                                                                                    \
+                hipLaunchKernelGGL((k_scatter<B, ITEMS, NT, true>), dim3(grid), dim3(NT), 0, s, in, out, m, \
+                                   shift, cursors, layout, nseg_stride, digit_base, side, shift2, mask2); \
+            else                                                                                         \
+                hipLaunchKernelGGL((k_scatter<B, ITEMS, NT, false>), dim3(grid), dim3(NT), 0, s, in, out, m, \
+                                   shift, cursors, layout, nseg_stride, digit_base, side, shift2, mask2); \
             break;                                                                                       \
         } else {                                                                                         \
             return hipErrorInvalidValue;                                                                 \
@@ -508,12 +577,12 @@ hipError_t launch_scatter_items(const uint64_t *in, uint64_t *out, const SegMap 
 
 hipError_t launch_scatter(const row_t *in, row_t *out, const SegMap &m, uint32_t grid, uint32_t shift,
                           uint32_t bits, const uint64_t *cursors, HistLayout layout, uint32_t nseg_stride,
-                          const uint64_t *digit_base, hipStream_t s) {
+                          const uint64_t *digit_base, const DigitSide *ds, hipStream_t s) {
     if (grid == 0) return hipSuccess;
     const uint64_t *i64 = reinterpret_cast<const uint64_t *>(in);
     uint64_t *o64 = reinterpret_cast<uint64_t *>(out);
     return launch_scatter_items<kScatterItems, kScatterThreads>(i64, o64, m, grid, shift, bits, cursors, layout,
-                                                                nseg_stride, digit_base, s);
+                                                                nseg_stride, digit_base, s, ds);
 }
 
 // ------------------------------------------------------------ build+probe ---

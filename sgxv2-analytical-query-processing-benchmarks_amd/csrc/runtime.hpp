@@ -75,6 +75,7 @@ struct Context {
     // join workspace
     DeviceBuffer inR, inS;         // staging of host relations
     DeviceBuffer t1R, t1S, t2R, t2S;
+    DeviceBuffer sideR, sideS;     // pass-2 digit per pass-1 output tuple (two-pass plans)
     Arena scratch;
     DeviceBuffer mat;              // materialised output_triple_t (when the caller's buffer is host memory)
     // TPC-H workspace: staged host columns, selection bits/offsets, intermediate

@@ -8,11 +8,12 @@
 // A 512-bit compare of the reference covers 64 uint8 codes; here one wave-wide
 // 16-byte-per-lane load covers 1024 uint8 codes or 256 int32 values, and the
 // predicate mask of 64 consecutive rows is assembled across 4 (u8) or 16 (i32)
-// lanes with xor-shuffles into exactly the reference's __mmask64 word layout.
+// lanes with DPP row operations into exactly the reference's __mmask64 word layout.
 // Index/value compaction is two-phase without inter-workgroup waiting: the
 // bitvector pass also emits one match count per chunk, a one-block scan turns
 // those into chunk output offsets, and the expand pass reads only the bitvector
-// (n/8 bytes) and writes the outputs coalesced (lane j of a wave writes output j).
+// (n/8 bytes), stages each wave's matches in LDS and writes them coalesced (lane j
+// of a wave writes output j).
 #include "common.hpp"
 #include "scan_internal.hpp"
 
@@ -305,55 +306,48 @@ hipError_t launch_chunk_scan(const uint64_t *counts, uint32_t nchunks, uint64_t 
     return hipGetLastError();
 }
 
-// Position of the r-th set bit (0-based) of x (r < popcount(x)).
-__device__ __forceinline__ uint32_t select_bit(uint64_t x, uint32_t r) {
-    uint32_t pos = 0;
-    uint32_t w = (uint32_t)x;
-    uint32_t c = __popc(w);
-    if (r >= c) {
-        r -= c;
-        w = (uint32_t)(x >> 32);
-        pos = 32;
-    }
-#pragma unroll
-    for (uint32_t half = 16; half >= 1; half >>= 1) {
-        const uint32_t lowmask = (1u << half) - 1u;
-        c = __popc(w & lowmask);
-        if (r >= c) {
-            r -= c;
-            w >>= half;
-            pos += half;
-        }
-    }
-    return pos;
+// LDS writes of a wave made visible to the other lanes of the same wave (no block
+// barrier: the staging area below is private to its wave).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // Expand the bitvector of one chunk into row indexes (MODE 0), values (MODE 1) or
 // dictionary-decoded values dict[code] (MODE 2, the dict_scan_* family).
-// Waves take 64 words at a time; lane j of a wave writes the wave's j-th, (j+64)-th,
-// ... output, locating its set bit by binary search over the wave's inclusive
-// word-popcount prefix held in LDS.
+// Each wave takes 64 words (4096 rows) per step, one word per lane.  A lane writes
+// the row offsets of its set bits into the wave's LDS staging area at its exclusive
+// word-popcount prefix, then the wave streams the staged outputs to HBM with lane j
+// writing the wave's j-th, (j+64)-th, ... output: every store instruction covers 64
+// consecutive output slots.  Steps with more than kStage matches in a wave (dense
+// predicates) stage in rounds of kStage.  The word of the next step is loaded before
+// the current one is expanded.
+constexpr uint32_t kStage = 1024;  // staged outputs per wave and round (u32 row offsets, 4 KiB)
+
 template <typename T, typename OutT, int MODE>
 __global__ __launch_bounds__(kBlock) void k_expand(const uint64_t *__restrict__ bv, const T *__restrict__ in,
                                                    uint64_t n, uint64_t rows_per_chunk,
                                                    const uint64_t *__restrict__ chunk_off, OutT *__restrict__ out,
                                                    uint64_t cap, const int64_t *__restrict__ dict) {
-    __shared__ uint32_t incl_s[kWaves][64];
-    __shared__ uint64_t word_s[kWaves][64];
+    __shared__ uint32_t stage_s[kWaves][kStage];
     __shared__ uint32_t wtot_s[kWaves];
     const uint32_t lane = __lane_id(), wave = threadIdx.x / kWave;
+    uint32_t *stage = stage_s[wave];
     const uint64_t nwords = (n + 63) / 64;
     const uint64_t w0 = (uint64_t)blockIdx.x * (rows_per_chunk / 64);
     uint64_t w1 = w0 + rows_per_chunk / 64;
     if (w1 > nwords) w1 = nwords;
     uint64_t base = chunk_off[blockIdx.x];
+    uint64_t wi = w0 + (uint64_t)wave * 64 + lane;
+    uint64_t x_next = wi < w1 ? ld_nt(bv + wi) : 0ull;
     for (uint64_t wb = w0; wb < w1; wb += kWaves * 64) {
-        const uint64_t wi = wb + (uint64_t)wave * 64 + lane;
-        const uint64_t x = wi < w1 ? ld_nt(bv + wi) : 0ull;
+        const uint64_t x = x_next;
+        wi += kWaves * 64;
+        x_next = wi < w1 ? ld_nt(bv + wi) : 0ull;
         const uint32_t c = __popcll(x);
         const uint32_t incl = wave_incl_scan_u32(c);
-        incl_s[wave][lane] = incl;
-        word_s[wave][lane] = x;
+        const uint32_t excl = incl - c;
         const uint32_t wtot = __shfl(incl, 63, kWave);
         if (lane == 0) wtot_s[wave] = wtot;
         __syncthreads();
@@ -365,22 +359,31 @@ __global__ __launch_bounds__(kBlock) void k_expand(const uint64_t *__restrict__ 
             if (w < (int)wave) woff += t;
             all += t;
         }
-        for (uint32_t m = lane; m < wtot; m += 64) {
-            uint32_t lo = 0, hi = 63;  // smallest l with incl[l] > m
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (incl_s[wave][mid] > m) hi = mid; else lo = mid + 1;
+        const uint64_t row0 = (wb + (uint64_t)wave * 64) * 64;  // first row of this wave's 64 words
+        for (uint32_t r0 = 0; r0 < wtot; r0 += kStage) {
+            const uint32_t r1 = r0 + kStage;
+            if (excl < r1 && incl > r0) {
+                uint64_t y = x;
+                uint32_t p = excl;
+                while (y) {
+                    const uint32_t bit = (uint32_t)__builtin_ctzll(y);
+                    y &= y - 1;
+                    if (p >= r0 && p < r1) stage[p - r0] = lane * 64 + bit;
+                    ++p;
+                }
             }
-            const uint64_t xw = word_s[wave][lo];
-            const uint32_t before = incl_s[wave][lo] - (uint32_t)__popcll(xw);
-            const uint32_t bit = select_bit(xw, m - before);
-            const uint64_t row = (wb + (uint64_t)wave * 64 + lo) * 64 + bit;
-            const uint64_t o = woff + m;
-            if (o < cap) {
-                if (MODE == 0) out[o] = (OutT)row;
-                else if (MODE == 1) out[o] = (OutT)in[row];
-                else out[o] = (OutT)dict[in[row]];
+            wave_lds_sync();
+            const uint32_t nr = min(kStage, wtot - r0);
+            for (uint32_t m = lane; m < nr; m += 64) {
+                const uint64_t row = row0 + stage[m];
+                const uint64_t o = woff + r0 + m;
+                if (o < cap) {
+                    if (MODE == 0) out[o] = (OutT)row;
+                    else if (MODE == 1) out[o] = (OutT)in[row];
+                    else out[o] = (OutT)dict[in[row]];
+                }
             }
+            wave_lds_sync();
         }
         base += all;
         __syncthreads();
