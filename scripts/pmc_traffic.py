@@ -25,6 +25,7 @@ ALIASES = {
     "k_join": ["join_build_probe"],
     "k_predicate": ["scan_count", "scan_bitvector"],
     "k_expand": ["scan_expand_index"],
+    "k_select": ["scan_select_index"],
 }
 # kernels whose bench-size launches differ per pass, told apart by grid size (pass 2's
 # grid is its segments + one per pass-1 bin, larger than pass 1's): smallest grid first

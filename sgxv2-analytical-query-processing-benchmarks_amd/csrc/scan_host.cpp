@@ -5,6 +5,7 @@
 // buffers are staged through HBM.  Device inputs that are not 16-byte aligned
 // are copied to an aligned buffer first (the kernels load 16 bytes per lane).
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -39,6 +40,17 @@ Geometry geometry(uint64_t n) {
 }
 
 enum class Op { kCount, kBitvector, kIndex, kValues };
+
+// Index / value / dictionary outputs in one pass (launch_select, decoupled look-back)
+// or, with SGXAMD_SCAN_ONEPASS=0 (development A/B switch), as bitvector pass + chunk
+// scan + expand pass.  Results are identical.
+bool one_pass_select() {
+    static const bool on = [] {
+        const char *e = std::getenv("SGXAMD_SCAN_ONEPASS");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return on;
+}
 
 // Device-resident, 16-byte aligned view of the input column.
 template <typename T>
@@ -79,14 +91,48 @@ int run(Op op, T lo, T hi, const T *in, size_t n, void *out, size_t cap, uint64_
     const size_t o_counts = A.reserve(sizeof(uint64_t) * g.nchunks);
     const size_t o_offs = A.reserve(sizeof(uint64_t) * g.nchunks);
     const size_t o_res = A.reserve(sizeof(uint64_t) * 2);
+    const bool select1 = (op == Op::kIndex || op == Op::kValues) && one_pass_select();
+    const size_t o_status = A.reserve(sizeof(uint64_t) * (select1 ? select_chunks(n) : 0) + 16);
     SCAN_HIP(A.buf.ensure(A.used));
     uint64_t *counts = A.at<uint64_t>(o_counts);
     uint64_t *offs = A.at<uint64_t>(o_offs);
     uint64_t *res = A.at<uint64_t>(o_res);
+    uint64_t *sel_status = A.at<uint64_t>(o_status) + 2;
+    uint32_t *ticket = A.at<uint32_t>(o_status);
 
+    const bool out_dev = out && is_device_pointer(out);
+    if (select1) {
+        OutT *o = static_cast<OutT *>(out);
+        if (!out_dev) {
+            SCAN_HIP(ctx->scan_out.ensure(std::max<size_t>(cap, 1) * sizeof(OutT)));
+            o = ctx->scan_out.as<OutT>();
+        }
+        tm.mark(op == Op::kIndex ? "scan_select_index" : "scan_select_values");
+        if (op == Op::kIndex)
+            SCAN_HIP((launch_select<T, OutT, 0>(din, n, lo, hi, ticket, sel_status, o, cap, res, s)));
+        else
+            SCAN_HIP((launch_select<T, OutT, 1>(din, n, lo, hi, ticket, sel_status, o, cap, res, s)));
+        tm.end_call();
+        SCAN_HIP(hipMemcpyAsync(ctx->host_result, res, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+        SCAN_HIP(hipMemcpyAsync(ctx->host_result + 1, ticket, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        SCAN_HIP(hipStreamSynchronize(s));
+        const uint64_t total = ctx->host_result[0];
+        if (reinterpret_cast<const uint32_t *>(ctx->host_result + 1)[1] != 0) {
+            set_last_error("one-pass selection: look-back poll gave up");
+            return MI355_ERR_HIP;
+        }
+        if (result) *result = total;
+        if (!out_dev && out && total)
+            SCAN_HIP(hipMemcpy(out, o, std::min<uint64_t>(total, cap) * sizeof(OutT), hipMemcpyDeviceToHost));
+        tm.collect();
+        if (total > cap) {
+            set_last_error("output capacity " + std::to_string(cap) + " < " + std::to_string(total) + " matches");
+            return MI355_ERR_CAPACITY;
+        }
+        return MI355_OK;
+    }
     // where the bitvector goes
     uint64_t *bv = nullptr;
-    const bool out_dev = out && is_device_pointer(out);
     if (op == Op::kBitvector && out_dev) {
         bv = static_cast<uint64_t *>(out);
     } else if (op != Op::kCount) {
@@ -201,6 +247,8 @@ int run_dict(int64_t lo, int64_t hi, const int64_t *dict, uint64_t dict_size, co
     const size_t o_offs = A.reserve(sizeof(uint64_t) * g.nchunks);
     const size_t o_res = A.reserve(sizeof(uint64_t) * 2);
     const size_t o_range = A.reserve(sizeof(uint64_t) * 2);
+    const bool select1 = one_pass_select();
+    const size_t o_status = A.reserve(sizeof(uint64_t) * (select1 ? select_chunks(n) : 0) + 16);
     SCAN_HIP(A.buf.ensure(A.used));
     uint64_t *range = A.at<uint64_t>(o_range);
     tm.mark("dict_range");
@@ -212,25 +260,38 @@ int run_dict(int64_t lo, int64_t hi, const int64_t *dict, uint64_t dict_size, co
     const CodeT clo = (CodeT)(CastT)ctx->host_result[0];
     const CodeT chi = (CodeT)(CastT)(int64_t)(ctx->host_result[1] - 1);
 
-    SCAN_HIP(ctx->scan_aux.ensure(std::max<uint64_t>(nwords, 1) * sizeof(uint64_t)));
-    uint64_t *bv = ctx->scan_aux.as<uint64_t>();
     uint64_t *counts = A.at<uint64_t>(o_counts), *offs = A.at<uint64_t>(o_offs), *res = A.at<uint64_t>(o_res);
-    tm.mark("dict_bitvector");
-    SCAN_HIP(launch_predicate<CodeT>(din, n, clo, chi, g.rows_per_chunk, g.nchunks, bv, counts, s));
-    tm.mark("dict_chunk_scan");
-    SCAN_HIP(launch_chunk_scan(counts, g.nchunks, offs, res, s));
     const bool out_dev = out && is_device_pointer(out);
     int64_t *o = out;
     if (!out_dev) {
         SCAN_HIP(ctx->scan_out.ensure(std::max<size_t>(cap, 1) * sizeof(int64_t)));
         o = ctx->scan_out.as<int64_t>();
     }
-    tm.mark("dict_decode");
-    SCAN_HIP((launch_expand<CodeT, int64_t, 2>(bv, din, n, g.rows_per_chunk, g.nchunks, offs, o, cap, s, ddict)));
+    if (select1) {
+        tm.mark("dict_select");
+        SCAN_HIP((launch_select<CodeT, int64_t, 2>(din, n, clo, chi, A.at<uint32_t>(o_status),
+                                                   A.at<uint64_t>(o_status) + 2, o, cap, res, s, ddict)));
+    } else {
+        SCAN_HIP(ctx->scan_aux.ensure(std::max<uint64_t>(nwords, 1) * sizeof(uint64_t)));
+        uint64_t *bv = ctx->scan_aux.as<uint64_t>();
+        tm.mark("dict_bitvector");
+        SCAN_HIP(launch_predicate<CodeT>(din, n, clo, chi, g.rows_per_chunk, g.nchunks, bv, counts, s));
+        tm.mark("dict_chunk_scan");
+        SCAN_HIP(launch_chunk_scan(counts, g.nchunks, offs, res, s));
+        tm.mark("dict_decode");
+        SCAN_HIP((launch_expand<CodeT, int64_t, 2>(bv, din, n, g.rows_per_chunk, g.nchunks, offs, o, cap, s, ddict)));
+    }
     tm.end_call();
     SCAN_HIP(hipMemcpyAsync(ctx->host_result, res, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    if (select1)
+        SCAN_HIP(hipMemcpyAsync(ctx->host_result + 1, A.at<uint32_t>(o_status), 2 * sizeof(uint32_t),
+                                hipMemcpyDeviceToHost, s));
     SCAN_HIP(hipStreamSynchronize(s));
     const uint64_t total = ctx->host_result[0];
+    if (select1 && reinterpret_cast<const uint32_t *>(ctx->host_result + 1)[1] != 0) {
+        set_last_error("one-pass selection: look-back poll gave up");
+        return MI355_ERR_HIP;
+    }
     *n_out = total;
     if (!out_dev && out && total) SCAN_HIP(hipMemcpy(out, o, std::min<uint64_t>(total, cap) * sizeof(int64_t),
                                                      hipMemcpyDeviceToHost));

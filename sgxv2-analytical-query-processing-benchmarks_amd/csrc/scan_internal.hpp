@@ -25,6 +25,15 @@ hipError_t launch_expand(const uint64_t *bv, const T *in, uint64_t n, uint64_t r
                          const uint64_t *chunk_off, OutT *out, uint64_t cap, hipStream_t s,
                          const int64_t *dict = nullptr);
 
+// One-pass index (MODE 0) / value (1) / dictionary (2) selection with decoupled
+// look-back over chunks (scan_kernels.hip k_select).  ticket: two u32 (ticket[1] != 0
+// after the launch = a look-back poll gave up), status: one u64 per chunk
+// (select_chunks(n)); both are reset by the launch.  *total = matches.
+template <typename T, typename OutT, int MODE>
+hipError_t launch_select(const T *in, uint64_t n, T lo, T hi, uint32_t *ticket, uint64_t *status, OutT *out,
+                         uint64_t cap, uint64_t *total, hipStream_t s, const int64_t *dict = nullptr);
+uint64_t select_chunks(uint64_t n);
+
 // Per-chunk sums of the u8 codes in [lo, hi] (SIMD512::sum).
 hipError_t launch_sum_u8(const uint8_t *in, uint64_t n, uint8_t lo, uint8_t hi, uint64_t rows_per_chunk,
                          uint32_t nchunks, uint64_t *chunk_sums, hipStream_t s);

@@ -422,6 +422,230 @@ template hipError_t launch_expand<uint32_t, int64_t, 2>(const uint64_t *, const 
                                                         uint32_t, const uint64_t *, int64_t *, uint64_t, hipStream_t,
                                                         const int64_t *);
 
+// ------------------------------------------------------- one-pass selection ---
+// Index / value / dictionary output in ONE pass over the column (implicit_index_scan,
+// scan and dict_scan_* of SIMD512.cpp:91-150, 251-287, 289-629): the column is read
+// once and the outputs written once; the bitvector never leaves LDS.
+//
+// Chunks of kSelChunk rows are claimed in order through a ticket counter, so every
+// chunk below a workgroup's own has been claimed by a workgroup that is already
+// running.  Per chunk:
+//   1. predicate over the chunk into an LDS bitvector (one 64-row word per 64 rows,
+//      assembled across the LPW lanes of a 64-row group as in k_predicate) + count;
+//   2. decoupled look-back over the chunk status words: status[c] is published as
+//      (kAgg | count) at once and as (kIncl | inclusive prefix) when known; the first
+//      wave reads 64 predecessors at a time with agent-scope atomics,
+//      sums aggregates back to the nearest inclusive prefix and publishes its own;
+//      a predecessor that has not counted yet (status 0) is polled again — it is
+//      already running, so the wait ends;
+//   3. the LDS bitvector expanded exactly like k_expand (per-wave LDS staging of
+//      the matches, coalesced stores) at the chunk's exclusive prefix.
+// The chunk that ends the column writes the total.
+constexpr uint32_t kSelChunk = 65536;  // rows per chunk (8 KiB LDS bitvector)
+constexpr uint64_t kAgg = 1ull << 62, kIncl = 2ull << 62, kValMask = kAgg - 1;
+
+// The status words are the data and the flag at once (MI355X_MICROARCH.md visibility
+// table, cdna_hip_programming.md Guideline 16 R2): one aligned 8-byte agent-scope
+// relaxed store (sc1, write-through) publishes, agent-scope relaxed loads (sc1) poll.
+__device__ __forceinline__ uint64_t ld_status(const uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_status(uint64_t *p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <typename T, typename OutT, int MODE>
+__global__ __launch_bounds__(kBlock) void k_select(const T *__restrict__ in, uint64_t n, T lo, T hi,
+                                                   uint32_t *__restrict__ ticket, uint64_t *__restrict__ status,
+                                                   OutT *__restrict__ out, uint64_t cap,
+                                                   const int64_t *__restrict__ dict, uint64_t *__restrict__ total) {
+    constexpr uint32_t V = 16 / sizeof(T), LPW = 64 / V, FULL = (1u << V) - 1u;
+    constexpr uint32_t CH = kSelChunk, NWORD = CH / 64;
+    constexpr int U = 8;  // 16-B loads in flight per lane
+    __shared__ uint64_t bits[NWORD];
+    __shared__ uint32_t stage_s[kWaves][kStage];
+    __shared__ uint32_t wtot_s[kWaves];
+    __shared__ uint64_t red[kWaves];
+    __shared__ uint32_t chunk_s;
+    __shared__ uint64_t excl_s;
+    const uint32_t lane = __lane_id(), wave = threadIdx.x / kWave;
+    if (threadIdx.x == 0) chunk_s = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const uint32_t c = chunk_s;
+    const uint64_t r0 = (uint64_t)c * CH;
+    if (r0 >= n) return;  // (the grid has exactly one workgroup per chunk)
+    const uint64_t r1 = min<uint64_t>(r0 + CH, n);
+    const uint32_t nw = (uint32_t)((r1 - r0 + 63) / 64);
+
+    // 1. predicate -> LDS bitvector + count
+    uint64_t count = 0;
+    constexpr uint32_t STEP = kWaves * 64 * V;  // rows per block per load round
+    // wave-uniform loop: lanes past r1 read nothing and contribute empty masks, so every
+    // lane takes part in the DPP word assembly
+    for (uint64_t wbase = r0 + (uint64_t)wave * 64 * V; wbase < r1; wbase += U * STEP) {
+        uint4 q[U];
+        uint32_t valid[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t row = wbase + (uint64_t)u * STEP + (uint64_t)lane * V;
+            if (row + V <= r1) {
+                q[u] = ld_nt(reinterpret_cast<const uint4 *>(in + row));
+                valid[u] = FULL;
+            } else if (row < r1) {
+                uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+                for (uint32_t j = 0; j < V; ++j) {
+                    constexpr uint32_t B = 8 * sizeof(T);
+                    constexpr uint32_t VM = B == 32 ? 0xFFFFFFFFu : ((1u << B) - 1u);
+                    const uint32_t val = (row + j < r1) ? (uint32_t)in[row + j] : 0u;
+                    w[(j * B) / 32] |= (val & VM) << ((j * B) % 32);
+                }
+                q[u] = make_uint4(w[0], w[1], w[2], w[3]);
+                valid[u] = (1u << (uint32_t)(r1 - row)) - 1u;
+            } else {
+                q[u] = make_uint4(0, 0, 0, 0);
+                valid[u] = 0;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t m = match_mask<T>(q[u], lo, hi, valid[u]);
+            count += __popc(m);
+            const uint64_t x = group_or<LPW>((uint64_t)m << (V * (lane % LPW)));
+            const uint64_t row = wbase + (uint64_t)u * STEP + (uint64_t)lane * V;
+            // the group's first lane stores the word of its 64 rows (every word of the
+            // chunk below nw has a first lane inside the chunk)
+            if ((lane % LPW) == 0 && row < r1) bits[(row - r0) / 64] = x;
+        }
+    }
+    count = wave_sum_u64(count);
+    if (lane == 0) red[wave] = count;
+    __syncthreads();
+    uint64_t agg = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) agg += red[w];
+
+    // 2. decoupled look-back (first wave)
+    if (wave == 0) {
+        uint64_t excl = 0;
+        if (c == 0) {
+            if (lane == 0) st_status(&status[0], kIncl | agg);
+        } else {
+            if (lane == 0) st_status(&status[c], kAgg | agg);
+            int64_t hi_idx = (int64_t)c - 1;  // next predecessor window ends here
+            while (true) {
+                const int64_t j = hi_idx - (int64_t)lane;
+                uint64_t st = j >= 0 ? ld_status(&status[j]) : kIncl;  // before chunk 0: prefix 0
+                // poll until every lane of the window has published something; a
+                // predecessor that never publishes (it cannot: it is running) would end
+                // the poll after ~2^20 rounds with ticket[1] set, not hang the device
+                uint32_t spins = 0;
+                while (__ballot(st == 0)) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (st == 0) st = ld_status(&status[j]);
+                    if (++spins == (1u << 20)) {
+                        if (lane == 0) atomicExch(&ticket[1], 1u);
+                        st = kIncl;
+                    }
+                }
+                const uint64_t incl_mask = __ballot((st & kIncl) != 0);
+                // lanes up to and including the nearest inclusive predecessor
+                const uint32_t stop = incl_mask ? (uint32_t)__builtin_ctzll(incl_mask) : 64u;
+                uint64_t v = (lane <= stop && j >= 0) ? (st & kValMask) : 0;
+                excl += wave_sum_u64(v);
+                if (incl_mask) break;
+                hi_idx -= 64;
+            }
+            if (lane == 0) st_status(&status[c], kIncl | (excl + agg));
+        }
+        if (lane == 0) excl_s = excl;
+    }
+    __syncthreads();
+    const uint64_t excl = excl_s;
+    if (r1 == n && threadIdx.x == 0) *total = excl + agg;
+
+    // 3. expand the LDS bitvector at the chunk's prefix
+    uint64_t base_out = excl;
+    for (uint32_t wb = 0; wb < nw; wb += kWaves * 64) {
+        const uint32_t wi = wb + wave * 64 + lane;
+        const uint64_t x = wi < nw ? bits[wi] : 0ull;
+        const uint32_t cnt = __popcll(x);
+        const uint32_t incl = wave_incl_scan_u32(cnt);
+        const uint32_t ex = incl - cnt;
+        const uint32_t wtot = __shfl(incl, 63, kWave);
+        if (lane == 0) wtot_s[wave] = wtot;
+        __syncthreads();
+        uint64_t woff = base_out, all = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) {
+            const uint32_t t = wtot_s[w];
+            if (w < (int)wave) woff += t;
+            all += t;
+        }
+        const uint64_t row0 = r0 + (uint64_t)(wb + wave * 64) * 64;
+        uint32_t *stage = stage_s[wave];
+        for (uint32_t s0 = 0; s0 < wtot; s0 += kStage) {
+            const uint32_t s1 = s0 + kStage;
+            if (ex < s1 && incl > s0) {
+                uint64_t y = x;
+                uint32_t p = ex;
+                while (y) {
+                    const uint32_t bit = (uint32_t)__builtin_ctzll(y);
+                    y &= y - 1;
+                    if (p >= s0 && p < s1) stage[p - s0] = lane * 64 + bit;
+                    ++p;
+                }
+            }
+            wave_lds_sync();
+            const uint32_t nr = min(kStage, wtot - s0);
+            for (uint32_t m = lane; m < nr; m += 64) {
+                const uint64_t row = row0 + stage[m];
+                const uint64_t o = woff + s0 + m;
+                if (o < cap) {
+                    if (MODE == 0) out[o] = (OutT)row;
+                    else if (MODE == 1) out[o] = (OutT)in[row];
+                    else out[o] = (OutT)dict[in[row]];
+                }
+            }
+            wave_lds_sync();
+        }
+        base_out += all;
+        __syncthreads();
+    }
+}
+
+uint64_t select_chunks(uint64_t n) { return (n + kSelChunk - 1) / kSelChunk; }
+
+template <typename T, typename OutT, int MODE>
+hipError_t launch_select(const T *in, uint64_t n, T lo, T hi, uint32_t *ticket, uint64_t *status, OutT *out,
+                         uint64_t cap, uint64_t *total, hipStream_t s, const int64_t *dict) {
+    const uint64_t nchunks = select_chunks(n);
+    if (nchunks == 0) return hipSuccess;
+    hipError_t e = hipMemsetAsync(ticket, 0, 2 * sizeof(uint32_t), s);
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(status, 0, nchunks * sizeof(uint64_t), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((k_select<T, OutT, MODE>), dim3((uint32_t)nchunks), dim3(kBlock), 0, s, in, n, lo, hi, ticket,
+                       status, out, cap, dict, total);
+    return hipGetLastError();
+}
+
+
+
+#define SGX_SELECT_INST(T, OutT, MODE)                                                                         \
+    template hipError_t launch_select<T, OutT, MODE>(const T *, uint64_t, T, T, uint32_t *, uint64_t *, OutT *, \
+                                                     uint64_t, uint64_t *, hipStream_t, const int64_t *);
+SGX_SELECT_INST(uint8_t, uint64_t, 0)
+SGX_SELECT_INST(int32_t, uint64_t, 0)
+SGX_SELECT_INST(uint8_t, uint32_t, 1)
+SGX_SELECT_INST(int32_t, int32_t, 1)
+SGX_SELECT_INST(uint8_t, uint64_t, 1)  // named by run<T, uint64_t>, never called
+SGX_SELECT_INST(int32_t, uint64_t, 1)
+SGX_SELECT_INST(uint8_t, int64_t, 2)
+SGX_SELECT_INST(uint16_t, int64_t, 2)
+SGX_SELECT_INST(uint32_t, int64_t, 2)
+#undef SGX_SELECT_INST
+
 // Dictionary code range of a predicate on values (dict_scan_* prologue,
 // SIMD512.cpp:297-305): lo_idx = first i with dict[i] >= lo (else dict_size),
 // hi_end = first j >= lo_idx with dict[j] > hi (else dict_size).  Two passes of

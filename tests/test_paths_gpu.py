@@ -1,0 +1,53 @@
+"""The development A/B switches select alternative kernel paths with identical results:
+SGXAMD_DIGIT_SIDE=0 (pass-2 histograms over the tuples instead of the digit side
+stream) and SGXAMD_SCAN_ONEPASS=0 (index / value / dictionary scans as bitvector pass +
+expand pass instead of the one-pass look-back selection).  Both switches are read
+once per process, so each setting runs in a child process against the oracle."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import PKG, ROOT
+
+pytestmark = pytest.mark.gpu
+
+CHILD = r"""
+import sys
+import numpy as np
+import sgxamd, oracle
+R, S = sgxamd.reference_relations(1 << 20, 1 << 20, selectivity=50)
+exp, _ = oracle.rho_join(R, S, 2)
+for bits, passes in [(12, 2), (16, 2), (18, 2)]:
+    got = sgxamd.rho_join(R, len(R), S, len(S), radix_bits=bits, passes=passes).matches
+    assert got == exp, (bits, passes, got, exp)
+rng = np.random.default_rng(5)
+for n in (1, 1000, 65536, 65537, (1 << 20) + 37):
+    col = rng.integers(0, 256, n).astype(np.int32)
+    for lo, hi in [(0, 26), (0, 255), (7, 7), (200, 100)]:
+        cnt = oracle.scan("count", "i32", lo, hi, col)
+        idx = np.zeros(max(cnt, 1), dtype=np.uint64)
+        assert sgxamd.scan_index(lo, hi, col, n, idx, cnt) == cnt
+        assert np.array_equal(idx[:cnt], oracle.scan("index", "i32", lo, hi, col)), (n, lo, hi)
+        vals = np.zeros(max(cnt, 1), dtype=np.int32)
+        assert sgxamd.scan_values(lo, hi, col, n, vals, cnt) == cnt
+        assert np.array_equal(vals[:cnt], oracle.scan("values", "i32", lo, hi, col)), (n, lo, hi)
+dictionary = np.sort(rng.integers(-10**9, 10**9, 256))
+codes = rng.integers(0, 256, 300_001).astype(np.uint8)
+ref = oracle.dict_scan(-10**8, 5 * 10**8, dictionary, codes)
+out = np.zeros(len(ref) + 1, dtype=np.int64)
+k = sgxamd.dict_scan(-10**8, 5 * 10**8, dictionary, codes, len(codes), out, len(out), 8, 256)
+assert k == len(ref) and np.array_equal(out[:k], ref)
+print("paths ok")
+"""
+
+
+@pytest.mark.parametrize("env", [{"SGXAMD_DIGIT_SIDE": "0", "SGXAMD_SCAN_ONEPASS": "0"},
+                                 {"SGXAMD_DIGIT_SIDE": "1", "SGXAMD_SCAN_ONEPASS": "1"}])
+def test_switch_paths_match_oracle(env):
+    e = dict(os.environ, **env)
+    e["PYTHONPATH"] = os.pathsep.join([os.path.join(PKG, "python"), os.path.join(ROOT, "oracle"),
+                                       e.get("PYTHONPATH", "")])
+    r = subprocess.run([sys.executable, "-c", CHILD], env=e, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "paths ok" in r.stdout, (env, r.stdout[-2000:], r.stderr[-2000:])
