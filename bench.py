@@ -235,6 +235,25 @@ def main():
     del R, S
     torch.cuda.empty_cache()
 
+    # measured stream-copy ceiling of this GPU: device-to-device copy of
+    # 2 GiB, read + write bytes over the event time of the copy kernel, best of 5
+    src = torch.empty(1 << 28, dtype=torch.int64, device=dev)
+    dst = torch.empty_like(src)
+    dst.copy_(src)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    best = float("inf")
+    for _ in range(5):
+        ev0.record()
+        dst.copy_(src)
+        ev1.record()
+        ev1.synchronize()
+        best = min(best, ev0.elapsed_time(ev1))
+    roofline["measured_copy_ceiling"] = {"GB_per_s": round(2 * src.numel() * 8 / (best * 1e-3) / 1e9, 1),
+                                         "how": "torch copy_ of 2 GiB device to device, read + write bytes, "
+                                                "best of 5 (HIP events)"}
+    del src, dst
+    torch.cuda.empty_cache()
+
     # ---------------- scan (BASELINE config 3): 2^30 int32, [0, 26] = 10 % (types.hpp:134)
     scan_info = None
     if not args.no_scan and args.workload == "c2":
