@@ -137,3 +137,38 @@ def test_scan_sum_u8(sgx, orc, gpu):
     col = (np.arange((1 << 20) + 77) % 256).astype(np.uint8)
     for lo, hi in [(0, 26), (0, 255), (200, 255), (7, 7), (9, 3)]:
         assert sgx.scan_sum_u8(lo, hi, col, len(col)) == orc.scan_sum_u8(lo, hi, col)
+
+
+# ------------------------------------------------- one-pass selection (k_select)
+def test_select_lookback_sparse_and_empty_chunks(sgx, orc, gpu):
+    """Index / value outputs when whole 65,536-row chunks have no match (zero aggregates
+    in the look-back), when only one middle chunk and the ragged last chunk match, and
+    when every row matches (dense staging rounds) — against the oracle."""
+    import torch
+
+    n = (1 << 22) + 5
+    col = np.full(n, 1000, dtype=np.int32)
+    col[37 * 65536 + 11: 37 * 65536 + 5000] = 7
+    col[-3:] = 7
+    d = torch.from_numpy(col).to(gpu)
+    for lo, hi in [(7, 7), (0, 2000), (5000, 6000)]:
+        cnt = orc.scan("count", "i32", lo, hi, col)
+        out = torch.zeros(max(cnt, 1), dtype=torch.int64, device=gpu)
+        assert sgx.scan_index(lo, hi, d, n, out, cnt) == cnt
+        assert np.array_equal(out[:cnt].cpu().numpy().view(np.uint64), orc.scan("index", "i32", lo, hi, col))
+
+
+def test_select_repeated_full_size_calls(sgx, gpu):
+    """20 back-to-back 2^26-row index scans (1,024 chunks each): the ticket and the
+    status words are re-armed per call, and every call ends with the exact count."""
+    import torch
+
+    n = 1 << 26
+    col = torch.empty(n, dtype=torch.int32, device=gpu)
+    sgx.gen_scan_dev(col, n, 0, 0, "i32")
+    exp = n // 256 * 27
+    idx = torch.empty(exp, dtype=torch.int64, device=gpu)
+    for _ in range(20):
+        assert sgx.scan_index(0, 26, col, n, idx, exp) == exp
+    assert int(idx[-1]) == n - 256 + 26 and int(idx[27]) == 256
+    del col, idx
