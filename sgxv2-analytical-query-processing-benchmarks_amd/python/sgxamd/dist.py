@@ -19,12 +19,17 @@ tmpR/tmpS arrays (:1421-1433) across sockets:
 
 Pipelining (one timeline per rank; RCCL runs on its own stream):
 
-    compute:  shard R | shard S | .... R' local passes | S' local passes, build/probe
-    xGMI:             | R exchange ......| S exchange ........|
+    compute:  R0 | R1 R2 R3 S0 S1 S2 S3 | ..... R' local passes | S' local passes, build/probe
+    xGMI:        | R exchange (4 chunks) ........| S exchange (4 chunks) ..|
 
-S is shard-partitioned while R is on the wire, and R's local partition passes
-(mi355_rho_join_begin) run while S is on the wire; S's passes and the build/probe
-(mi355_rho_join_finish) follow S's arrival in stream order.
+Each relation is shard-partitioned in `chunks` contiguous pieces; a piece's tuple
+all-to-all is posted as soon as its counts are known, so R is on the wire after the
+first piece instead of after the whole shard pass, and the other pieces (and all of S)
+are partitioned meanwhile.  R's local partition passes (mi355_rho_join_begin) run
+while S is on the wire; S's passes and the build/probe (mi355_rho_join_finish) follow
+S's arrival in stream order.  The pieces of one relation land back to back in one
+receive buffer (sized for the worst case, every sender's piece coming to this rank:
+world x the local slice), so R' and S' are contiguous for the local join.
 
 G must be a power of two.  The local compute (steps 1 and 4) defaults to the
 HIP library; tests inject CPU restatements to run the exchange logic on gloo.
@@ -154,28 +159,66 @@ def _exchange_counts(send_counts: list[int], cgroup) -> list[int]:
     return [int(x) for x in rc.tolist()]
 
 
-def _exchange_tuples(t: torch.Tensor, send_counts: list[int], recv_counts: list[int], group):
-    """all_to_all_single of the tuples, left in flight: (out, total, work).  A gloo
-    group with device tensors (single-GPU rehearsal of the multi-rank path) stages
-    through host memory synchronously."""
-    total = sum(recv_counts)
-    out = torch.empty(max(total, 1), dtype=torch.int64, device=t.device)
-    if t.is_cuda and dist.get_backend(group) == "gloo":
-        host_out = torch.empty(max(total, 1), dtype=torch.int64)
-        dist.all_to_all_single(host_out[:total], t[:sum(send_counts)].cpu(), recv_counts, send_counts, group=group)
-        out[:total].copy_(host_out[:total])
-        return out, total, _Done()
-    work = dist.all_to_all_single(out[:total], t[:sum(send_counts)], recv_counts, send_counts, group=group,
-                                  async_op=True)
-    return out, total, work
+class _Exchange:
+    """One relation's chunked shard partition + tuple all-to-all (see the module doc)."""
+
+    def __init__(self, t: torch.Tensor, dest_bits: int, partition_fn, cgroup, group, chunks: int):
+        world = 1 << dest_bits
+        n = t.numel()
+        chunks = max(1, chunks)
+        # every rank makes exactly `chunks` pieces (some may be empty), so all ranks issue
+        # the same sequence of collectives whatever their slice sizes
+        per = -(-n // chunks)
+        self.bounds = [(min(n, i * per), min(n, (i + 1) * per)) for i in range(chunks)]
+        # worst case for the receive buffer: every rank's piece i comes to this rank, and
+        # no rank's piece is larger than the largest slice's
+        nmax = torch.tensor([n], dtype=torch.int64)
+        dist.all_reduce(nmax, op=dist.ReduceOp.MAX, group=cgroup)
+        cap = world * chunks * -(-int(nmax.item()) // chunks)
+        self.out = torch.empty(max(cap, 1), dtype=torch.int64, device=t.device)
+        self.world = world
+        self.total = 0
+        self.works = []
+        self.keep = []  # send buffers stay alive until their exchange completed
+        self.t, self.dest_bits, self.partition_fn = t, dest_bits, partition_fn
+        self.cgroup, self.group = cgroup, group
+
+    def piece(self, i: int) -> None:
+        a, b = self.bounds[i]
+        if b > a:
+            p, c = self.partition_fn(self.t[a:b], b - a, self.dest_bits)
+        else:
+            p, c = self.t[:0], [0] * self.world
+        rc = _exchange_counts(c, self.cgroup)
+        got = sum(rc)
+        dst = self.out[self.total:self.total + got]
+        self.total += got
+        self.works.append(_post_exchange(dst, p, c, rc, self.group))
+        self.keep.append(p)
+
+    def wait(self) -> None:
+        for w in self.works:
+            w.wait()
+
+
+def _post_exchange(dst: torch.Tensor, src: torch.Tensor, send_counts: list[int], recv_counts: list[int], group):
+    """all_to_all_single of one piece into dst, left in flight; a gloo group with device
+    tensors (single-GPU rehearsal) stages through host memory synchronously."""
+    ns, nr = sum(send_counts), sum(recv_counts)
+    if src.is_cuda and dist.get_backend(group) == "gloo":
+        host = torch.empty(max(nr, 1), dtype=torch.int64)
+        dist.all_to_all_single(host[:nr], src[:ns].cpu(), recv_counts, send_counts, group=group)
+        dst[:nr].copy_(host[:nr])
+        return _Done()
+    return dist.all_to_all_single(dst[:nr], src[:ns], recv_counts, send_counts, group=group, async_op=True)
 
 
 def sharded_rho_join(R: torch.Tensor, S: torch.Tensor, *, group=None, partition_fn=None,
-                     local_join_fn=None, algorithm: str = "RHO") -> ShardedJoinResult:
+                     local_join_fn=None, algorithm: str = "RHO", chunks: int = 4) -> ShardedJoinResult:
     """Global RHO join of the row slices R and S (int64 tensors, one tuple each).
 
-    Collective: every rank of `group` must call it.  Returns the global match count
-    on every rank.
+    Collective: every rank of `group` must call it (with the same `chunks`).  Returns
+    the global match count on every rank.
     """
     partition_fn = partition_fn or _default_partition
     local = _InjectedLocalJoin(local_join_fn) if local_join_fn is not None else _LibraryLocalJoin(algorithm)
@@ -192,31 +235,32 @@ def sharded_rho_join(R: torch.Tensor, S: torch.Tensor, *, group=None, partition_
         return ShardedJoinResult(int(m), int(m), R.numel(), S.numel(), ms, st)
 
     cgroup = _count_group(group)
-    # R: shard partition, counts, tuple exchange left in flight on the RCCL stream
-    pR, cR = partition_fn(R, R.numel(), dest_bits)
-    rcR = _exchange_counts(cR, cgroup)
-    rR, nR, wR = _exchange_tuples(pR, cR, rcR, group)
-    # S: shard partition on the compute stream while R is on the wire
-    pS, cS = partition_fn(S, S.numel(), dest_bits)
-    rcS = _exchange_counts(cS, cgroup)
+    # R piece by piece: each piece's exchange is in flight on the RCCL stream while the
+    # next pieces (and then S) are shard-partitioned on the compute stream
+    xR = _Exchange(R, dest_bits, partition_fn, cgroup, group, chunks)
+    xS = _Exchange(S, dest_bits, partition_fn, cgroup, group, chunks)
+    for i in range(len(xR.bounds)):
+        xR.piece(i)
+    for i in range(len(xS.bounds)):
+        xS.piece(i)
     t1 = time.perf_counter()
-    ms["shard_partition"] = (t1 - t0) * 1e3
-    rS, nS, wS = _exchange_tuples(pS, cS, rcS, group)
+    ms["shard_partition_and_post_exchange"] = (t1 - t0) * 1e3  # host time; pieces are on the wire
+    rR, nR, rS, nS = xR.out, xR.total, xS.out, xS.total
     # R's local passes once R has arrived (stream order), while S is on the wire
-    wR.wait()
+    xR.wait()
     if nR and nS:
         local.begin(rR, nR, nS, dest_bits)
-        wS.wait()
+        xS.wait()
         m, st = local.finish(rS, nS)
     else:
-        wS.wait()
+        xS.wait()
         m, st = 0, {}
     sync()
     t2 = time.perf_counter()
-    ms["exchange_and_local_join"] = (t2 - t1) * 1e3
+    ms["exchange_wait_and_local_join"] = (t2 - t1) * 1e3
     tot = torch.tensor([int(m)], dtype=torch.int64)
     dist.all_reduce(tot, op=dist.ReduceOp.SUM, group=cgroup)
     ms["all_reduce"] = (time.perf_counter() - t2) * 1e3
     # keep the send buffers alive until both exchanges completed
-    del pR, pS
+    del xR, xS
     return ShardedJoinResult(int(tot.item()), int(m), nR, nS, ms, st)

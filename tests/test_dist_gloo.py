@@ -24,7 +24,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, nR, nS, kind, q):
+def _worker(rank, world, port, nR, nS, kind, q, chunks=4):
     import sys
 
     from conftest import PKG, ROOT
@@ -70,20 +70,25 @@ def _worker(rank, world, port, nR, nS, kind, q):
         return oracle.rho_join(r, s, 1)[0] if nr and ns else 0, {}
 
     res = sharded_rho_join(torch.from_numpy(Rl.view(np.int64)), torch.from_numpy(Sl.view(np.int64)),
-                           partition_fn=partition_fn, local_join_fn=local_join_fn)
+                           partition_fn=partition_fn, local_join_fn=local_join_fn, chunks=chunks)
+    # no local join runs on a rank that received no R or no S tuple
+    seen.setdefault("low_bits_ok", res.recv_r == 0 or res.recv_s == 0)
     tot = torch.tensor([res.recv_r, res.recv_s], dtype=torch.int64)
     dist.all_reduce(tot)
     q.put((rank, res.matches, expected, seen.get("low_bits_ok"), tot.tolist()))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,nR,nS,kind", [(2, 1 << 14, 1 << 15, "ref"), (2, 9999, 7777, "dup"),
-                                              (4, 1 << 13, 1 << 13, "ref")])
-def test_sharded_join_gloo(world, nR, nS, kind):
+# chunks: the shard partition + exchange in pieces (4), in one piece (1), and with
+# slices too small for every rank to fill its pieces (empty pieces, uneven slices)
+@pytest.mark.parametrize("world,nR,nS,kind,chunks", [(2, 1 << 14, 1 << 15, "ref", 4), (2, 9999, 7777, "dup", 4),
+                                                     (4, 1 << 13, 1 << 13, "ref", 4), (2, 9999, 7777, "dup", 1),
+                                                     (4, 7, 13, "dup", 4)])
+def test_sharded_join_gloo(world, nR, nS, kind, chunks):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, nR, nS, kind, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, nR, nS, kind, q, chunks)) for r in range(world)]
     for p in procs:
         p.start()
     out = [q.get(timeout=240) for _ in range(world)]
