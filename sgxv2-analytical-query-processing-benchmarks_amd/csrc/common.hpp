@@ -119,6 +119,61 @@ __device__ __forceinline__ uint64_t block_excl_scan_u64(uint64_t v, uint64_t *sc
     return r;
 }
 
+// ---------------------------------------------------- decoupled look-back ---
+// Single-pass exclusive prefix over chunks claimed in order through a ticket counter
+// (so every lower chunk belongs to a workgroup that is already running: the look-back
+// cannot deadlock).  status[c] = kLbAgg | count as soon as chunk c is counted, then
+// kLbIncl | inclusive prefix; zeroed before the launch.  Each status word is data and
+// flag at once: one aligned 8-byte agent-scope relaxed store (sc1, write-through)
+// publishes, agent-scope relaxed loads (sc1) poll (MI355X_MICROARCH.md visibility
+// table, cdna_hip_programming.md Guideline 16 R2).
+constexpr uint64_t kLbAgg = 1ull << 62, kLbIncl = 2ull << 62, kLbVal = kLbAgg - 1;
+
+__device__ __forceinline__ uint64_t lb_load(const uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void lb_store(uint64_t *p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Called by ONE whole wave for chunk c with its count agg: publishes, walks back over
+// the predecessors 64 at a time (summing aggregates back to the nearest inclusive
+// prefix), publishes the inclusive prefix and returns the exclusive one in every lane.
+// A poll that never completes (a predecessor cannot fail to publish: it is running)
+// gives up after ~2^20 rounds and sets *fail instead of hanging the device.
+__device__ __forceinline__ uint64_t lookback_exclusive(uint64_t *status, uint32_t c, uint64_t agg,
+                                                       uint32_t *fail) {
+    const uint32_t lane = __lane_id();
+    if (c == 0) {
+        if (lane == 0) lb_store(&status[0], kLbIncl | agg);
+        return 0;
+    }
+    if (lane == 0) lb_store(&status[c], kLbAgg | agg);
+    uint64_t excl = 0;
+    int64_t hi_idx = (int64_t)c - 1;  // the window ends here
+    while (true) {
+        const int64_t j = hi_idx - (int64_t)lane;
+        uint64_t st = j >= 0 ? lb_load(&status[j]) : kLbIncl;  // before chunk 0: prefix 0
+        uint32_t spins = 0;
+        while (__ballot(st == 0)) {
+            __builtin_amdgcn_s_sleep(1);
+            if (st == 0) st = lb_load(&status[j]);
+            if (++spins == (1u << 20)) {
+                if (lane == 0) atomicExch(fail, 1u);
+                st = kLbIncl;
+            }
+        }
+        const uint64_t incl_mask = __ballot((st & kLbIncl) != 0);
+        // lanes up to and including the nearest inclusive predecessor
+        const uint32_t stop = incl_mask ? (uint32_t)__builtin_ctzll(incl_mask) : 64u;
+        excl += wave_sum_u64((lane <= stop && j >= 0) ? (st & kLbVal) : 0);
+        if (incl_mask) break;
+        hi_idx -= 64;
+    }
+    if (lane == 0) lb_store(&status[c], kLbIncl | (excl + agg));
+    return excl;
+}
+
 // ------------------------------------------------------------------ host ---
 
 // Thread-local error text, exposed through mi355_last_error().

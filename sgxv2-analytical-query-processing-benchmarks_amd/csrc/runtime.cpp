@@ -1,6 +1,8 @@
 // Per-device runtime (see runtime.hpp) and the error / timing C-ABI.
 #include "runtime.hpp"
 
+#include <cstdlib>
+
 #include <map>
 #include <memory>
 
@@ -114,6 +116,14 @@ hipStream_t side_stream(Context *ctx) {
 }
 bool thread_timing_enabled() { return t_timing; }
 bool thread_partition_overlap() { return t_overlap; }
+
+bool one_pass_selection() {
+    static const bool on = [] {
+        const char *e = std::getenv("SGXAMD_SCAN_ONEPASS");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return on;
+}
 
 Context *current_context(int *status) {
     int ndev = 0;

@@ -41,17 +41,6 @@ Geometry geometry(uint64_t n) {
 
 enum class Op { kCount, kBitvector, kIndex, kValues };
 
-// Index / value / dictionary outputs in one pass (launch_select, decoupled look-back)
-// or, with SGXAMD_SCAN_ONEPASS=0 (development A/B switch), as bitvector pass + chunk
-// scan + expand pass.  Results are identical.
-bool one_pass_select() {
-    static const bool on = [] {
-        const char *e = std::getenv("SGXAMD_SCAN_ONEPASS");
-        return !(e && std::atoi(e) == 0);
-    }();
-    return on;
-}
-
 // Device-resident, 16-byte aligned view of the input column.
 template <typename T>
 int stage_input(Context *ctx, hipStream_t s, const T *in, size_t n, const T **dev) {
@@ -91,7 +80,7 @@ int run(Op op, T lo, T hi, const T *in, size_t n, void *out, size_t cap, uint64_
     const size_t o_counts = A.reserve(sizeof(uint64_t) * g.nchunks);
     const size_t o_offs = A.reserve(sizeof(uint64_t) * g.nchunks);
     const size_t o_res = A.reserve(sizeof(uint64_t) * 2);
-    const bool select1 = (op == Op::kIndex || op == Op::kValues) && one_pass_select();
+    const bool select1 = (op == Op::kIndex || op == Op::kValues) && one_pass_selection();
     const size_t o_status = A.reserve(sizeof(uint64_t) * (select1 ? select_chunks(n) : 0) + 16);
     SCAN_HIP(A.buf.ensure(A.used));
     uint64_t *counts = A.at<uint64_t>(o_counts);
@@ -247,7 +236,7 @@ int run_dict(int64_t lo, int64_t hi, const int64_t *dict, uint64_t dict_size, co
     const size_t o_offs = A.reserve(sizeof(uint64_t) * g.nchunks);
     const size_t o_res = A.reserve(sizeof(uint64_t) * 2);
     const size_t o_range = A.reserve(sizeof(uint64_t) * 2);
-    const bool select1 = one_pass_select();
+    const bool select1 = one_pass_selection();
     const size_t o_status = A.reserve(sizeof(uint64_t) * (select1 ? select_chunks(n) : 0) + 16);
     SCAN_HIP(A.buf.ensure(A.used));
     uint64_t *range = A.at<uint64_t>(o_range);

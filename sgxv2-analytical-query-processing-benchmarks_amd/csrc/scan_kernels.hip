@@ -436,27 +436,15 @@ template hipError_t launch_expand<uint32_t, int64_t, 2>(const uint64_t *, const 
 // running.  Per chunk:
 //   1. predicate over the chunk into an LDS bitvector (one 64-row word per 64 rows,
 //      assembled across the LPW lanes of a 64-row group as in k_predicate) + count;
-//   2. decoupled look-back over the chunk status words: status[c] is published as
-//      (kAgg | count) at once and as (kIncl | inclusive prefix) when known; the first
-//      wave reads 64 predecessors at a time with agent-scope atomics,
-//      sums aggregates back to the nearest inclusive prefix and publishes its own;
-//      a predecessor that has not counted yet (status 0) is polled again — it is
+//   2. decoupled look-back by the first wave (common.hpp lookback_exclusive): the
+//      chunk's count is published at once, the predecessors are read 64 at a time
+//      back to the nearest inclusive prefix, and the chunk's own inclusive prefix is
+//      published; a predecessor that has not counted yet is polled again — it is
 //      already running, so the wait ends;
 //   3. the LDS bitvector expanded exactly like k_expand (per-wave LDS staging of
 //      the matches, coalesced stores) at the chunk's exclusive prefix.
 // The chunk that ends the column writes the total.
 constexpr uint32_t kSelChunk = 65536;  // rows per chunk (8 KiB LDS bitvector)
-constexpr uint64_t kAgg = 1ull << 62, kIncl = 2ull << 62, kValMask = kAgg - 1;
-
-// The status words are the data and the flag at once (MI355X_MICROARCH.md visibility
-// table, cdna_hip_programming.md Guideline 16 R2): one aligned 8-byte agent-scope
-// relaxed store (sc1, write-through) publishes, agent-scope relaxed loads (sc1) poll.
-__device__ __forceinline__ uint64_t ld_status(const uint64_t *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_status(uint64_t *p, uint64_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 template <typename T, typename OutT, int MODE>
 __global__ __launch_bounds__(kBlock) void k_select(const T *__restrict__ in, uint64_t n, T lo, T hi,
@@ -532,37 +520,7 @@ __global__ __launch_bounds__(kBlock) void k_select(const T *__restrict__ in, uin
 
     // 2. decoupled look-back (first wave)
     if (wave == 0) {
-        uint64_t excl = 0;
-        if (c == 0) {
-            if (lane == 0) st_status(&status[0], kIncl | agg);
-        } else {
-            if (lane == 0) st_status(&status[c], kAgg | agg);
-            int64_t hi_idx = (int64_t)c - 1;  // next predecessor window ends here
-            while (true) {
-                const int64_t j = hi_idx - (int64_t)lane;
-                uint64_t st = j >= 0 ? ld_status(&status[j]) : kIncl;  // before chunk 0: prefix 0
-                // poll until every lane of the window has published something; a
-                // predecessor that never publishes (it cannot: it is running) would end
-                // the poll after ~2^20 rounds with ticket[1] set, not hang the device
-                uint32_t spins = 0;
-                while (__ballot(st == 0)) {
-                    __builtin_amdgcn_s_sleep(1);
-                    if (st == 0) st = ld_status(&status[j]);
-                    if (++spins == (1u << 20)) {
-                        if (lane == 0) atomicExch(&ticket[1], 1u);
-                        st = kIncl;
-                    }
-                }
-                const uint64_t incl_mask = __ballot((st & kIncl) != 0);
-                // lanes up to and including the nearest inclusive predecessor
-                const uint32_t stop = incl_mask ? (uint32_t)__builtin_ctzll(incl_mask) : 64u;
-                uint64_t v = (lane <= stop && j >= 0) ? (st & kValMask) : 0;
-                excl += wave_sum_u64(v);
-                if (incl_mask) break;
-                hi_idx -= 64;
-            }
-            if (lane == 0) st_status(&status[c], kIncl | (excl + agg));
-        }
+        const uint64_t excl = lookback_exclusive(status, c, agg, &ticket[1]);
         if (lane == 0) excl_s = excl;
     }
     __syncthreads();

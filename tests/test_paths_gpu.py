@@ -2,7 +2,8 @@
 SGXAMD_DIGIT_SIDE=0 (pass-2 histograms over the tuples instead of the digit side
 stream) and SGXAMD_SCAN_ONEPASS=0 (index / value / dictionary scans as bitvector pass +
 expand pass instead of the one-pass look-back selection).  Both switches are read
-once per process, so each setting runs in a child process against the oracle."""
+once per process, so each setting runs in a child process against the oracle (the
+TPC-H selections ride along: they share the library's workspace)."""
 import os
 import subprocess
 import sys
@@ -39,6 +40,10 @@ ref = oracle.dict_scan(-10**8, 5 * 10**8, dictionary, codes)
 out = np.zeros(len(ref) + 1, dtype=np.int64)
 k = sgxamd.dict_scan(-10**8, 5 * 10**8, dictionary, codes, len(codes), out, len(out), 8, 256)
 assert k == len(ref) and np.array_equal(out[:k], ref)
+import sgxamd.tpch as T
+tb = T.generate(20, 5)  # SF 0.02
+for q, w in [(3, 1), (3, 2), (3, 3), (10, 1), (10, 2), (12, 1), (19, 1), (19, 2)]:
+    assert np.array_equal(T.filter_rows(q, w, tb), oracle.tpch_filter(q, w, tb)), (q, w)
 print("paths ok")
 """
 
