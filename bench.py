@@ -74,6 +74,8 @@ def main():
                          "multi-rank path (ranks share the visible GPUs, tuples staged through host memory)")
     ap.add_argument("--no-scan", action="store_true")
     ap.add_argument("--no-tpch", action="store_true")
+    ap.add_argument("--no-paper", action="store_true",
+                    help="skip the runs at the shapes of the reference's own published numbers")
     ap.add_argument("--tpch-scale-milli", type=int, default=10000, help="TPC-H scale factor x 1000 (10000 = SF10)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -299,6 +301,66 @@ def main():
         del col, bv, idx
         torch.cuda.empty_cache()
 
+    # ---------------- the shapes of the reference's own published numbers (BASELINE.md §1,
+    # Xeon Gold 6326, 16 threads, native): RHO at |R| = 13,107,200, |S| = 52,428,800
+    # (scaling-perf.csv, 1493.97 M rec/s) and the uint8 scans of SimdScanMulti
+    # (bitvector at 1 % selectivity 107.79 GiB/s, scale-up.csv; index list at 10 %
+    # 48.37 GiB/s, write-rate.csv).  Context lines, not the headline metric.
+    paper_info = None
+    if not args.no_paper and world == 1 and args.workload == "c2":
+        nRp, nSp = 13_107_200, 52_428_800
+        Rp = torch.empty(nRp, dtype=torch.int64, device=dev)
+        Sp = torch.empty(nSp, dtype=torch.int64, device=dev)
+        sgxamd.gen_pk_dev(Rp, nRp, 0, nRp, 11111, stream)
+        sgxamd.gen_fk_dev(Sp, nSp, 0, nRp, 22222, stream)  # 4 shuffled copies of 1..|R|
+        torch.cuda.synchronize()
+        for _ in range(max(1, args.warmup)):
+            assert sgxamd.rho_join(Rp, nRp, Sp, nSp, stream=stream).matches == nSp
+        barrier()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            assert sgxamd.rho_join(Rp, nRp, Sp, nSp, stream=stream).matches == nSp
+        barrier()
+        el = (time.perf_counter() - t1) / args.steps
+        rho_p = round((nRp + nSp) / el / 1e6, 1)
+        paper_info = {"rho": {"shape": "|R|=13,107,200 |S|=52,428,800 (100/400 MiB), pk/fk, count only",
+                              "M_rec_per_s": rho_p, "ms": round(el * 1e3, 4),
+                              "reference_M_rec_per_s": 1493.97,
+                              "reference": "Xeon Gold 6326, 16 threads, native, UNROLL+FORCE_2_PHASES "
+                                           "(scaling-perf.csv median)",
+                              "ratio": round(rho_p / 1493.97, 1)}}
+        del Rp, Sp
+        torch.cuda.empty_cache()
+        nu = 1 << 32  # uint8 entries (the reference's index-list runs use 2^32)
+        col = torch.empty(nu, dtype=torch.uint8, device=dev)
+        sgxamd.gen_scan_dev(col, nu, 0, 0, "u8", stream)  # i % 256 (Allocator.hpp)
+        bvu = torch.empty(nu // 64, dtype=torch.int64, device=dev)
+        # selectivity -> [0, round(sel / 100 * 255)] (types.hpp:134): 1 % -> [0, 3], 10 % -> [0, 26]
+        k10 = nu // 256 * 27
+        idxu = torch.empty(k10, dtype=torch.int64, device=dev)
+        for kind, hi, ref, src in (("bitvector_1pct", 3, 107.79, "scale-up.csv, 2^34 entries"),
+                                   ("index_10pct", 26, 48.37, "write-rate.csv, 2^32 entries")):
+            def run():
+                if kind.startswith("bitvector"):
+                    sgxamd.scan_bitvector(0, hi, col, nu, bvu, "u8")
+                else:
+                    assert sgxamd.scan_index(0, hi, col, nu, idxu, k10, "u8") == k10
+            for _ in range(max(1, args.warmup)):
+                run()
+            barrier()
+            t1 = time.perf_counter()
+            for _ in range(args.steps):
+                run()
+            barrier()
+            el = (time.perf_counter() - t1) / args.steps
+            gib = nu / el / 2**30
+            paper_info[f"scan_u8_{kind}"] = {"entries": nu, "predicate": [0, hi], "GiB_per_s": round(gib, 1),
+                                             "ms": round(el * 1e3, 4), "reference_GiB_per_s": ref,
+                                             "reference": f"Xeon Gold 6326, 16 threads, native ({src})",
+                                             "ratio": round(gib / ref, 1)}
+        del col, bvu, idxu
+        torch.cuda.empty_cache()
+
     # ---------------- TPC-H callers: Q3/Q10/Q12/Q19 on device-resident
     # synthetic tables, one GPU (the pipelines are single-device; skipped for N > 1)
     tpch_info = None
@@ -384,6 +446,7 @@ def main():
                        **({"dist_backend": "gloo (single-GPU rehearsal, not a scaling number)"}
                           if world > 1 and args.dist_backend == "gloo" else {})},
             "roofline": roofline, "cpu_baseline": cpu, "rho": rho_info, "scan": scan_info, "tpch": tpch_info,
+            "reference_shapes": paper_info,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
