@@ -430,6 +430,12 @@ def main():
                "sample": f"oracle RHO (radix_join.cpp restated, pthreads) on reference-generated "
                          f"pk/fk |R|=|S|=2^26 (native.cpp seeds), median of {len(tp)} joins",
                "M_rec_per_s_reference_formula": round(2 * statistics.median(tp), 1)}
+        try:  # the host the baseline ran on (the reference's numbers are a Xeon Gold 6326's)
+            with open("/proc/cpuinfo") as f:
+                cpu["host_cpu"] = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), None)
+            cpu["host_logical_cpus"] = os.cpu_count()
+        except OSError:
+            pass
         del Rh, Sh
 
     if rank == 0:
