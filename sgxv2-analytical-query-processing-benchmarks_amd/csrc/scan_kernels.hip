@@ -444,7 +444,10 @@ template hipError_t launch_expand<uint32_t, int64_t, 2>(const uint64_t *, const 
 //   3. the LDS bitvector expanded exactly like k_expand (per-wave LDS staging of
 //      the matches, coalesced stores) at the chunk's exclusive prefix.
 // The chunk that ends the column writes the total.
-constexpr uint32_t kSelChunk = 65536;  // rows per chunk (8 KiB LDS bitvector)
+constexpr uint32_t kSelChunk = 65536;  // rows per chunk of 32-bit values (8 KiB LDS bitvector)
+// narrower codes take proportionally more rows per chunk (the same 256 KiB of input)
+template <typename T>
+constexpr uint32_t sel_chunk() { return kSelChunk * (uint32_t)(4 / sizeof(T)); }
 
 template <typename T, typename OutT, int MODE>
 __global__ __launch_bounds__(kBlock) void k_select(const T *__restrict__ in, uint64_t n, T lo, T hi,
@@ -452,7 +455,7 @@ __global__ __launch_bounds__(kBlock) void k_select(const T *__restrict__ in, uin
                                                    OutT *__restrict__ out, uint64_t cap,
                                                    const int64_t *__restrict__ dict, uint64_t *__restrict__ total) {
     constexpr uint32_t V = 16 / sizeof(T), LPW = 64 / V, FULL = (1u << V) - 1u;
-    constexpr uint32_t CH = kSelChunk, NWORD = CH / 64;
+    constexpr uint32_t CH = sel_chunk<T>(), NWORD = CH / 64;
     constexpr int U = 8;  // 16-B loads in flight per lane
     __shared__ uint64_t bits[NWORD];
     constexpr uint32_t STG = kStage;
@@ -581,12 +584,12 @@ __global__ __launch_bounds__(kBlock) void k_select(const T *__restrict__ in, uin
     }
 }
 
-uint64_t select_chunks(uint64_t n) { return (n + kSelChunk - 1) / kSelChunk; }
+uint64_t select_chunks(uint64_t n) { return (n + kSelChunk - 1) / kSelChunk; }  // bound for every T
 
 template <typename T, typename OutT, int MODE>
 hipError_t launch_select(const T *in, uint64_t n, T lo, T hi, uint32_t *ticket, uint64_t *status, OutT *out,
                          uint64_t cap, uint64_t *total, hipStream_t s, const int64_t *dict) {
-    const uint64_t nchunks = select_chunks(n);
+    const uint64_t nchunks = (n + sel_chunk<T>() - 1) / sel_chunk<T>();
     if (nchunks == 0) return hipSuccess;
     hipError_t e = hipMemsetAsync(ticket, 0, 2 * sizeof(uint32_t), s);
     if (e != hipSuccess) return e;
