@@ -1,4 +1,4 @@
-"""Multi-GPU RHO: radix-partition sharding with one all-to-all exchange per relation.
+"""Multi-GPU RHO: radix-partition sharding with a pieced all-to-all exchange per relation.
 
 One process per GPU (torch.distributed; backend "nccl" is RCCL over xGMI on
 ROCm, "gloo" runs the same code on CPU tensors in tests).  Every rank holds a
