@@ -3,8 +3,8 @@
 
 Step = one full RHO join (partition pass 1 + pass 2 + build/probe, count-only) over
 |R| = |S| = 2^28 uniform tuples per GPU (BASELINE config 2; weak scaling: with N GPUs
-the global relations are N * 2^28 and are radix-sharded with one RCCL all-to-all per
-relation, sgxamd.dist).  Inputs are resident in HBM before the timed region.
+the global relations are N * 2^28 and are radix-sharded with an RCCL all-to-all of
+each relation in pieces, sgxamd.dist).  Inputs are resident in HBM before the timed region.
 
 One JSON line (rank 0):
   value = probed tuples (|S|, all ranks) per second over the whole join, in millions;
