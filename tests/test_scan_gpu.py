@@ -172,3 +172,38 @@ def test_select_repeated_full_size_calls(sgx, gpu):
         assert sgx.scan_index(0, 26, col, n, idx, exp) == exp
     assert int(idx[-1]) == n - 256 + 26 and int(idx[27]) == 256
     del col, idx
+
+
+def test_scan_beyond_2pow32_rows(sgx, gpu):
+    """Maximum sizes: a u8 column of 2^32 + 4,099 rows (row ids past 32 bits, ragged
+    tail).  Count / index / bitvector against torch's own predicate on the device:
+    the index list is strictly ascending, every entry satisfies the predicate and the
+    count equals torch's, which together pin the exact set; bitvector words across the
+    2^32 boundary and at the tail match the predicate bit for bit."""
+    import torch
+
+    n = (1 << 32) + 4099
+    col = torch.empty(n, dtype=torch.uint8, device=gpu)
+    sgx.gen_scan_dev(col, n, 1, 77, "u8")
+    lo, hi = 3, 5
+    exp = int(((col >= lo) & (col <= hi)).sum())
+    assert sgx.scan_count(lo, hi, col, n, "u8") == exp
+    idx = torch.empty(exp, dtype=torch.int64, device=gpu)
+    assert sgx.scan_index(lo, hi, col, n, idx, exp, "u8") == exp
+    assert bool((idx[1:] > idx[:-1]).all())
+    v = col[idx]
+    assert bool(((v >= lo) & (v <= hi)).all())
+    assert int(idx[-1]) < n and int((idx >= (1 << 32)).sum()) > 0
+    del v, idx
+    nwords = (n + 63) // 64
+    bv = torch.empty(nwords, dtype=torch.int64, device=gpu)
+    sgx.scan_bitvector(lo, hi, col, n, bv, "u8")
+    weights = torch.tensor([1 << b for b in range(63)] + [-(1 << 63)], dtype=torch.int64, device=gpu)
+    for w0 in ((1 << 26) - 8, nwords - 8):
+        rows = col[w0 * 64: min((w0 + 8) * 64, n)]
+        bits = ((rows >= lo) & (rows <= hi)).to(torch.int64)
+        bits = torch.nn.functional.pad(bits, (0, 8 * 64 - len(bits)))
+        words = (bits.view(8, 64) * weights).sum(1)
+        assert torch.equal(bv[w0: w0 + 8], words[: nwords - w0]), w0
+    del col, bv
+    torch.cuda.empty_cache()
