@@ -26,6 +26,7 @@ namespace {
 
 constexpr uint64_t kTargetPartition = 4096;  // R tuples per partition (= RCAP of an 8192-slot table)
 constexpr uint32_t kMaxBits = 18;
+constexpr uint64_t kMaxRChunk = 8192;         // largest LDS chain table (k_join RCAP)
 constexpr uint32_t kSegTarget = 2048;        // workgroups per partition pass and relation
 
 inline uint32_t ceil_log2(uint64_t x) {
@@ -48,9 +49,17 @@ Policy choose_policy(uint64_t nR, uint64_t nS, const mi355_rho_opts *o) {
         // every further S chunk of a partition rebuilds its R table.
         // The S-driven bits stop at 16 (two passes of <= 8 bits: a 9-bit pass-1 scatter
         // holds 512 digits in LDS and runs at half speed).
+        // Past 2^28 R tuples the partition target asks for 17-18 bits, i.e. a 9-bit pass;
+        // that costs more than giving the join two 8192-tuple R chunks per partition
+        // (each S chunk probed twice), so the R-driven bits stay at 16 until an average
+        // partition would exceed two chunks (scripts/size_sweep.py, DESIGN.md §4:
+        // 2^29: 16 bits 12.4 ms vs 17 bits 15.0 ms; 2^30: 16 / 17 / 18 bits 32.2 / 32.8
+        // / 41.5 ms; 2^31: 17 bits 79.4 ms vs 18 bits 88.1 ms).
         const uint64_t need_r = (nR + kTargetPartition - 1) / kTargetPartition;
         const uint64_t need_s = (nS + kSChunk - 1) / kSChunk;
-        const uint32_t bits_r = ceil_log2(std::max<uint64_t>(need_r, 1));
+        const uint64_t need_r2 = (nR + 2 * kMaxRChunk - 1) / (2 * kMaxRChunk);
+        const uint32_t bits_r = std::min(ceil_log2(std::max<uint64_t>(need_r, 1)),
+                                         std::max<uint32_t>(16, ceil_log2(std::max<uint64_t>(need_r2, 1))));
         const uint32_t bits_s = std::min<uint32_t>(ceil_log2(std::max<uint64_t>(need_s, 1)), 16);
         p.bits = std::min(std::max(bits_r, bits_s), kMaxBits);
     }

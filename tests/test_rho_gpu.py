@@ -160,6 +160,28 @@ def test_full_size_config2_property(sgx, gpu):
     torch.cuda.empty_cache()
 
 
+def test_max_size_pk_fk(sgx, gpu):
+    """|R| = |S| = 2^31 + 12,345 (ragged, 8x the headline size, 17 GB per relation):
+    the planner goes past 16 radix bits, so the pass-2 digit no longer fits the side
+    stream and the tuple-histogram path runs at scale; matches == |S|, and with foreign
+    keys drawn from [1, 1.5 |R|] exactly the ones that fall inside R's key range."""
+    import torch
+
+    n = (1 << 31) + 12_345
+    R = torch.empty(n, dtype=torch.int64, device=gpu)
+    S = torch.empty(n, dtype=torch.int64, device=gpu)
+    sgx.gen_pk_dev(R, n, 0, n, 11111)
+    sgx.gen_fk_dev(S, n, 0, n, 22222)
+    res = sgx.rho_join(R, n, S, n)
+    assert res.matches == n
+    assert res.stats["passes"] == 2 and res.stats["radix_bits"] > 16
+    sgx.gen_fk_dev(S, n, 0, n + n // 2, 33333)
+    m = sgx.rho_join(R, n, S, n).matches
+    assert m == int(((S & 0xFFFFFFFF) <= n).sum()) and n // 2 < m < n
+    del R, S
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("alg,extra", [("RHO", []), ("RHT", []), ("RHO", ["-m"]), ("RHT", ["-m", "-l", "50"])])
 def test_native_driver_binary(gpu, alg, extra):
     exe = os.path.join(PKG, "bin", "native_mi355")
