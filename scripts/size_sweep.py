@@ -2,7 +2,7 @@
 at the largest sizes the radix-bit splits the planner could take, to check that the
 plan chosen past 2^28 is the fastest one.  Development measurement, not a bench input:
 
-    python3 scripts/size_sweep.py [log2 sizes ...]      (default 24 26 28 29 30 31)
+    python3 scripts/size_sweep.py [--auto] [log2 sizes ...]   (default 24 26 28 29 30 31)
 """
 import os
 import sys
@@ -28,7 +28,8 @@ def timed(R, S, n, reps, **kw):
 
 
 def main():
-    logs = [int(a) for a in sys.argv[1:]] or [24, 26, 28, 29, 30, 31]
+    auto_only = "--auto" in sys.argv
+    logs = [int(a) for a in sys.argv[1:] if a != "--auto"] or [24, 26, 28, 29, 30, 31]
     for lg in logs:
         n = 1 << lg
         R = torch.empty(n, dtype=torch.int64, device="cuda")
@@ -37,7 +38,9 @@ def main():
         sgxamd.gen_fk_dev(S, n, 0, n, 22222)
         reps = max(3, min(20, (1 << 30) // n))
         plans = [{}]
-        if lg >= 29:
+        if os.environ.get("SWEEP_BITS"):  # e.g. SWEEP_BITS=13,14,15,16
+            plans += [{"radix_bits": int(b), "passes": 2} for b in os.environ["SWEEP_BITS"].split(",")]
+        elif lg >= 29 and not auto_only:
             plans += [{"radix_bits": b, "passes": 2} for b in (16, 17, 18)]
         for kw in plans:
             ms, st = timed(R, S, n, reps, **kw)

@@ -38,6 +38,22 @@ inline uint32_t ceil_log2(uint64_t x) {
 struct Policy {
     uint32_t bits, passes, b1, b2, rcap;
 };
+// Development A/B switch for the 16,384-tuple counting table (SGXAMD_BIG_JOIN=0: R
+// partitions above 8192 tuples are built in 8192-tuple chunks, each S chunk probed once
+// per chunk).  Read once per process.
+inline bool big_join_enabled() {
+    static const bool on = [] {
+        const char *e = std::getenv("SGXAMD_BIG_JOIN");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return on;
+}
+
+// Counting RHO joins (no materialisation) build partitions above 8192 R tuples in
+// kBigRcap-tuple LDS tables; the other modes in 8192-tuple chunks.
+inline bool uses_big_table(const mi355_rho_opts *o) {
+    return !(o && (o->materialize || o->algorithm == MI355_ALGO_RHT)) && big_join_enabled();
+}
 
 Policy choose_policy(uint64_t nR, uint64_t nS, const mi355_rho_opts *o) {
     Policy p{};
@@ -50,17 +66,27 @@ Policy choose_policy(uint64_t nR, uint64_t nS, const mi355_rho_opts *o) {
         // The S-driven bits stop at 16 (two passes of <= 8 bits: a 9-bit pass-1 scatter
         // holds 512 digits in LDS and runs at half speed).
         // Past 2^28 R tuples the partition target asks for 17-18 bits, i.e. a 9-bit pass;
-        // that costs more than giving the join two 8192-tuple R chunks per partition
-        // (each S chunk probed twice), so the R-driven bits stay at 16 until an average
-        // partition would exceed two chunks (scripts/size_sweep.py, DESIGN.md §4:
-        // 2^29: 16 bits 12.4 ms vs 17 bits 15.0 ms; 2^30: 16 / 17 / 18 bits 32.2 / 32.8
-        // / 41.5 ms; 2^31: 17 bits 79.4 ms vs 18 bits 88.1 ms).
-        const uint64_t need_r = (nR + kTargetPartition - 1) / kTargetPartition;
-        const uint64_t need_s = (nS + kSChunk - 1) / kSChunk;
-        const uint64_t need_r2 = (nR + 2 * kMaxRChunk - 1) / (2 * kMaxRChunk);
-        const uint32_t bits_r = std::min(ceil_log2(std::max<uint64_t>(need_r, 1)),
-                                         std::max<uint32_t>(16, ceil_log2(std::max<uint64_t>(need_r2, 1))));
-        const uint32_t bits_s = std::min<uint32_t>(ceil_log2(std::max<uint64_t>(need_s, 1)), 16);
+        // that costs more than giving the join two LDS tables per partition (each S
+        // chunk probed twice), so the R-driven bits stay at 16 until an average
+        // partition would exceed two tables.
+        // Counting joins with the 16,384-tuple table size partitions for that table
+        // once there are enough of them to fill the chip (>= 2^13 tasks): fewer digits
+        // per partition pass, one task per partition.
+        // scripts/size_sweep.py, DESIGN.md §3 (|R| = |S|, ms): 2^28: 14 / 15 / 16 bits
+        // 5.53 / 5.58 / 5.71; 2^30: 16 / 17 / 18 bits 23.2 / 30.4 / 41.3; 2^31: 16 / 17
+        // / 18 bits 47.2 / 60.7 / 83.5.
+        const bool big = uses_big_table(o);
+        const uint64_t table = big ? kBigRcap : kMaxRChunk;
+        const auto clog2 = [](uint64_t num, uint64_t den) {
+            return ceil_log2(std::max<uint64_t>((num + den - 1) / den, 1));
+        };
+        const uint32_t cap_r = std::max<uint32_t>(16, clog2(nR, 2 * table));
+        uint32_t bits_r = std::min(clog2(nR, kTargetPartition), cap_r);
+        uint32_t bits_s = std::min<uint32_t>(clog2(nS, kSChunk), 16);
+        if (big && clog2(nR, kBigRcap) >= 13) {
+            bits_r = std::min(clog2(nR, kBigRcap), cap_r);
+            bits_s = std::min<uint32_t>(clog2(nS, kBigSChunk), 16);
+        }
         p.bits = std::min(std::max(bits_r, bits_s), kMaxBits);
     }
     p.passes = (o && o->passes > 0) ? (uint32_t)o->passes : (p.bits <= 8 ? 1u : 2u);
@@ -92,6 +118,7 @@ inline bool digit_side_enabled() {
     return on;
 }
 inline bool uses_digit_side(const Policy &p) { return p.passes == 2 && p.b2 <= 8 && digit_side_enabled(); }
+
 
 inline uint64_t seg_size_for(uint64_t n) {
     uint64_t s = (n + kSegTarget - 1) / kSegTarget;
@@ -207,6 +234,7 @@ struct PendingJoin {
     const uint64_t *psR = nullptr, *pcR = nullptr;
     size_t off_over = 0, off_counts = 0, off_toff = 0, off_result = 0;
     uint32_t over_cap = 0, join_grid = 0;
+    uint64_t s_chunk = kSChunk;  // S tuples per build/probe task
 };
 
 namespace {
@@ -256,7 +284,11 @@ int join_begin(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, uint64
     plan_relation(A, pj.pr, nR, pol);
     plan_relation(A, pj.ps, nS, pol);
     const uint64_t P = 1ull << pol.bits;
-    pj.over_cap = (uint32_t)(nS / kSChunk + 1);
+    if (uses_big_table(opts) && pol.rcap == 8192 && (nR + P - 1) / P > 8192) {
+        pj.pol.rcap = kBigRcap;
+        pj.s_chunk = kBigSChunk;
+    }
+    pj.over_cap = (uint32_t)(nS / pj.s_chunk + 1);
     // one workgroup per task up to 2048 (few partitions with a large S — a tiny build
     // side — still spread their S chunks over the chip)
     pj.join_grid = (uint32_t)std::min<uint64_t>(P + pj.over_cap - 1, 2048);
@@ -338,16 +370,16 @@ int join_finish(Context *ctx, PendingJoin &pj, const row_t *dS, uint64_t nS, mi3
     uint32_t *n_over = reinterpret_cast<uint32_t *>(result + 3);
     const uint32_t hash_shift = pj.key_shift + pol.bits;
     tm.mark("join_tasks");
-    RHO_HIP(launch_make_tasks(pcR, pcS, P, over, pj.over_cap, result + 1, s));
+    RHO_HIP(launch_make_tasks(pcR, pcS, P, over, pj.over_cap, result + 1, pj.s_chunk, s));
     if (!pj.materialize) {
         tm.mark("join_build_probe");
-        RHO_HIP(launch_join(fR, fS, psR, pcR, psS, pcS, P, over, n_over, hash_shift, pol.rcap, join_grid, kJoinCount,
-                            algo, counts, nullptr, nullptr, s));
+        RHO_HIP(launch_join(fR, fS, psR, pcR, psS, pcS, P, over, n_over, hash_shift, pol.rcap, pj.s_chunk, join_grid,
+                            kJoinCount, algo, counts, nullptr, nullptr, s));
         tm.mark("join_reduce");
         RHO_HIP(launch_reduce(counts, join_grid, result, s));
     } else {
         tm.mark("join_build_probe");
-        RHO_HIP(launch_join(fR, fS, psR, pcR, psS, pcS, P, over, n_over, hash_shift, pol.rcap, join_grid,
+        RHO_HIP(launch_join(fR, fS, psR, pcR, psS, pcS, P, over, n_over, hash_shift, pol.rcap, pj.s_chunk, join_grid,
                             kJoinTaskCount, algo, counts, nullptr, nullptr, s));
         tm.mark("join_offsets");
         RHO_HIP(launch_excl_scan(counts, n_over, P, task_off, result, s));
@@ -367,8 +399,8 @@ int join_finish(Context *ctx, PendingJoin &pj, const row_t *dS, uint64_t nS, mi3
             return MI355_ERR_CAPACITY;
         }
         tm.mark("join_materialize");
-        RHO_HIP(launch_join(fR, fS, psR, pcR, psS, pcS, P, over, n_over, hash_shift, pol.rcap, join_grid, kJoinWrite,
-                            algo, counts, task_off, out, s));
+        RHO_HIP(launch_join(fR, fS, psR, pcR, psS, pcS, P, over, n_over, hash_shift, pol.rcap, pj.s_chunk, join_grid,
+                            kJoinWrite, algo, counts, task_off, out, s));
     }
     tm.end_call();
     if (s2) RHO_HIP(hipEventRecord(ctx->ev_t1, s));

@@ -69,25 +69,33 @@ hipError_t launch_scatter(const row_t *in, row_t *out, const SegMap &m, uint32_t
                           uint32_t bits, const uint64_t *cursors, HistLayout layout, uint32_t nseg_stride,
                           const uint64_t *digit_base, const DigitSide *ds, hipStream_t s);
 
-// Build + probe over tasks (partition x S chunk of at most kSChunk tuples).
+// Build + probe over tasks (partition x S chunk of at most s_chunk tuples: kSChunk, or
+// kBigSChunk with the kBigRcap table).
 // Tasks 0..P-1 are the partitions' first chunks; over[0 .. *n_over) holds the
 // further chunks of large S partitions as p | chunk << 32 (launch_make_tasks).
-// rcap (2048 / 4096 / 8192) = R tuples per LDS chain table.
+// rcap (2048 / 4096 / 8192, or kBigRcap for counting) = R tuples per LDS chain table.
 // mode 0: counts[blockIdx] = per-workgroup partial count (grid entries);
 // mode 1: counts[t] = per-task count (P + *n_over entries);
 // mode 2: write every match to out[task_off[t] + ...] as output_triple_t.
 constexpr uint64_t kSChunk = 8192;
+// Counting joins of partitions above 8192 R tuples: a 16,384-tuple chain table per
+// 1,024-thread workgroup (160 KiB of LDS) and 32,768-tuple S chunks, so that neither
+// side is read twice at the 2^30-tuple sizes.
+constexpr uint32_t kBigRcap = 16384;
+constexpr int kBigJoinBlock = 1024;
+constexpr uint64_t kBigSChunk = 32768;
 enum JoinMode : int { kJoinCount = 0, kJoinTaskCount = 1, kJoinWrite = 2 };
 // Build/probe algorithm of one task: RHO's bucket chaining or RHT's histogram join.
 enum JoinAlgo : int { kAlgoChaining = 0, kAlgoHistogram = 1 };
 // meta (zeroed here): [0] = largest R partition, [1] = largest S partition,
 // [2] = the number of extra tasks (u32 n_over, read by launch_join / launch_excl_scan).
 hipError_t launch_make_tasks(const uint64_t *r_count, const uint64_t *s_count, uint64_t P, uint64_t *over,
-                             uint32_t over_cap, uint64_t *meta, hipStream_t s);
+                             uint32_t over_cap, uint64_t *meta, uint64_t s_chunk, hipStream_t s);
 hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, const uint64_t *r_count,
                        const uint64_t *s_start, const uint64_t *s_count, uint64_t P, const uint64_t *over,
-                       const uint32_t *n_over, uint32_t hash_shift, uint32_t rcap, uint32_t grid, int mode,
-                       int algo, uint64_t *counts, const uint64_t *task_off, output_triple_t *out, hipStream_t s);
+                       const uint32_t *n_over, uint32_t hash_shift, uint32_t rcap, uint64_t s_chunk, uint32_t grid,
+                       int mode, int algo, uint64_t *counts, const uint64_t *task_off, output_triple_t *out,
+                       hipStream_t s);
 // One-block exclusive scan of n_base + *n_extra values; *total = their sum.
 hipError_t launch_excl_scan(const uint64_t *in, const uint32_t *n_extra, uint64_t n_base, uint64_t *out,
                             uint64_t *total, hipStream_t s);

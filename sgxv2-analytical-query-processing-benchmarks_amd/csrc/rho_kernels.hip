@@ -599,7 +599,7 @@ hipError_t launch_scatter(const row_t *in, row_t *out, const SegMap &m, uint32_t
 // 1-based positions (:393 "we start pos's from 1").  The build links tuple i with
 // one LDS atomic exchange on its bucket head (chain order differs from the
 // reference's serial build; the count does not).  The probe walks every chain and
-// counts key equality (:429-436).  Each thread handles U = RCAP / kBlock tuples at
+// counts key equality (:429-436).  Each thread handles U = RCAP / BLOCK tuples at
 // a time; their chain walks advance in lockstep so the LDS reads of independent
 // tuples overlap.  Partitions whose R side exceeds RCAP are built chunk by chunk
 // with the task's S chunk re-probed per R chunk.
@@ -625,20 +625,20 @@ __device__ __forceinline__ void decode_task(uint64_t t, uint64_t P, const uint64
 // LDS of one build/probe workgroup: exactly 10 * RCAP bytes when counting (4
 // workgroups per CU at RCAP 4096), + 4 * RCAP of R payloads when writing.  The
 // reduction slots reuse the bucket heads, which are dead after each probe.
-template <int RCAP, int MODE>
+template <int RCAP, int MODE, int NW>
 struct JoinLds {
     union {
         __attribute__((aligned(16))) uint32_t head[RCAP];
-        uint64_t red[kWaves];
+        uint64_t red[NW];
     };
     uint32_t keys[RCAP];
     uint16_t next[RCAP];
 };
-template <int RCAP>
-struct JoinLds<RCAP, kJoinWrite> {
+template <int RCAP, int NW>
+struct JoinLds<RCAP, kJoinWrite, NW> {
     union {
         __attribute__((aligned(16))) uint32_t head[RCAP];
-        uint64_t red[kWaves];
+        uint64_t red[NW];
     };
     uint32_t keys[RCAP];
     uint16_t next[RCAP];
@@ -646,19 +646,19 @@ struct JoinLds<RCAP, kJoinWrite> {
     uint32_t cursor;
 };
 
-template <int RCAP, int MODE>
-__global__ __launch_bounds__(kBlock) void k_join(const uint64_t *__restrict__ R, const uint64_t *__restrict__ S,
+template <int RCAP, int MODE, int BLOCK = kBlock>
+__global__ __launch_bounds__(BLOCK) void k_join(const uint64_t *__restrict__ R, const uint64_t *__restrict__ S,
                                                  const uint64_t *__restrict__ r_start,
                                                  const uint64_t *__restrict__ r_count,
                                                  const uint64_t *__restrict__ s_start,
                                                  const uint64_t *__restrict__ s_count, uint64_t P,
                                                  const uint64_t *__restrict__ over,
-                                                 const uint32_t *__restrict__ n_over, uint32_t hash_shift,
+                                                 const uint32_t *__restrict__ n_over, uint32_t hash_shift, uint64_t s_chunk,
                                                  uint64_t *__restrict__ counts,
                                                  const uint64_t *__restrict__ task_off,
                                                  output_triple_t *__restrict__ out) {
-    constexpr int U = RCAP / kBlock;
-    __shared__ JoinLds<RCAP, MODE> L;
+    constexpr int U = RCAP / BLOCK, NW = BLOCK / kWave;
+    __shared__ JoinLds<RCAP, MODE, NW> L;
     const uint32_t tid = threadIdx.x, lane = __lane_id();
     const uint64_t T = P + *n_over;
     uint64_t matches = 0;
@@ -666,8 +666,8 @@ __global__ __launch_bounds__(kBlock) void k_join(const uint64_t *__restrict__ R,
         uint64_t p, chunk;
         decode_task(t, P, over, p, chunk);
         const uint64_t nR = r_count[p], nSp = s_count[p];
-        const uint64_t s_lo = chunk * kSChunk;
-        const uint64_t nS = (nR == 0 || s_lo >= nSp) ? 0 : min<uint64_t>(nSp - s_lo, kSChunk);
+        const uint64_t s_lo = chunk * s_chunk;
+        const uint64_t nS = (nR == 0 || s_lo >= nSp) ? 0 : min<uint64_t>(nSp - s_lo, s_chunk);
         uint64_t tmatch = 0;
         if constexpr (MODE == kJoinWrite) {
             if (tid == 0) L.cursor = 0;
@@ -683,15 +683,15 @@ __global__ __launch_bounds__(kBlock) void k_join(const uint64_t *__restrict__ R,
                 uint64_t kr[U];
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
-                    const uint32_t i = tid + u * kBlock;
+                    const uint32_t i = tid + u * BLOCK;
                     kr[u] = i < nrc ? ld_nt(rp + rc + i) : 0ull;
                 }
-                for (uint32_t i = tid; i < (N + 3) / 4; i += kBlock)
+                for (uint32_t i = tid; i < (N + 3) / 4; i += BLOCK)
                     reinterpret_cast<uint4 *>(L.head)[i] = make_uint4(0, 0, 0, 0);
                 __syncthreads();
 #pragma unroll
                 for (int u = 0; u < U; ++u) {  // BUILD-LOOP (:407-411)
-                    const uint32_t i = tid + u * kBlock;
+                    const uint32_t i = tid + u * BLOCK;
                     if (i < nrc) {
                         const uint32_t k = (uint32_t)kr[u];
                         L.keys[i] = k;
@@ -707,7 +707,7 @@ __global__ __launch_bounds__(kBlock) void k_join(const uint64_t *__restrict__ R,
                     if constexpr (MODE == kJoinWrite) {
 #pragma unroll
                         for (int u = 0; u < U; ++u) {
-                            const uint64_t i = s0 + tid + u * kBlock;
+                            const uint64_t i = s0 + tid + u * BLOCK;
                             const uint64_t x = i < nS ? ld_nt(sp + i) : 0ull;
                             ks[u] = (uint32_t)x;
                             sv[u] = (uint32_t)(x >> 32);
@@ -715,13 +715,13 @@ __global__ __launch_bounds__(kBlock) void k_join(const uint64_t *__restrict__ R,
                     } else {
 #pragma unroll
                         for (int u = 0; u < U; ++u) {
-                            const uint64_t i = s0 + tid + u * kBlock;
+                            const uint64_t i = s0 + tid + u * BLOCK;
                             ks[u] = i < nS ? __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(sp + i)) : 0u;
                         }
                     }
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
-                        const uint64_t i = s0 + tid + u * kBlock;
+                        const uint64_t i = s0 + tid + u * BLOCK;
                         cur[u] = i < nS ? L.head[(ks[u] >> hash_shift) & hmask] : 0u;
                     }
                     bool more = true;
@@ -776,7 +776,7 @@ __global__ __launch_bounds__(kBlock) void k_join(const uint64_t *__restrict__ R,
             __syncthreads();
             if (tid == 0) {
                 uint64_t acc = 0;
-                for (int w = 0; w < kWaves; ++w) acc += L.red[w];
+                for (int w = 0; w < NW; ++w) acc += L.red[w];
                 counts[t] = acc;
             }
             __syncthreads();
@@ -792,7 +792,7 @@ __global__ __launch_bounds__(kBlock) void k_join(const uint64_t *__restrict__ R,
         __syncthreads();
         if (tid == 0) {
             uint64_t acc = 0;
-            for (int w = 0; w < kWaves; ++w) acc += L.red[w];
+            for (int w = 0; w < NW; ++w) acc += L.red[w];
             counts[blockIdx.x] = acc;
         }
     }
@@ -825,7 +825,7 @@ __global__ __launch_bounds__(kBlock) void k_join_hist(const uint64_t *__restrict
                                                       const uint64_t *__restrict__ s_start,
                                                       const uint64_t *__restrict__ s_count, uint64_t P,
                                                       const uint64_t *__restrict__ over,
-                                                      const uint32_t *__restrict__ n_over, uint32_t hash_shift,
+                                                      const uint32_t *__restrict__ n_over, uint32_t hash_shift, uint64_t s_chunk,
                                                       uint64_t *__restrict__ counts,
                                                       const uint64_t *__restrict__ task_off,
                                                       output_triple_t *__restrict__ out) {
@@ -840,8 +840,8 @@ __global__ __launch_bounds__(kBlock) void k_join_hist(const uint64_t *__restrict
         uint64_t p, chunk;
         decode_task(t, P, over, p, chunk);
         const uint64_t nR = r_count[p], nSp = s_count[p];
-        const uint64_t s_lo = chunk * kSChunk;
-        const uint64_t nS = (nR == 0 || s_lo >= nSp) ? 0 : min<uint64_t>(nSp - s_lo, kSChunk);
+        const uint64_t s_lo = chunk * s_chunk;
+        const uint64_t nS = (nR == 0 || s_lo >= nSp) ? 0 : min<uint64_t>(nSp - s_lo, s_chunk);
         uint64_t tmatch = 0;
         if constexpr (MODE == kJoinWrite) {
             if (tid == 0) L.cursor = 0;
@@ -983,13 +983,14 @@ __global__ __launch_bounds__(kBlock) void k_join_hist(const uint64_t *__restrict
 
 hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, const uint64_t *r_count,
                        const uint64_t *s_start, const uint64_t *s_count, uint64_t P, const uint64_t *over,
-                       const uint32_t *n_over, uint32_t hash_shift, uint32_t rcap, uint32_t grid, int mode,
-                       int algo, uint64_t *counts, const uint64_t *task_off, output_triple_t *out, hipStream_t s) {
+                       const uint32_t *n_over, uint32_t hash_shift, uint32_t rcap, uint64_t s_chunk, uint32_t grid,
+                       int mode, int algo, uint64_t *counts, const uint64_t *task_off, output_triple_t *out,
+                       hipStream_t s) {
     const uint64_t *R64 = reinterpret_cast<const uint64_t *>(R);
     const uint64_t *S64 = reinterpret_cast<const uint64_t *>(S);
 #define JOIN_LAUNCH(K, RC, MD)                                                                             \
     hipLaunchKernelGGL((K<RC, MD>), dim3(grid), dim3(kBlock), 0, s, R64, S64, r_start, r_count, s_start,    \
-                       s_count, P, over, n_over, hash_shift, counts, task_off, out)
+                       s_count, P, over, n_over, hash_shift, s_chunk, counts, task_off, out)
 #define JOIN_MODES(K, RC)                                                    \
     case RC:                                                                 \
         if (mode == kJoinCount) JOIN_LAUNCH(K, RC, kJoinCount);              \
@@ -1004,6 +1005,13 @@ hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, 
             default:
                 return hipErrorInvalidValue;
         }
+    } else if (rcap == kBigRcap) {
+        // one 16,384-tuple chain table per 1,024-thread workgroup: all 160 KiB of LDS
+        // (plain counting only; the materialising table carries 4 B more per tuple)
+        if (mode != kJoinCount) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((k_join<kBigRcap, kJoinCount, kBigJoinBlock>), dim3(grid), dim3(kBigJoinBlock), 0, s, R64,
+                           S64, r_start, r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts,
+                           task_off, out);
     } else {
         switch (rcap) {
             JOIN_MODES(k_join, 2048)
@@ -1023,14 +1031,15 @@ hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, 
 __global__ __launch_bounds__(kBlock) void k_make_tasks(const uint64_t *__restrict__ r_count,
                                                        const uint64_t *__restrict__ s_count, uint64_t P,
                                                        uint64_t *__restrict__ over, uint32_t over_cap,
-                                                       uint32_t *__restrict__ n_over, uint64_t *__restrict__ max_rs) {
+                                                       uint32_t *__restrict__ n_over, uint64_t *__restrict__ max_rs,
+                                                       uint64_t s_chunk) {
     uint64_t mr = 0, ms = 0;  // largest partitions (diagnostics), folded into this pass over the counts
     for (uint64_t p = blockIdx.x * (uint64_t)kBlock + threadIdx.x; p < P; p += (uint64_t)gridDim.x * kBlock) {
         const uint64_t nS = s_count[p], nR = r_count[p];
         mr = nR > mr ? nR : mr;
         ms = nS > ms ? nS : ms;
-        if (nR == 0 || nS <= kSChunk) continue;
-        const uint32_t k = (uint32_t)((nS + kSChunk - 1) / kSChunk) - 1;
+        if (nR == 0 || nS <= s_chunk) continue;
+        const uint32_t k = (uint32_t)((nS + s_chunk - 1) / s_chunk) - 1;
         const uint32_t base = atomicAdd(n_over, k);
         for (uint32_t j = 0; j < k && base + j < over_cap; ++j) over[base + j] = p | ((uint64_t)(j + 1) << 32);
     }
@@ -1056,14 +1065,14 @@ __global__ __launch_bounds__(kBlock) void k_make_tasks(const uint64_t *__restric
 }
 
 hipError_t launch_make_tasks(const uint64_t *r_count, const uint64_t *s_count, uint64_t P, uint64_t *over,
-                             uint32_t over_cap, uint64_t *meta, hipStream_t s) {
+                             uint32_t over_cap, uint64_t *meta, uint64_t s_chunk, hipStream_t s) {
     hipError_t e = hipMemsetAsync(meta, 0, 3 * sizeof(uint64_t), s);
     if (e != hipSuccess) return e;
     uint32_t *n_over = reinterpret_cast<uint32_t *>(meta + 2);
     uint64_t blocks = (P + kBlock - 1) / kBlock;
     if (blocks > 1024) blocks = 1024;
     hipLaunchKernelGGL(k_make_tasks, dim3((uint32_t)blocks), dim3(kBlock), 0, s, r_count, s_count, P, over, over_cap,
-                       n_over, meta);
+                       n_over, meta, s_chunk);
     return hipGetLastError();
 }
 

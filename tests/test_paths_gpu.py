@@ -1,7 +1,9 @@
 """The development A/B switches select alternative kernel paths with identical results:
 SGXAMD_DIGIT_SIDE=0 (pass-2 histograms over the tuples instead of the digit side
-stream) and SGXAMD_SCAN_ONEPASS=0 (index / value / dictionary scans as bitvector pass +
-expand pass instead of the one-pass look-back selection).  Both switches are read
+stream), SGXAMD_BIG_JOIN=0 (R partitions above 8192 tuples in 8192-tuple chain tables
+instead of the 16,384-tuple counting table; the 5-bit plan below has 32,768-tuple
+partitions) and SGXAMD_SCAN_ONEPASS=0 (index / value / dictionary scans as bitvector
+pass + expand pass instead of the one-pass look-back selection).  Both switches are read
 once per process, so each setting runs in a child process against the oracle (the
 TPC-H selections ride along: they share the library's workspace)."""
 import os
@@ -20,7 +22,7 @@ import numpy as np
 import sgxamd, oracle
 R, S = sgxamd.reference_relations(1 << 20, 1 << 20, selectivity=50)
 exp, _ = oracle.rho_join(R, S, 2)
-for bits, passes in [(12, 2), (16, 2), (18, 2)]:
+for bits, passes in [(12, 2), (16, 2), (18, 2), (5, 1)]:
     got = sgxamd.rho_join(R, len(R), S, len(S), radix_bits=bits, passes=passes).matches
     assert got == exp, (bits, passes, got, exp)
 rng = np.random.default_rng(5)
@@ -48,8 +50,8 @@ print("paths ok")
 """
 
 
-@pytest.mark.parametrize("env", [{"SGXAMD_DIGIT_SIDE": "0", "SGXAMD_SCAN_ONEPASS": "0"},
-                                 {"SGXAMD_DIGIT_SIDE": "1", "SGXAMD_SCAN_ONEPASS": "1"}])
+@pytest.mark.parametrize("env", [{"SGXAMD_DIGIT_SIDE": "0", "SGXAMD_SCAN_ONEPASS": "0", "SGXAMD_BIG_JOIN": "0"},
+                                 {"SGXAMD_DIGIT_SIDE": "1", "SGXAMD_SCAN_ONEPASS": "1", "SGXAMD_BIG_JOIN": "1"}])
 def test_switch_paths_match_oracle(env):
     e = dict(os.environ, **env)
     e["PYTHONPATH"] = os.pathsep.join([os.path.join(PKG, "python"), os.path.join(ROOT, "oracle"),

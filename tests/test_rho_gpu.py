@@ -75,6 +75,27 @@ def test_random_with_duplicates(sgx, orc, gpu, seed, nR, nS, kmax):
         assert gpu_join(sgx, R, S, radix_bits=bits, passes=passes).matches == exp
 
 
+@pytest.mark.parametrize("bits,kmax", [(6, 1 << 22), (5, 2**32 - 1), (4, 1 << 19), (1, 1 << 12)])
+def test_big_table_partitions(sgx, orc, gpu, bits, kmax):
+    """Partitions above 8192 R tuples take the 16,384-tuple counting table (one
+    1,024-thread workgroup per CU, 32,768-tuple S chunks): |R| = 2^20 over 2^bits
+    partitions gives 16,384 (one table, ragged), 32,768 (two), 65,536 (four, duplicate
+    keys) and 2^19 (32 tables, long chains, 16 S chunks per partition) R tuples per
+    partition; the materialising join of the same plan keeps 8192-tuple chunks."""
+    rng = np.random.default_rng(bits)
+    nR, nS = 1 << 20, (1 << 20) + 777
+    R = rel(rng.integers(0, kmax + 1, nR, dtype=np.uint64).astype(np.uint32))
+    S = rel(rng.integers(0, kmax + 1, nS, dtype=np.uint64).astype(np.uint32))
+    exp = orc.count_join_sort(R, S)
+    passes = 1 if bits <= 8 else 2
+    res = gpu_join(sgx, R, S, radix_bits=bits, passes=passes)
+    assert res.matches == exp
+    assert res.stats["max_part_r"] > 8192
+    if bits == 6:
+        got = gpu_triples(sgx, R, S, radix_bits=bits, passes=passes)
+        assert np.array_equal(sorted_triples(got), sorted_triples(orc.rho_join_triples(R, S, 4)))
+
+
 def test_extreme_keys(sgx, orc, gpu):
     # 0 and 0xFFFFFFFF (the LDS empty marker) must join like any other key
     keys = np.array([0, 0xFFFFFFFF, 0xFFFFFFFF, 1, 0x80000000, 0xFFFFFFFE] * 50, dtype=np.uint32)
@@ -155,16 +176,19 @@ def test_full_size_config2_property(sgx, gpu):
     sgx.gen_fk_dev(S, n, 0, n, 22222)
     res = sgx.rho_join(R, n, S, n)
     assert res.matches == n
-    assert res.stats["radix_bits"] == 16 and res.stats["passes"] == 2
+    # 2^14 partitions of 16,384 R tuples (7 + 7 bits), one 16,384-tuple table each
+    assert res.stats["radix_bits"] == 14 and res.stats["passes"] == 2
     del R, S
     torch.cuda.empty_cache()
 
 
 def test_max_size_pk_fk(sgx, gpu):
     """|R| = |S| = 2^31 + 12,345 (ragged, 8x the headline size, 17 GB per relation):
-    the planner goes past 16 radix bits, so the pass-2 digit no longer fits the side
-    stream and the tuple-histogram path runs at scale; matches == |S|, and with foreign
-    keys drawn from [1, 1.5 |R|] exactly the ones that fall inside R's key range."""
+    the planner goes past 16 radix bits (17: average partitions of 16,384 R tuples in
+    the big counting table); an explicit 18-bit plan runs the 9-bit pass-2 digit,
+    which does not fit the side stream, through the tuple histogram at scale.
+    matches == |S|, and with foreign keys drawn from [1, 1.5 |R|] exactly the ones that
+    fall inside R's key range."""
     import torch
 
     n = (1 << 31) + 12_345
@@ -174,7 +198,8 @@ def test_max_size_pk_fk(sgx, gpu):
     sgx.gen_fk_dev(S, n, 0, n, 22222)
     res = sgx.rho_join(R, n, S, n)
     assert res.matches == n
-    assert res.stats["passes"] == 2 and res.stats["radix_bits"] > 16
+    assert res.stats["passes"] == 2 and res.stats["radix_bits"] == 17
+    assert sgx.rho_join(R, n, S, n, radix_bits=18, passes=2).matches == n
     sgx.gen_fk_dev(S, n, 0, n + n // 2, 33333)
     m = sgx.rho_join(R, n, S, n).matches
     assert m == int(((S & 0xFFFFFFFF) <= n).sum()) and n // 2 < m < n
