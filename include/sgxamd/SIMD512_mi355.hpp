@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstdlib>
 
+#include "sgxamd/rho.h"
 #include "sgxamd/scan.h"
 
 extern "C" const char *mi355_last_error(void);
@@ -58,20 +59,62 @@ inline void implicit_index_scan(pred_t lo, pred_t hi, const void *input_compress
                   "implicit_index_scan");
 }
 
-// SIMD512.cpp:251-287; grows the vector as needed, trims it to the match count when cut.
+// SIMD512.cpp:152-208.  index_compressed is the reference's __m512i array of 8 u64 lanes
+// per vector; every 8-row sub-block j of 64-row block i gathers from vector i + j, as the
+// reference does (read as written).  The reference reads only vectors of sub-blocks with a
+// match and has no bound to check; this adapter passes the largest array any row can
+// reach, 8 * (input_size / 64 + 7) u64 — a caller's array must be that long.
+inline void explicit_index_scan(pred_t lo, pred_t hi, const void *index_compressed, const void *input_compressed,
+                                size_t input_size, size_t *output_buffer) {
+    uint64_t n = 0;
+    const size_t m = detail::whole(input_size);
+    detail::check(mi355_scan_explicit_index_u8(lo, hi, static_cast<const uint64_t *>(index_compressed),
+                                               m ? 8 * (m / 64 + 7) : 0, static_cast<const uint8_t *>(input_compressed),
+                                               m, reinterpret_cast<uint64_t *>(output_buffer), m, &n),
+                  "explicit_index_scan");
+}
+
+namespace detail {
+// Size the reference's vector ends with (SIMD512.cpp:262-266): before each 64-row block
+// it grows once, to (64 + size) * 3, when matches-so-far + 64 exceed the size; the last
+// check happens before the last block, with the matches of all blocks before it.
+inline size_t self_alloc_size(size_t size, size_t blocks, size_t matches_before_last) {
+    if (blocks == 0) return size;
+    while (matches_before_last + 64 > size) size = (64 + size) * 3;
+    return size;
+}
+}  // namespace detail
+
+// SIMD512.cpp:251-287, in one pass over the column: the scan runs straight into the
+// vector; only if it held fewer slots than matches (MI355_ERR_CAPACITY reports how many)
+// is the vector grown and the scan repeated.  The vector then takes the size the
+// reference's growth rule gives, or the match count when cut.
 template <typename Vec>
 inline void implicit_index_scan_self_alloc(pred_t lo, pred_t hi, const void *input_compressed, size_t input_size,
                                            Vec &output_buffer, bool cut = false) {
     const size_t m = detail::whole(input_size);
-    uint64_t c = 0;
-    detail::check(mi355_scan_count_u8(lo, hi, static_cast<const uint8_t *>(input_compressed), m, &c),
-                  "implicit_index_scan_self_alloc");
-    if (output_buffer.size() < c) output_buffer.resize(c);
+    const auto *in = static_cast<const uint8_t *>(input_compressed);
+    const size_t size0 = output_buffer.size();
     uint64_t n = 0;
-    detail::check(mi355_scan_index_u8(lo, hi, static_cast<const uint8_t *>(input_compressed), m,
-                                      reinterpret_cast<uint64_t *>(output_buffer.data()), output_buffer.size(), &n),
-                  "implicit_index_scan_self_alloc");
-    if (cut) output_buffer.resize(n);
+    int rc = mi355_scan_index_u8(lo, hi, in, m, reinterpret_cast<uint64_t *>(output_buffer.data()),
+                                 output_buffer.size(), &n);
+    if (rc == MI355_ERR_CAPACITY) {
+        output_buffer.resize(detail::self_alloc_size(output_buffer.size(), m / 64, n));
+        rc = mi355_scan_index_u8(lo, hi, in, m, reinterpret_cast<uint64_t *>(output_buffer.data()),
+                                 output_buffer.size(), &n);
+    }
+    detail::check(rc, "implicit_index_scan_self_alloc");
+    if (cut) {
+        output_buffer.resize(n);
+        return;
+    }
+    // matches before the last 64-row block: the indexes are ascending
+    size_t before_last = n;
+    const uint64_t last_row0 = m >= 64 ? m - 64 : 0;
+    const auto *ix = reinterpret_cast<const uint64_t *>(output_buffer.data());
+    while (before_last > 0 && ix[before_last - 1] >= last_row0) --before_last;
+    const size_t final_size = detail::self_alloc_size(size0, m / 64, before_last);
+    if (final_size != output_buffer.size()) output_buffer.resize(final_size);
 }
 
 // SIMD512.cpp:91-150: matching codes zero-extended to uint32; returns the match count.

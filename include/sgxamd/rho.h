@@ -69,6 +69,15 @@ typedef struct mi355_rho_stats {
     double ms_pass2;
     double ms_join;           /* build + probe ("Build+Join Overall"), device time */
     double ms_total;          /* partition + join, device time */
+    /* the reference's finer phase timers (radix_timers_t, radix_join.cpp:94-107) */
+    double ms_pass1_r;        /* pass 1 of R ("Partition R") */
+    double ms_pass1_s;        /* pass 1 of S ("Partition S") */
+    double ms_pass1_hist;     /* pass-1 histograms + prefix sums, R and S ("One Hist") */
+    double ms_pass1_copy;     /* pass-1 scatters, R and S ("One Copy") */
+    double ms_pass2_hist;     /* "Two Hist" */
+    double ms_pass2_copy;     /* "Two Copy" */
+    double ms_build;          /* "Build": ms_join split by the build/probe wall-clock ticks the */
+    double ms_probe;          /* "Join":   fused build+probe kernel measures per workgroup */
 } mi355_rho_stats;
 
 /* Number of gfx950 devices visible (0 on a CPU-only host). */

@@ -7,6 +7,7 @@
  *   count                          SIMD512.cpp:7-32    -> mi355_scan_count_*
  *   bitvector_scan                 SIMD512.cpp:210-222 -> mi355_scan_bitvector_*
  *   implicit_index_scan(_self_alloc) SIMD512.cpp:225-287 -> mi355_scan_index_*
+ *   explicit_index_scan            SIMD512.cpp:152-208 -> mi355_scan_explicit_index_u8
  *   scan (value materialisation)   SIMD512.cpp:91-150  -> mi355_scan_values_*
  *   sum                            SIMD512.cpp:34-88   -> mi355_scan_sum_u8
  *   dict_scan_8bit_64bit           SIMD512.cpp:289-338 -> mi355_dict_scan_8bit_64bit
@@ -48,6 +49,16 @@ int mi355_scan_index_u8(uint8_t lo, uint8_t hi, const uint8_t *in, size_t n,
                         uint64_t *out, size_t cap, uint64_t *n_out);
 int mi355_scan_index_i32(int32_t lo, int32_t hi, const int32_t *in, size_t n,
                          uint64_t *out, size_t cap, uint64_t *n_out);
+
+/* SIMD512::explicit_index_scan (SIMD512.cpp:152-208, SIMD512.hpp:60-65): like the index
+ * scan, but each match of row r emits the u64 entry index[8*(r/64 + (r%64)/8) + r%8] of a
+ * caller-supplied index array (index_len entries, host or device) — the reference's
+ * index_compressed[i + j] for 64-row block i and 8-row sub-block j, restated as written.
+ * A caller covering every row allocates 8*((n-1)/64 + 7) + 8 entries; a match whose
+ * entry lies past index_len fails with MI355_ERR_INVALID.  cap / n_out / CAPACITY as
+ * for mi355_scan_index_u8. */
+int mi355_scan_explicit_index_u8(uint8_t lo, uint8_t hi, const uint64_t *index, size_t index_len,
+                                 const uint8_t *in, size_t n, uint64_t *out, size_t cap, uint64_t *n_out);
 
 /* Matching values in row order: u8 codes zero-extended to uint32 (SIMD512::scan),
  * i32 values as int32. */

@@ -79,6 +79,10 @@ void oracle_scan_bitvector_u8(uint8_t lo, uint8_t hi, const uint8_t *in, size_t 
 void oracle_scan_bitvector_i32(int32_t lo, int32_t hi, const int32_t *in, size_t n, uint64_t *out);
 uint64_t oracle_scan_index_u8(uint8_t lo, uint8_t hi, const uint8_t *in, size_t n, uint64_t *out);
 uint64_t oracle_scan_index_i32(int32_t lo, int32_t hi, const int32_t *in, size_t n, uint64_t *out);
+/* SIMD512::explicit_index_scan (SIMD512.cpp:152-208): row r takes
+ * index[8*(r/64 + (r%64)/8) + r%8] (the reference's index_compressed[i + j]). */
+uint64_t oracle_scan_explicit_index_u8(uint8_t lo, uint8_t hi, const uint64_t *index, const uint8_t *in, size_t n,
+                                       uint64_t *out);
 uint64_t oracle_scan_values_u8(uint8_t lo, uint8_t hi, const uint8_t *in, size_t n, uint32_t *out);
 uint64_t oracle_scan_values_i32(int32_t lo, int32_t hi, const int32_t *in, size_t n, int32_t *out);
 /* Multithreaded count for the CPU baseline (contiguous slices, like scan_wrapper). */

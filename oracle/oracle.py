@@ -50,6 +50,7 @@ def _load() -> C.CDLL:
         "oracle_scan_index_u8": (C.c_uint64, [C.c_uint8, C.c_uint8, P, C.c_size_t, P]),
         "oracle_scan_index_i32": (C.c_uint64, [C.c_int32, C.c_int32, P, C.c_size_t, P]),
         "oracle_scan_values_u8": (C.c_uint64, [C.c_uint8, C.c_uint8, P, C.c_size_t, P]),
+        "oracle_scan_explicit_index_u8": (C.c_uint64, [C.c_uint8, C.c_uint8, P, P, C.c_size_t, P]),
         "oracle_scan_values_i32": (C.c_uint64, [C.c_int32, C.c_int32, P, C.c_size_t, P]),
         "oracle_scan_count_i32_mt": (C.c_uint64, [C.c_int32, C.c_int32, P, C.c_size_t, C.c_int]),
         "oracle_scan_sum_u8": (C.c_uint64, [C.c_uint8, C.c_uint8, P, C.c_size_t]),
@@ -147,6 +148,20 @@ def scan(kind: str, dtype: str, lo: int, hi: int, col):
     out = np.empty(max(n, 1), dtype=np.uint32 if dtype == "u8" else np.int32)
     k = fn(lo, hi, _p(col), n, _p(out))
     return out[:k]
+
+
+def explicit_index_scan(lo: int, hi: int, index, col):
+    """SIMD512::explicit_index_scan restated: uint64 index entries of the matching u8 rows."""
+    idx = np.ascontiguousarray(index, dtype=np.uint64)
+    c = np.ascontiguousarray(col, dtype=np.uint8)
+    out = np.empty(max(len(c), 1), dtype=np.uint64)
+    k = lib.oracle_scan_explicit_index_u8(lo, hi, _p(idx), _p(c), len(c), _p(out))
+    return out[:k]
+
+
+def explicit_index_len(n: int) -> int:
+    """Index entries row n-1 can reach (8*((n-1)/64 + 7) + 8): what a caller allocates."""
+    return 0 if n == 0 else 8 * ((n - 1) // 64 + 7) + 8
 
 
 def scan_count_mt(lo: int, hi: int, col, nthreads: int) -> int:

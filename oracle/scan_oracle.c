@@ -151,3 +151,19 @@ uint64_t oracle_dict_scan(int64_t lo, int64_t hi, const int64_t *dict, uint64_t 
     }
     return k;
 }
+
+/* SIMD512::explicit_index_scan (SIMD512.cpp:152-208), restated as written: for the
+ * 64-row block i and its 8-row sub-block j (rows 64i+8j .. 64i+8j+7), the matching
+ * rows' entries are compress-stored from the 8 u64 lanes of index_compressed[i + j]
+ * (:174, :198) — the vector index is block + sub-block, not 8·block + sub-block — so
+ * row r takes index[8·(r/64 + (r%64)/8) + r%8].  Both of the reference's branches
+ * (lo == hi via cmpeq, else cmpge & cmple) select the same rows.  The reference only
+ * reads index vectors of sub-blocks with a match; so does this loop.  Scans all n
+ * rows (the AVX-512 loop drops the n % 64 tail: callers that want it round down). */
+uint64_t oracle_scan_explicit_index_u8(uint8_t lo, uint8_t hi, const uint64_t *index, const uint8_t *in, size_t n,
+                                       uint64_t *out) {
+    uint64_t k = 0;
+    for (size_t r = 0; r < n; r++)
+        if (PRED(in[r])) out[k++] = index[8 * (r / 64 + (r % 64) / 8) + r % 8];
+    return k;
+}

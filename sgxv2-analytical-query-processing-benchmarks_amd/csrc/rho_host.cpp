@@ -232,7 +232,7 @@ struct PendingJoin {
     hipStream_t s2 = nullptr;
     const row_t *fR = nullptr;
     const uint64_t *psR = nullptr, *pcR = nullptr;
-    size_t off_over = 0, off_counts = 0, off_toff = 0, off_result = 0;
+    size_t off_over = 0, off_counts = 0, off_toff = 0, off_result = 0, off_cyc = 0;
     uint32_t over_cap = 0, join_grid = 0;
     uint64_t s_chunk = kSChunk;  // S tuples per build/probe task
 };
@@ -296,8 +296,9 @@ int join_begin(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, uint64
     pj.off_counts = A.reserve(sizeof(uint64_t) * (pj.materialize ? P + pj.over_cap : pj.join_grid));
     pj.off_toff = A.reserve(sizeof(uint64_t) * (pj.materialize ? P + pj.over_cap : 1));
     // result[0] = matches, [1] / [2] = largest R / S partition, [3] = extra S-chunk tasks
-    // (u32): one zeroing and one read-back for all four
-    pj.off_result = A.reserve(sizeof(uint64_t) * 4);
+    // (u32), [4] / [5] = build / probe ticks: one read-back for all six
+    pj.off_result = A.reserve(sizeof(uint64_t) * 6);
+    pj.off_cyc = A.reserve(sizeof(uint64_t) * 2 * pj.join_grid);
     RHO_HIP(A.buf.ensure(A.used));
 
     // R's and S's partition chains are independent: with overlap on, S's runs on the
@@ -367,6 +368,7 @@ int join_finish(Context *ctx, PendingJoin &pj, const row_t *dS, uint64_t nS, mi3
     uint64_t *counts = A.at<uint64_t>(pj.off_counts);
     uint64_t *task_off = A.at<uint64_t>(pj.off_toff);
     uint64_t *result = A.at<uint64_t>(pj.off_result);
+    uint64_t *cyc = A.at<uint64_t>(pj.off_cyc);
     uint32_t *n_over = reinterpret_cast<uint32_t *>(result + 3);
     const uint32_t hash_shift = pj.key_shift + pol.bits;
     tm.mark("join_tasks");
@@ -374,13 +376,13 @@ int join_finish(Context *ctx, PendingJoin &pj, const row_t *dS, uint64_t nS, mi3
     if (!pj.materialize) {
         tm.mark("join_build_probe");
         RHO_HIP(launch_join(fR, fS, psR, pcR, psS, pcS, P, over, n_over, hash_shift, pol.rcap, pj.s_chunk, join_grid,
-                            kJoinCount, algo, counts, nullptr, nullptr, s));
+                            kJoinCount, algo, counts, nullptr, nullptr, cyc, s));
         tm.mark("join_reduce");
-        RHO_HIP(launch_reduce(counts, join_grid, result, s));
+        RHO_HIP(launch_reduce(counts, join_grid, result, cyc, join_grid, s));
     } else {
         tm.mark("join_build_probe");
         RHO_HIP(launch_join(fR, fS, psR, pcR, psS, pcS, P, over, n_over, hash_shift, pol.rcap, pj.s_chunk, join_grid,
-                            kJoinTaskCount, algo, counts, nullptr, nullptr, s));
+                            kJoinTaskCount, algo, counts, nullptr, nullptr, cyc, s));
         tm.mark("join_offsets");
         RHO_HIP(launch_excl_scan(counts, n_over, P, task_off, result, s));
         RHO_HIP(hipMemcpyAsync(ctx->host_result, result, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
@@ -400,11 +402,13 @@ int join_finish(Context *ctx, PendingJoin &pj, const row_t *dS, uint64_t nS, mi3
         }
         tm.mark("join_materialize");
         RHO_HIP(launch_join(fR, fS, psR, pcR, psS, pcS, P, over, n_over, hash_shift, pol.rcap, pj.s_chunk, join_grid,
-                            kJoinWrite, algo, counts, task_off, out, s));
+                            kJoinWrite, algo, counts, task_off, out, nullptr, s));
+        tm.mark("join_reduce");
+        RHO_HIP(launch_reduce(nullptr, 0, result, cyc, join_grid, s));  // ticks of the count pass
     }
     tm.end_call();
     if (s2) RHO_HIP(hipEventRecord(ctx->ev_t1, s));
-    RHO_HIP(hipMemcpyAsync(ctx->host_result, result, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    RHO_HIP(hipMemcpyAsync(ctx->host_result, result, 6 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     RHO_HIP(hipStreamSynchronize(s));
     tm.collect();
     float wall = -1.f;
@@ -430,6 +434,20 @@ int join_finish(Context *ctx, PendingJoin &pj, const row_t *dS, uint64_t nS, mi3
         st->ms_join = tm.ms_of_prefix("join_");
         // with two streams the phase spans overlap: the total is the wall span
         st->ms_total = wall >= 0.f ? (double)wall : st->ms_partition + st->ms_join;
+        st->ms_pass1_r = tm.ms_of_prefix("R_pass1");
+        st->ms_pass1_s = tm.ms_of_prefix("S_pass1");
+        st->ms_pass1_hist = tm.ms_of_prefix("R_pass1_hist") + tm.ms_of_prefix("R_pass1_scan") +
+                            tm.ms_of_prefix("S_pass1_hist") + tm.ms_of_prefix("S_pass1_scan");
+        st->ms_pass1_copy = tm.ms_of_prefix("R_pass1_scatter") + tm.ms_of_prefix("S_pass1_scatter");
+        st->ms_pass2_hist = tm.ms_of_prefix("R_pass2_hist") + tm.ms_of_prefix("R_pass2_scan") +
+                            tm.ms_of_prefix("S_pass2_hist") + tm.ms_of_prefix("S_pass2_scan");
+        st->ms_pass2_copy = tm.ms_of_prefix("R_pass2_scatter") + tm.ms_of_prefix("S_pass2_scatter");
+        // the build/probe kernel is one launch: its time is split by the ticks its
+        // workgroups spent building and probing
+        const double b = (double)ctx->host_result[4], pr = (double)ctx->host_result[5];
+        const double bp = tm.ms_of_prefix("join_build_probe") + tm.ms_of_prefix("join_materialize");
+        st->ms_build = b + pr > 0 ? bp * b / (b + pr) : 0.0;
+        st->ms_probe = bp - st->ms_build;
     }
     return MI355_OK;
 }

@@ -77,6 +77,9 @@ hipError_t launch_scatter(const row_t *in, row_t *out, const SegMap &m, uint32_t
 // mode 0: counts[blockIdx] = per-workgroup partial count (grid entries);
 // mode 1: counts[t] = per-task count (P + *n_over entries);
 // mode 2: write every match to out[task_off[t] + ...] as output_triple_t.
+// cyc (nullable): per workgroup, the wall-clock ticks spent building and probing
+// (cyc[2g], cyc[2g+1]); they split the fused kernel's time into the reference's
+// Build / Join phases (radix_join.cpp:1291-1352 build_in_depth / join_in_depth timers).
 constexpr uint64_t kSChunk = 8192;
 // Counting joins of partitions above 8192 R tuples: a 16,384-tuple chain table per
 // 1,024-thread workgroup (160 KiB of LDS) and 32,768-tuple S chunks, so that neither
@@ -95,12 +98,15 @@ hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, 
                        const uint64_t *s_start, const uint64_t *s_count, uint64_t P, const uint64_t *over,
                        const uint32_t *n_over, uint32_t hash_shift, uint32_t rcap, uint64_t s_chunk, uint32_t grid,
                        int mode, int algo, uint64_t *counts, const uint64_t *task_off, output_triple_t *out,
-                       hipStream_t s);
+                       uint64_t *cyc, hipStream_t s);
 // One-block exclusive scan of n_base + *n_extra values; *total = their sum.
 hipError_t launch_excl_scan(const uint64_t *in, const uint32_t *n_extra, uint64_t n_base, uint64_t *out,
                             uint64_t *total, hipStream_t s);
 
-hipError_t launch_reduce(const uint64_t *partials, uint32_t n, uint64_t *result, hipStream_t s);
+// result[0] = sum of the n partials (skipped when partials is null); cyc (nullable, two
+// u64 per join workgroup: build / probe wall-clock ticks) -> result[4] / result[5].
+hipError_t launch_reduce(const uint64_t *partials, uint32_t n, uint64_t *result, const uint64_t *cyc, uint32_t ncyc,
+                         hipStream_t s);
 
 }  // namespace rho
 }  // namespace sgxamd

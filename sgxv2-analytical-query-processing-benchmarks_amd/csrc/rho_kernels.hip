@@ -656,12 +656,13 @@ __global__ __launch_bounds__(BLOCK) void k_join(const uint64_t *__restrict__ R, 
                                                  const uint32_t *__restrict__ n_over, uint32_t hash_shift, uint64_t s_chunk,
                                                  uint64_t *__restrict__ counts,
                                                  const uint64_t *__restrict__ task_off,
-                                                 output_triple_t *__restrict__ out) {
+                                                 output_triple_t *__restrict__ out, uint64_t *__restrict__ cyc) {
     constexpr int U = RCAP / BLOCK, NW = BLOCK / kWave;
     __shared__ JoinLds<RCAP, MODE, NW> L;
     const uint32_t tid = threadIdx.x, lane = __lane_id();
     const uint64_t T = P + *n_over;
     uint64_t matches = 0;
+    uint64_t bcyc = 0, pcyc = 0;  // build / probe wall-clock ticks of this workgroup
     for (uint64_t t = blockIdx.x; t < T; t += gridDim.x) {
         uint64_t p, chunk;
         decode_task(t, P, over, p, chunk);
@@ -676,6 +677,7 @@ __global__ __launch_bounds__(BLOCK) void k_join(const uint64_t *__restrict__ R, 
             const uint64_t *rp = R + r_start[p];
             const uint64_t *sp = S + s_start[p] + s_lo;
             for (uint64_t rc = 0; rc < nR; rc += RCAP) {
+                const uint64_t c_build = wall_clock64();
                 const uint32_t nrc = (uint32_t)((nR - rc) < RCAP ? (nR - rc) : RCAP);
                 uint32_t N = 1;
                 while (N < nrc) N <<= 1;  // NEXT_POW_2(numR)
@@ -701,6 +703,8 @@ __global__ __launch_bounds__(BLOCK) void k_join(const uint64_t *__restrict__ R, 
                     }
                 }
                 __syncthreads();
+                const uint64_t c_probe = wall_clock64();
+                bcyc += c_probe - c_build;
                 for (uint64_t s0 = 0; s0 < nS; s0 += RCAP) {  // PROBE-LOOP (:429-436)
                     uint32_t ks[U], cur[U];
                     uint32_t sv[MODE == kJoinWrite ? U : 1];
@@ -767,6 +771,7 @@ __global__ __launch_bounds__(BLOCK) void k_join(const uint64_t *__restrict__ R, 
                     }
                 }
                 __syncthreads();
+                pcyc += wall_clock64() - c_probe;
             }
         }
         if constexpr (MODE == kJoinTaskCount) {
@@ -795,6 +800,10 @@ __global__ __launch_bounds__(BLOCK) void k_join(const uint64_t *__restrict__ R, 
             for (int w = 0; w < NW; ++w) acc += L.red[w];
             counts[blockIdx.x] = acc;
         }
+    }
+    if (cyc && tid == 0) {
+        cyc[2 * blockIdx.x] = bcyc;
+        cyc[2 * blockIdx.x + 1] = pcyc;
     }
 }
 
@@ -828,7 +837,7 @@ __global__ __launch_bounds__(kBlock) void k_join_hist(const uint64_t *__restrict
                                                       const uint32_t *__restrict__ n_over, uint32_t hash_shift, uint64_t s_chunk,
                                                       uint64_t *__restrict__ counts,
                                                       const uint64_t *__restrict__ task_off,
-                                                      output_triple_t *__restrict__ out) {
+                                                      output_triple_t *__restrict__ out, uint64_t *__restrict__ cyc) {
     constexpr int U = RCAP / kBlock;
     constexpr int NB = HistJoinLds<RCAP, MODE>::NB;
     __shared__ HistJoinLds<RCAP, MODE> L;
@@ -836,6 +845,7 @@ __global__ __launch_bounds__(kBlock) void k_join_hist(const uint64_t *__restrict
     const uint32_t tid = threadIdx.x, lane = __lane_id();
     const uint64_t T = P + *n_over;
     uint64_t matches = 0;
+    uint64_t bcyc = 0, pcyc = 0;  // build / probe wall-clock ticks of this workgroup
     for (uint64_t t = blockIdx.x; t < T; t += gridDim.x) {
         uint64_t p, chunk;
         decode_task(t, P, over, p, chunk);
@@ -850,6 +860,7 @@ __global__ __launch_bounds__(kBlock) void k_join_hist(const uint64_t *__restrict
             const uint64_t *rp = R + r_start[p];
             const uint64_t *sp = S + s_start[p] + s_lo;
             for (uint64_t rc = 0; rc < nR; rc += RCAP) {
+                const uint64_t c_build = wall_clock64();
                 const uint32_t nrc = (uint32_t)((nR - rc) < RCAP ? (nR - rc) : RCAP);
                 uint32_t N = 1;
                 while (N < nrc) N <<= 1;
@@ -900,6 +911,8 @@ __global__ __launch_bounds__(kBlock) void k_join_hist(const uint64_t *__restrict
                     }
                 }
                 __syncthreads();
+                const uint64_t c_probe = wall_clock64();
+                bcyc += c_probe - c_build;
                 for (uint64_t s0 = 0; s0 < nS; s0 += RCAP) {  // PROBE PHASE (:570-600)
                     uint32_t ks[U], j[U], end[U];
                     uint32_t sv[MODE == kJoinWrite ? U : 1];
@@ -952,6 +965,7 @@ __global__ __launch_bounds__(kBlock) void k_join_hist(const uint64_t *__restrict
                     }
                 }
                 __syncthreads();
+                pcyc += wall_clock64() - c_probe;
             }
         }
         if constexpr (MODE == kJoinTaskCount) {
@@ -979,18 +993,22 @@ __global__ __launch_bounds__(kBlock) void k_join_hist(const uint64_t *__restrict
             counts[blockIdx.x] = acc;
         }
     }
+    if (cyc && tid == 0) {
+        cyc[2 * blockIdx.x] = bcyc;
+        cyc[2 * blockIdx.x + 1] = pcyc;
+    }
 }
 
 hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, const uint64_t *r_count,
                        const uint64_t *s_start, const uint64_t *s_count, uint64_t P, const uint64_t *over,
                        const uint32_t *n_over, uint32_t hash_shift, uint32_t rcap, uint64_t s_chunk, uint32_t grid,
                        int mode, int algo, uint64_t *counts, const uint64_t *task_off, output_triple_t *out,
-                       hipStream_t s) {
+                       uint64_t *cyc, hipStream_t s) {
     const uint64_t *R64 = reinterpret_cast<const uint64_t *>(R);
     const uint64_t *S64 = reinterpret_cast<const uint64_t *>(S);
 #define JOIN_LAUNCH(K, RC, MD)                                                                             \
     hipLaunchKernelGGL((K<RC, MD>), dim3(grid), dim3(kBlock), 0, s, R64, S64, r_start, r_count, s_start,    \
-                       s_count, P, over, n_over, hash_shift, s_chunk, counts, task_off, out)
+                       s_count, P, over, n_over, hash_shift, s_chunk, counts, task_off, out, cyc)
 #define JOIN_MODES(K, RC)                                                    \
     case RC:                                                                 \
         if (mode == kJoinCount) JOIN_LAUNCH(K, RC, kJoinCount);              \
@@ -1011,7 +1029,7 @@ hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, 
         if (mode != kJoinCount) return hipErrorInvalidValue;
         hipLaunchKernelGGL((k_join<kBigRcap, kJoinCount, kBigJoinBlock>), dim3(grid), dim3(kBigJoinBlock), 0, s, R64,
                            S64, r_start, r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts,
-                           task_off, out);
+                           task_off, out, cyc);
     } else {
         switch (rcap) {
             JOIN_MODES(k_join, 2048)
@@ -1101,23 +1119,40 @@ hipError_t launch_excl_scan(const uint64_t *in, const uint32_t *n_extra, uint64_
 }
 
 // ---------------------------------------------------------------- reduce ---
+// out[0] = sum of the n partial counts (skipped when v is null); with cyc: out[4] /
+// out[5] = the build / probe ticks summed over the ncyc join workgroups.
 __global__ __launch_bounds__(kBlock) void k_reduce(const uint64_t *__restrict__ v, uint32_t n,
-                                                   uint64_t *__restrict__ out) {
-    __shared__ uint64_t red[kWaves];
-    uint64_t acc = 0;
-    for (uint32_t i = threadIdx.x; i < n; i += kBlock) acc += v[i];
+                                                   uint64_t *__restrict__ out, const uint64_t *__restrict__ cyc,
+                                                   uint32_t ncyc) {
+    __shared__ uint64_t red[3][kWaves];
+    uint64_t acc = 0, b = 0, p = 0;
+    if (v)
+        for (uint32_t i = threadIdx.x; i < n; i += kBlock) acc += v[i];
+    if (cyc)
+        for (uint32_t i = threadIdx.x; i < ncyc; i += kBlock) {
+            b += cyc[2 * i];
+            p += cyc[2 * i + 1];
+        }
     acc = wave_sum_u64(acc);
-    if (__lane_id() == 0) red[threadIdx.x / kWave] = acc;
+    b = wave_sum_u64(b);
+    p = wave_sum_u64(p);
+    if (__lane_id() == 0) {
+        red[0][threadIdx.x / kWave] = acc;
+        red[1][threadIdx.x / kWave] = b;
+        red[2][threadIdx.x / kWave] = p;
+    }
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (threadIdx.x < 3) {
         uint64_t t = 0;
-        for (int w = 0; w < kWaves; ++w) t += red[w];
-        *out = t;
+        for (int w = 0; w < kWaves; ++w) t += red[threadIdx.x][w];
+        if (threadIdx.x == 0 && v) out[0] = t;
+        if (threadIdx.x > 0 && cyc) out[3 + threadIdx.x] = t;
     }
 }
 
-hipError_t launch_reduce(const uint64_t *partials, uint32_t n, uint64_t *result, hipStream_t s) {
-    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kBlock), 0, s, partials, n, result);
+hipError_t launch_reduce(const uint64_t *partials, uint32_t n, uint64_t *result, const uint64_t *cyc, uint32_t ncyc,
+                         hipStream_t s) {
+    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kBlock), 0, s, partials, n, result, cyc, ncyc);
     return hipGetLastError();
 }
 

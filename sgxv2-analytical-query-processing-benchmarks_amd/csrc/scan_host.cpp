@@ -8,6 +8,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <type_traits>
 
 #include "common.hpp"
 #include "runtime.hpp"
@@ -39,7 +40,7 @@ Geometry geometry(uint64_t n) {
     return {rpc, (uint32_t)((n + rpc - 1) / rpc)};
 }
 
-enum class Op { kCount, kBitvector, kIndex, kValues };
+enum class Op { kCount, kBitvector, kIndex, kValues, kExplicit };
 
 // Device-resident, 16-byte aligned view of the input column.
 template <typename T>
@@ -59,8 +60,11 @@ int stage_input(Context *ctx, hipStream_t s, const T *in, size_t n, const T **de
     return MI355_OK;
 }
 
+// kExplicit: SIMD512::explicit_index_scan, the outputs are entries of the index array
+// `aux` (aux_len u64 entries, host or device) instead of row numbers.
 template <typename T, typename OutT>
-int run(Op op, T lo, T hi, const T *in, size_t n, void *out, size_t cap, uint64_t *result) {
+int run(Op op, T lo, T hi, const T *in, size_t n, void *out, size_t cap, uint64_t *result,
+        const uint64_t *aux = nullptr, uint64_t aux_len = 0) {
     int status = MI355_OK;
     Context *ctx = current_context(&status);
     if (!ctx) return status;
@@ -74,13 +78,20 @@ int run(Op op, T lo, T hi, const T *in, size_t n, void *out, size_t cap, uint64_
     if (rc) return rc;
     const Geometry g = geometry(n);
     const uint64_t nwords = (n + 63) / 64;
+    const int64_t *daux = reinterpret_cast<const int64_t *>(aux);
+    if (op == Op::kExplicit && aux_len && !is_device_pointer(aux)) {
+        SCAN_HIP(ctx->scan_dict.ensure(aux_len * sizeof(uint64_t)));
+        SCAN_HIP(hipMemcpyAsync(ctx->scan_dict.ptr, aux, aux_len * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+        daux = ctx->scan_dict.as<int64_t>();
+    }
+    const bool selects = op == Op::kIndex || op == Op::kValues || op == Op::kExplicit;
 
     Arena &A = ctx->scratch;
     A.reset();
     const size_t o_counts = A.reserve(sizeof(uint64_t) * g.nchunks);
     const size_t o_offs = A.reserve(sizeof(uint64_t) * g.nchunks);
     const size_t o_res = A.reserve(sizeof(uint64_t) * 2);
-    const bool select1 = (op == Op::kIndex || op == Op::kValues) && one_pass_selection();
+    const bool select1 = selects && one_pass_selection();
     const size_t o_status = A.reserve(sizeof(uint64_t) * (select1 ? select_chunks(n) : 0) + 16);
     SCAN_HIP(A.buf.ensure(A.used));
     uint64_t *counts = A.at<uint64_t>(o_counts);
@@ -96,19 +107,27 @@ int run(Op op, T lo, T hi, const T *in, size_t n, void *out, size_t cap, uint64_
             SCAN_HIP(ctx->scan_out.ensure(std::max<size_t>(cap, 1) * sizeof(OutT)));
             o = ctx->scan_out.as<OutT>();
         }
-        tm.mark(op == Op::kIndex ? "scan_select_index" : "scan_select_values");
+        tm.mark(op == Op::kIndex ? "scan_select_index" : op == Op::kValues ? "scan_select_values"
+                                                                              : "scan_select_explicit");
         if (op == Op::kIndex)
             SCAN_HIP((launch_select<T, OutT, 0>(din, n, lo, hi, ticket, sel_status, o, cap, res, s)));
-        else
+        else if (op == Op::kValues)
             SCAN_HIP((launch_select<T, OutT, 1>(din, n, lo, hi, ticket, sel_status, o, cap, res, s)));
+        else if constexpr (std::is_same<T, uint8_t>::value && std::is_same<OutT, uint64_t>::value)
+            SCAN_HIP((launch_select<T, OutT, 3>(din, n, lo, hi, ticket, sel_status, o, cap, res, s, daux, aux_len)));
         tm.end_call();
         SCAN_HIP(hipMemcpyAsync(ctx->host_result, res, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
         SCAN_HIP(hipMemcpyAsync(ctx->host_result + 1, ticket, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
         SCAN_HIP(hipStreamSynchronize(s));
         const uint64_t total = ctx->host_result[0];
-        if (reinterpret_cast<const uint32_t *>(ctx->host_result + 1)[1] != 0) {
+        const uint32_t flags = reinterpret_cast<const uint32_t *>(ctx->host_result + 1)[1];
+        if (flags & 1u) {
             set_last_error("one-pass selection: look-back poll gave up");
             return MI355_ERR_HIP;
+        }
+        if (flags & 2u) {
+            set_last_error("explicit_index_scan: a match's index entry lies past the index array");
+            return MI355_ERR_INVALID;
         }
         if (result) *result = total;
         if (!out_dev && out && total)
@@ -149,23 +168,35 @@ int run(Op op, T lo, T hi, const T *in, size_t n, void *out, size_t cap, uint64_
             o = ctx->scan_out.as<OutT>();
             dev_out = o;
         }
-        tm.mark(op == Op::kIndex ? "scan_expand_index" : "scan_expand_values");
+        tm.mark(op == Op::kIndex ? "scan_expand_index" : op == Op::kValues ? "scan_expand_values"
+                                                                              : "scan_expand_explicit");
         if (op == Op::kIndex)
             SCAN_HIP((launch_expand<T, OutT, 0>(bv, din, n, g.rows_per_chunk, g.nchunks, offs, o, cap, s)));
-        else
+        else if (op == Op::kValues)
             SCAN_HIP((launch_expand<T, OutT, 1>(bv, din, n, g.rows_per_chunk, g.nchunks, offs, o, cap, s)));
+        else if constexpr (std::is_same<T, uint8_t>::value && std::is_same<OutT, uint64_t>::value) {
+            SCAN_HIP(hipMemsetAsync(ticket, 0, 2 * sizeof(uint32_t), s));
+            SCAN_HIP((launch_expand<T, OutT, 3>(bv, din, n, g.rows_per_chunk, g.nchunks, offs, o, cap, s, daux,
+                                                aux_len, ticket + 1)));
+        }
     }
     tm.end_call();
     SCAN_HIP(hipMemcpyAsync(ctx->host_result, res, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    if (op == Op::kExplicit)
+        SCAN_HIP(hipMemcpyAsync(ctx->host_result + 1, ticket, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     SCAN_HIP(hipStreamSynchronize(s));
     const uint64_t total = ctx->host_result[0];
+    if (op == Op::kExplicit && (reinterpret_cast<const uint32_t *>(ctx->host_result + 1)[1] & 2u)) {
+        set_last_error("explicit_index_scan: a match's index entry lies past the index array");
+        return MI355_ERR_INVALID;
+    }
     if (result) *result = total;
     if (dev_out && out) {
-        if (op == Op::kIndex || op == Op::kValues) copy_bytes = std::min<uint64_t>(total, cap) * sizeof(OutT);
+        if (selects) copy_bytes = std::min<uint64_t>(total, cap) * sizeof(OutT);
         if (copy_bytes) SCAN_HIP(hipMemcpy(out, dev_out, copy_bytes, hipMemcpyDeviceToHost));
     }
     tm.collect();
-    if ((op == Op::kIndex || op == Op::kValues) && total > cap) {
+    if (selects && total > cap) {
         set_last_error("output capacity " + std::to_string(cap) + " < " + std::to_string(total) + " matches");
         return MI355_ERR_CAPACITY;
     }
@@ -353,6 +384,13 @@ int mi355_scan_index_i32(int32_t lo, int32_t hi, const int32_t *in, size_t n, ui
     SCAN_ARGCHECK(sgxamd::scan::bad(in, n, out, cap > 0) || !n_out);
     if (n == 0) { *n_out = 0; return MI355_OK; }
     return run<int32_t, uint64_t>(Op::kIndex, lo, hi, in, n, out, cap, n_out);
+}
+
+int mi355_scan_explicit_index_u8(uint8_t lo, uint8_t hi, const uint64_t *index, size_t index_len, const uint8_t *in,
+                                 size_t n, uint64_t *out, size_t cap, uint64_t *n_out) {
+    SCAN_ARGCHECK(sgxamd::scan::bad(in, n, out, cap > 0) || !n_out || (!index && index_len));
+    if (n == 0) { *n_out = 0; return MI355_OK; }
+    return run<uint8_t, uint64_t>(Op::kExplicit, lo, hi, in, n, out, cap, n_out, index, index_len);
 }
 
 int mi355_scan_values_u8(uint8_t lo, uint8_t hi, const uint8_t *in, size_t n, uint32_t *out, size_t cap,

@@ -325,13 +325,36 @@ __device__ __forceinline__ void wave_lds_sync() {
 // consecutive output slots.  Steps with more than kStage matches in a wave (dense
 // predicates) stage in rounds of kStage.  The word of the next step is loaded before
 // the current one is expanded.
+// SIMD512::explicit_index_scan (SIMD512.cpp:152-208) gathers the matches of row r from
+// the u64 index vector index_compressed[i + j] (block i = r / 64, sub-block j = (r % 64) / 8),
+// lane r % 8: entry 8 * (r / 64 + (r % 64) / 8) + r % 8, restated as written.
+__device__ __forceinline__ uint64_t explicit_pos(uint64_t r) { return 8 * (r / 64 + (r % 64) / 8) + r % 8; }
+
+// Output value of a selected row: its index (MODE 0), value (1), dictionary value (2) or
+// explicit index entry (3; aux = the index array of aux_len entries, an out-of-range
+// entry reads 0 and sets bit 2 of *err).
+template <typename T, typename OutT, int MODE>
+__device__ __forceinline__ OutT select_value(uint64_t row, const T *__restrict__ in, const int64_t *__restrict__ aux,
+                                             uint64_t aux_len, uint32_t *err) {
+    if constexpr (MODE == 0) return (OutT)row;
+    else if constexpr (MODE == 1) return (OutT)in[row];
+    else if constexpr (MODE == 2) return (OutT)aux[in[row]];
+    else {
+        const uint64_t q = explicit_pos(row);
+        if (q < aux_len) return (OutT)aux[q];
+        atomicOr(err, 2u);
+        return (OutT)0;
+    }
+}
+
 constexpr uint32_t kStage = 1024;  // staged outputs per wave and round (u32 row offsets, 4 KiB)
 
 template <typename T, typename OutT, int MODE>
 __global__ __launch_bounds__(kBlock) void k_expand(const uint64_t *__restrict__ bv, const T *__restrict__ in,
                                                    uint64_t n, uint64_t rows_per_chunk,
                                                    const uint64_t *__restrict__ chunk_off, OutT *__restrict__ out,
-                                                   uint64_t cap, const int64_t *__restrict__ dict) {
+                                                   uint64_t cap, const int64_t *__restrict__ dict, uint64_t aux_len,
+                                                   uint32_t *__restrict__ err) {
     __shared__ uint32_t stage_s[kWaves][kStage];
     __shared__ uint32_t wtot_s[kWaves];
     const uint32_t lane = __lane_id(), wave = threadIdx.x / kWave;
@@ -380,10 +403,7 @@ __global__ __launch_bounds__(kBlock) void k_expand(const uint64_t *__restrict__ 
                 const uint64_t row = row0 + stage[m];
                 const uint64_t o = woff + r0 + m;
                 if (o < cap) {
-                    OutT v;
-                    if (MODE == 0) v = (OutT)row;
-                    else if (MODE == 1) v = (OutT)in[row];
-                    else v = (OutT)dict[in[row]];
+                    const OutT v = select_value<T, OutT, MODE>(row, in, dict, aux_len, err);
                     __builtin_nontemporal_store(v, out + o);
                 }
             }
@@ -396,35 +416,46 @@ __global__ __launch_bounds__(kBlock) void k_expand(const uint64_t *__restrict__ 
 
 template <typename T, typename OutT, int MODE>
 hipError_t launch_expand(const uint64_t *bv, const T *in, uint64_t n, uint64_t rows_per_chunk, uint32_t nchunks,
-                         const uint64_t *chunk_off, OutT *out, uint64_t cap, hipStream_t s, const int64_t *dict) {
+                         const uint64_t *chunk_off, OutT *out, uint64_t cap, hipStream_t s, const int64_t *dict,
+                         uint64_t aux_len, uint32_t *err) {
     if (nchunks == 0) return hipSuccess;
     hipLaunchKernelGGL((k_expand<T, OutT, MODE>), dim3(nchunks), dim3(kBlock), 0, s, bv, in, n, rows_per_chunk,
-                       chunk_off, out, cap, dict);
+                       chunk_off, out, cap, dict, aux_len, err);
     return hipGetLastError();
 }
 
 template hipError_t launch_expand<uint8_t, uint64_t, 0>(const uint64_t *, const uint8_t *, uint64_t, uint64_t,
                                                         uint32_t, const uint64_t *, uint64_t *, uint64_t,
-                                                        hipStream_t, const int64_t *);
+                                                        hipStream_t, const int64_t *, uint64_t, uint32_t *);
 template hipError_t launch_expand<int32_t, uint64_t, 0>(const uint64_t *, const int32_t *, uint64_t, uint64_t,
                                                         uint32_t, const uint64_t *, uint64_t *, uint64_t,
-                                                        hipStream_t, const int64_t *);
+                                                        hipStream_t, const int64_t *, uint64_t, uint32_t *);
 template hipError_t launch_expand<uint8_t, uint32_t, 1>(const uint64_t *, const uint8_t *, uint64_t, uint64_t,
                                                         uint32_t, const uint64_t *, uint32_t *, uint64_t,
-                                                        hipStream_t, const int64_t *);
+                                                        hipStream_t, const int64_t *, uint64_t, uint32_t *);
 template hipError_t launch_expand<int32_t, int32_t, 1>(const uint64_t *, const int32_t *, uint64_t, uint64_t,
                                                        uint32_t, const uint64_t *, int32_t *, uint64_t,
-                                                       hipStream_t, const int64_t *);
+                                                       hipStream_t, const int64_t *, uint64_t, uint32_t *);
 
 template hipError_t launch_expand<uint8_t, int64_t, 2>(const uint64_t *, const uint8_t *, uint64_t, uint64_t,
                                                        uint32_t, const uint64_t *, int64_t *, uint64_t, hipStream_t,
-                                                       const int64_t *);
+                                                       const int64_t *, uint64_t, uint32_t *);
 template hipError_t launch_expand<uint16_t, int64_t, 2>(const uint64_t *, const uint16_t *, uint64_t, uint64_t,
                                                         uint32_t, const uint64_t *, int64_t *, uint64_t, hipStream_t,
-                                                        const int64_t *);
+                                                        const int64_t *, uint64_t, uint32_t *);
 template hipError_t launch_expand<uint32_t, int64_t, 2>(const uint64_t *, const uint32_t *, uint64_t, uint64_t,
                                                         uint32_t, const uint64_t *, int64_t *, uint64_t, hipStream_t,
-                                                        const int64_t *);
+                                                        const int64_t *, uint64_t, uint32_t *);
+// named by run<T, uint64_t>'s value branch, never called
+template hipError_t launch_expand<uint8_t, uint64_t, 1>(const uint64_t *, const uint8_t *, uint64_t, uint64_t,
+                                                        uint32_t, const uint64_t *, uint64_t *, uint64_t, hipStream_t,
+                                                        const int64_t *, uint64_t, uint32_t *);
+template hipError_t launch_expand<int32_t, uint64_t, 1>(const uint64_t *, const int32_t *, uint64_t, uint64_t,
+                                                        uint32_t, const uint64_t *, uint64_t *, uint64_t, hipStream_t,
+                                                        const int64_t *, uint64_t, uint32_t *);
+template hipError_t launch_expand<uint8_t, uint64_t, 3>(const uint64_t *, const uint8_t *, uint64_t, uint64_t,
+                                                        uint32_t, const uint64_t *, uint64_t *, uint64_t, hipStream_t,
+                                                        const int64_t *, uint64_t, uint32_t *);
 
 // ------------------------------------------------------- one-pass selection ---
 // Index / value / dictionary output in ONE pass over the column (implicit_index_scan,
@@ -453,7 +484,8 @@ template <typename T, typename OutT, int MODE>
 __global__ __launch_bounds__(kBlock) void k_select(const T *__restrict__ in, uint64_t n, T lo, T hi,
                                                    uint32_t *__restrict__ ticket, uint64_t *__restrict__ status,
                                                    OutT *__restrict__ out, uint64_t cap,
-                                                   const int64_t *__restrict__ dict, uint64_t *__restrict__ total) {
+                                                   const int64_t *__restrict__ dict, uint64_t aux_len,
+                                                   uint64_t *__restrict__ total) {
     constexpr uint32_t V = 16 / sizeof(T), LPW = 64 / V, FULL = (1u << V) - 1u;
     constexpr uint32_t CH = sel_chunk<T>(), NWORD = CH / 64;
     constexpr int U = 8;  // 16-B loads in flight per lane
@@ -570,10 +602,7 @@ __global__ __launch_bounds__(kBlock) void k_select(const T *__restrict__ in, uin
                 if (o < cap) {
                     // non-temporal: the outputs are not re-read here (measured 4 % faster
                     // than plain stores at C3)
-                    OutT v;
-                    if (MODE == 0) v = (OutT)row;
-                    else if (MODE == 1) v = (OutT)in[row];
-                    else v = (OutT)dict[in[row]];
+                    const OutT v = select_value<T, OutT, MODE>(row, in, dict, aux_len, &ticket[1]);
                     __builtin_nontemporal_store(v, out + o);
                 }
             }
@@ -588,7 +617,7 @@ uint64_t select_chunks(uint64_t n) { return (n + kSelChunk - 1) / kSelChunk; }  
 
 template <typename T, typename OutT, int MODE>
 hipError_t launch_select(const T *in, uint64_t n, T lo, T hi, uint32_t *ticket, uint64_t *status, OutT *out,
-                         uint64_t cap, uint64_t *total, hipStream_t s, const int64_t *dict) {
+                         uint64_t cap, uint64_t *total, hipStream_t s, const int64_t *dict, uint64_t aux_len) {
     const uint64_t nchunks = (n + sel_chunk<T>() - 1) / sel_chunk<T>();
     if (nchunks == 0) return hipSuccess;
     hipError_t e = hipMemsetAsync(ticket, 0, 2 * sizeof(uint32_t), s);
@@ -596,13 +625,14 @@ hipError_t launch_select(const T *in, uint64_t n, T lo, T hi, uint32_t *ticket, 
     e = hipMemsetAsync(status, 0, nchunks * sizeof(uint64_t), s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((k_select<T, OutT, MODE>), dim3((uint32_t)nchunks), dim3(kBlock), 0, s, in, n, lo, hi, ticket,
-                       status, out, cap, dict, total);
+                       status, out, cap, dict, aux_len, total);
     return hipGetLastError();
 }
 
 #define SGX_SELECT_INST(T, OutT, MODE)                                                                         \
     template hipError_t launch_select<T, OutT, MODE>(const T *, uint64_t, T, T, uint32_t *, uint64_t *, OutT *, \
-                                                     uint64_t, uint64_t *, hipStream_t, const int64_t *);
+                                                     uint64_t, uint64_t *, hipStream_t, const int64_t *, \
+                                                     uint64_t);
 SGX_SELECT_INST(uint8_t, uint64_t, 0)
 SGX_SELECT_INST(int32_t, uint64_t, 0)
 SGX_SELECT_INST(uint8_t, uint32_t, 1)
@@ -612,6 +642,7 @@ SGX_SELECT_INST(int32_t, uint64_t, 1)
 SGX_SELECT_INST(uint8_t, int64_t, 2)
 SGX_SELECT_INST(uint16_t, int64_t, 2)
 SGX_SELECT_INST(uint32_t, int64_t, 2)
+SGX_SELECT_INST(uint8_t, uint64_t, 3)
 #undef SGX_SELECT_INST
 
 // Dictionary code range of a predicate on values (dict_scan_* prologue,

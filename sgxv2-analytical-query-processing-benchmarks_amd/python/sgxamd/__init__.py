@@ -107,6 +107,14 @@ class rho_stats(C.Structure):
         ("ms_pass2", C.c_double),
         ("ms_join", C.c_double),
         ("ms_total", C.c_double),
+        ("ms_pass1_r", C.c_double),
+        ("ms_pass1_s", C.c_double),
+        ("ms_pass1_hist", C.c_double),
+        ("ms_pass1_copy", C.c_double),
+        ("ms_pass2_hist", C.c_double),
+        ("ms_pass2_copy", C.c_double),
+        ("ms_build", C.c_double),
+        ("ms_probe", C.c_double),
     ]
 
     def as_dict(self) -> dict:
@@ -181,6 +189,8 @@ SIGNATURES = {
     "mi355_scan_bitvector_i32": (C.c_int, [C.c_int32, C.c_int32, _P, C.c_size_t, _P]),
     "mi355_scan_index_u8": (C.c_int, [C.c_uint8, C.c_uint8, _P, C.c_size_t, _P, C.c_size_t, _U64P]),
     "mi355_scan_index_i32": (C.c_int, [C.c_int32, C.c_int32, _P, C.c_size_t, _P, C.c_size_t, _U64P]),
+    "mi355_scan_explicit_index_u8": (C.c_int, [C.c_uint8, C.c_uint8, _P, C.c_size_t, _P, C.c_size_t, _P,
+                                               C.c_size_t, _U64P]),
     "mi355_scan_values_u8": (C.c_int, [C.c_uint8, C.c_uint8, _P, C.c_size_t, _P, C.c_size_t, _U64P]),
     "mi355_scan_values_i32": (C.c_int, [C.c_int32, C.c_int32, _P, C.c_size_t, _P, C.c_size_t, _U64P]),
     "mi355_scan_sum_u8": (C.c_int, [C.c_uint8, C.c_uint8, _P, C.c_size_t, _U64P]),
@@ -428,6 +438,14 @@ def scan_bitvector(lo: int, hi: int, col, n: int, out_words, dtype: str = "i32")
 def scan_index(lo: int, hi: int, col, n: int, out, cap: int, dtype: str = "i32") -> int:
     c = C.c_uint64()
     _check(_scan_fn("index", dtype)(lo, hi, ptr(col), n, ptr(out), cap, C.byref(c)))
+    return int(c.value)
+
+
+def scan_explicit_index(lo: int, hi: int, index, index_len: int, col, n: int, out, cap: int) -> int:
+    """SIMD512::explicit_index_scan over a u8 column: the index entries of the matching rows."""
+    c = C.c_uint64()
+    _check(lib.mi355_scan_explicit_index_u8(lo, hi, ptr(index), index_len, ptr(col), n, ptr(out), cap,
+                                            C.byref(c)))
     return int(c.value)
 
 

@@ -217,6 +217,42 @@ def test_native_driver_binary(gpu, alg, extra):
     assert "Throughput (M rec/sec)" in out and f"Running {alg}" in out
     if "-m" in extra:
         assert f"Materialized {m} tuples" in out
+    throughput, phases = parse_teebench_output(out)
+    assert throughput > 0
+    assert set(phases) == set(TEEBENCH_TIMED_PHASES), sorted(phases)
+    # One Hist + One Copy = pass 1; Build + Join = the build/probe kernels inside Build+Join Overall
+    assert phases["build"] > 0 and phases["probe"] > 0
+    assert phases["build"] + phases["probe"] <= phases["join_total"] + 2
+    assert abs(phases["partition_r"] + phases["partition_s"] - phases["partition_1"]) <= 2 + phases["partition_1"] // 100
+    assert phases["total"] >= phases["partition"] + phases["join_total"] - 2
+
+
+# The phase keys the reference's harness extracts from print_timing
+# (SGXv2Scripts/scripts/helpers/runner.py:14-55; its "Partition One Hist/Copy" lines
+# land in partition_r / partition_s).  The regexes below restate that parser.
+TEEBENCH_TIMED_PHASES = ["total", "partition", "partition_1", "partition_r", "partition_s", "partition_2",
+                         "partition_2_h", "partition_2_c", "join_total", "build", "probe"]
+_PHASE_LINES = [("Total Join Time (cycles)", "total"), ("Partition Overall (cycles)", "partition"),
+                ("Partition Pass One (cycles)", "partition_1"), ("Partition One Hist (cycles)", "partition_r"),
+                ("Partition One Copy (cycles)", "partition_s"), ("Partition Pass Two (cycles)", "partition_2"),
+                ("Partition Two Hist (cycles)", "partition_2_h"), ("Partition Two Copy (cycles)", "partition_2_c"),
+                ("Build+Join Overall (cycles)", "join_total"), ("Build (cycles)", "build"),
+                ("Join (cycles)", "probe")]
+
+
+def parse_teebench_output(stdout):
+    import re
+
+    phases, throughput = {}, 0.0
+    for line in stdout.splitlines():
+        if "Throughput" in line:
+            throughput = float(re.findall(r"\d+\.\d+", line)[1])
+            continue
+        for text, key in _PHASE_LINES:  # first match wins, like runner.py's elif chain
+            if text in line:
+                phases[key] = int(re.findall(r"\d+", line)[-2])  # -2: the colour reset ends in 0
+                break
+    return throughput, phases
 
 
 # ---------------------------------------------------------------- materialisation
@@ -418,3 +454,21 @@ def test_pipelined_guards(sgx, gpu):
     sgx.rho_join_begin(dR, len(R), len(S))
     assert sgx.rho_join_finish(dS, len(S)).matches == len(S)
     assert sgx.rho_join(dR, len(R), dS, len(S)).matches == len(S)
+
+
+# ---------------------------------------------------------------- golden fixtures
+def test_golden_join_counts(sgx, gpu):
+    """Every committed join fixture (tests/golden/golden.json): GPU RHO and RHT counts equal
+    the fixture's, with the GPU policy and a forced 2-pass plan."""
+    from test_golden import GOLDEN, relation, zipf_relation
+
+    for case in GOLDEN["joins"]:
+        R, S = relation(sgx, case["R"]), relation(sgx, case["S"])
+        assert gpu_join(sgx, R, S).matches == case["matches"], case
+        assert gpu_join(sgx, R, S, radix_bits=10, passes=2).matches == case["matches"], case
+        assert gpu_join(sgx, R, S, algorithm="RHT").matches == case["matches"], case
+    z = GOLDEN["zipf"]
+    Z = zipf_relation(sgx)
+    R = relation(sgx, f"pk_{z['n']}_11111")
+    assert gpu_join(sgx, R, Z).matches == z["pk_join_matches"]
+    assert gpu_join(sgx, Z, Z).matches == z["self_join_matches"]

@@ -207,3 +207,160 @@ def test_scan_beyond_2pow32_rows(sgx, gpu):
         assert torch.equal(bv[w0: w0 + 8], words[: nwords - w0]), w0
     del col, bv
     torch.cuda.empty_cache()
+
+
+# ------------------------------------------------------- explicit index scan
+@pytest.mark.parametrize("n", [64, 1000, 16384, (1 << 20) + 37])
+def test_explicit_index_scan_matches_oracle(sgx, orc, gpu, n):
+    """SIMD512::explicit_index_scan (SIMD512.cpp:152-208): row r emits the index entry
+    8*(r/64 + (r%64)/8) + r%8 (the reference's index_compressed[i + j])."""
+    rng = np.random.default_rng(n)
+    L = orc.explicit_index_len(n)
+    index = rng.integers(0, 2**63, L, dtype=np.int64).astype(np.uint64)
+    for kind in ("mod", "rand"):
+        col = column(n, "u8", kind)
+        for lo, hi in PREDS:
+            exp = orc.explicit_index_scan(lo, hi, index, col)
+            out = np.zeros(max(len(exp), 1), dtype=np.uint64)
+            assert sgx.scan_explicit_index(lo, hi, index, L, col, n, out, len(exp)) == len(exp)
+            assert np.array_equal(out[: len(exp)], exp)
+
+
+def test_explicit_index_scan_short_index_fails_loudly(sgx, gpu):
+    col = column(4096, "u8", "mod")
+    index = np.arange(100, dtype=np.uint64)
+    out = np.zeros(4096, dtype=np.uint64)
+    with pytest.raises(sgx.Mi355Error) as e:
+        sgx.scan_explicit_index(0, 255, index, len(index), col, len(col), out, len(out))
+    assert e.value.code == sgx.MI355_ERR_INVALID
+    # a predicate whose matches stay inside the index array is fine: rows 0..3 -> entries 0..3
+    assert sgx.scan_explicit_index(0, 3, index, len(index), col[:64], 64, out, 64) == 4
+    assert out[:4].tolist() == [0, 1, 2, 3]
+
+
+# ----------------------------------------------- SIMD512:: adapter, compiled caller
+def _self_alloc_size(size, blocks, before_last):
+    """SIMD512.cpp:262-266 growth rule restated: the vector size the reference ends with."""
+    if blocks == 0:
+        return size
+    while before_last + 64 > size:
+        size = (64 + size) * 3
+    return size
+
+
+def test_simd512_adapter_binary(orc, gpu, tmp_path):
+    """bin/simd512_check calls every SIMD512:: function through sgxamd/SIMD512_mi355.hpp with a
+    64-B aligned CacheAlignedVector, like the reference's drivers and Catch2 tests; every
+    output equals the oracle's on the reference's n / 64 whole blocks."""
+    import os
+    import subprocess
+
+    from conftest import PKG
+
+    n = (1 << 18) + 100  # the adapter drops the n % 64 tail, like the reference
+    m = n // 64 * 64
+    rng = np.random.default_rng(5)
+    col = rng.integers(0, 256, n).astype(np.uint8)
+    col[: 1 << 16] = np.arange(1 << 16) % 256  # the i % 256 column of Allocator.hpp:94-110
+    index = rng.integers(0, 2**63, 8 * (m // 64 + 7), dtype=np.int64).astype(np.uint64)
+    dict8 = np.sort(rng.integers(-1000, 1000, 256)).astype(np.int64)
+    codes16 = rng.integers(0, 65536, n).astype(np.uint16)
+    dict16 = np.sort(rng.integers(-50_000, 50_000, 65536)).astype(np.int64)
+    codes32 = rng.integers(0, 3000, n).astype(np.uint32)
+    dict32 = np.sort(rng.integers(-5000, 5000, 3000)).astype(np.int64)
+    preds = [(0, 26), (7, 7), (1, 100), (0, 255), (200, 100)]
+    sizes = [0, 5, 10_000, 1 << 20]
+    for name, a in [("col_u8", col), ("index_u64", index), ("dict8", dict8), ("codes16", codes16),
+                    ("dict16", dict16), ("codes32", codes32), ("dict32", dict32)]:
+        a.tofile(tmp_path / f"{name}.bin")
+    (tmp_path / "preds.txt").write_text("".join(f"{lo} {hi}\n" for lo, hi in preds))
+    (tmp_path / "self_alloc.txt").write_text("".join(f"{s}\n" for s in sizes))
+    (tmp_path / "out").mkdir()
+    exe = os.path.join(PKG, "bin", "simd512_check")
+    subprocess.run([exe, str(tmp_path)], check=True, timeout=120, capture_output=True)
+    res = dict(line.split() for line in (tmp_path / "out" / "results.txt").read_text().splitlines())
+    o = tmp_path / "out"
+    cw = col[:m]
+    for k, (lo, hi) in enumerate(preds):
+        cnt = orc.scan("count", "u8", lo, hi, cw)
+        assert int(res[f"p{k}_count"]) == cnt
+        assert int(res[f"p{k}_sum"]) == orc.scan_sum_u8(lo, hi, cw)
+        assert np.array_equal(np.fromfile(o / f"p{k}_bitvector.bin", np.uint64), orc.scan("bitvector", "u8", lo, hi, cw))
+        idx = orc.scan("index", "u8", lo, hi, cw)
+        assert np.array_equal(np.fromfile(o / f"p{k}_implicit.bin", np.uint64)[:cnt], idx)
+        assert np.array_equal(np.fromfile(o / f"p{k}_explicit.bin", np.uint64)[:cnt],
+                              orc.explicit_index_scan(lo, hi, index, cw))
+        assert int(res[f"p{k}_scan"]) == cnt
+        assert np.array_equal(np.fromfile(o / f"p{k}_scan.bin", np.uint32), orc.scan("values", "u8", lo, hi, cw))
+        before_last = int((idx < m - 64).sum())
+        for j, s0 in enumerate(sizes):
+            assert int(res[f"p{k}_self_alloc_{j}_1"]) == cnt
+            assert np.array_equal(np.fromfile(o / f"p{k}_self_alloc_{j}.bin", np.uint64), idx)
+            assert int(res[f"p{k}_self_alloc_{j}_0"]) == _self_alloc_size(s0, m // 64, before_last)
+        assert np.array_equal(np.fromfile(o / f"p{k}_dict8.bin", np.int64), orc.dict_scan(lo, hi, dict8, cw))
+        assert np.array_equal(np.fromfile(o / f"p{k}_dict16.bin", np.int64),
+                              orc.dict_scan(lo, hi, dict16, codes16[: n // 32 * 32]))
+        assert np.array_equal(np.fromfile(o / f"p{k}_dict32.bin", np.int64),
+                              orc.dict_scan(lo, hi, dict32, codes32[: n // 16 * 16]))
+
+
+def test_golden_scan_fixtures(sgx, orc, gpu):
+    """Every committed scan fixture (tests/golden/golden.json): GPU outputs hash to the fixture."""
+    from test_golden import GOLDEN, explicit_index, scan_columns, sha
+
+    cols = scan_columns()
+    for e in GOLDEN["scans"]:
+        c = cols[e["column"]]
+        c = c if e["dtype"] == "u8" else c.astype(np.int32)
+        lo, hi, dt, n, k = e["lo"], e["hi"], e["dtype"], len(c), e["count"]
+        assert sgx.scan_count(lo, hi, c, n, dt) == k
+        bv = np.zeros((n + 63) // 64, dtype=np.uint64)
+        sgx.scan_bitvector(lo, hi, c, n, bv, dt)
+        assert sha(bv) == e["bitvector_sha256"]
+        idx = np.zeros(max(k, 1), dtype=np.uint64)
+        assert sgx.scan_index(lo, hi, c, n, idx, k, dt) == k
+        assert sha(idx[:k]) == e["index_sha256"]
+        vals = np.zeros(max(k, 1), dtype=np.uint32 if dt == "u8" else np.int32)
+        assert sgx.scan_values(lo, hi, c, n, vals, k, dt) == k
+        assert sha(vals[:k]) == e["values_sha256"]
+        if dt == "u8":
+            assert sgx.scan_sum_u8(lo, hi, c, n) == e["sum"]
+            ix = explicit_index(orc, n)
+            assert sgx.scan_explicit_index(lo, hi, ix, len(ix), c, n, idx, k) == k
+            assert sha(idx[:k]) == e["explicit_index_sha256"]
+
+
+# ----------------------------------------------------- SimdScanMulti driver
+def test_simdmulti_driver_csv(gpu, tmp_path):
+    """bin/simdmulti_mi355 takes SimdScanMulti's flags (flags.hpp:8-40), enumerates the same
+    configuration spectrum (types.hpp:140-190), maps selectivity to [0, round(sel/100*255)]
+    (types.hpp:125,134) and prints CSV rows results/plot.py reads (plot.py:20-24)."""
+    import io
+    import os
+    import subprocess
+
+    import pandas as pd
+
+    from conftest import PKG
+
+    exe = os.path.join(PKG, "bin", "simdmulti_mi355")
+    args = ["--mode=noIndex,bitvector,dict,scalar", "--min_entries_exp=16", "--max_entries_exp=20",
+            "--min_selectivity=1", "--max_selectivity=10", "--step_selectivity=9", "--num_reruns=2",
+            "--unique_data=b", "--num_runs=3", "--num_warmup_runs=1", "--min_threads=1", "--max_threads=2"]
+    out = subprocess.run([exe] + args, capture_output=True, text=True, timeout=300, check=True).stdout
+    df = pd.read_csv(io.StringIO(out), header=0, skipinitialspace=True)
+    # 4 modes x unique {f, t} x threads {1, 2} x entries {2^16 .. 2^20} x selectivity {1, 10}
+    assert len(df) == 4 * 2 * 2 * 5 * 2
+    for col in ("entries", "numRuns", "numThreads", "reruns", "selectivity", "writeMode", "enclaveMode",
+                "dataLoading", "datasizeKiB", "timeMicroSec", "cpuCycles", "unique", "warmup"):
+        assert col in df.columns, col
+    assert set(df["writeMode"]) == {"bitvector", "noindex", "dict", "scalar"}
+    hi = (df["selectivity"] * 255).round().astype(int)  # 1 % -> 3, 10 % -> 26
+    assert set(hi) == {3, 26}
+    # the column is i % 256: every rerun of `entries` rows matches entries / 256 * (hi + 1)
+    assert (df["matches"] == df["entries"] // 256 * (hi + 1)).all()
+    assert ((df["numRuns"] == 1) == (df["unique"] == 1)).all()
+    # plot.py's throughput formula is finite and positive
+    time_s = df["cpuCycles"] / df["reruns"] / 2.9e9
+    gib = df["entries"] * df["numRuns"] / time_s / 2**30
+    assert (gib > 0).all() and (df["deviceMicroSec"] > 0).all()
