@@ -36,6 +36,123 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def host_topology() -> dict:
+    """CPU model, sockets, cores, NUMA nodes and the cgroup CPU quota of this host."""
+    info: dict = {}
+    try:
+        with open("/proc/cpuinfo") as f:
+            txt = f.read()
+        info["model"] = next((ln.split(":", 1)[1].strip() for ln in txt.splitlines()
+                              if ln.startswith("model name")), None)
+        info["sockets"] = len({ln.split(":", 1)[1].strip() for ln in txt.splitlines() if ln.startswith("physical id")})
+        info["logical_cpus"] = os.cpu_count()
+    except OSError:
+        pass
+    cores = set()
+    for c in range(os.cpu_count() or 0):
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list") as f:
+                cores.add(f.read().strip())
+        except OSError:
+            break
+    if cores:
+        info["physical_cores"] = len(cores)
+        if info.get("sockets"):
+            info["cores_per_socket"] = len(cores) // info["sockets"]
+    nodes = {}
+    base = "/sys/devices/system/node"
+    if os.path.isdir(base):
+        for d in sorted(os.listdir(base)):
+            if d.startswith("node") and d[4:].isdigit():
+                with open(os.path.join(base, d, "cpulist")) as f:
+                    nodes[int(d[4:])] = f.read().strip()
+    info["numa_nodes"] = nodes
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+        info["cgroup_cpu_quota"] = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        info["cgroup_cpu_quota"] = None
+    info["affinity_cpus"] = len(os.sched_getaffinity(0))
+    return info
+
+
+def _cpulist(text: str) -> list[int]:
+    out = []
+    for part in text.split(","):
+        if "-" in part:
+            a, b = part.split("-")
+            out.extend(range(int(a), int(b) + 1))
+        elif part:
+            out.append(int(part))
+    return out
+
+
+def pinned_physical_cores(k: int) -> list[int]:
+    """Up to k physical cores (one hardware thread each) of the first NUMA node this
+    process may run on -- numactl --physcpubind=0-15 in the reference's runs.  The
+    cores are dealt round-robin over the node's L3 domains: on chiplet CPUs (EPYC:
+    8 cores per L3 / CCD) the first 16 core ids sit on two CCDs whose fabric links
+    cap the memory bandwidth, while the reference's Xeon node is one die."""
+    allowed = os.sched_getaffinity(0)
+    base = "/sys/devices/system/node"
+    nodes = []
+    if os.path.isdir(base):
+        for d in sorted(os.listdir(base)):
+            if d.startswith("node") and d[4:].isdigit():
+                with open(os.path.join(base, d, "cpulist")) as f:
+                    nodes.append(_cpulist(f.read().strip()))
+    if not nodes:
+        nodes = [sorted(allowed)]
+
+    def read(path: str, default: str) -> str:
+        try:
+            with open(path) as f:
+                return f.read().strip()
+        except OSError:
+            return default
+
+    for cpus in nodes:
+        domains: dict[str, list[int]] = {}
+        for c in cpus:
+            if c not in allowed:
+                continue
+            sib = read(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list", str(c))
+            if _cpulist(sib)[0] != c:
+                continue  # a second hardware thread of a core already listed
+            l3 = read(f"/sys/devices/system/cpu/cpu{c}/cache/index3/shared_cpu_list", "all")
+            domains.setdefault(l3, []).append(c)
+        picked = []
+        lists = list(domains.values())
+        while len(picked) < k and any(lists):
+            for lst in lists:
+                if lst and len(picked) < k:
+                    picked.append(lst.pop(0))
+        if picked:
+            return sorted(picked)
+    return sorted(allowed)[:k]
+
+
+class cpu_affinity:
+    """Pins this thread (and the threads it creates) to `cpus` for the duration of a
+    with-block; None leaves the affinity alone."""
+
+    def __init__(self, cpus):
+        self.cpus = cpus
+        self.saved = None
+
+    def __enter__(self):
+        if self.cpus:
+            self.saved = os.sched_getaffinity(0)
+            os.sched_setaffinity(0, self.cpus)
+        return self
+
+    def __exit__(self, *exc):
+        if self.saved is not None:
+            os.sched_setaffinity(0, self.saved)
+        return False
+
+
 def algorithmic_bytes(kernel: str, nR: int, nS: int, passes: int = 2, pass2_bits: int = 8) -> int:
     """Bytes a kernel must move per launch (DESIGN.md 'Kernels and their rooflines').
 
@@ -73,13 +190,17 @@ def main():
                     help="nccl = RCCL over xGMI (one GPU per rank); gloo = single-GPU rehearsal of the "
                          "multi-rank path (ranks share the visible GPUs, tuples staged through host memory)")
     ap.add_argument("--no-scan", action="store_true")
+    ap.add_argument("--no-configs", action="store_true", help="skip the BASELINE config 4 / 5 sections")
+    ap.add_argument("--zipf-source", choices=["host", "device"], default="host",
+                    help="config 5's Zipf stream: host mt19937_64 seed 22222 staged to HBM (BASELINE.md row 5) "
+                         "or the device generator")
     ap.add_argument("--no-tpch", action="store_true")
     ap.add_argument("--no-paper", action="store_true",
                     help="skip the runs at the shapes of the reference's own published numbers")
     ap.add_argument("--tpch-scale-milli", type=int, default=10000, help="TPC-H scale factor x 1000 (10000 = SF10)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="time budget per CPU baseline leg")
     args = ap.parse_args()
 
     import numpy as np
@@ -88,6 +209,8 @@ def main():
 
     import sgxamd
     from sgxamd.dist import sharded_rho_join
+
+    ROW_DT = np.dtype([("key", "<u4"), ("payload", "<u4")])  # row_t (data-types.h:44-47)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -124,49 +247,103 @@ def main():
     sgxamd.set_stream(stream)
     sgxamd.timing_enable(True)  # per-kernel HIP events on `stream` (roofline "achieved")
 
-    # ---------------- RHO workload: this rank's slice of the global relations
-    if args.workload == "c2":  # weak: pk(N n) and fk(N n, maxid N n), n per GPU
-        n = 1 << args.log2n
-        gR = gS = n * world
-        workload = f"RHO join |R|=|S|=2^{args.log2n} uniform per GPU (BASELINE config 2)"
-    elif args.workload == "c4":  # strong: pk(2^27) and fk(2^30, maxid 2^27) = 8 shuffled copies
-        gR, gS = 1 << 27, 1 << 30
-        workload = "RHO join |R|=2^27 |S|=2^30 uniform, global (BASELINE config 4)"
-    else:  # strong: pk(2^28) and Zipf(0.75) over 1..2^28
-        gR = gS = 1 << 28
-        workload = "RHO join |R|=|S|=2^28, S Zipf theta=0.75, global (BASELINE config 5)"
-    if gR % world or gS % world:
-        raise SystemExit("relation sizes must divide by the number of GPUs")
-    nR_loc, nS_loc = gR // world, gS // world
-    R = torch.empty(nR_loc, dtype=torch.int64, device=dev)
-    S = torch.empty(nS_loc, dtype=torch.int64, device=dev)
-    sgxamd.gen_pk_dev(R, nR_loc, rank * nR_loc, gR, 11111, stream)
-    if args.workload == "c5":
-        sgxamd.gen_zipf_dev(S, nS_loc, rank * nS_loc, gR, 0.75, 22222, stream)
-    else:
-        sgxamd.gen_fk_dev(S, nS_loc, rank * nS_loc, gR, 22222, stream)
-    N_glob = gS  # every S tuple matches exactly one R tuple in all three configs
-    torch.cuda.synchronize()
+    # ---------------- RHO workloads: this rank's slice of the global relations
+    def make_relations(workload: str):
+        """Device-resident slices of BASELINE config 2, 4 or 5 (generation is untimed)."""
+        if workload == "c2":  # weak: pk(N n) and fk(N n, maxid N n), n per GPU
+            n = 1 << args.log2n
+            gR = gS = n * world
+            desc = f"RHO join |R|=|S|=2^{args.log2n} uniform per GPU (BASELINE config 2)"
+        elif workload == "c4":  # strong: pk(2^27) and fk(2^30, maxid 2^27) = 8 shuffled copies
+            gR, gS = 1 << 27, 1 << 30
+            desc = "RHO join |R|=2^27 |S|=2^30 uniform, global (BASELINE config 4)"
+        else:  # strong: pk(2^28) and Zipf(0.75) over 1..2^28
+            gR = gS = 1 << 28
+            desc = "RHO join |R|=|S|=2^28, S Zipf theta=0.75, global (BASELINE config 5)"
+        if gR % world or gS % world:
+            raise SystemExit("relation sizes must divide by the number of GPUs")
+        nR_loc, nS_loc = gR // world, gS // world
+        R = torch.empty(nR_loc, dtype=torch.int64, device=dev)
+        S = torch.empty(nS_loc, dtype=torch.int64, device=dev)
+        sgxamd.gen_pk_dev(R, nR_loc, rank * nR_loc, gR, 11111, stream)
+        gen = "device pk/fk (keyed-bijection shuffles)"
+        if workload == "c5" and args.zipf_source == "host":
+            # BASELINE.md row 5: one mt19937_64 (seed 22222) Zipf stream for alphabet and
+            # draws (genzipf.cpp:87-144), generated once on the host, staged to HBM and
+            # shared: rank 0 generates, the other ranks receive it by broadcast
+            t_gen = time.perf_counter()
+            full = torch.empty(gS, dtype=torch.int64, device=dev)
+            if rank == 0:
+                host = np.empty(gS, dtype=np.int64)
+                sgxamd.gen_zipf(host, gS, gR, 0.75, 22222, args.cpu_threads)
+                full.copy_(torch.from_numpy(host))
+                del host
+            if world > 1:
+                if args.dist_backend == "nccl":
+                    dist.broadcast(full, 0)
+                else:
+                    cpu_full = full.cpu()
+                    dist.broadcast(cpu_full, 0)
+                    full.copy_(cpu_full)
+            S.copy_(full[rank * nS_loc:(rank + 1) * nS_loc])
+            del full
+            gen = (f"host Zipf(0.75) over 1..|R|, mt19937_64 seed 22222 (generator.cpp restating "
+                   f"genzipf.cpp), staged to HBM in {time.perf_counter() - t_gen:.1f} s; R device pk")
+        elif workload == "c5":
+            sgxamd.gen_zipf_dev(S, nS_loc, rank * nS_loc, gR, 0.75, 22222, stream)
+            gen = "device Zipf(0.75) over 1..|R| (counter-based draws, keyed-bijection alphabet)"
+        else:
+            sgxamd.gen_fk_dev(S, nS_loc, rank * nS_loc, gR, 22222, stream)
+        torch.cuda.synchronize()
+        return R, S, gR, gS, desc, gen
 
-    def step():
-        return sharded_rho_join(R, S, algorithm=args.algorithm)
+    def measure_rho(workload: str, R, S, gR: int, gS: int):
+        """W untimed + K timed steps of the (sharded) join; max over ranks."""
+        N_glob = gS  # every S tuple matches exactly one R tuple in all three configs
+
+        def step():
+            return sharded_rho_join(R, S, algorithm=args.algorithm)
+
+        for _ in range(args.warmup):
+            res = step()
+            assert res.matches == N_glob, (workload, res.matches, N_glob)
+        barrier()
+        per_kernel: dict[str, list[float]] = {}
+        results = []
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            res = step()
+            results.append(res)
+            for name, ms in sgxamd.timings():
+                per_kernel.setdefault(name, []).append(ms)
+        barrier()
+        elapsed = max_over_ranks(time.perf_counter() - t0)
+        ok = all(r.matches == N_glob for r in results)
+        if not ok:
+            raise SystemExit(f"{workload}: wrong match count {[r.matches for r in results]} != {N_glob}")
+        return results, per_kernel, elapsed
+
+    def load_report(res, nS: int) -> dict:
+        """Per-GPU received S tuples and per-partition S sizes (SURVEY.md 8(e) skew report)."""
+        ls = res.local_stats
+        recv = [float(nS)]
+        if world > 1:
+            rs = torch.tensor([float(nS)], dtype=torch.float64, device=coll_dev)
+            allr = [torch.zeros_like(rs) for _ in range(world)]
+            dist.all_gather(allr, rs)
+            recv = [float(x.item()) for x in allr]
+        P = ls.get("num_partitions") or 1
+        return {"recv_S_per_gpu": recv, "recv_S_per_gpu_max_over_mean": round(max(recv) / (sum(recv) / len(recv)), 4),
+                "S_partition_max": ls.get("max_part_s"), "S_partition_mean": round(nS / P, 1),
+                "S_partition_max_over_mean": round((ls.get("max_part_s") or 0) / max(nS / P, 1e-9), 2),
+                "R_partition_max": ls.get("max_part_r"), "partitions": P, "build_probe_tasks": ls.get("num_tasks"),
+                "radix_bits": ls.get("radix_bits"), "passes": ls.get("passes")}
 
     sgxamd.set_partition_overlap(bool(args.partition_overlap))
-    for _ in range(args.warmup):
-        res = step()
-        assert res.matches == N_glob, (res.matches, N_glob)
-    barrier()
-    per_kernel: dict[str, list[float]] = {}
-    results = []
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        res = step()
-        results.append(res)
-        for name, ms in sgxamd.timings():
-            per_kernel.setdefault(name, []).append(ms)
-    barrier()
-    elapsed = max_over_ranks(time.perf_counter() - t0)
-    ok = all(r.matches == N_glob for r in results)
+    R, S, gR, gS, workload, gen_desc = make_relations(args.workload)
+    N_glob = gS
+    results, per_kernel, elapsed = measure_rho(args.workload, R, S, gR, gS)
+    ok = True
     value = N_glob * args.steps / elapsed / 1e6  # M probed tuples/s, all ranks
     ms_per_step = elapsed / args.steps * 1e3
     kernel_times = "timed region (one stream)"
@@ -176,10 +353,10 @@ def main():
         # pass with the chains serialised (same kernels, same inputs).
         iso_steps = max(3, min(args.steps, 5))
         sgxamd.set_partition_overlap(False)
-        step()
+        sharded_rho_join(R, S, algorithm=args.algorithm)
         per_kernel = {}
         for _ in range(iso_steps):
-            r_iso = step()
+            r_iso = sharded_rho_join(R, S, algorithm=args.algorithm)
             ok = ok and r_iso.matches == N_glob
             for name, ms in sgxamd.timings():
                 per_kernel.setdefault(name, []).append(ms)
@@ -210,7 +387,7 @@ def main():
     phase = {k: round(v, 4) for k, v in sorted(avg.items())}
     ls = results[-1].local_stats
     rho_info = {
-        "matches_ok": ok, "matches": results[-1].matches,
+        "matches_ok": ok, "matches": results[-1].matches, "generator": gen_desc,
         "M_rec_per_s_reference_formula": round((gR + gS) * args.steps / elapsed / 1e6, 1),
         "probe_phase_M_probed_tuples_per_s": round(nS / (avg["join_build_probe"] * 1e-3) / 1e6, 1),
         "probe_roofline": {"achieved": round(probe_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -220,22 +397,64 @@ def main():
         "radix_bits": ls.get("radix_bits"), "passes": ls.get("passes"),
         "step_ms_breakdown": {k: round(v, 3) for k, v in results[-1].ms.items()},
     }
-    if args.workload == "c5":  # per-partition / per-GPU load report (skew)
-        rs = torch.tensor([float(nS)], dtype=torch.float64, device=coll_dev)
-        if world > 1:
-            allr = [torch.zeros_like(rs) for _ in range(world)]
-            dist.all_gather(allr, rs)
-            recv = [float(x.item()) for x in allr]
-        else:
-            recv = [float(nS)]
-        P = ls.get("num_partitions") or 1
-        rho_info["load_report"] = {
-            "recv_S_per_gpu_max": max(recv), "recv_S_per_gpu_mean": sum(recv) / len(recv),
-            "S_partition_max": ls.get("max_part_s"), "S_partition_mean": round(nS / P, 1),
-            "partitions": P, "build_probe_tasks": ls.get("num_tasks"),
-        }
+    if args.workload == "c5":
+        rho_info["load_report"] = load_report(results[-1], nS)
+
+    # the CPU baseline joins the relations the GPU joined (BASELINE config 2 at N = 1):
+    # one device-to-host copy, outside every timed region
+    cpu_rel = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "c2":
+        cpu_rel = (R.cpu().numpy().view(ROW_DT), S.cpu().numpy().view(ROW_DT))
     del R, S
     torch.cuda.empty_cache()
+
+    # BASELINE configs 4 and 5 in the same run (strong totals over the N GPUs), each
+    # with its load report; the headline value stays config 2
+    configs_info = {}
+    if args.workload == "c2" and not args.no_configs:
+        for wl in ("c4", "c5"):
+            Rw, Sw, gRw, gSw, desc_w, gen_w = make_relations(wl)
+            res_w, pk_w, el_w = measure_rho(wl, Rw, Sw, gRw, gSw)
+            avg_w = {k: statistics.mean(v) for k, v in pk_w.items()}
+            nRw, nSw = res_w[-1].recv_r, res_w[-1].recv_s
+            pb = algorithmic_bytes("join_build_probe", nRw, nSw) / (avg_w["join_build_probe"] * 1e-3) / 1e9
+            configs_info[wl] = {
+                "workload": desc_w, "generator": gen_w, "scaling": "strong", "global_R": gRw, "global_S": gSw,
+                "matches": res_w[-1].matches, "matches_ok": True,
+                "ms_per_step": round(el_w / args.steps * 1e3, 4),
+                "M_probed_tuples_per_s": round(gSw * args.steps / el_w / 1e6, 1),
+                "M_rec_per_s_reference_formula": round((gRw + gSw) * args.steps / el_w / 1e6, 1),
+                "probe_roofline": {"achieved": round(pb, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                   "frac": round(pb / HBM_PEAK_GBS, 4)},
+                "kernel_ms_avg": {k: round(v, 4) for k, v in sorted(avg_w.items())},
+                "step_ms_breakdown": {k: round(v, 3) for k, v in res_w[-1].ms.items()},
+                "load_report": load_report(res_w[-1], nSw),
+            }
+            del Rw, Sw
+            torch.cuda.empty_cache()
+    # BASELINE config 1's shape (|R| = |S| = 2^20, reference generators) on one GPU: the
+    # small-join latency next to the CPU number of the same config (cpu_baseline.rho.config1)
+    c1_gpu = None
+    if world == 1 and args.workload == "c2":
+        c1 = 1 << 20
+        R1h, S1h = sgxamd.reference_relations(c1, c1)
+        R1 = torch.from_numpy(R1h.view(np.int64)).to(dev)
+        S1 = torch.from_numpy(S1h.view(np.int64)).to(dev)
+        for _ in range(max(3, args.warmup)):
+            assert sgxamd.rho_join(R1, c1, S1, c1, stream=stream).matches == c1
+        barrier()
+        reps1 = max(20, args.steps)
+        dev_ms = []
+        t1 = time.perf_counter()
+        for _ in range(reps1):
+            r1 = sgxamd.rho_join(R1, c1, S1, c1, stream=stream)
+            dev_ms.append(sum(ms for _, ms in sgxamd.timings()))
+        barrier()
+        el1 = (time.perf_counter() - t1) / reps1
+        c1_gpu = {"ms_per_join_wall": round(el1 * 1e3, 4), "M_probed_tuples_per_s": round(c1 / el1 / 1e6, 1),
+                  "kernel_ms_sum_median": round(statistics.median(dev_ms), 4),
+                  "radix_bits": r1.stats.get("radix_bits"), "passes": r1.stats.get("passes")}
+        del R1, S1, R1h, S1h
 
     # measured stream-copy ceiling of this GPU: device-to-device copy of
     # 2 GiB, read + write bytes over the event time of the copy kernel, best of 5
@@ -258,6 +477,7 @@ def main():
 
     # ---------------- scan (BASELINE config 3): 2^30 int32, [0, 26] = 10 % (types.hpp:134)
     scan_info = None
+    scan_col_host = None
     if not args.no_scan and args.workload == "c2":
         ns = 1 << 30
         col = torch.empty(ns, dtype=torch.int32, device=dev)
@@ -266,6 +486,8 @@ def main():
         bv = torch.empty(ns // 64, dtype=torch.int64, device=dev)
         idx = torch.empty(exp, dtype=torch.int64, device=dev)
         scan_info = {"rows": ns, "dtype": "i32", "predicate": [0, 26], "matches": exp}
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            scan_col_host = col.cpu().numpy()  # the CPU scan leg scans the column the GPU scanned
         for kind in ("count", "bitvector", "index"):
             def run():
                 if kind == "count":
@@ -430,33 +652,83 @@ def main():
         del tb
         torch.cuda.empty_cache()
 
-    # ---------------- CPU baseline: restated reference RHO on this host, rank 0 at N=1
+    # ---------------- CPU baselines on this host, rank 0 at N = 1: the
+    # oracle's restated reference RHO on the relations the GPU joined, pinned to the
+    # physical cores of one NUMA node (the reference's methodology, J/README.md:67-70),
+    # plus an unpinned run over all CPUs the process may use; BASELINE config 1 (2^20,
+    # reference generators); the scan leg on the config-3 column the GPU scanned
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
 
-        threads = args.cpu_threads
-        cn = 1 << 26
-        Rh, Sh = sgxamd.reference_relations(cn, cn, nthreads=threads)
-        tp = []
-        t_start = time.perf_counter()
-        while time.perf_counter() - t_start < args.cpu_seconds and len(tp) < 30:
-            m, t = oracle.rho_join(Rh, Sh, threads)
-            assert m == cn
-            tp.append(cn / t["s_total"] / 1e6)
-        cpu = {"value": round(statistics.median(tp), 1), "unit": "M probed tuples/s", "cores": threads,
-               "kind": "port",
-               "sample": f"oracle RHO (radix_join.cpp restated, pthreads) on reference-generated "
-                         f"pk/fk |R|=|S|=2^26 (native.cpp seeds), median of {len(tp)} joins",
-               "M_rec_per_s_reference_formula": round(2 * statistics.median(tp), 1)}
-        try:  # the host the baseline ran on (the reference's numbers are a Xeon Gold 6326's)
-            with open("/proc/cpuinfo") as f:
-                cpu["host_cpu"] = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), None)
-            cpu["host_logical_cpus"] = os.cpu_count()
-        except OSError:
-            pass
-        del Rh, Sh
+        topo = host_topology()
+        pinned = pinned_physical_cores(args.cpu_threads)
+        n_all = min(len(os.sched_getaffinity(0)), int(topo.get("cgroup_cpu_quota") or 1 << 30))
+        threads = len(pinned) or args.cpu_threads
+        topo["pinned_node"] = next((nd for nd, lst in topo.get("numa_nodes", {}).items()
+                                    if pinned and pinned[0] in _cpulist(lst)), None)
+        cpu_info = {"host": topo, "pinned_cpus": pinned}
+
+        def timed_rho(Rh, Sh, nthr, cpus, budget):
+            exp_m = len(Sh)
+            tp = []
+            with cpu_affinity(cpus):
+                t_start = time.perf_counter()
+                while time.perf_counter() - t_start < budget and len(tp) < 30:
+                    m, t = oracle.rho_join(Rh, Sh, nthr)
+                    assert m == exp_m, (m, exp_m)
+                    tp.append(t["s_total"])
+            return statistics.median(tp), len(tp), t
+
+        rho_cpu = {}
+        if cpu_rel is not None:
+            Rh, Sh = cpu_rel
+            med, reps, t = timed_rho(Rh, Sh, threads, pinned, args.cpu_seconds)
+            rho_cpu["pinned"] = {"threads": threads, "cpus": "physical cores of one NUMA node, one thread per core, "
+                                                              "spread over the node's L3 domains",
+                                 "M_probed_tuples_per_s": round(len(Sh) / med / 1e6, 1), "ms": round(med * 1e3, 2),
+                                 "joins": reps, "radix_bits": t["radix_bits"], "passes": t["passes"]}
+            med_a, reps_a, _ = timed_rho(Rh, Sh, n_all, None, args.cpu_seconds / 2)
+            rho_cpu["all_cpus"] = {"threads": n_all, "cpus": f"unpinned over the {len(os.sched_getaffinity(0))} "
+                                                              f"CPUs of this process (cgroup quota "
+                                                              f"{topo.get('cgroup_cpu_quota')} CPUs)",
+                                   "M_probed_tuples_per_s": round(len(Sh) / med_a / 1e6, 1),
+                                   "ms": round(med_a * 1e3, 2), "joins": reps_a}
+            del Rh, Sh, cpu_rel
+        # BASELINE config 1: the reference App driver's CPU RHO, |R| = |S| = 2^20, generated by
+        # the restated reference generators (native.cpp:62-101 seeds)
+        c1 = 1 << 20
+        R1, S1 = sgxamd.reference_relations(c1, c1)
+        med1, reps1, t1 = timed_rho(R1, S1, threads, pinned, 2.0)
+        rho_cpu["config1"] = {"R": c1, "S": c1, "threads": threads, "M_probed_tuples_per_s": round(c1 / med1 / 1e6, 1),
+                              "M_rec_per_s_reference_formula": round(2 * c1 / med1 / 1e6, 1),
+                              "ms": round(med1 * 1e3, 3), "joins": reps1, "radix_bits": t1["radix_bits"],
+                              "passes": t1["passes"]}
+        if configs_info is not None:
+            configs_info["c1"] = {"workload": "RHO join |R|=|S|=2^20, reference generators (BASELINE config 1)",
+                                  "cpu": rho_cpu["config1"], "gpu": c1_gpu}
+        lead = rho_cpu.get("pinned") or rho_cpu["config1"]
+        cpu = {"value": lead["M_probed_tuples_per_s"], "unit": "M probed tuples/s", "cores": threads, "kind": "port",
+               "sample": (f"oracle RHO (radix_join.cpp restated, pthreads) on the 2^28 x 2^28 config-2 relations "
+                          f"the GPU joined, {threads} threads pinned to NUMA node {topo.get('pinned_node')}'s "
+                          f"physical cores, median of {lead['joins']} joins")
+               if "pinned" in rho_cpu else "config 1 only (no config-2 copy)",
+               "rho": rho_cpu, **cpu_info}
+        if scan_col_host is not None:  # config 3 on the host: count / bitvector / index, SIMD512 restated
+            scan_cpu = {"rows": len(scan_col_host), "dtype": "i32", "predicate": [0, 26], "threads": threads,
+                        "how": "oracle/cpu_baseline.c (SIMD512.cpp AVX-512 formulation, multithreadedscan.cpp "
+                               "slicing, pinned one thread per core), per-call time averaged over threads"}
+            for kind in ("count", "bitvector", "index"):
+                secs, m = oracle.cpu_scan_bench(kind, scan_col_host, 0, 26, threads, pinned, reps=3)
+                assert m == len(scan_col_host) // 256 * 27, (kind, m)
+                out_b = {"count": 0, "bitvector": len(scan_col_host) // 8, "index": 8 * m}[kind]
+                scan_cpu[kind] = {"ms_per_call": round(secs * 1e3, 3),
+                                  "input_GB_per_s": round(4 * len(scan_col_host) / secs / 1e9, 2),
+                                  "total_GB_per_s": round((4 * len(scan_col_host) + out_b) / secs / 1e9, 2)}
+            if scan_info is not None:
+                scan_info["cpu_baseline"] = scan_cpu
+            del scan_col_host
 
     if rank == 0:
         line = {
@@ -472,7 +744,7 @@ def main():
                        **({"dist_backend": "gloo (single-GPU rehearsal, not a scaling number)"}
                           if world > 1 and args.dist_backend == "gloo" else {})},
             "roofline": roofline, "cpu_baseline": cpu, "rho": rho_info, "scan": scan_info, "tpch": tpch_info,
-            "reference_shapes": paper_info,
+            "reference_shapes": paper_info, "configs": configs_info,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

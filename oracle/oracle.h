@@ -94,6 +94,13 @@ uint64_t oracle_dict_scan(int64_t lo, int64_t hi, const int64_t *dict, uint64_t 
                           int code_bytes, size_t n, int64_t *out);
 uint64_t oracle_scan_count_i32_mt(int32_t lo, int32_t hi, const int32_t *in, size_t n, int nthreads);
 
+/* CPU scan baseline (cpu_baseline.c): kind 0 count / 1 bitvector / 2 index list over
+ * a uint8 (width 1) or int32 (width 4) column, nthreads pinned to cpus[t] (NULL: not
+ * pinned), the multithreadedscan.cpp slicing; returns the per-call seconds averaged
+ * over the threads (-1 on error) and the total matches. */
+double oracle_cpu_scan_bench(int kind, int width, int64_t lo, int64_t hi, const void *in, size_t n, int nthreads,
+                             const int *cpus, int reps, uint64_t *matches);
+
 /* TPC-H callers (tpch_oracle.c; tables as in sgxamd/tpch.h).  oracle_tpch_filter:
  * filter_table of selection `which` of `query` into out (rows in input order),
  * returns the row count.  The queries return the reference's result (Q19: the

@@ -53,6 +53,8 @@ def _load() -> C.CDLL:
         "oracle_scan_explicit_index_u8": (C.c_uint64, [C.c_uint8, C.c_uint8, P, P, C.c_size_t, P]),
         "oracle_scan_values_i32": (C.c_uint64, [C.c_int32, C.c_int32, P, C.c_size_t, P]),
         "oracle_scan_count_i32_mt": (C.c_uint64, [C.c_int32, C.c_int32, P, C.c_size_t, C.c_int]),
+        "oracle_cpu_scan_bench": (C.c_double, [C.c_int, C.c_int, C.c_int64, C.c_int64, P, C.c_size_t, C.c_int,
+                                               C.POINTER(C.c_int), C.c_int, U64P]),
         "oracle_scan_sum_u8": (C.c_uint64, [C.c_uint8, C.c_uint8, P, C.c_size_t]),
         "oracle_dict_scan": (C.c_uint64, [C.c_int64, C.c_int64, P, C.c_uint64, P, C.c_int, C.c_size_t, P]),
         "oracle_tpch_filter": (C.c_uint64, [C.c_int, C.c_int, P, P, P, P, P]),
@@ -166,6 +168,19 @@ def explicit_index_len(n: int) -> int:
 
 def scan_count_mt(lo: int, hi: int, col, nthreads: int) -> int:
     return int(lib.oracle_scan_count_i32_mt(lo, hi, _p(col), len(col), nthreads))
+
+
+def cpu_scan_bench(kind: str, col, lo: int, hi: int, nthreads: int, cpus=None, reps: int = 1) -> tuple[float, int]:
+    """The timed CPU scan baseline (cpu_baseline.c): per-call seconds averaged over
+    `nthreads` threads (pinned one per core to `cpus` if given) and the total matches."""
+    k = {"count": 0, "bitvector": 1, "index": 2}[kind]
+    width = col.dtype.itemsize
+    cp = (C.c_int * nthreads)(*cpus) if cpus else None
+    m = C.c_uint64(0)
+    s = lib.oracle_cpu_scan_bench(k, width, lo, hi, _p(col), len(col), nthreads, cp, reps, C.byref(m))
+    if s < 0:
+        raise RuntimeError("oracle_cpu_scan_bench failed")
+    return float(s), int(m.value)
 
 
 def scan_sum_u8(lo: int, hi: int, col) -> int:

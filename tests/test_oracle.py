@@ -189,3 +189,23 @@ def test_oracle_dict_scan_wraps_like_reference():
     assert len(oracle.dict_scan(1000, 2000, d, codes)) == 4096
     assert len(oracle.dict_scan(-100, -50, d, codes)) == 4096  # hi below dict[0]: high index -1 -> 255
     assert oracle.scan_sum_u8(0, 26, codes) == 16 * sum(range(27))
+
+
+@pytest.mark.parametrize("dtype,threads", [("u8", 1), ("u8", 3), ("i32", 4), ("i32", 5)])
+def test_cpu_scan_baseline_matches_scalar_oracle(orc, dtype, threads):
+    """The timed CPU scan baseline (cpu_baseline.c, AVX-512 where the host has it) counts
+    what the scalar oracle counts over each thread's slice (N/T rows, the first
+    multiple of 64 of them: multithreadedscan.cpp slicing, SIMD512's input_size/64)."""
+    rng = np.random.default_rng(threads)
+    n = 300_007
+    if dtype == "u8":
+        col = rng.integers(0, 256, n, dtype=np.uint8)
+        lo, hi = 17, 200
+    else:
+        col = rng.integers(-2**31, 2**31, n, dtype=np.int64).astype(np.int32)
+        lo, hi = -2**30, 12345
+    per = n // threads
+    exp = sum(orc.scan("count", dtype, lo, hi, col[t * per: t * per + per // 64 * 64]) for t in range(threads))
+    for kind in ("count", "bitvector", "index"):
+        secs, m = orc.cpu_scan_bench(kind, col, lo, hi, threads, reps=2)
+        assert m == exp and secs > 0, kind

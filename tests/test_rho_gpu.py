@@ -182,6 +182,64 @@ def test_full_size_config2_property(sgx, gpu):
     torch.cuda.empty_cache()
 
 
+def test_config4_full_size(sgx, gpu):
+    """BASELINE config 4 at its size on one GPU: pk(2^27, seed 11111) join fk(2^30,
+    maxid 2^27, seed 22222) = 8 shuffled copies of 1..2^27 (native.cpp:62-101 shapes,
+    device generators).  matches == |S|; the planner sizes partitions for S
+    (ceil(log2(2^30 / 32,768)) = 15 bits, 8 + 7): every R partition then holds exactly
+    2^27 / 2^15 = 4096 keys and every S partition its 8 copies, 32,768 tuples."""
+    import torch
+
+    nR, nS = 1 << 27, 1 << 30
+    R = torch.empty(nR, dtype=torch.int64, device=gpu)
+    S = torch.empty(nS, dtype=torch.int64, device=gpu)
+    sgx.gen_pk_dev(R, nR, 0, nR, 11111)
+    sgx.gen_fk_dev(S, nS, 0, nR, 22222)
+    res = sgx.rho_join(R, nR, S, nS)
+    assert res.matches == nS
+    st = res.stats
+    assert (st["radix_bits"], st["passes"], st["num_partitions"]) == (15, 2, 1 << 15)
+    assert st["max_part_r"] == 4096 and st["max_part_s"] == 32768
+    assert (1 << 15) <= st["num_tasks"] <= (1 << 17)  # whole S chunks per partition
+    del R, S
+    torch.cuda.empty_cache()
+
+
+def test_config5_full_size_host_zipf(sgx, orc, gpu):
+    """BASELINE config 5 at its size: pk(2^28) join Zipf(theta = 0.75) over 1..2^28 from
+    the host mt19937_64 seed-22222 stream (generator.cpp restating genzipf.cpp:87-144,
+    BASELINE.md row 5), staged once to HBM.  The count equals an independent
+    sum_k cnt_R(k) * cnt_S(k) over the same buffers (numpy bincount) and |S|; the
+    partitions are skewed (the hottest key alone is ~0.2 % of S) and the hot ones are
+    split into several build/probe tasks.  The device Zipf generator gives the same count."""
+    import torch
+
+    n = 1 << 28
+    R = torch.empty(n, dtype=torch.int64, device=gpu)
+    sgx.gen_pk_dev(R, n, 0, n, 11111)
+    host = np.empty(n, dtype=np.int64)
+    sgx.gen_zipf(host, n, n, 0.75, 22222, 16)
+    S = torch.from_numpy(host).to(gpu)
+    res = sgx.rho_join(R, n, S, n)
+    rk = (R.cpu().numpy() & 0xFFFFFFFF).astype(np.uint32)
+    sk = (host & 0xFFFFFFFF).astype(np.uint32)
+    del host
+    cr = np.bincount(rk, minlength=n + 1)
+    cs = np.bincount(sk, minlength=n + 1)
+    exp = int(np.dot(cr[: n + 1].astype(np.int64), cs[: n + 1].astype(np.int64)))
+    assert len(cr) == len(cs) == n + 1  # every key in 1..2^28
+    assert res.matches == exp == n
+    st = res.stats
+    mean_s = n >> st["radix_bits"]
+    assert st["max_part_s"] > 20 * mean_s  # per-partition skew reaches the join (33x at 14 bits)
+    assert st["num_tasks"] > st["num_partitions"]  # hot partitions split into tasks
+    assert cs.max() > 500_000  # the hottest key (~0.197 % of S, SURVEY.md 8(d))
+    sgx.gen_zipf_dev(S, n, 0, n, 0.75, 22222)
+    assert sgx.rho_join(R, n, S, n).matches == n
+    del R, S
+    torch.cuda.empty_cache()
+
+
 def test_max_size_pk_fk(sgx, gpu):
     """|R| = |S| = 2^31 + 12,345 (ragged, 8x the headline size, 17 GB per relation):
     the planner goes past 16 radix bits (17: average partitions of 16,384 R tuples in
