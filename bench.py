@@ -741,6 +741,8 @@ def main():
                     + " relations, 8-byte {key, payload} tuples",
             "config": {"workload": workload, "algorithm": args.algorithm, "global_R": gR, "global_S": gS,
                        "parallelism": f"radix-shard{world}",
+                       **({"exchange": results[-1].ms.get("impl", "torch.distributed all_to_all_single (sgxamd.dist)")}
+                          if world > 1 else {}),
                        **({"dist_backend": "gloo (single-GPU rehearsal, not a scaling number)"}
                           if world > 1 and args.dist_backend == "gloo" else {})},
             "roofline": roofline, "cpu_baseline": cpu, "rho": rho_info, "scan": scan_info, "tpch": tpch_info,

@@ -1,0 +1,99 @@
+/*
+ * sgxamd/multi.h — C-ABI of the multi-GPU RHO join (radix-shard exchange).
+ *
+ * The reference runs RHO with NTHREADS pthreads, each owning a contiguous slice of
+ * R and S (radix_join.cpp:1457-1500), sharing the partitioned tmpR/tmpS arrays
+ * (:1421-1433) through memory.  Across GPUs the slices stay where they are; the
+ * first radix level (the low log2(G) key bits) picks the owning GPU, and one
+ * exchange step moves every tuple to its owner:
+ *   1. per relation, in pieces: stable shard partition of the local slice by
+ *      d = key & (G - 1) (the pass-1 machinery of radix_join.cpp:851-931 with G bins);
+ *   2. the G x G piece counts (RCCL all-gather of the per-destination counts);
+ *   3. the tuples (RCCL send/recv per peer, on a communication stream, while the next
+ *      piece is partitioned), into a contiguous receive buffer per relation;
+ *   4. the local join of the received relations with key_shift = log2(G) (R's local
+ *      passes while S is still on the wire);
+ *   5. an RCCL all-reduce of the match counts.
+ * The caller, native.cpp:137 -> run_join -> RHO, is unchanged: RHO() (joins.hpp)
+ * takes this path when SGXAMD_GPUS > 1 (joinconfig_t has no spare field for a GPU
+ * count).
+ *
+ * Transports:
+ *   MI355_TRANSPORT_RCCL      — RCCL over xGMI, one rank per GPU (librccl.so.1 is
+ *                               loaded on first use);
+ *   MI355_TRANSPORT_REHEARSAL — G logical ranks on the current GPU, each with its own
+ *                               stream and workspace, the exchange done by device-to-
+ *                               device copies: the whole C++ path on one GPU, for tests;
+ *   MI355_TRANSPORT_AUTO      — RCCL when G devices are visible, else rehearsal.
+ *   SGXAMD_MULTI_TRANSPORT=rccl|rehearsal overrides AUTO.
+ * G must be a power of two (1..256).  Counting joins only (MATERIALIZE stays on one GPU).
+ */
+#ifndef SGXAMD_MULTI_H
+#define SGXAMD_MULTI_H
+
+#include "sgxamd/rho.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MI355_TRANSPORT_AUTO 0
+#define MI355_TRANSPORT_RCCL 1
+#define MI355_TRANSPORT_REHEARSAL 2
+
+#define MI355_ERR_COMM (-6) /* an RCCL call failed (or librccl.so.1 is missing); see mi355_last_error() */
+
+typedef struct mi355_multi_stats {
+    uint64_t matches;          /* global join cardinality (sum over ranks) */
+    int world;                 /* ranks (GPUs) */
+    int transport;             /* MI355_TRANSPORT_RCCL or MI355_TRANSPORT_REHEARSAL */
+    int pieces;                /* pieces per relation in the exchange */
+    int rank;                  /* the calling rank (one process per GPU), else 0 */
+    uint64_t local_matches;    /* this rank's matches (rank 0 in single-process mode) */
+    uint64_t recv_r_max, recv_r_min;  /* received R tuples per rank (load report) */
+    uint64_t recv_s_max, recv_s_min;  /* received S tuples per rank */
+    uint64_t max_part_s;       /* largest local S partition over the ranks seen */
+    uint64_t sent_bytes;       /* tuple bytes sent to other ranks (ranks seen) */
+    double ms_total;           /* wall time of the call (max over the ranks seen) */
+    double ms_exchange_post;   /* shard partitions + count exchanges + posting the pieces */
+    double ms_local;           /* from the last piece posted to the local join's end */
+    double ms_allreduce;       /* final match-count all-reduce */
+    mi355_rho_stats local;     /* the local join of rank 0 (or of the calling rank) */
+} mi355_multi_stats;
+
+/* Single process, `ngpus` ranks driven by one host thread each.  R and S are host or
+ * device memory (device memory of the current GPU); rank g joins the slice
+ * [g*floor(n/G), ...) of each relation (the last rank takes the remainder), staged to
+ * its GPU.  opts: algorithm / radix_bits / passes of the local joins (NULL = defaults);
+ * key_shift, materialize and stream must be 0. */
+int mi355_rho_join_multi_ex(const struct row_t *R, uint64_t nR, const struct row_t *S, uint64_t nS, int ngpus,
+                            int transport, const mi355_rho_opts *opts, mi355_multi_stats *stats);
+
+/* Drop-in multi-GPU RHO on reference relations (counting join; fills out like
+ * mi355_rho_join, throughput = (|R|+|S|) / call time). */
+int mi355_rho_join_multi(const struct table_t *relR, const struct table_t *relS, const struct joinconfig_t *config,
+                         int ngpus, struct result_t *out);
+
+/* One process per GPU (torchrun / MPI style).  Rank 0 creates a unique id
+ * (128 bytes), the caller distributes it, every rank creates its communicator on
+ * its current device (collective), then calls mi355_rho_join_sharded with its
+ * device-resident slices (collective; the same `pieces` everywhere).  The rank's
+ * compute runs on opts->stream (else the mi355_set_stream stream, else the library's);
+ * the exchange on a communication stream of its own. */
+int mi355_multi_unique_id(void *id128);
+int mi355_multi_comm_init(const void *id128, int nranks, int rank, void **comm);
+int mi355_multi_comm_destroy(void *comm);
+int mi355_rho_join_sharded(void *comm, const struct row_t *R, uint64_t nR, const struct row_t *S, uint64_t nS,
+                           const mi355_rho_opts *opts, mi355_multi_stats *stats);
+
+/* Statistics of this thread's last multi-GPU join (either entry point). */
+int mi355_last_multi_stats(mi355_multi_stats *out);
+
+/* Pieces each relation is exchanged in (default 4; 1..64); applies to later calls. */
+void mi355_multi_set_pieces(int pieces);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* SGXAMD_MULTI_H */

@@ -5,6 +5,7 @@
 //      SGXv2Scripts/scripts/helpers/runner.py:14-55 parses our output unchanged.
 // run_join: joins.cpp:55-78 (strcmp lookup in an algorithm table, memcpy of the
 //      result; like the reference, the callee's result_t is not freed).
+#include <algorithm>
 #include <chrono>
 #include <cstdarg>
 #include <cstdio>
@@ -12,6 +13,7 @@
 #include <cstring>
 
 #include "sgxamd/joins.hpp"
+#include "sgxamd/multi.h"
 #include "sgxamd/rho.h"
 
 namespace {
@@ -35,6 +37,19 @@ void logger(const char *level, const char *color, const char *fmt, ...) {
 uint64_t cpms() {  // CYCLES_PER_MICROSECOND of the reference build (J/CMakeLists.txt:17)
     const char *e = std::getenv("SGXAMD_CPMS");
     return e ? std::strtoull(e, nullptr, 10) : 2900ull;
+}
+
+// GPUs for RHO(): SGXAMD_GPUS (joinconfig_t has no spare field); > 1 runs
+// the radix-shard exchange of sgxamd/multi.h (counting joins).
+int gpus_from_env() {
+    const char *e = std::getenv("SGXAMD_GPUS");
+    return e ? std::max(1, std::atoi(e)) : 1;
+}
+
+int rho_entry(const table_t *relR, const table_t *relS, const joinconfig_t *config, result_t *out) {
+    const int g = gpus_from_env();
+    if (g > 1 && !(config && config->MATERIALIZE)) return mi355_rho_join_multi(relR, relS, config, g, out);
+    return mi355_rho_join(relR, relS, config, out);
 }
 
 const algorithm_t mi355_algorithms[] = {  // joins.cpp:33-53, the radix joins this library replaces
@@ -66,6 +81,15 @@ result_t *radix_dropin(const char *name, const table_t *relR, const table_t *rel
     const uint64_t C = cpms();
     auto cyc = [&](double ms) { return static_cast<unsigned long>(ms * 1000.0 * C); };
     const double n = num ? (double)num : 1.0;
+    if (join == rho_entry && gpus_from_env() > 1 && !(config && config->MATERIALIZE)) {
+        mi355_multi_stats ms{};
+        mi355_last_multi_stats(&ms);
+        LOG_INFO("Radix-shard exchange over %d GPUs (%s, %d pieces per relation): received R %lu..%lu, "
+                 "S %lu..%lu tuples per GPU, %lu bytes over the links; phase lines below: GPU 0's local join",
+                 ms.world, ms.transport == MI355_TRANSPORT_RCCL ? "RCCL" : "one-GPU rehearsal", ms.pieces,
+                 (unsigned long)ms.recv_r_min, (unsigned long)ms.recv_r_max, (unsigned long)ms.recv_s_min,
+                 (unsigned long)ms.recv_s_max, (unsigned long)ms.sent_bytes);
+    }
     LOG_INFO("Running %s with %u passes and %u radix bits", name, st.passes, st.radix_bits);
     LOG_INFO("Total input tuples : %u", (unsigned)num);
     LOG_INFO("Result tuples : %lu", (unsigned long)st.matches);
@@ -99,7 +123,7 @@ result_t *radix_dropin(const char *name, const table_t *relR, const table_t *rel
 }  // namespace
 
 result_t *RHO(const table_t *relR, const table_t *relS, const joinconfig_t *config) {
-    return radix_dropin("RHO", relR, relS, config, mi355_rho_join);
+    return radix_dropin("RHO", relR, relS, config, rho_entry);
 }
 
 result_t *RHT(const table_t *relR, const table_t *relS, const joinconfig_t *config) {

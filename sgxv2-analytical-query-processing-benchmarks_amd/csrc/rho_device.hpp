@@ -15,6 +15,18 @@ int join_device(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const
                 const mi355_rho_opts *opts, mi355_rho_stats *st, output_triple_t *out, uint64_t out_cap,
                 DeviceBuffer *grow = nullptr);
 
+// Multi-GPU building blocks (multi_host.cpp), on a context the caller holds:
+// the stable shard partition by destination (host counts; synchronises s), and the
+// two halves of the pipelined local join (begin enqueues R's passes on s and returns;
+// finish runs S's passes and the build/probe on the same stream and waits).
+int shard_partition_device(Context *ctx, hipStream_t s, const row_t *in, uint64_t n, uint32_t key_shift,
+                           uint32_t dest_bits, row_t *out, uint64_t *dest_counts);
+int join_pipelined_begin(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, uint64_t nS,
+                         const mi355_rho_opts *opts);
+int join_pipelined_finish(Context *ctx, const row_t *dS, uint64_t nS, mi355_rho_stats *st);
+// What mi355_last_join_stats reports for this thread's last join (multi-GPU calls).
+void set_last_join_stats(const mi355_rho_stats &st);
+
 // Host chunked table (ChunkedTable.cpp layout) holding a copy of n triples.
 chunked_table_t *make_chunked_table(const output_triple_t *src, uint64_t n);
 

@@ -472,6 +472,22 @@ int join_device(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const
     return join_finish(ctx, pj, dS, nS, st, out, out_cap, grow, false);
 }
 
+int join_pipelined_begin(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, uint64_t nS,
+                         const mi355_rho_opts *opts) {
+    PendingJoin &pj = pending_of(ctx);
+    if (pj.active) {
+        set_last_error("a pipelined join is already pending on this context");
+        return MI355_ERR_INVALID;
+    }
+    const int rc = join_begin(ctx, s, dR, nR, nS, opts, pj);
+    if (rc) pj.active = false;
+    return rc;
+}
+
+int join_pipelined_finish(Context *ctx, const row_t *dS, uint64_t nS, mi355_rho_stats *st) {
+    return join_finish(ctx, pending_of(ctx), dS, nS, st, nullptr, 0, nullptr, true);
+}
+
 // Stable partition by destination shard (multi-GPU exchange step).
 int shard_partition_device(Context *ctx, hipStream_t s, const row_t *in, uint64_t n, uint32_t key_shift,
                            uint32_t dest_bits, row_t *out, uint64_t *dest_counts) {
@@ -510,6 +526,8 @@ using namespace sgxamd;
 namespace {
 thread_local mi355_rho_stats g_last_stats{};
 }
+
+void rho::set_last_join_stats(const mi355_rho_stats &st) { g_last_stats = st; }
 
 extern "C" {
 

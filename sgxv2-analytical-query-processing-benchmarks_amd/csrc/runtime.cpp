@@ -142,17 +142,31 @@ Context *current_context(int *status) {
     std::lock_guard<std::mutex> lk(g_ctx_mu);
     auto it = g_ctx.find(dev);
     if (it != g_ctx.end()) return it->second.get();
+    auto ctx = make_context(dev, status);
+    if (!ctx) return nullptr;
+    Context *raw = ctx.get();
+    g_ctx[dev] = std::move(ctx);
+    return raw;
+}
+
+std::unique_ptr<Context> make_context(int device, int *status) {
+    int prev = 0;
+    if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(device) != hipSuccess) {
+        set_last_error("hipSetDevice failed");
+        if (status) *status = MI355_ERR_HIP;
+        return nullptr;
+    }
     auto ctx = std::make_unique<Context>();
-    ctx->device = dev;
-    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipHostMalloc(reinterpret_cast<void **>(&ctx->host_result), 64 * sizeof(uint64_t)) != hipSuccess) {
+    ctx->device = device;
+    const bool ok = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) == hipSuccess &&
+                    hipHostMalloc(reinterpret_cast<void **>(&ctx->host_result), 64 * sizeof(uint64_t)) == hipSuccess;
+    (void)hipSetDevice(prev);
+    if (!ok) {
         set_last_error("stream / pinned allocation failed");
         if (status) *status = MI355_ERR_HIP;
         return nullptr;
     }
-    Context *raw = ctx.get();
-    g_ctx[dev] = std::move(ctx);
-    return raw;
+    return ctx;
 }
 
 hipStream_t thread_stream(Context *ctx, void *explicit_stream) {

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -84,11 +85,18 @@ struct Context {
     // scan workspace
     DeviceBuffer scan_in, scan_out, scan_aux, scan_dict;
     uint64_t *host_result = nullptr;  // pinned 64 x u64
+    // multi-GPU exchange workspace (multi_host.cpp): shard-partitioned send buffers and
+    // the receive buffers the peers' pieces land in
+    DeviceBuffer xsendR, xsendS, xrecvR, xrecvS;
 };
 
 // Context of the calling thread's current HIP device (created on first use).
 // Returns nullptr (and sets the last error) when no device is available.
 Context *current_context(int *status);
+// A context of its own on `device` (its own stream and workspace), for callers that run
+// several independent joins on one device: the multi-GPU rehearsal's logical ranks.
+// The caller keeps it for the process lifetime.  nullptr (last error set) on failure.
+std::unique_ptr<Context> make_context(int device, int *status);
 
 Timer &thread_timer();
 Timer &thread_side_timer();

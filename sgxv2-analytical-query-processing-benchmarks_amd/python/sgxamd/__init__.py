@@ -121,6 +121,34 @@ class rho_stats(C.Structure):
         return {f: getattr(self, f) for f, _ in self._fields_}
 
 
+class multi_stats(C.Structure):  # sgxamd/multi.h
+    _fields_ = [
+        ("matches", C.c_uint64),
+        ("world", C.c_int),
+        ("transport", C.c_int),
+        ("pieces", C.c_int),
+        ("rank", C.c_int),
+        ("local_matches", C.c_uint64),
+        ("recv_r_max", C.c_uint64),
+        ("recv_r_min", C.c_uint64),
+        ("recv_s_max", C.c_uint64),
+        ("recv_s_min", C.c_uint64),
+        ("max_part_s", C.c_uint64),
+        ("sent_bytes", C.c_uint64),
+        ("ms_total", C.c_double),
+        ("ms_exchange_post", C.c_double),
+        ("ms_local", C.c_double),
+        ("ms_allreduce", C.c_double),
+        ("local", rho_stats),
+    ]
+
+    def as_dict(self) -> dict:
+        d = {f: getattr(self, f) for f, _ in self._fields_ if f != "local"}
+        d["local"] = self.local.as_dict()
+        d["transport"] = {1: "rccl", 2: "rehearsal"}.get(self.transport, "?")
+        return d
+
+
 # TPC-H tables (sgxamd/tpch.h = TpcHTypes.hpp:53-87): column pointers, host or device.
 class LineItemTable(C.Structure):
     _fields_ = [("numTuples", C.c_uint64), ("l_orderkey", C.c_void_p), ("l_shipdate", C.c_void_p),
@@ -182,6 +210,18 @@ SIGNATURES = {
     "mi355_set_partition_overlap": (None, [C.c_int]),
     "mi355_timing_get": (C.c_int, [C.POINTER(C.c_char_p), C.POINTER(C.c_double), C.c_int]),
     "mi355_set_stream": (None, [_P]),
+    # multi.h
+    "mi355_rho_join_multi_ex": (C.c_int, [_P, C.c_uint64, _P, C.c_uint64, C.c_int, C.c_int, C.POINTER(rho_opts),
+                                          C.POINTER(multi_stats)]),
+    "mi355_rho_join_multi": (C.c_int, [C.POINTER(table_t), C.POINTER(table_t), C.POINTER(joinconfig_t), C.c_int,
+                                       C.POINTER(result_t)]),
+    "mi355_multi_unique_id": (C.c_int, [_P]),
+    "mi355_multi_comm_init": (C.c_int, [_P, C.c_int, C.c_int, C.POINTER(C.c_void_p)]),
+    "mi355_multi_comm_destroy": (C.c_int, [_P]),
+    "mi355_rho_join_sharded": (C.c_int, [_P, _P, C.c_uint64, _P, C.c_uint64, C.POINTER(rho_opts),
+                                         C.POINTER(multi_stats)]),
+    "mi355_last_multi_stats": (C.c_int, [C.POINTER(multi_stats)]),
+    "mi355_multi_set_pieces": (None, [C.c_int]),
     # scan.h
     "mi355_scan_count_u8": (C.c_int, [C.c_uint8, C.c_uint8, _P, C.c_size_t, _U64P]),
     "mi355_scan_count_i32": (C.c_int, [C.c_int32, C.c_int32, _P, C.c_size_t, _U64P]),
@@ -342,6 +382,51 @@ def rho_join_finish(S, nS: int, *, key_shift: int = 0, stream: int | None = None
     st = rho_stats()
     _check(lib.mi355_rho_join_finish(ptr(S), nS, C.byref(o), C.byref(st)))
     return JoinResult(int(st.matches), st.as_dict())
+
+
+TRANSPORTS = {"auto": 0, "rccl": 1, "rehearsal": 2}  # MI355_TRANSPORT_*
+
+
+def rho_join_multi(R, nR: int, S, nS: int, ngpus: int, *, transport: str = "auto", algorithm: str = "RHO",
+                   radix_bits: int = 0, passes: int = 0) -> JoinResult:
+    """Multi-GPU count join in one process (mi355_rho_join_multi_ex): ngpus ranks, the
+    radix-shard exchange over RCCL or the one-GPU rehearsal transport."""
+    o = rho_opts(radix_bits, passes, 0, 0, 0, ALGORITHMS[algorithm], None, None, 0)
+    st = multi_stats()
+    _check(lib.mi355_rho_join_multi_ex(ptr(R), nR, ptr(S), nS, ngpus, TRANSPORTS[transport], C.byref(o),
+                                       C.byref(st)))
+    return JoinResult(int(st.matches), st.as_dict())
+
+
+def multi_unique_id() -> bytes:
+    """128-byte RCCL unique id (rank 0 creates it, every rank passes it to multi_comm_init)."""
+    buf = C.create_string_buffer(128)
+    _check(lib.mi355_multi_unique_id(buf))
+    return buf.raw
+
+
+def multi_comm_init(uid: bytes, nranks: int, rank: int) -> int:
+    """This process's RCCL communicator on its current device (collective)."""
+    h = C.c_void_p()
+    buf = C.create_string_buffer(bytes(uid), 128)
+    _check(lib.mi355_multi_comm_init(buf, nranks, rank, C.byref(h)))
+    return h.value
+
+
+def multi_comm_destroy(handle: int) -> None:
+    _check(lib.mi355_multi_comm_destroy(handle))
+
+
+def rho_join_sharded(handle: int, R, nR: int, S, nS: int, *, algorithm: str = "RHO") -> JoinResult:
+    """One rank's part of the multi-GPU count join (collective; device-resident slices)."""
+    o = rho_opts(0, 0, 0, 0, 0, ALGORITHMS[algorithm], None, None, 0)
+    st = multi_stats()
+    _check(lib.mi355_rho_join_sharded(handle, ptr(R), nR, ptr(S), nS, C.byref(o), C.byref(st)))
+    return JoinResult(int(st.matches), st.as_dict())
+
+
+def multi_set_pieces(pieces: int) -> None:
+    lib.mi355_multi_set_pieces(pieces)
 
 
 def rho_join_tables(R, nR: int, S, nS: int, nthreads: int = 1, materialize: bool = False,

@@ -33,6 +33,13 @@ world x the local slice), so R' and S' are contiguous for the local join.
 
 G must be a power of two.  The local compute (steps 1 and 4) defaults to the
 HIP library; tests inject CPU restatements to run the exchange logic on gloo.
+
+With the "nccl" backend (RCCL) and device tensors the whole pipeline runs in C++
+(sgxamd/multi.h, mi355_rho_join_sharded): this module only hands rank 0's RCCL unique
+id to the other ranks and calls the library, whose rank pipeline is the one above
+(pieced shard partition, all-gather of the piece counts, send/recv of the tuples on a
+communication stream, pipelined local join, all-reduce).  SGXAMD_DIST_IMPL=python keeps
+the torch.distributed implementation below, which the gloo tests also exercise.
 """
 from __future__ import annotations
 
@@ -45,7 +52,8 @@ from dataclasses import dataclass, field
 import torch
 import torch.distributed as dist
 
-from . import rho_join, rho_join_begin, rho_join_finish, shard_partition
+from . import (Mi355Error, multi_comm_init, multi_unique_id, rho_join, rho_join_begin, rho_join_finish,
+               rho_join_sharded, shard_partition)
 
 
 def _log2_exact(g: int) -> int:
@@ -213,6 +221,42 @@ def _post_exchange(dst: torch.Tensor, src: torch.Tensor, send_counts: list[int],
     return dist.all_to_all_single(dst[:nr], src[:ns], recv_counts, send_counts, group=group, async_op=True)
 
 
+_comms: dict = {}
+_cxx_failed: list = []
+
+
+def _cxx_comm(group) -> int:
+    """This rank's RCCL communicator of the C++ path for `group` (collective on first use)."""
+    key = id(group)
+    if key not in _comms:
+        rank = dist.get_rank(group)
+        obj = [multi_unique_id() if rank == 0 else None]
+        src = dist.get_global_rank(group, 0) if group is not None else 0
+        dist.broadcast_object_list(obj, src=src, group=group)
+        _comms[key] = multi_comm_init(obj[0], dist.get_world_size(group), rank)
+    return _comms[key]
+
+
+def _use_cxx(R: torch.Tensor, group, partition_fn, local_join_fn) -> bool:
+    return (R.is_cuda and partition_fn is None and local_join_fn is None and not _cxx_failed
+            and dist.get_backend(group) == "nccl" and os.environ.get("SGXAMD_DIST_IMPL", "cxx") == "cxx")
+
+
+def _sharded_cxx(R: torch.Tensor, S: torch.Tensor, group, algorithm: str, chunks: int) -> ShardedJoinResult:
+    from . import multi_set_pieces
+
+    h = _cxx_comm(group)
+    multi_set_pieces(chunks)
+    t0 = time.perf_counter()
+    res = rho_join_sharded(h, R, R.numel(), S, S.numel(), algorithm=algorithm)
+    st = res.stats
+    ms = {"total": (time.perf_counter() - t0) * 1e3, "shard_partition_and_post_exchange": st["ms_exchange_post"],
+          "exchange_wait_and_local_join": st["ms_local"], "all_reduce": st["ms_allreduce"],
+          "impl": "cxx-rccl (mi355_rho_join_sharded)"}
+    return ShardedJoinResult(res.matches, int(st["local_matches"]), int(st["recv_r_max"]), int(st["recv_s_max"]), ms,
+                             st["local"])
+
+
 def sharded_rho_join(R: torch.Tensor, S: torch.Tensor, *, group=None, partition_fn=None,
                      local_join_fn=None, algorithm: str = "RHO", chunks: int = 4) -> ShardedJoinResult:
     """Global RHO join of the row slices R and S (int64 tensors, one tuple each).
@@ -234,6 +278,15 @@ def sharded_rho_join(R: torch.Tensor, S: torch.Tensor, *, group=None, partition_
         ms["local_join"] = (time.perf_counter() - t0) * 1e3
         return ShardedJoinResult(int(m), int(m), R.numel(), S.numel(), ms, st)
 
+    if _use_cxx(R, group, partition_fn, local_join_fn):
+        # RCCL through the C++ library; torch's stream is synchronised first (the library
+        # runs on its own streams unless mi355_set_stream named torch's)
+        torch.cuda.current_stream(R.device).synchronize()
+        try:
+            return _sharded_cxx(R, S, group, algorithm, chunks)
+        except Mi355Error as e:  # keep running on the torch.distributed path, and say so
+            print(f"sgxamd.dist: C++ RCCL path failed ({e}); using the torch.distributed path", file=sys.stderr)
+            _cxx_failed.append(str(e))
     cgroup = _count_group(group)
     # R piece by piece: each piece's exchange is in flight on the RCCL stream while the
     # next pieces (and then S) are shard-partitioned on the compute stream

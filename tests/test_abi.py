@@ -26,7 +26,7 @@ CXX_SYMBOLS = {
 
 def declared_c_functions():
     names = set()
-    for h in ("rho.h", "scan.h", "generator.h", "tpch.h"):
+    for h in ("rho.h", "scan.h", "generator.h", "tpch.h", "multi.h"):
         text = open(os.path.join(INCLUDE, h)).read()
         text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
         names |= set(re.findall(r"\b(mi355_\w+)\s*\(", text))
@@ -75,7 +75,7 @@ def test_struct_layouts_match_reference(sgx):
 def test_static_asserts_compile_as_c_and_cxx(tmp_path):
     src = tmp_path / "t.c"
     src.write_text('#include "sgxamd/data_types.h"\n#include "sgxamd/rho.h"\n#include "sgxamd/scan.h"\n'
-                   '#include "sgxamd/generator.h"\nint main(void){return 0;}\n')
+                   '#include "sgxamd/generator.h"\n#include "sgxamd/multi.h"\nint main(void){return 0;}\n')
     subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(tmp_path / "a")],
                    check=True)
     cpp = tmp_path / "t.cpp"
@@ -112,3 +112,22 @@ def test_compute_without_gpu_fails_loudly(sgx):
         assert e.code == sgx.MI355_ERR_NO_DEVICE
     else:
         raise AssertionError("join ran without a GPU")
+    try:
+        sgx.rho_join_multi(R, 16, R, 16, 4, transport="rehearsal")
+    except sgx.Mi355Error as e:
+        assert e.code == sgx.MI355_ERR_NO_DEVICE
+    else:
+        raise AssertionError("multi-GPU join ran without a GPU")
+
+
+def test_multi_rejects_bad_world(sgx):
+    import numpy as np
+
+    R = np.zeros(16, dtype=np.uint64)
+    for g in (0, 3, 6, 512):
+        try:
+            sgx.rho_join_multi(R, 16, R, 16, g)
+        except sgx.Mi355Error as e:
+            assert e.code == sgx.MI355_ERR_INVALID
+        else:
+            raise AssertionError(g)

@@ -1,0 +1,149 @@
+"""Multi-GPU RHO in C++ (sgxamd/multi.h) on one MI355X through the rehearsal transport:
+G logical ranks with their own streams and workspaces, the radix-shard exchange done by
+device-to-device copies.  The same rank pipeline (pieced shard partition, count
+exchange, tuple exchange on a communication stream, pipelined local join with
+key_shift = log2 G, all-reduce) runs over RCCL when G GPUs are visible.
+
+Counts are compared bit-exactly with the oracle's restated RHO (radix_join.cpp) on
+the reference's relations (native.cpp:62-101) and with the sort counter."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import PKG
+
+pytestmark = pytest.mark.gpu
+
+DT = np.dtype([("key", "<u4"), ("payload", "<u4")])
+
+
+def rel(keys):
+    x = np.empty(len(keys), dtype=DT)
+    x["key"] = keys
+    x["payload"] = np.arange(len(keys), dtype=np.uint32)
+    return x
+
+
+def multi(sgx, R, S, g, **kw):
+    return sgx.rho_join_multi(R, len(R), S, len(S), g, transport="rehearsal", **kw)
+
+
+@pytest.mark.parametrize("g", [2, 4, 8])
+def test_reference_pk_fk(sgx, orc, gpu, g):
+    n = 1 << 18
+    R, S = sgx.reference_relations(n, n)
+    res = multi(sgx, R, S, g)
+    assert res.matches == orc.rho_join(R, S, 4)[0] == n
+    st = res.stats
+    assert st["world"] == g and st["transport"] == "rehearsal" and st["pieces"] == 4
+    # every key lands on the rank of its low log2(g) bits: pk keys 1..n spread evenly
+    assert st["recv_r_min"] == st["recv_r_max"] == n // g
+    assert 0 < st["sent_bytes"] <= 8 * 2 * n
+
+
+@pytest.mark.parametrize("seed,nR,nS,kmax,g", [(1, 5000, 7001, 300, 4), (2, 100_003, 77_777, 2**32 - 1, 8),
+                                               (3, 3, 5, 2, 4), (4, 1 << 17, 1 << 16, 1 << 10, 2)])
+def test_random_with_duplicates(sgx, orc, gpu, seed, nR, nS, kmax, g):
+    rng = np.random.default_rng(seed)
+    R = rel(rng.integers(0, kmax + 1, nR, dtype=np.uint64).astype(np.uint32))
+    S = rel(rng.integers(0, kmax + 1, nS, dtype=np.uint64).astype(np.uint32))
+    exp = orc.count_join_sort(R, S)
+    assert multi(sgx, R, S, g).matches == exp
+    assert multi(sgx, R, S, g, algorithm="RHT").matches == exp
+    assert multi(sgx, R, S, g, radix_bits=12, passes=2).matches == exp
+
+
+def test_zipf_and_sel(sgx, orc, gpu):
+    n = 1 << 18
+    R, S = sgx.reference_relations(n, n, skew=0.75)
+    res = multi(sgx, R, S, 8)
+    assert res.matches == orc.rho_join(R, S, 4)[0] == n
+    assert res.stats["recv_s_max"] < 1.2 * n / 8  # hot keys spread over the ranks by the alphabet shuffle
+    R, S = sgx.reference_relations(n, n, selectivity=10)
+    assert multi(sgx, R, S, 4).matches == orc.rho_join(R, S, 4)[0]
+
+
+@pytest.mark.parametrize("pieces", [1, 3, 7])
+def test_pieces(sgx, orc, gpu, pieces):
+    R, S = sgx.reference_relations(100_000, 150_001, selectivity=50)
+    exp = orc.rho_join(R, S, 4)[0]
+    sgx.multi_set_pieces(pieces)
+    try:
+        res = multi(sgx, R, S, 4)
+    finally:
+        sgx.multi_set_pieces(4)
+    assert res.matches == exp and res.stats["pieces"] == pieces
+
+
+@pytest.mark.parametrize("nR,nS,g", [(0, 100, 4), (100, 0, 4), (3, 1000, 8), (1000, 5, 8), (1, 1, 2)])
+def test_empty_and_tiny_slices(sgx, orc, gpu, nR, nS, g):
+    R = rel(np.arange(1, nR + 1, dtype=np.uint32))
+    S = rel((np.arange(nS, dtype=np.uint32) % max(nR, 1)) + 1)
+    exp = orc.count_join_sort(R, S) if nR and nS else 0
+    assert multi(sgx, R, S, g).matches == exp
+
+
+def test_device_resident_and_repeat(sgx, orc, gpu):
+    import torch
+
+    R, S = sgx.reference_relations(1 << 17, (1 << 17) + 33)
+    dR = torch.from_numpy(R.view(np.int64)).to(gpu)
+    dS = torch.from_numpy(S.view(np.int64)).to(gpu)
+    exp = orc.rho_join(R, S, 4)[0]
+    for g in (4, 2, 4, 1):  # workspaces are reused across calls and world sizes
+        assert sgx.rho_join_multi(dR, len(R), dS, len(S), g, transport="rehearsal").matches == exp
+    assert np.array_equal(dR.cpu().numpy().view(DT), R)  # inputs untouched
+
+
+def test_dropin_table_api(sgx, gpu):
+    import ctypes as C
+
+    R, S = sgx.reference_relations(1 << 16, 1 << 16)
+    tR = sgx.table_t(R.ctypes.data, len(R), 0, 0)
+    tS = sgx.table_t(S.ctypes.data, len(S), 0, 0)
+    cfg = sgx.joinconfig_t()
+    cfg.NTHREADS = 8
+    out = sgx.result_t()
+    os.environ["SGXAMD_MULTI_TRANSPORT"] = "rehearsal"
+    try:
+        rc = sgx.lib.mi355_rho_join_multi(C.byref(tR), C.byref(tS), C.byref(cfg), 4, C.byref(out))
+    finally:
+        del os.environ["SGXAMD_MULTI_TRANSPORT"]
+    assert rc == 0, sgx.last_error()
+    assert out.totalresults == 1 << 16 and out.nthreads == 8 and out.throughput > 0
+
+
+def test_native_driver_multi_gpu_rehearsal(gpu):
+    """The reference driver's call chain (native.cpp:137 -> run_join -> RHO) with
+    SGXAMD_GPUS=4: RHO() takes the radix-shard exchange; the count is exact and the
+    reference's timing lines are all there."""
+    exe = os.path.join(PKG, "bin", "native_mi355")
+    env = dict(os.environ, SGXAMD_GPUS="4", SGXAMD_MULTI_TRANSPORT="rehearsal")
+    out = subprocess.run([exe, "-a", "RHO", "-r", "1000000", "-s", "3000000"], capture_output=True, text=True,
+                         env=env, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "Radix-shard exchange over 4 GPUs (one-GPU rehearsal" in out.stdout
+    assert "Matches = 3000000" in out.stdout
+    for key in ("Partition Overall (cycles)", "Build+Join Overall (cycles)", "Throughput (M rec/sec)"):
+        assert key in out.stdout
+
+
+def test_rccl_comm_single_rank(sgx, orc, gpu):
+    """One-process-per-GPU entry points on a world of one: RCCL loads, the unique id and
+    communicator are created, and the sharded join of the slice is the local join."""
+    import torch
+
+    uid = sgx.multi_unique_id()
+    assert len(uid) == 128
+    h = sgx.multi_comm_init(uid, 1, 0)
+    try:
+        R, S = sgx.reference_relations(1 << 16, 1 << 16, selectivity=50)
+        dR = torch.from_numpy(R.view(np.int64)).to(gpu)
+        dS = torch.from_numpy(S.view(np.int64)).to(gpu)
+        res = sgx.rho_join_sharded(h, dR, len(R), dS, len(S))
+        assert res.matches == orc.rho_join(R, S, 4)[0]
+        assert res.stats["transport"] == "rccl" and res.stats["world"] == 1
+    finally:
+        sgx.multi_comm_destroy(h)
