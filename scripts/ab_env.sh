@@ -10,7 +10,7 @@ OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 for rep in 1 2; do
   for v in $VALS; do
-    env "$VAR=$v" timeout -k 10 300 python bench.py --no-scan --no-tpch --no-cpu-baseline "$@" \
+    env "$VAR=$v" timeout -k 10 300 python bench.py --no-scan --no-tpch --no-cpu-baseline --no-paper --no-configs "$@" \
       > "$OUT/bench_${v}_$rep.json" 2> "$OUT/bench_${v}_$rep.err" || { echo "bench $v failed"; tail -20 "$OUT/bench_${v}_$rep.err"; exit 1; }
     python3 -c "
 import json,sys; b=json.load(open('$OUT/bench_${v}_$rep.json')); k=b['rho']['kernel_ms_avg']

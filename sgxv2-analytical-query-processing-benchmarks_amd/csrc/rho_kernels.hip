@@ -610,6 +610,8 @@ hipError_t launch_scatter(const row_t *in, row_t *out, const SegMap &m, uint32_t
 //                     (radix_join.cpp:437-446) at task_off[t] + a task-local slot
 //                     taken with one LDS atomic per wave and chain step.
 
+__device__ __forceinline__ void tmatch_add(uint64_t &m, bool hit) { m += hit ? 1u : 0u; }
+
 __device__ __forceinline__ void decode_task(uint64_t t, uint64_t P, const uint64_t *__restrict__ over, uint64_t &p,
                                             uint64_t &chunk) {
     if (t < P) {
@@ -800,6 +802,147 @@ __global__ __launch_bounds__(BLOCK) void k_join(const uint64_t *__restrict__ R, 
             for (int w = 0; w < NW; ++w) acc += L.red[w];
             counts[blockIdx.x] = acc;
         }
+    }
+    if (cyc && tid == 0) {
+        cyc[2 * blockIdx.x] = bcyc;
+        cyc[2 * blockIdx.x + 1] = pcyc;
+    }
+}
+
+// ------------------------------------------- 16,384-tuple counting table in 80 KiB ---
+// The counting join of bucket_chaining_join (:359-458) with the chain table of one R
+// chunk packed into half a CU's LDS, so that two workgroups share a CU and overlap
+// each other's phases (R load, head clear, build, probe), which a single 160 KiB
+// table per CU leaves serial:
+//   head[N]  u16, 1-based (0 = empty), two per 32-bit word; the build links tuple i
+//            with a compare-and-swap on its bucket's word (LDS has no 16-bit exchange);
+//   next[i]  u16, 1-based;
+//   tag[i]   u8 = the key bits [hash_shift + log2 N, +8).
+// Inside a task every key agrees on the bits below hash_shift (the radix partition,
+// and the rank bits of a shard exchange) and inside a chain on the bucket bits
+// [hash_shift, hash_shift + log2 N), so with hash_shift + log2 N + 8 >= 32 the tag
+// holds all remaining key bits and tag equality is key equality (2^28 tuples at 14
+// radix bits: 14 + 14 + 4).  Otherwise a tag match is confirmed against the R key,
+// re-read from the partitioned relation (an L2 hit).
+template <int RCAP, int NW>
+struct JoinLdsTag {
+    union {
+        __attribute__((aligned(16))) uint32_t head2[RCAP / 2];
+        uint64_t red[NW];
+    };
+    uint16_t next[RCAP];
+    uint8_t tag[RCAP];
+};
+
+__device__ __forceinline__ uint32_t key_tag(uint32_t k, uint32_t tshift) {
+    return tshift >= 32 ? 0u : ((k >> tshift) & 0xFFu);
+}
+
+// Each thread builds and probes in strips of UP tuples (UP chain walks in lock step).
+template <int RCAP, int BLOCK, int UP>
+__global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_join_tag(
+    const uint64_t *__restrict__ R, const uint64_t *__restrict__ S, const uint64_t *__restrict__ r_start,
+    const uint64_t *__restrict__ r_count, const uint64_t *__restrict__ s_start, const uint64_t *__restrict__ s_count,
+    uint64_t P, const uint64_t *__restrict__ over, const uint32_t *__restrict__ n_over, uint32_t hash_shift,
+    uint64_t s_chunk, uint64_t *__restrict__ counts, uint64_t *__restrict__ cyc) {
+    constexpr int NW = BLOCK / kWave;
+    constexpr uint32_t STRIP = BLOCK * UP;
+    __shared__ JoinLdsTag<RCAP, NW> L;
+    const uint32_t tid = threadIdx.x, lane = __lane_id();
+    const uint64_t T = P + *n_over;
+    uint64_t matches = 0;
+    uint64_t bcyc = 0, pcyc = 0;
+    for (uint64_t t = blockIdx.x; t < T; t += gridDim.x) {
+        uint64_t p, chunk;
+        decode_task(t, P, over, p, chunk);
+        const uint64_t nR = r_count[p], nSp = s_count[p];
+        const uint64_t s_lo = chunk * s_chunk;
+        const uint64_t nS = (nR == 0 || s_lo >= nSp) ? 0 : min<uint64_t>(nSp - s_lo, s_chunk);
+        if (nS == 0) continue;
+        const uint32_t *rk = reinterpret_cast<const uint32_t *>(R + r_start[p]);  // key = low word of a tuple
+        const uint32_t *sk = reinterpret_cast<const uint32_t *>(S + s_start[p] + s_lo);
+        for (uint64_t rc = 0; rc < nR; rc += RCAP) {
+            const uint64_t c_build = wall_clock64();
+            const uint32_t nrc = (uint32_t)((nR - rc) < RCAP ? (nR - rc) : RCAP);
+            uint32_t lgN = 0;
+            while ((1u << lgN) < nrc) ++lgN;  // N = NEXT_POW_2(numR)
+            const uint32_t hmask = (1u << lgN) - 1;
+            const uint32_t tshift = hash_shift + lgN;
+            const bool exact = tshift + 8 >= 32;
+            const uint32_t *rkc = rk + 2 * rc;
+            for (uint32_t i = tid; i < ((1u << lgN) + 7) / 8; i += BLOCK)
+                reinterpret_cast<uint4 *>(L.head2)[i] = make_uint4(0, 0, 0, 0);
+            __syncthreads();
+            for (uint32_t r0 = 0; r0 < nrc; r0 += STRIP) {  // BUILD-LOOP (:407-411)
+                uint32_t kr[UP];
+#pragma unroll
+                for (int u = 0; u < UP; ++u) {
+                    const uint32_t i = r0 + tid + u * BLOCK;
+                    kr[u] = i < nrc ? __builtin_nontemporal_load(rkc + 2 * i) : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < UP; ++u) {
+                    const uint32_t i = r0 + tid + u * BLOCK;
+                    if (i < nrc) {
+                        const uint32_t k = kr[u];
+                        L.tag[i] = (uint8_t)key_tag(k, tshift);
+                        const uint32_t b = (k >> hash_shift) & hmask;
+                        const uint32_t sh = (b & 1u) * 16u;
+                        uint32_t *w = &L.head2[b >> 1];
+                        uint32_t old = *w;
+                        while (true) {
+                            const uint32_t nw = (old & ~(0xFFFFu << sh)) | ((i + 1) << sh);
+                            const uint32_t prev = atomicCAS(w, old, nw);
+                            if (prev == old) break;
+                            old = prev;
+                        }
+                        L.next[i] = (uint16_t)(old >> sh);
+                    }
+                }
+            }
+            __syncthreads();
+            const uint64_t c_probe = wall_clock64();
+            bcyc += c_probe - c_build;
+            for (uint64_t s0 = 0; s0 < nS; s0 += STRIP) {  // PROBE-LOOP (:429-436)
+                uint32_t ks[UP], cur[UP];
+#pragma unroll
+                for (int u = 0; u < UP; ++u) {
+                    const uint64_t i = s0 + tid + u * BLOCK;
+                    ks[u] = i < nS ? __builtin_nontemporal_load(sk + 2 * i) : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < UP; ++u) {
+                    const uint64_t i = s0 + tid + u * BLOCK;
+                    const uint32_t b = (ks[u] >> hash_shift) & hmask;
+                    cur[u] = i < nS ? (L.head2[b >> 1] >> ((b & 1u) * 16u)) & 0xFFFFu : 0u;
+                }
+                bool more = true;
+                while (more) {
+                    more = false;
+#pragma unroll
+                    for (int u = 0; u < UP; ++u) {
+                        if (cur[u] != 0) {
+                            const uint32_t e = cur[u] - 1;
+                            if (L.tag[e] == key_tag(ks[u], tshift))
+                                tmatch_add(matches, exact || rkc[2 * e] == ks[u]);
+                            cur[u] = L.next[e];
+                            more |= cur[u] != 0;
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+            pcyc += wall_clock64() - c_probe;
+        }
+    }
+    matches = wave_sum_u64(matches);
+    __syncthreads();
+    if (lane == 0) L.red[tid / kWave] = matches;
+    __syncthreads();
+    if (tid == 0) {
+        uint64_t acc = 0;
+        for (int w = 0; w < NW; ++w) acc += L.red[w];
+        counts[blockIdx.x] = acc;
     }
     if (cyc && tid == 0) {
         cyc[2 * blockIdx.x] = bcyc;
@@ -1027,9 +1170,24 @@ hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, 
         // one 16,384-tuple chain table per 1,024-thread workgroup: all 160 KiB of LDS
         // (plain counting only; the materialising table carries 4 B more per tuple)
         if (mode != kJoinCount) return hipErrorInvalidValue;
-        hipLaunchKernelGGL((k_join<kBigRcap, kJoinCount, kBigJoinBlock>), dim3(grid), dim3(kBigJoinBlock), 0, s, R64,
-                           S64, r_start, r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts,
-                           task_off, out, cyc);
+        // SGXAMD_TAG_JOIN (development A/B switch, read once): 1024 (default) / 512 = the
+        // 80 KiB tagged table (two workgroups per CU) with that many threads; 0 = the
+        // 160 KiB table, one 1,024-thread workgroup per CU.  2^28 build/probe, one box,
+        // alternating: 0.849-0.851 ms (0), 0.794-0.796 (512), 0.696-0.698 (1024)
+        static const int tag_block = [] {
+            const char *e = std::getenv("SGXAMD_TAG_JOIN");
+            return e ? std::atoi(e) : 1024;
+        }();
+        if (tag_block == 512)
+            hipLaunchKernelGGL((k_join_tag<kBigRcap, 512, 16>), dim3(grid), dim3(512), 0, s, R64, S64, r_start, r_count,
+                               s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts, cyc);
+        else if (tag_block == 1024)
+            hipLaunchKernelGGL((k_join_tag<kBigRcap, 1024, 8>), dim3(grid), dim3(1024), 0, s, R64, S64, r_start, r_count,
+                               s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts, cyc);
+        else
+            hipLaunchKernelGGL((k_join<kBigRcap, kJoinCount, kBigJoinBlock>), dim3(grid), dim3(kBigJoinBlock), 0, s,
+                               R64, S64, r_start, r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk,
+                               counts, task_off, out, cyc);
     } else {
         switch (rcap) {
             JOIN_MODES(k_join, 2048)

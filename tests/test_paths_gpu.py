@@ -3,7 +3,9 @@ SGXAMD_DIGIT_SIDE=0 (pass-2 histograms over the tuples instead of the digit side
 stream), SGXAMD_BIG_JOIN=0 (R partitions above 8192 tuples in 8192-tuple chain tables
 instead of the 16,384-tuple counting table; the 5-bit plan below has 32,768-tuple
 partitions) and SGXAMD_SCAN_ONEPASS=0 (index / value / dictionary scans as bitvector
-pass + expand pass instead of the one-pass look-back selection).  Both switches are read
+pass + expand pass instead of the one-pass look-back selection), SGXAMD_TAG_JOIN=0 / 512
+(the 16,384-tuple counting table as one 160 KiB table per CU, or the 80 KiB tagged
+table with 512 threads, instead of the tagged table with 1,024).  The switches are read
 once per process, so each setting runs in a child process against the oracle (the
 TPC-H selections ride along: they share the library's workspace)."""
 import os
@@ -26,6 +28,14 @@ for bits, passes in [(12, 2), (16, 2), (18, 2), (5, 1)]:
     got = sgxamd.rho_join(R, len(R), S, len(S), radix_bits=bits, passes=passes).matches
     assert got == exp, (bits, passes, got, exp)
 rng = np.random.default_rng(5)
+# full-range keys with duplicates: big-table partitions whose 8-bit tags are not the whole
+# remaining key (hash_shift + log2 N + 8 < 32), confirmed against the R keys
+dt = np.dtype([("key", "<u4"), ("payload", "<u4")])
+for kmax, bits in ((2**32 - 1, 5), (1 << 22, 4)):
+    R2 = np.zeros(1 << 20, dtype=dt); R2["key"] = rng.integers(0, kmax + 1, 1 << 20)
+    S2 = np.zeros((1 << 20) + 99, dtype=dt); S2["key"] = rng.integers(0, kmax + 1, (1 << 20) + 99)
+    got = sgxamd.rho_join(R2, len(R2), S2, len(S2), radix_bits=bits, passes=1).matches
+    assert got == oracle.count_join_sort(R2, S2), (kmax, bits, got)
 for n in (1, 1000, 65536, 65537, (1 << 20) + 37):
     col = rng.integers(0, 256, n).astype(np.int32)
     for lo, hi in [(0, 26), (0, 255), (7, 7), (200, 100)]:
@@ -51,7 +61,8 @@ print("paths ok")
 
 
 @pytest.mark.parametrize("env", [{"SGXAMD_DIGIT_SIDE": "0", "SGXAMD_SCAN_ONEPASS": "0", "SGXAMD_BIG_JOIN": "0"},
-                                 {"SGXAMD_DIGIT_SIDE": "1", "SGXAMD_SCAN_ONEPASS": "1", "SGXAMD_BIG_JOIN": "1"}])
+                                 {"SGXAMD_DIGIT_SIDE": "1", "SGXAMD_SCAN_ONEPASS": "1", "SGXAMD_BIG_JOIN": "1"},
+                                 {"SGXAMD_TAG_JOIN": "0"}, {"SGXAMD_TAG_JOIN": "512"}])
 def test_switch_paths_match_oracle(env):
     e = dict(os.environ, **env)
     e["PYTHONPATH"] = os.pathsep.join([os.path.join(PKG, "python"), os.path.join(ROOT, "oracle"),
