@@ -15,8 +15,8 @@ import sgxamd  # noqa: E402
 torch.cuda.set_device(0)
 stream = torch.cuda.current_stream().cuda_stream
 sgxamd.set_stream(stream)
-sgxamd.timing_enable(True)
-for lg in (14, 16, 18, 20, 22):
+sgxamd.timing_enable(os.environ.get("SMALL_TIMING", "1") == "1")
+for lg in [int(x) for x in os.environ.get("SMALL_LGS", "14,16,18,20,22").split(",")]:
     n = 1 << lg
     R, S = sgxamd.reference_relations(n, n) if lg <= 20 else (None, None)
     if R is not None:

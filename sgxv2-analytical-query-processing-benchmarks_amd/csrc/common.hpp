@@ -119,6 +119,24 @@ __device__ __forceinline__ uint64_t block_excl_scan_u64(uint64_t v, uint64_t *sc
     return r;
 }
 
+// Block-wide max of one u64 per thread (every thread gets it); `scratch` holds
+// blockDim.x / 64 entries.  Contains __syncthreads().
+__device__ __forceinline__ uint64_t block_max_u64(uint64_t v, uint64_t *scratch) {
+#pragma unroll
+    for (int off = kWave / 2; off > 0; off >>= 1) {
+        const uint64_t o = __shfl_xor(v, off, kWave);
+        v = o > v ? o : v;
+    }
+    const uint32_t nwaves = blockDim.x / kWave;
+    __syncthreads();
+    if (__lane_id() == 0) scratch[threadIdx.x / kWave] = v;
+    __syncthreads();
+    uint64_t m = 0;
+    for (uint32_t w = 0; w < nwaves; ++w) m = scratch[w] > m ? scratch[w] : m;
+    __syncthreads();
+    return m;
+}
+
 // ---------------------------------------------------- decoupled look-back ---
 // Single-pass exclusive prefix over chunks claimed in order through a ticket counter
 // (so every lower chunk belongs to a workgroup that is already running: the look-back

@@ -251,8 +251,8 @@ PendingJoin &pending_of(const Context *ctx) {
 // enqueues R's partition passes on s and returns without waiting.  The second half
 // may start after S has been produced later in the stream order of s (multi-GPU:
 // R's local passes run while S is still being exchanged).  Caller holds ctx->mu.
-int join_begin(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, uint64_t nS, const mi355_rho_opts *opts,
-               PendingJoin &pj) {
+// Policy, workspace and scratch layout of a join of nR x nS tuples (no launches).
+int plan_join(Context *ctx, hipStream_t s, uint64_t nR, uint64_t nS, const mi355_rho_opts *opts, PendingJoin &pj) {
     pj = PendingJoin{};
     pj.s = s;
     pj.nR = nR;
@@ -266,9 +266,6 @@ int join_begin(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, uint64
         set_last_error("key_shift + radix bits must stay below 32");
         return MI355_ERR_INVALID;
     }
-    Timer &tm = thread_timer();
-    tm.begin_call(s, true);  // phase events are always recorded (throughput in result_t)
-
     RHO_HIP(ctx->t1R.ensure(std::max<uint64_t>(nR, 1) * sizeof(row_t)));
     RHO_HIP(ctx->t1S.ensure(std::max<uint64_t>(nS, 1) * sizeof(row_t)));
     if (pol.passes == 2) {
@@ -300,6 +297,24 @@ int join_begin(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, uint64
     pj.off_result = A.reserve(sizeof(uint64_t) * 6);
     pj.off_cyc = A.reserve(sizeof(uint64_t) * 2 * pj.join_grid);
     RHO_HIP(A.buf.ensure(A.used));
+    return MI355_OK;
+}
+
+// First half: plans both relations (|S| = nS, its tuples are not read yet), then
+// enqueues R's partition passes on s and returns without waiting.  The second half
+// may start after S has been produced later in the stream order of s (multi-GPU:
+// R's local passes run while S is still being exchanged).  Caller holds ctx->mu.
+int join_begin(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, uint64_t nS, const mi355_rho_opts *opts,
+               PendingJoin &pj) {
+    int prc = plan_join(ctx, s, nR, nS, opts, pj);
+    if (prc) return prc;
+    const Policy &pol = pj.pol;
+    Timer &tm = thread_timer();
+    // the call's device time is always recorded (throughput in result_t); per kernel
+    // only with timing on (mi355_timing_enable / opts->timing): each event record is a
+    // few microseconds of GPU time, a large part of a small join
+    const bool per_kernel = thread_timing_enabled() || (opts && opts->timing);
+    tm.begin_call(s, true, !per_kernel);
 
     // R's and S's partition chains are independent: with overlap on, S's runs on the
     // side stream so that one relation's scatter shares the chip with the other's
@@ -317,6 +332,47 @@ int join_begin(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, uint64
             return rc;
     pj.active = true;
     return MI355_OK;
+}
+
+// Statistics of a finished join from the read-back result words and the call's events.
+void fill_join_stats(const Context *ctx, const PendingJoin &pj, const Timer &tm, float wall, mi355_rho_stats *st) {
+    const Policy &pol = pj.pol;
+    const uint64_t P = 1ull << pol.bits;
+    if (st) {
+        st->matches = ctx->host_result[0];
+        st->radix_bits = pol.bits;
+        st->passes = pol.passes;
+        st->pass1_bits = pol.b1;
+        st->pass2_bits = pol.b2;
+        st->num_partitions = P;
+        st->num_tasks = P + (uint32_t)ctx->host_result[3];
+        st->max_part_r = ctx->host_result[1];
+        st->max_part_s = ctx->host_result[2];
+        // (RS_: both relations in one launch, the small-join path)
+        st->ms_pass1 = tm.ms_of_prefix("R_pass1") + tm.ms_of_prefix("S_pass1") + tm.ms_of_prefix("RS_pass1");
+        st->ms_pass2 = tm.ms_of_prefix("R_pass2") + tm.ms_of_prefix("S_pass2");
+        st->ms_partition = st->ms_pass1 + st->ms_pass2;
+        st->ms_join = tm.ms_of_prefix("join_");
+        // with two streams the phase spans overlap: the total is the wall span
+        st->ms_total = wall >= 0.f ? (double)wall
+                                   : (tm.coarse() ? tm.ms_of_prefix("total") : st->ms_partition + st->ms_join);
+        st->ms_pass1_r = tm.ms_of_prefix("R_pass1");
+        st->ms_pass1_s = tm.ms_of_prefix("S_pass1");
+        st->ms_pass1_hist = tm.ms_of_prefix("R_pass1_hist") + tm.ms_of_prefix("R_pass1_scan") +
+                            tm.ms_of_prefix("S_pass1_hist") + tm.ms_of_prefix("S_pass1_scan") +
+                            tm.ms_of_prefix("RS_pass1_hist");
+        st->ms_pass1_copy = tm.ms_of_prefix("R_pass1_scatter") + tm.ms_of_prefix("S_pass1_scatter") +
+                            tm.ms_of_prefix("RS_pass1_scatter");
+        st->ms_pass2_hist = tm.ms_of_prefix("R_pass2_hist") + tm.ms_of_prefix("R_pass2_scan") +
+                            tm.ms_of_prefix("S_pass2_hist") + tm.ms_of_prefix("S_pass2_scan");
+        st->ms_pass2_copy = tm.ms_of_prefix("R_pass2_scatter") + tm.ms_of_prefix("S_pass2_scatter");
+        // the build/probe kernel is one launch: its time is split by the ticks its
+        // workgroups spent building and probing
+        const double b = (double)ctx->host_result[4], pr = (double)ctx->host_result[5];
+        const double bp = tm.ms_of_prefix("join_build_probe") + tm.ms_of_prefix("join_materialize");
+        st->ms_build = b + pr > 0 ? bp * b / (b + pr) : 0.0;
+        st->ms_probe = bp - st->ms_build;
+    }
 }
 
 // Second half: S's partition passes, build/probe (and materialisation), then the
@@ -342,7 +398,7 @@ int join_finish(Context *ctx, PendingJoin &pj, const row_t *dS, uint64_t nS, mi3
     if (s2) {
         if (fork_now) RHO_HIP(hipEventRecord(ctx->ev_fork, s));
         RHO_HIP(hipStreamWaitEvent(s2, ctx->ev_fork, 0));
-        tm2.begin_call(s2, true);
+        tm2.begin_call(s2, true, tm.coarse());
     }
     hipStream_t sS = s2 ? s2 : s;
     Timer &tmS = s2 ? tm2 : tm;
@@ -418,37 +474,77 @@ int join_finish(Context *ctx, PendingJoin &pj, const row_t *dS, uint64_t nS, mi3
         if (hipEventElapsedTime(&wall, ctx->ev_t0, ctx->ev_t1) != hipSuccess) wall = -1.f;
     }
 
-    if (st) {
-        st->matches = ctx->host_result[0];
-        st->radix_bits = pol.bits;
-        st->passes = pol.passes;
-        st->pass1_bits = pol.b1;
-        st->pass2_bits = pol.b2;
-        st->num_partitions = P;
-        st->num_tasks = P + (uint32_t)ctx->host_result[3];
-        st->max_part_r = ctx->host_result[1];
-        st->max_part_s = ctx->host_result[2];
-        st->ms_pass1 = tm.ms_of_prefix("R_pass1") + tm.ms_of_prefix("S_pass1");
-        st->ms_pass2 = tm.ms_of_prefix("R_pass2") + tm.ms_of_prefix("S_pass2");
-        st->ms_partition = st->ms_pass1 + st->ms_pass2;
-        st->ms_join = tm.ms_of_prefix("join_");
-        // with two streams the phase spans overlap: the total is the wall span
-        st->ms_total = wall >= 0.f ? (double)wall : st->ms_partition + st->ms_join;
-        st->ms_pass1_r = tm.ms_of_prefix("R_pass1");
-        st->ms_pass1_s = tm.ms_of_prefix("S_pass1");
-        st->ms_pass1_hist = tm.ms_of_prefix("R_pass1_hist") + tm.ms_of_prefix("R_pass1_scan") +
-                            tm.ms_of_prefix("S_pass1_hist") + tm.ms_of_prefix("S_pass1_scan");
-        st->ms_pass1_copy = tm.ms_of_prefix("R_pass1_scatter") + tm.ms_of_prefix("S_pass1_scatter");
-        st->ms_pass2_hist = tm.ms_of_prefix("R_pass2_hist") + tm.ms_of_prefix("R_pass2_scan") +
-                            tm.ms_of_prefix("S_pass2_hist") + tm.ms_of_prefix("S_pass2_scan");
-        st->ms_pass2_copy = tm.ms_of_prefix("R_pass2_scatter") + tm.ms_of_prefix("S_pass2_scatter");
-        // the build/probe kernel is one launch: its time is split by the ticks its
-        // workgroups spent building and probing
-        const double b = (double)ctx->host_result[4], pr = (double)ctx->host_result[5];
-        const double bp = tm.ms_of_prefix("join_build_probe") + tm.ms_of_prefix("join_materialize");
-        st->ms_build = b + pr > 0 ? bp * b / (b + pr) : 0.0;
-        st->ms_probe = bp - st->ms_build;
+    fill_join_stats(ctx, pj, tm, wall, st);
+    return MI355_OK;
+}
+
+// Small one-pass counting joins in three launches (DESIGN.md §3 "Small joins"): a join
+// of 2^20 x 2^20 tuples is a dozen ~5 us launches on the regular path (histogram, two
+// scans and scatter per relation, a memset and the task list, build/probe, reduce).
+// Here: k_hist_pair (both histograms, digit layout and task list, with in-launch
+// hand-offs), k_scatter_pair (both scatters) and the build/probe with its own
+// last-workgroup reduction.  SGXAMD_SMALL_JOIN=0 turns it off (A/B; results identical).
+constexpr uint64_t kSmallJoinMax = 1ull << 23;  // |R| + |S| up to which the path is taken
+
+bool small_join_enabled() {
+    static const bool on = [] {
+        const char *e = std::getenv("SGXAMD_SMALL_JOIN");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return on;
+}
+
+int join_small(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const row_t *dS, uint64_t nS,
+               const mi355_rho_opts *opts, mi355_rho_stats *st) {
+    PendingJoin &pj = pending_of(ctx);
+    int rc = plan_join(ctx, s, nR, nS, opts, pj);
+    if (rc) return rc;
+    const Policy &pol = pj.pol;
+    if (!ctx->sync.ptr) {  // hand-off words: zero once, every kernel leaves them zero
+        RHO_HIP(ctx->sync.ensure(kSyncWords * sizeof(uint64_t)));
+        RHO_HIP(hipMemsetAsync(ctx->sync.ptr, 0, kSyncWords * sizeof(uint64_t), s));
     }
+    Timer &tm = thread_timer();
+    const bool per_kernel = thread_timing_enabled() || (opts && opts->timing);
+    tm.begin_call(s, true, !per_kernel);
+    // segments of at least 8192 tuples: fewer digit-total atomics per address (2^20 x 2^20:
+    // 4096 / 8192 / 16384 / 32768-tuple segments 67.9 / 58.5 / 64.6 / 85.3 us per join;
+    // SGXAMD_SMALL_SEG overrides, development)
+    static const uint64_t small_seg = [] {
+        const char *e = std::getenv("SGXAMD_SMALL_SEG");
+        const uint64_t v = e ? std::strtoull(e, nullptr, 10) : 8192;
+        return std::max<uint64_t>(kTile, (v + kTile - 1) / kTile * kTile);
+    }();
+    for (RelPlan *rp : {&pj.pr, &pj.ps}) {
+        rp->seg1 = std::max<uint64_t>(rp->seg1, small_seg);
+        rp->nseg1 = (uint32_t)((rp->n + rp->seg1 - 1) / rp->seg1);
+    }
+    Arena &A = ctx->scratch;
+    uint64_t *sync = ctx->sync.as<uint64_t>();
+    uint64_t *result = A.at<uint64_t>(pj.off_result);
+    uint64_t *over = A.at<uint64_t>(pj.off_over);
+    const SegMap mR{nullptr, nullptr, nullptr, 1, pj.pr.seg1, nR}, mS{nullptr, nullptr, nullptr, 1, pj.ps.seg1, nS};
+    uint64_t *offsR = A.at<uint64_t>(pj.pr.hist1), *offsS = A.at<uint64_t>(pj.ps.hist1);
+    uint64_t *startR = A.at<uint64_t>(pj.pr.start1), *cntR = A.at<uint64_t>(pj.pr.cnt1);
+    uint64_t *startS = A.at<uint64_t>(pj.ps.start1), *cntS = A.at<uint64_t>(pj.ps.cnt1);
+    row_t *oR = ctx->t1R.as<row_t>(), *oS = ctx->t1S.as<row_t>();
+    tm.mark("RS_pass1_hist");
+    RHO_HIP(launch_hist_pair(dR, mR, pj.pr.nseg1, dS, mS, pj.ps.nseg1, pj.key_shift, pol.b1, offsR, offsS, startR, cntR,
+                             startS, cntS, sync, over, pj.over_cap, result + 1, pj.s_chunk, s));
+    tm.mark("RS_pass1_scatter");
+    RHO_HIP(launch_scatter_pair(dR, oR, mR, pj.pr.nseg1, offsR, startR, dS, oS, mS, pj.ps.nseg1, offsS, startS,
+                                pj.key_shift, pol.b1, s));
+    tm.mark("join_build_probe");
+    const uint64_t P = 1ull << pol.bits;
+    const JoinReduce red{result, sync + kSyncTicketJoin};
+    RHO_HIP(launch_join(oR, oS, startR, cntR, startS, cntS, P, over, reinterpret_cast<uint32_t *>(result + 3),
+                        pj.key_shift + pol.bits, pol.rcap, pj.s_chunk, pj.join_grid, kJoinCount, pj.algo,
+                        A.at<uint64_t>(pj.off_counts), nullptr, nullptr, A.at<uint64_t>(pj.off_cyc), s, &red));
+    tm.end_call();
+    RHO_HIP(hipMemcpyAsync(ctx->host_result, result, 6 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    RHO_HIP(hipStreamSynchronize(s));
+    tm.collect();
+    fill_join_stats(ctx, pj, tm, -1.f, st);
     return MI355_OK;
 }
 
@@ -463,6 +559,12 @@ int join_device(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const
     if (pj.active) {
         set_last_error("a pipelined join (mi355_rho_join_begin) is pending on this device");
         return MI355_ERR_INVALID;
+    }
+    if (small_join_enabled() && nR > 0 && nS > 0 && nR + nS <= kSmallJoinMax && !(opts && opts->materialize) &&
+        !thread_partition_overlap() && choose_policy(nR, nS, opts).passes == 1) {
+        const int rc = join_small(ctx, s, dR, nR, dS, nS, opts, st);
+        pj.active = false;
+        return rc;
     }
     int rc = join_begin(ctx, s, dR, nR, nS, opts, pj);
     if (rc) {
@@ -652,6 +754,7 @@ static int table_join(const table_t *relR, const table_t *relS, const joinconfig
     output_triple_t *host = nullptr;
     mi355_rho_opts o{};
     o.algorithm = algorithm;
+    o.timing = 1;  // the drop-in logs the reference's phase lines (print_timing)
     if (!materialize) {
         rc = mi355_rho_join_ex(relR->tuples, relR->num_tuples, relS->tuples, relS->num_tuples, &o, &st);
     } else {

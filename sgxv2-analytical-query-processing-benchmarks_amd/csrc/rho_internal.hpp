@@ -48,6 +48,25 @@ hipError_t launch_scan_regions(uint64_t *hist, const uint32_t *seg_base, const u
                                uint32_t nreg, uint32_t bits, uint64_t *part_start, uint64_t *part_count,
                                hipStream_t s);
 
+// Context::sync (u64 words, zero when allocated, left zero by every kernel that uses
+// them): the tickets and digit totals of the in-launch hand-offs of the one-launch
+// histogram (launch_hist_pair) and of the build/probe count reduction.
+constexpr uint32_t kSyncTicketR = 0, kSyncTicketS = 1, kSyncTicket2 = 2, kSyncTicketJoin = 3;
+constexpr uint32_t kSyncTotR = 8, kSyncTotS = kSyncTotR + kMaxF, kSyncWords = kSyncTotS + kMaxF;
+
+// Small one-pass joins: histograms of R and S, digit starts / counts and the build/probe
+// task list (meta as launch_make_tasks) in one launch.  offs: [d][g] segment offsets
+// inside digit d (cursors for launch_scatter_pair with the starts as digit_base).
+hipError_t launch_hist_pair(const row_t *R, const SegMap &mR, uint32_t gridR, const row_t *S, const SegMap &mS,
+                            uint32_t gridS, uint32_t shift, uint32_t bits, uint64_t *offsR, uint64_t *offsS,
+                            uint64_t *startR, uint64_t *cntR, uint64_t *startS, uint64_t *cntS, uint64_t *sync,
+                            uint64_t *over, uint32_t over_cap, uint64_t *meta, uint64_t s_chunk, hipStream_t s);
+// Both relations' one-pass scatters in one launch (digit-major cursors + digit starts).
+hipError_t launch_scatter_pair(const row_t *R, row_t *outR, const SegMap &mR, uint32_t gridR, const uint64_t *offsR,
+                               const uint64_t *startR, const row_t *S, row_t *outS, const SegMap &mS, uint32_t gridS,
+                               const uint64_t *offsS, const uint64_t *startS, uint32_t shift, uint32_t bits,
+                               hipStream_t s);
+
 // Digit side stream of a two-pass partition: the pass-1 scatter also writes, for the
 // tuple it stores at position a of its output, the tuple's pass-2 digit
 // (key >> shift2) & (2^bits2 - 1) to side[a].  Pass 2's histogram then reads one byte
@@ -94,11 +113,17 @@ enum JoinAlgo : int { kAlgoChaining = 0, kAlgoHistogram = 1 };
 // [2] = the number of extra tasks (u32 n_over, read by launch_join / launch_excl_scan).
 hipError_t launch_make_tasks(const uint64_t *r_count, const uint64_t *s_count, uint64_t P, uint64_t *over,
                              uint32_t over_cap, uint64_t *meta, uint64_t s_chunk, hipStream_t s);
+// reduce (mode 0, nullable): the last workgroup to finish sums the partial counts and
+// ticks into reduce->result as launch_reduce does (reduce->ticket: a Context::sync word).
+struct JoinReduce {
+    uint64_t *result;
+    uint64_t *ticket;
+};
 hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, const uint64_t *r_count,
                        const uint64_t *s_start, const uint64_t *s_count, uint64_t P, const uint64_t *over,
                        const uint32_t *n_over, uint32_t hash_shift, uint32_t rcap, uint64_t s_chunk, uint32_t grid,
                        int mode, int algo, uint64_t *counts, const uint64_t *task_off, output_triple_t *out,
-                       uint64_t *cyc, hipStream_t s);
+                       uint64_t *cyc, hipStream_t s, const JoinReduce *reduce = nullptr);
 // One-block exclusive scan of n_base + *n_extra values; *total = their sum.
 hipError_t launch_excl_scan(const uint64_t *in, const uint32_t *n_extra, uint64_t n_base, uint64_t *out,
                             uint64_t *total, hipStream_t s);

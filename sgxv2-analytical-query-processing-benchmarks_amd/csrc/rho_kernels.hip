@@ -51,19 +51,14 @@ __device__ __forceinline__ uint64_t hist_index(HistLayout layout, uint32_t g, ui
 }
 
 // ------------------------------------------------------------------ hist ---
-__global__ __launch_bounds__(kBlock) void k_hist(const uint32_t *__restrict__ in_words, SegMap m, uint32_t shift,
-                                                 uint32_t bits, uint64_t *__restrict__ hist, HistLayout layout,
-                                                 uint32_t nseg_stride) {
-    __shared__ uint32_t h[kMaxF];
-    __shared__ uint32_t sbase[kMaxF + 1];
-    // XCD-contiguous segments for one-region passes (measured faster there, slower
-    // over pass 2's many regions)
-    const uint32_t g = layout == kDigitMajor ? xcd_contiguous(blockIdx.x, gridDim.x) : blockIdx.x;
+// Histogram of segment g's digits into LDS h[F] (zeroed here).  false: empty segment.
+__device__ __forceinline__ bool hist_segment(const uint32_t *__restrict__ in_words, const SegMap &m, uint32_t g,
+                                             uint32_t shift, uint32_t bits, uint32_t *h, uint32_t *sbase) {
     uint32_t r;
     uint64_t b, e;
-    if (!seg_lookup(m, g, sbase, r, b, e)) return;
+    if (!seg_lookup(m, g, sbase, r, b, e)) return false;
     const uint32_t F = 1u << bits, mask = F - 1;
-    for (uint32_t d = threadIdx.x; d < F; d += kBlock) h[d] = 0;
+    for (uint32_t d = threadIdx.x; d < F; d += blockDim.x) h[d] = 0;
     __syncthreads();
     // 16-B non-temporal loads (two tuples per lane); an odd leading tuple first
     const uint64_t *in64 = reinterpret_cast<const uint64_t *>(in_words);
@@ -93,7 +88,143 @@ __global__ __launch_bounds__(kBlock) void k_hist(const uint32_t *__restrict__ in
     }
     if (((e - b2) & 1) && threadIdx.x == 0) atomicAdd(&h[(in_words[2 * (e - 1)] >> shift) & mask], 1u);
     __syncthreads();
+    return true;
+}
+
+__global__ __launch_bounds__(kBlock) void k_hist(const uint32_t *__restrict__ in_words, SegMap m, uint32_t shift,
+                                                 uint32_t bits, uint64_t *__restrict__ hist, HistLayout layout,
+                                                 uint32_t nseg_stride) {
+    __shared__ uint32_t h[kMaxF];
+    __shared__ uint32_t sbase[kMaxF + 1];
+    // XCD-contiguous segments for one-region passes (measured faster there, slower
+    // over pass 2's many regions)
+    const uint32_t g = layout == kDigitMajor ? xcd_contiguous(blockIdx.x, gridDim.x) : blockIdx.x;
+    if (!hist_segment(in_words, m, g, shift, bits, h, sbase)) return;
+    const uint32_t F = 1u << bits;
     for (uint32_t d = threadIdx.x; d < F; d += kBlock) hist[hist_index(layout, g, d, F, nseg_stride)] = h[d];
+}
+
+// ------------------------------------------- in-launch hand-off (last arriver) ---
+// Counter form of cdna_hip_programming.md §6 Guideline 16: every wave drains its
+// stores, the workgroup meets, one lane releases at agent scope and takes a ticket; the
+// last of n arrivers acquires at agent scope before the workgroup reads what the others
+// wrote.  The ticket is reset by the last arriver (atomic store) for the next call; the
+// words start at zero (Context::sync, zeroed when allocated).  True in every thread of
+// the last workgroup.
+__device__ __forceinline__ bool arrive_last(uint64_t *ticket, uint64_t n, uint32_t *lds_flag) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint64_t t = __hip_atomic_fetch_add(ticket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool last = t == n - 1;
+        if (last) {
+            __hip_atomic_store(ticket, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        *lds_flag = last ? 1u : 0u;
+    }
+    __syncthreads();
+    return *lds_flag != 0;
+}
+
+__device__ __forceinline__ uint64_t ld_agent(const uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(uint64_t *p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ----------------------------------------- one-launch histogram + digit layout ---
+// For small one-pass joins: the histograms of R and S, the digit layout and the
+// build/probe task list in ONE launch instead of hist / scan_cols / scan_digits per
+// relation plus make_tasks.  Segment g of a relation adds its digit counts to the
+// relation's digit totals with one device atomic per digit; the value returned is
+// the segment's offset inside the digit (segments take their places in arrival order;
+// the join count does not depend on the order inside a partition).  The relation's
+// last segment turns the totals into digit starts (the scan of radix_join.cpp:901-914);
+// the last of the two relations then builds the task list (k_make_tasks's rule).
+struct HistPairRel {
+    const uint32_t *in;   // tuples as u32 words
+    SegMap m;
+    uint32_t grid;        // segments of the relation
+    uint32_t shift;
+    uint64_t *offs;       // [d][g] (stride grid): segment g's offset inside digit d
+    uint64_t *tot;        // F digit totals, zero at entry (reset by the last segment)
+    uint64_t *start;      // F digit starts
+    uint64_t *cnt;        // F digit counts
+    uint64_t *ticket;
+};
+
+__global__ __launch_bounds__(kBlock) void k_hist_pair(HistPairRel A, HistPairRel B, uint32_t bits,
+                                                      uint64_t *__restrict__ ticket2, uint64_t *__restrict__ over,
+                                                      uint32_t over_cap, uint64_t *__restrict__ meta,
+                                                      uint64_t s_chunk) {
+    __shared__ uint32_t h[kMaxF];
+    __shared__ uint32_t sbase[kMaxF + 1];
+    __shared__ uint64_t scratch[kWaves + 1];
+    __shared__ uint32_t flag;
+    const bool isB = blockIdx.x >= A.grid;
+    const HistPairRel &H = isB ? B : A;
+    const uint32_t g = isB ? blockIdx.x - A.grid : blockIdx.x;
+    const uint32_t F = 1u << bits;
+    const bool any = hist_segment(H.in, H.m, g, H.shift, bits, h, sbase);
+    for (uint32_t d = threadIdx.x; d < F; d += kBlock) {
+        const uint32_t v = any ? h[d] : 0u;
+        H.offs[(uint64_t)d * H.grid + g] =
+            v ? __hip_atomic_fetch_add(&H.tot[d], (uint64_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+    }
+    if (!arrive_last(H.ticket, H.grid, &flag)) return;
+    // the relation's last segment: digit starts and counts
+    uint64_t carry = 0;
+    for (uint32_t d0 = 0; d0 < F; d0 += kBlock) {
+        const uint32_t d = d0 + threadIdx.x;
+        const uint64_t v = d < F ? ld_agent(&H.tot[d]) : 0ull;
+        uint64_t tot;
+        const uint64_t ex = block_excl_scan_u64(v, scratch, &tot);
+        if (d < F) {
+            H.start[d] = carry + ex;
+            H.cnt[d] = v;
+            st_agent(&H.tot[d], 0ull);
+        }
+        carry += tot;
+    }
+    if (!arrive_last(ticket2, 2, &flag)) return;
+    // the last of the two relations: build/probe tasks over P = F partitions (A = R, B = S)
+    uint64_t base = 0, mr = 0, ms = 0;
+    for (uint32_t p0 = 0; p0 < F; p0 += kBlock) {
+        const uint32_t p = p0 + threadIdx.x;
+        const uint64_t nR = p < F ? A.cnt[p] : 0, nS = p < F ? B.cnt[p] : 0;
+        mr = nR > mr ? nR : mr;
+        ms = nS > ms ? nS : ms;
+        const uint64_t k = (nR == 0 || nS <= s_chunk) ? 0 : (nS + s_chunk - 1) / s_chunk - 1;
+        uint64_t tot;
+        const uint64_t ex = base + block_excl_scan_u64(k, scratch, &tot);
+        for (uint64_t j = 0; j < k && ex + j < over_cap; ++j) over[ex + j] = p | ((j + 1) << 32);
+        base += tot;
+    }
+    mr = block_max_u64(mr, scratch);
+    ms = block_max_u64(ms, scratch);
+    if (threadIdx.x == 0) {
+        meta[0] = mr;
+        meta[1] = ms;
+        meta[2] = base;  // n_over (u32, low word; the high word is 0)
+    }
+}
+
+hipError_t launch_hist_pair(const row_t *R, const SegMap &mR, uint32_t gridR, const row_t *S, const SegMap &mS,
+                            uint32_t gridS, uint32_t shift, uint32_t bits, uint64_t *offsR, uint64_t *offsS,
+                            uint64_t *startR, uint64_t *cntR, uint64_t *startS, uint64_t *cntS, uint64_t *sync,
+                            uint64_t *over, uint32_t over_cap, uint64_t *meta, uint64_t s_chunk, hipStream_t s) {
+    const HistPairRel A{reinterpret_cast<const uint32_t *>(R), mR, gridR, shift, offsR, sync + kSyncTotR, startR,
+                        cntR, sync + kSyncTicketR};
+    const HistPairRel B{reinterpret_cast<const uint32_t *>(S), mS, gridS, shift, offsS, sync + kSyncTotS, startS,
+                        cntS, sync + kSyncTicketS};
+    hipLaunchKernelGGL(k_hist_pair, dim3(gridR + gridS), dim3(kBlock), 0, s, A, B, bits, sync + kSyncTicket2, over,
+                       over_cap, meta, s_chunk);
+    return hipGetLastError();
 }
 
 hipError_t launch_hist(const row_t *in, const SegMap &m, uint32_t grid, uint32_t shift, uint32_t bits,
@@ -462,17 +593,18 @@ __device__ __forceinline__ void scatter_tile_write(ScatterLds<BITS, ITEMS, NT> &
     }
 }
 
+// Scatter of segment g (the body of k_scatter; k_scatter_pair runs two relations' segments
+// in one launch).
 template <int BITS, int ITEMS, int NT, bool SIDE>
-__global__ __launch_bounds__(NT, (scatter_waves_per_simd<BITS, ITEMS, NT>())) void k_scatter(const uint64_t *__restrict__ in, uint64_t *__restrict__ out,
-                                                SegMap m, uint32_t shift, const uint64_t *__restrict__ cur_init,
+__device__ __forceinline__ void scatter_segment(ScatterLds<BITS, ITEMS, NT> &L, uint32_t g,
+                                                const uint64_t *__restrict__ in, uint64_t *__restrict__ out,
+                                                const SegMap &m, uint32_t shift, const uint64_t *__restrict__ cur_init,
                                                 HistLayout layout, uint32_t nseg_stride,
-                                                const uint64_t *__restrict__ digit_base,
-                                                uint8_t *__restrict__ side, uint32_t shift2, uint32_t mask2) {
+                                                const uint64_t *__restrict__ digit_base, uint8_t *__restrict__ side,
+                                                uint32_t shift2, uint32_t mask2) {
     constexpr uint32_t TILE = NT * ITEMS;
     constexpr uint32_t F = 1u << BITS, NG = NT / kGran, CS = kGran - 1;
     static_assert(F <= NT, "one owner thread per digit");
-    __shared__ ScatterLds<BITS, ITEMS, NT> L;
-    const uint32_t g = xcd_contiguous(blockIdx.x, gridDim.x);
     uint32_t r;
     uint64_t b, e;
     if (!seg_lookup(m, g, L.sbase, r, b, e)) return;
@@ -536,6 +668,75 @@ __global__ __launch_bounds__(NT, (scatter_waves_per_simd<BITS, ITEMS, NT>())) vo
             if (SIDE) side[L.pend[d] + lane] = (uint8_t)(((uint32_t)x >> shift2) & mask2);
         }
     }
+}
+
+template <int BITS, int ITEMS, int NT, bool SIDE>
+__global__ __launch_bounds__(NT, (scatter_waves_per_simd<BITS, ITEMS, NT>())) void k_scatter(
+    const uint64_t *__restrict__ in, uint64_t *__restrict__ out, SegMap m, uint32_t shift,
+    const uint64_t *__restrict__ cur_init, HistLayout layout, uint32_t nseg_stride,
+    const uint64_t *__restrict__ digit_base, uint8_t *__restrict__ side, uint32_t shift2, uint32_t mask2) {
+    __shared__ ScatterLds<BITS, ITEMS, NT> L;
+    scatter_segment<BITS, ITEMS, NT, SIDE>(L, xcd_contiguous(blockIdx.x, gridDim.x), in, out, m, shift, cur_init,
+                                           layout, nseg_stride, digit_base, side, shift2, mask2);
+}
+
+// Both relations' one-pass scatters in one launch (small joins): workgroups
+// [0, gridR) take R's segments, the rest S's; cursors = the digit-major segment
+// offsets of k_hist_pair plus the digit starts.
+struct ScatterPairRel {
+    const uint64_t *in;
+    uint64_t *out;
+    SegMap m;
+    uint32_t grid;
+    const uint64_t *offs;
+    const uint64_t *start;
+};
+
+template <int BITS, int ITEMS, int NT>
+__global__ __launch_bounds__(NT, (scatter_waves_per_simd<BITS, ITEMS, NT>())) void k_scatter_pair(
+    ScatterPairRel A, ScatterPairRel B, uint32_t shift) {
+    __shared__ ScatterLds<BITS, ITEMS, NT> L;
+    const bool isB = blockIdx.x >= A.grid;
+    const ScatterPairRel &P = isB ? B : A;
+    const uint32_t g = isB ? blockIdx.x - A.grid : blockIdx.x;
+    scatter_segment<BITS, ITEMS, NT, false>(L, g, P.in, P.out, P.m, shift, P.offs, kDigitMajor, P.grid, P.start,
+                                            nullptr, 0, 0);
+}
+
+hipError_t launch_scatter_pair(const row_t *R, row_t *outR, const SegMap &mR, uint32_t gridR, const uint64_t *offsR,
+                               const uint64_t *startR, const row_t *S, row_t *outS, const SegMap &mS, uint32_t gridS,
+                               const uint64_t *offsS, const uint64_t *startS, uint32_t shift, uint32_t bits,
+                               hipStream_t s) {
+    constexpr int ITEMS = kScatterItems, NT = kScatterThreads;
+    const ScatterPairRel A{reinterpret_cast<const uint64_t *>(R), reinterpret_cast<uint64_t *>(outR), mR, gridR,
+                           offsR, startR};
+    const ScatterPairRel B{reinterpret_cast<const uint64_t *>(S), reinterpret_cast<uint64_t *>(outS), mS, gridS,
+                           offsS, startS};
+    const dim3 grid(gridR + gridS);
+#define PAIR_CASE(BB)                                                                                       \
+    case BB:                                                                                                \
+        if constexpr (sizeof(ScatterLds<BB, ITEMS, NT>) <= 160 * 1024 && (1 << BB) <= NT) {                   \
+            hipLaunchKernelGGL((k_scatter_pair<BB, ITEMS, NT>), grid, dim3(NT), 0, s, A, B, shift);           \
+            break;                                                                                          \
+        } else {                                                                                            \
+            return hipErrorInvalidValue;                                                                    \
+        }
+    switch (bits) {
+        PAIR_CASE(0)
+        PAIR_CASE(1)
+        PAIR_CASE(2)
+        PAIR_CASE(3)
+        PAIR_CASE(4)
+        PAIR_CASE(5)
+        PAIR_CASE(6)
+        PAIR_CASE(7)
+        PAIR_CASE(8)
+        PAIR_CASE(9)
+        default:
+            return hipErrorInvalidValue;
+    }
+#undef PAIR_CASE
+    return hipGetLastError();
 }
 
 template <int ITEMS, int NT>
@@ -610,6 +811,33 @@ hipError_t launch_scatter(const row_t *in, row_t *out, const SegMap &m, uint32_t
 //                     (radix_join.cpp:437-446) at task_off[t] + a task-local slot
 //                     taken with one LDS atomic per wave and chain step.
 
+// Count-mode reduction in the join launch itself (replaces k_reduce): the last
+// workgroup to finish sums every workgroup's partial count and build / probe ticks into
+// result[0] / [4] / [5].  red: NW + 2 u64 of LDS (NW = waves per workgroup).
+__device__ __forceinline__ void join_reduce_last(const uint64_t *__restrict__ counts, const uint64_t *__restrict__ cyc,
+                                                 uint64_t *__restrict__ result, uint64_t *__restrict__ ticket,
+                                                 uint64_t *red) {
+    const uint32_t nw = blockDim.x / kWave;
+    if (!arrive_last(ticket, gridDim.x, reinterpret_cast<uint32_t *>(red + nw + 1))) return;
+    uint64_t acc = 0, b = 0, p = 0;
+    for (uint32_t i = threadIdx.x; i < gridDim.x; i += blockDim.x) {
+        acc += counts[i];
+        if (cyc) {
+            b += cyc[2 * i];
+            p += cyc[2 * i + 1];
+        }
+    }
+    uint64_t t;
+    (void)block_excl_scan_u64(acc, red, &t);
+    if (threadIdx.x == 0) result[0] = t;
+    if (cyc) {
+        (void)block_excl_scan_u64(b, red, &t);
+        if (threadIdx.x == 0) result[4] = t;
+        (void)block_excl_scan_u64(p, red, &t);
+        if (threadIdx.x == 0) result[5] = t;
+    }
+}
+
 __device__ __forceinline__ void tmatch_add(uint64_t &m, bool hit) { m += hit ? 1u : 0u; }
 
 __device__ __forceinline__ void decode_task(uint64_t t, uint64_t P, const uint64_t *__restrict__ over, uint64_t &p,
@@ -631,7 +859,7 @@ template <int RCAP, int MODE, int NW>
 struct JoinLds {
     union {
         __attribute__((aligned(16))) uint32_t head[RCAP];
-        uint64_t red[NW];
+        uint64_t red[NW + 2];
     };
     uint32_t keys[RCAP];
     uint16_t next[RCAP];
@@ -640,7 +868,7 @@ template <int RCAP, int NW>
 struct JoinLds<RCAP, kJoinWrite, NW> {
     union {
         __attribute__((aligned(16))) uint32_t head[RCAP];
-        uint64_t red[NW];
+        uint64_t red[NW + 2];
     };
     uint32_t keys[RCAP];
     uint16_t next[RCAP];
@@ -658,7 +886,8 @@ __global__ __launch_bounds__(BLOCK) void k_join(const uint64_t *__restrict__ R, 
                                                  const uint32_t *__restrict__ n_over, uint32_t hash_shift, uint64_t s_chunk,
                                                  uint64_t *__restrict__ counts,
                                                  const uint64_t *__restrict__ task_off,
-                                                 output_triple_t *__restrict__ out, uint64_t *__restrict__ cyc) {
+                                                 output_triple_t *__restrict__ out, uint64_t *__restrict__ cyc,
+                                                 uint64_t *__restrict__ red_result, uint64_t *__restrict__ red_ticket) {
     constexpr int U = RCAP / BLOCK, NW = BLOCK / kWave;
     __shared__ JoinLds<RCAP, MODE, NW> L;
     const uint32_t tid = threadIdx.x, lane = __lane_id();
@@ -807,6 +1036,9 @@ __global__ __launch_bounds__(BLOCK) void k_join(const uint64_t *__restrict__ R, 
         cyc[2 * blockIdx.x] = bcyc;
         cyc[2 * blockIdx.x + 1] = pcyc;
     }
+    if constexpr (MODE == kJoinCount) {
+        if (red_ticket) join_reduce_last(counts, cyc, red_result, red_ticket, L.red);
+    }
 }
 
 // ------------------------------------------- 16,384-tuple counting table in 80 KiB ---
@@ -828,7 +1060,7 @@ template <int RCAP, int NW>
 struct JoinLdsTag {
     union {
         __attribute__((aligned(16))) uint32_t head2[RCAP / 2];
-        uint64_t red[NW];
+        uint64_t red[NW + 2];
     };
     uint16_t next[RCAP];
     uint8_t tag[RCAP];
@@ -844,7 +1076,8 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_join_tag(
     const uint64_t *__restrict__ R, const uint64_t *__restrict__ S, const uint64_t *__restrict__ r_start,
     const uint64_t *__restrict__ r_count, const uint64_t *__restrict__ s_start, const uint64_t *__restrict__ s_count,
     uint64_t P, const uint64_t *__restrict__ over, const uint32_t *__restrict__ n_over, uint32_t hash_shift,
-    uint64_t s_chunk, uint64_t *__restrict__ counts, uint64_t *__restrict__ cyc) {
+    uint64_t s_chunk, uint64_t *__restrict__ counts, uint64_t *__restrict__ cyc, uint64_t *__restrict__ red_result,
+    uint64_t *__restrict__ red_ticket) {
     constexpr int NW = BLOCK / kWave;
     constexpr uint32_t STRIP = BLOCK * UP;
     __shared__ JoinLdsTag<RCAP, NW> L;
@@ -948,6 +1181,7 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_join_tag(
         cyc[2 * blockIdx.x] = bcyc;
         cyc[2 * blockIdx.x + 1] = pcyc;
     }
+    if (red_ticket) join_reduce_last(counts, cyc, red_result, red_ticket, L.red);
 }
 
 // ------------------------------------------------------- histogram join (RHT) ---
@@ -967,7 +1201,7 @@ struct HistJoinLds {
     uint32_t keys[RCAP];
     uint32_t rpay[MODE == kJoinWrite ? RCAP : 1];
     uint32_t cursor;
-    uint64_t red[kWaves];
+    uint64_t red[kWaves + 2];
 };
 
 template <int RCAP, int MODE>
@@ -980,7 +1214,9 @@ __global__ __launch_bounds__(kBlock) void k_join_hist(const uint64_t *__restrict
                                                       const uint32_t *__restrict__ n_over, uint32_t hash_shift, uint64_t s_chunk,
                                                       uint64_t *__restrict__ counts,
                                                       const uint64_t *__restrict__ task_off,
-                                                      output_triple_t *__restrict__ out, uint64_t *__restrict__ cyc) {
+                                                      output_triple_t *__restrict__ out, uint64_t *__restrict__ cyc,
+                                                      uint64_t *__restrict__ red_result,
+                                                      uint64_t *__restrict__ red_ticket) {
     constexpr int U = RCAP / kBlock;
     constexpr int NB = HistJoinLds<RCAP, MODE>::NB;
     __shared__ HistJoinLds<RCAP, MODE> L;
@@ -1140,18 +1376,23 @@ __global__ __launch_bounds__(kBlock) void k_join_hist(const uint64_t *__restrict
         cyc[2 * blockIdx.x] = bcyc;
         cyc[2 * blockIdx.x + 1] = pcyc;
     }
+    if constexpr (MODE == kJoinCount) {
+        if (red_ticket) join_reduce_last(counts, cyc, red_result, red_ticket, L.red);
+    }
 }
 
 hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, const uint64_t *r_count,
                        const uint64_t *s_start, const uint64_t *s_count, uint64_t P, const uint64_t *over,
                        const uint32_t *n_over, uint32_t hash_shift, uint32_t rcap, uint64_t s_chunk, uint32_t grid,
                        int mode, int algo, uint64_t *counts, const uint64_t *task_off, output_triple_t *out,
-                       uint64_t *cyc, hipStream_t s) {
+                       uint64_t *cyc, hipStream_t s, const JoinReduce *reduce) {
     const uint64_t *R64 = reinterpret_cast<const uint64_t *>(R);
     const uint64_t *S64 = reinterpret_cast<const uint64_t *>(S);
+    uint64_t *rres = (reduce && mode == kJoinCount) ? reduce->result : nullptr;
+    uint64_t *rtick = (reduce && mode == kJoinCount) ? reduce->ticket : nullptr;
 #define JOIN_LAUNCH(K, RC, MD)                                                                             \
     hipLaunchKernelGGL((K<RC, MD>), dim3(grid), dim3(kBlock), 0, s, R64, S64, r_start, r_count, s_start,    \
-                       s_count, P, over, n_over, hash_shift, s_chunk, counts, task_off, out, cyc)
+                       s_count, P, over, n_over, hash_shift, s_chunk, counts, task_off, out, cyc, rres, rtick)
 #define JOIN_MODES(K, RC)                                                    \
     case RC:                                                                 \
         if (mode == kJoinCount) JOIN_LAUNCH(K, RC, kJoinCount);              \
@@ -1180,14 +1421,30 @@ hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, 
         }();
         if (tag_block == 512)
             hipLaunchKernelGGL((k_join_tag<kBigRcap, 512, 16>), dim3(grid), dim3(512), 0, s, R64, S64, r_start, r_count,
-                               s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts, cyc);
+                               s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts, cyc, rres, rtick);
         else if (tag_block == 1024)
             hipLaunchKernelGGL((k_join_tag<kBigRcap, 1024, 8>), dim3(grid), dim3(1024), 0, s, R64, S64, r_start, r_count,
-                               s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts, cyc);
+                               s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts, cyc, rres, rtick);
         else
             hipLaunchKernelGGL((k_join<kBigRcap, kJoinCount, kBigJoinBlock>), dim3(grid), dim3(kBigJoinBlock), 0, s,
                                R64, S64, r_start, r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk,
-                               counts, task_off, out, cyc);
+                               counts, task_off, out, cyc, rres, rtick);
+    } else if (mode == kJoinCount && grid <= 512 && rcap <= 4096) {
+        // few tasks (small joins: one workgroup per CU at most): 1,024 threads per table
+        // instead of 256, so that a CU holds 16 waves to hide the load latencies
+#define JOIN_WIDE(RC)                                                                                        \
+    case RC:                                                                                                 \
+        hipLaunchKernelGGL((k_join<RC, kJoinCount, 1024>), dim3(grid), dim3(1024), 0, s, R64, S64, r_start,   \
+                           r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts, task_off, out, \
+                           cyc, rres, rtick);                                                                \
+        break;
+        switch (rcap) {
+            JOIN_WIDE(2048)
+            JOIN_WIDE(4096)
+            default:
+                return hipErrorInvalidValue;
+        }
+#undef JOIN_WIDE
     } else {
         switch (rcap) {
             JOIN_MODES(k_join, 2048)

@@ -53,8 +53,9 @@ hipEvent_t Timer::get_event() {
     return pool_[used_++];
 }
 
-void Timer::begin_call(hipStream_t s, bool enabled) {
+void Timer::begin_call(hipStream_t s, bool enabled, bool coarse) {
     enabled_ = enabled;
+    coarse_ = coarse;
     stream_ = s;
     used_ = 0;
     spans_.clear();
@@ -64,12 +65,12 @@ void Timer::begin_call(hipStream_t s, bool enabled) {
 }
 
 void Timer::mark(const char *name) {
-    if (!enabled_) return;
+    if (!enabled_ || (coarse_ && open_ev_)) return;
     hipEvent_t ev = get_event();
     if (!ev) return;
     (void)hipEventRecord(ev, stream_);
     if (open_ev_) spans_.push_back({open_name_, {open_ev_, ev}});
-    open_name_ = name;
+    open_name_ = coarse_ ? "total" : name;
     open_ev_ = ev;
 }
 

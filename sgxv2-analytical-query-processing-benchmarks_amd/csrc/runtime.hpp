@@ -42,7 +42,9 @@ struct Arena {
 // Per-kernel HIP event timing, enabled per thread.
 class Timer {
    public:
-    void begin_call(hipStream_t s, bool enabled);
+    // coarse: one span "total" from the first mark to end_call (two events per call
+    // instead of one per kernel: what a join records when per-kernel timing is off)
+    void begin_call(hipStream_t s, bool enabled, bool coarse = false);
     void mark(const char *name);  // closes the previous span, opens `name`
     void end_call();              // closes the last span (before the final sync)
     // after the stream synchronised: fold event pairs into (name, ms)
@@ -54,8 +56,10 @@ class Timer {
         records_.insert(records_.end(), other.records_.begin(), other.records_.end());
     }
     bool enabled() const { return enabled_; }
+    bool coarse() const { return coarse_; }
 
    private:
+    bool coarse_ = false;
     hipEvent_t get_event();
     bool enabled_ = false;
     hipStream_t stream_ = nullptr;
@@ -88,6 +92,9 @@ struct Context {
     // multi-GPU exchange workspace (multi_host.cpp): shard-partitioned send buffers and
     // the receive buffers the peers' pieces land in
     DeviceBuffer xsendR, xsendS, xrecvR, xrecvS;
+    // in-launch hand-off words (tickets, digit totals) of the small-join path: zeroed
+    // once when allocated, left zero by every kernel that uses them
+    DeviceBuffer sync;
 };
 
 // Context of the calling thread's current HIP device (created on first use).
