@@ -119,6 +119,27 @@ inline bool digit_side_enabled() {
 }
 inline bool uses_digit_side(const Policy &p) { return p.passes == 2 && p.b2 <= 8 && digit_side_enabled(); }
 
+// Two-pass plans with the digit side stream take the pooled pass 1 (no pass-1
+// histogram: rho_internal.hpp PoolOut).  SGXAMD_POOL=0 keeps the histogram
+// + cursor pass 1 (development A/B switch; results are identical).  SGXAMD_POOL_SEGS:
+// pass-1 workgroups per relation (development; default kPoolSegs).
+inline bool pool_enabled() {
+    static const bool on = [] {
+        const char *e = std::getenv("SGXAMD_POOL");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return on;
+}
+constexpr uint32_t kPoolSegs = 512;  // two 512-thread workgroups per CU: one wave of workgroups
+inline uint32_t pool_segs() {
+    static const uint32_t v = [] {
+        const char *e = std::getenv("SGXAMD_POOL_SEGS");
+        const long x = e ? std::atol(e) : 0;
+        return x > 0 ? (uint32_t)x : kPoolSegs;
+    }();
+    return v;
+}
+
 
 inline uint64_t seg_size_for(uint64_t n) {
     uint64_t s = (n + kSegTarget - 1) / kSegTarget;
@@ -132,8 +153,12 @@ struct RelPlan {
     uint32_t nseg1;
     uint64_t seg2;
     uint32_t grid2;
-    // scratch offsets
+    bool pooled;           // pooled pass 1 + block-list pass 2
+    uint32_t pool_blocks;  // blocks per pass-1 segment pool
+    uint64_t t1_tuples;    // capacity of the pass-1 output (and side stream) in tuples
+    // scratch offsets (pooled: hist1 holds the chain records, tot1 their column totals)
     size_t hist1, tot1, start1, cnt1, segbase2, hist2, pstart, pcnt;
+    size_t binfo, used, lbase, lcount, list;
 };
 
 #define RHO_HIP(call)                                                                      \
@@ -144,6 +169,50 @@ struct RelPlan {
             return (_e == hipErrorOutOfMemory) ? MI355_ERR_OOM : MI355_ERR_HIP;            \
         }                                                                                  \
     } while (0)
+
+// Pooled two-pass partition of one relation (pass 1 when !pass2_now, else pass 2).
+int partition_relation_pooled(Context *ctx, hipStream_t s, Timer &tm, const std::string &t, const row_t *in,
+                              row_t *t1, row_t *t2, uint8_t *side, RelPlan &rp, const Policy &pol, uint32_t key_shift,
+                              const row_t **final_rel, const uint64_t **pstart, const uint64_t **pcnt,
+                              bool pass2_now) {
+    Arena &A = ctx->scratch;
+    uint64_t *start1 = A.at<uint64_t>(rp.start1);
+    uint64_t *cnt1 = A.at<uint64_t>(rp.cnt1);
+    uint32_t *segbase2 = A.at<uint32_t>(rp.segbase2);
+    uint64_t *lbase = A.at<uint64_t>(rp.lbase), *lcount = A.at<uint64_t>(rp.lcount);
+    uint64_t *list = A.at<uint64_t>(rp.list);
+    const uint32_t F1 = 1u << pol.b1;
+    if (!pass2_now) {
+        const SegMap m1{nullptr, nullptr, nullptr, 1, rp.seg1, rp.n};
+        const PoolOut po{A.at<uint32_t>(rp.binfo), A.at<uint64_t>(rp.hist1), A.at<uint32_t>(rp.used), rp.pool_blocks,
+                         rp.nseg1};
+        const DigitSide ds{side, key_shift + pol.b1, pol.b2};
+        tm.mark((t + "pass1_scatter").c_str());
+        RHO_HIP(launch_scatter_pool(in, t1, m1, rp.nseg1, key_shift, pol.b1, po, ds, s));
+        tm.mark((t + "pass1_scan").c_str());
+        RHO_HIP(launch_pool_layout(po.cnt, rp.nseg1, pol.b1, A.at<uint64_t>(rp.tot1), start1, cnt1, lbase, lcount,
+                                   segbase2, s));
+        RHO_HIP(launch_block_list(po, lbase, list, s));
+        *final_rel = t1;
+        *pstart = start1;
+        *pcnt = cnt1;
+        return MI355_OK;
+    }
+    uint64_t *hist2 = A.at<uint64_t>(rp.hist2);
+    uint64_t *ps = A.at<uint64_t>(rp.pstart);
+    uint64_t *pc = A.at<uint64_t>(rp.pcnt);
+    const SegMap m2{lbase, lcount, segbase2, F1, kPass2Ents, rp.n};
+    tm.mark((t + "pass2_hist").c_str());
+    RHO_HIP(launch_hist_side_blk(side, list, m2, rp.grid2, pol.b2, hist2, s));
+    tm.mark((t + "pass2_scan").c_str());
+    RHO_HIP(launch_scan_regions(hist2, segbase2, start1, F1, pol.b2, ps, pc, s));
+    tm.mark((t + "pass2_scatter").c_str());
+    RHO_HIP(launch_scatter_blk(t1, list, t2, m2, rp.grid2, key_shift + pol.b1, pol.b2, hist2, s));
+    *final_rel = t2;
+    *pstart = ps;
+    *pcnt = pc;
+    return MI355_OK;
+}
 
 // One relation through pass 1 (and pass 2).  Returns the final buffer and
 // partition table pointers through *final / *pstart / *pcnt.  side (n bytes, two-pass
@@ -160,6 +229,8 @@ int partition_relation(Context *ctx, hipStream_t s, Timer &tm, const char *tag, 
     uint32_t *segbase2 = A.at<uint32_t>(rp.segbase2);
     std::string t(tag);
     const bool use_side = side != nullptr && uses_digit_side(pol);
+    if (rp.pooled) return partition_relation_pooled(ctx, s, tm, t, in, t1, t2, side, rp, pol, key_shift, final_rel,
+                                                    pstart, pcnt, pass2_now);
     if (!pass2_now) {
         SegMap m1{nullptr, nullptr, nullptr, 1, rp.seg1, rp.n};
         tm.mark((t + "pass1_hist").c_str());
@@ -204,6 +275,26 @@ void plan_relation(Arena &A, RelPlan &rp, uint64_t n, const Policy &pol) {
     const uint32_t F1 = 1u << pol.b1, F2 = 1u << pol.b2;
     rp.seg2 = seg_size_for(n);
     rp.grid2 = (uint32_t)((n + rp.seg2 - 1) / rp.seg2) + F1;
+    rp.t1_tuples = n;
+    rp.pooled = false;
+    if (pol.passes == 2 && uses_digit_side(pol) && pool_enabled() && n > 0) {
+        // pass-1 segments of whole tiles, about pool_segs() of them; every digit of a
+        // segment fills ceil(tuples / kBlk) blocks, so a pool of ceil(seg1 / kBlk) + F1
+        // blocks always suffices.  Chain records pack blocks << 40 | tuples.
+        uint64_t seg = (n + pool_segs() - 1) / pool_segs();
+        seg = std::max<uint64_t>((seg + kTile - 1) / kTile * kTile, kTile);
+        const uint32_t nseg = (uint32_t)((n + seg - 1) / seg);
+        const uint64_t pb = (seg + kBlk - 1) / kBlk + F1;
+        const uint64_t max_blocks = n / kBlk + (uint64_t)nseg * F1;
+        if (max_blocks < (1ull << 24) && (uint64_t)nseg * pb < (1ull << 27)) {
+            rp.pooled = true;
+            rp.seg1 = seg;
+            rp.nseg1 = nseg;
+            rp.pool_blocks = (uint32_t)pb;
+            rp.t1_tuples = (uint64_t)nseg * pb * kBlk;
+            rp.grid2 = (uint32_t)(max_blocks / kPass2Ents) + F1 + 1;
+        }
+    }
     rp.hist1 = A.reserve(sizeof(uint64_t) * (size_t)F1 * std::max<uint32_t>(rp.nseg1, 1));
     rp.tot1 = A.reserve(sizeof(uint64_t) * F1);
     rp.start1 = A.reserve(sizeof(uint64_t) * F1);
@@ -213,6 +304,13 @@ void plan_relation(Arena &A, RelPlan &rp, uint64_t n, const Policy &pol) {
         rp.hist2 = A.reserve(sizeof(uint64_t) * (size_t)rp.grid2 * F2);
         rp.pstart = A.reserve(sizeof(uint64_t) * (size_t)F1 * F2);
         rp.pcnt = A.reserve(sizeof(uint64_t) * (size_t)F1 * F2);
+    }
+    if (rp.pooled) {
+        rp.binfo = A.reserve(sizeof(uint32_t) * (size_t)rp.nseg1 * rp.pool_blocks);
+        rp.used = A.reserve(sizeof(uint32_t) * rp.nseg1);
+        rp.lbase = A.reserve(sizeof(uint64_t) * F1);
+        rp.lcount = A.reserve(sizeof(uint64_t) * F1);
+        rp.list = A.reserve(sizeof(uint64_t) * (size_t)(rp.n / kBlk + (uint64_t)rp.nseg1 * F1));
     }
 }
 
@@ -266,20 +364,21 @@ int plan_join(Context *ctx, hipStream_t s, uint64_t nR, uint64_t nS, const mi355
         set_last_error("key_shift + radix bits must stay below 32");
         return MI355_ERR_INVALID;
     }
-    RHO_HIP(ctx->t1R.ensure(std::max<uint64_t>(nR, 1) * sizeof(row_t)));
-    RHO_HIP(ctx->t1S.ensure(std::max<uint64_t>(nS, 1) * sizeof(row_t)));
+    Arena &A = ctx->scratch;
+    A.reset();
+    plan_relation(A, pj.pr, nR, pol);
+    plan_relation(A, pj.ps, nS, pol);
+    const uint64_t c1R = pj.pr.t1_tuples, c1S = pj.ps.t1_tuples;  // pooled pass 1 needs room for its pools
+    RHO_HIP(ctx->t1R.ensure(std::max<uint64_t>(c1R, 1) * sizeof(row_t)));
+    RHO_HIP(ctx->t1S.ensure(std::max<uint64_t>(c1S, 1) * sizeof(row_t)));
     if (pol.passes == 2) {
         RHO_HIP(ctx->t2R.ensure(std::max<uint64_t>(nR, 1) * sizeof(row_t)));
         RHO_HIP(ctx->t2S.ensure(std::max<uint64_t>(nS, 1) * sizeof(row_t)));
     }
     if (uses_digit_side(pol)) {
-        RHO_HIP(ctx->sideR.ensure(std::max<uint64_t>(nR, 16)));
-        RHO_HIP(ctx->sideS.ensure(std::max<uint64_t>(nS, 16)));
+        RHO_HIP(ctx->sideR.ensure(std::max<uint64_t>(c1R, 16)));
+        RHO_HIP(ctx->sideS.ensure(std::max<uint64_t>(c1S, 16)));
     }
-    Arena &A = ctx->scratch;
-    A.reset();
-    plan_relation(A, pj.pr, nR, pol);
-    plan_relation(A, pj.ps, nS, pol);
     const uint64_t P = 1ull << pol.bits;
     if (uses_big_table(opts) && pol.rcap == 8192 && (nR + P - 1) / P > 8192) {
         pj.pol.rcap = kBigRcap;

@@ -81,6 +81,42 @@ struct DigitSide {
 hipError_t launch_hist_side(const uint8_t *side, const SegMap &m, uint32_t grid, uint32_t bits, uint64_t *hist,
                             hipStream_t s);
 
+// ---- pooled pass 1 (two-pass plans without a pass-1 histogram) ----
+// Every pass-1 workgroup owns a pool of pool_blocks blocks of kBlk tuples in the
+// pass-1 output and fills one chain of blocks per digit (one LDS atomic per new block,
+// no global atomics).  A block holds tuples of one digit: every block of a chain is
+// full except its last.  Pass 2 reads each region (pass-1 digit) through a list of its
+// blocks, so the pass-1 scatter needs no cursors and the relation is read once in pass 1
+// instead of twice (histogram + scatter).
+constexpr uint32_t kBlkShift = 8;
+constexpr uint32_t kBlk = 1u << kBlkShift;          // tuples per block (2 KiB)
+constexpr uint32_t kPass2Ents = 512;                // blocks per pass-2 segment (LDS list copy)
+struct PoolOut {
+    uint32_t *binfo;       // per pool block: digit | fill << 16
+    uint64_t *cnt;         // [d][g] (stride nseg): blocks << 40 | tuples of digit d in segment g
+    uint32_t *used;        // per segment: blocks taken from its pool
+    uint32_t pool_blocks;  // blocks per segment pool
+    uint32_t nseg;
+};
+// Pass 1 of a pooled plan: contiguous input segments (m), pooled output in out, digit
+// side stream ds (required) beside every stored tuple.
+hipError_t launch_scatter_pool(const row_t *in, row_t *out, const SegMap &m, uint32_t grid, uint32_t shift,
+                               uint32_t bits, const PoolOut &po, const DigitSide &ds, hipStream_t s);
+// After launch_scan_single-style column scans of po.cnt (k_scan_cols, in place): region
+// tuple starts / counts (the pass-2 output layout), region block-list bases / lengths
+// and the pass-2 segment table (kPass2Ents blocks per segment).
+hipError_t launch_pool_layout(uint64_t *cnt, uint32_t nseg, uint32_t bits, uint64_t *totals, uint64_t *start,
+                              uint64_t *count, uint64_t *lbase, uint64_t *lcount, uint32_t *seg_base, hipStream_t s);
+// The block list: region d's blocks at [lbase[d], lbase[d] + lcount[d]) as
+// physical block | fill << 32.
+hipError_t launch_block_list(const PoolOut &po, const uint64_t *lbase, uint64_t *list, hipStream_t s);
+// Pass-2 histogram / scatter over block-list segments (m: reg_start = lbase,
+// reg_count = lcount, seg_size = kPass2Ents).
+hipError_t launch_hist_side_blk(const uint8_t *side, const uint64_t *list, const SegMap &m, uint32_t grid,
+                                uint32_t bits, uint64_t *hist, hipStream_t s);
+hipError_t launch_scatter_blk(const row_t *in, const uint64_t *list, row_t *out, const SegMap &m, uint32_t grid,
+                              uint32_t shift, uint32_t bits, const uint64_t *cursors, hipStream_t s);
+
 // Stable scatter of every segment into `out` at the cursors of the scan.
 // digit_base (nullable) is added to the cursors: base[r * F + d].
 // ds (nullable): also write the digit side stream for the next pass.

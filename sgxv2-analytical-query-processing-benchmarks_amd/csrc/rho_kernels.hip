@@ -412,7 +412,9 @@ hipError_t launch_scan_regions(uint64_t *hist, const uint32_t *seg_base, const u
 // register sets).  The last carries of the segment are flushed at the end.
 constexpr uint32_t kGran = 16;  // tuples per output granule = one 128-B line
 
-template <int BITS, int ITEMS, int NT>
+// EXT: 0 = cursor output, contiguous input; 1 = pooled output (PoolOut); 2 = block-list
+// input (the segment's list entries staged in ents).
+template <int BITS, int ITEMS, int NT, int EXT = 0>
 struct ScatterLds {
     static constexpr uint32_t F = 1u << BITS;
     static constexpr uint32_t TILE = NT * ITEMS;
@@ -430,14 +432,27 @@ struct ScatterLds {
     uint32_t gbase[F];                // first granule descriptor of d
     uint16_t desc[MAXDESC];           // granule j belongs to digit desc[j]
     uint32_t wt[NW][2];
+    uint2 gaddr[EXT == 1 ? F : 1];    // pooled: {granule of d's first write in its current block,
+                                      //          first granule of the blocks d took for this tile}
+    uint64_t ents[EXT == 2 ? kPass2Ents : 1];  // block-list input: phys block | fill << 32
+    uint32_t pool_next;               // pooled: blocks taken from the segment's pool
 };
+
+// Pooled output, per owner thread (digit): its chain's current block and length.
+struct PoolState {
+    uint32_t cur;
+    uint32_t nb;
+    uint32_t pool0;  // first block of the segment's pool
+    uint32_t *binfo;
+};
+constexpr uint32_t kGPB = kBlk / kGran;  // granules per pool block
 
 // Waves per SIMD that the LDS footprint allows (__launch_bounds__ second argument:
 // k workgroups per CU of NT threads <=> k * NT / 256 waves per SIMD), so the
 // register allocation never becomes the tighter occupancy limit.
-template <int BITS, int ITEMS, int NT>
+template <int BITS, int ITEMS, int NT, int EXT = 0>
 constexpr int scatter_waves_per_simd() {
-    constexpr int k = (160 * 1024) / (int)sizeof(ScatterLds<BITS, ITEMS, NT>);
+    constexpr int k = (160 * 1024) / (int)sizeof(ScatterLds<BITS, ITEMS, NT, EXT>);
     constexpr int w = (k < 1 ? 1 : k) * NT / 256;
     // at most 4 waves/SIMD (128 VGPRs): fewer registers spill, and a scratch reload is
     // a vector-memory op whose wait would also wait for every store in flight
@@ -481,25 +496,29 @@ __device__ __forceinline__ void block_scan2(uint32_t a, uint32_t b, uint32_t (&w
 }
 
 // Phases A-C of one tile: the tile ends up digit-sorted in L.tile (v is dead after).
-template <int BITS, int ITEMS, int NT>
-__device__ __forceinline__ uint32_t scatter_tile_sort(ScatterLds<BITS, ITEMS, NT> &L, uint64_t &pend,
+// tn: valid tuples of the tile (items tid + k * NT < tn); with block-list input (EXT 2)
+// a bit mask instead, bit k = item k valid.  ps: the owner thread's chain (EXT 1).
+template <int BITS, int ITEMS, int NT, int EXT = 0>
+__device__ __forceinline__ uint32_t scatter_tile_sort(ScatterLds<BITS, ITEMS, NT, EXT> &L, uint64_t &pend,
                                                       uint32_t &carried, const uint64_t (&v)[ITEMS],
                                                       uint64_t *__restrict__ out, uint32_t tn, uint32_t shift,
-                                                      uint64_t tbase_global) {
+                                                      uint64_t tbase_global, PoolState *ps = nullptr) {
     constexpr uint32_t F = 1u << BITS, mask = F - 1, NW = NT / kWave;
     const uint32_t tid = threadIdx.x;
+    const auto valid = [&](int k) { return EXT == 2 ? ((tn >> k) & 1u) != 0 : tid + k * NT < tn; };
 #ifdef SGXAMD_ABLATE_NOSORT  // development ablation (tools/part_bench): the memory pipeline alone
 #pragma unroll
     for (int k = 0; k < ITEMS; ++k)
-        if (tid + k * NT < tn) st_nt(out + tbase_global + tid + k * NT, v[k]);
+        if (valid(k)) st_nt(out + tbase_global + tid + k * NT, v[k]);
     return 0;
 #endif
     (void)tbase_global;
+    (void)ps;
     // A. slot of every tuple inside its digit
     uint32_t slot[ITEMS];
 #pragma unroll
     for (int k = 0; k < ITEMS; ++k)
-        if (tid + k * NT < tn) slot[k] = atomicAdd(&L.cnt[((uint32_t)v[k] >> shift) & mask], 1u);
+        if (valid(k)) slot[k] = atomicAdd(&L.cnt[((uint32_t)v[k] >> shift) & mask], 1u);
     __syncthreads();
     // B. per digit: what is written now (w), what is carried on (r), granules touched (g)
     uint32_t t = 0, g = 0, w = 0, r = 0, c = 0;
@@ -520,9 +539,29 @@ __device__ __forceinline__ uint32_t scatter_tile_sort(ScatterLds<BITS, ITEMS, NT
     block_scan2<NW>(t, g, L.wt, tb, gb, ttot, gtot);
     (void)ttot;
     if (tid < F) {
+        uint32_t mx = tb;
+        if constexpr (EXT == 1) {
+            // pooled: pend is granule-aligned (only whole granules are written before the
+            // segment's end).  g0 granules fill the current block, the rest go to nnew
+            // fresh blocks of the pool, taken together (consecutive, so contiguous).
+            const uint32_t off = (uint32_t)(p0 / kGran) & (kGPB - 1);
+            const uint32_t g0 = off ? min(g, kGPB - off) : 0u;
+            const uint32_t nnew = (g - g0 + kGPB - 1) / kGPB;
+            uint32_t nb0 = 0;
+            if (nnew) {
+                nb0 = ps->pool0 + atomicAdd(&L.pool_next, nnew);
+                for (uint32_t j = 0; j < nnew; ++j) ps->binfo[nb0 + j] = tid | (kBlk << 16);
+            }
+            L.gaddr[tid] = make_uint2(ps->cur * kGPB + off, nb0 * kGPB);
+            mx |= g0 << 16;
+            if (nnew) {
+                ps->cur = nb0 + nnew - 1;
+                ps->nb += nnew;
+            }
+        }
         L.tbase[tid] = tb;
         L.gbase[tid] = gb;
-        L.meta[tid] = make_uint2(tb, c | (r << 8) | (w << 16));
+        L.meta[tid] = make_uint2(mx, c | (r << 8) | (w << 16));
         L.pend[tid] = p0;
         for (uint32_t j = 0; j < g; ++j) L.desc[gb + j] = (uint16_t)tid;
         pend = p0 + w;
@@ -532,7 +571,7 @@ __device__ __forceinline__ uint32_t scatter_tile_sort(ScatterLds<BITS, ITEMS, NT
     // C. the tile, digit-sorted
 #pragma unroll
     for (int k = 0; k < ITEMS; ++k) {
-        if (tid + k * NT < tn) {
+        if (valid(k)) {
             const uint32_t d = ((uint32_t)v[k] >> shift) & mask;
             L.tile[L.tbase[d] + slot[k]] = v[k];
         }
@@ -544,18 +583,35 @@ __device__ __forceinline__ uint32_t scatter_tile_sort(ScatterLds<BITS, ITEMS, NT
 // Phases D-E of the tile sorted by scatter_tile_sort (gtot = its granule count).
 // SIDE: every stored tuple's next-pass digit also goes to side[a] (a 16-lane group
 // writes 16 consecutive bytes next to its 128-B granule).
-template <int BITS, int ITEMS, int NT, bool SIDE>
-__device__ __forceinline__ void scatter_tile_write(ScatterLds<BITS, ITEMS, NT> &L, uint64_t *__restrict__ out,
+template <int BITS, int ITEMS, int NT, bool SIDE, int EXT = 0>
+__device__ __forceinline__ void scatter_tile_write(ScatterLds<BITS, ITEMS, NT, EXT> &L, uint64_t *__restrict__ out,
                                                    uint32_t gtot, uint8_t *__restrict__ side, uint32_t shift2,
                                                    uint32_t mask2) {
     constexpr uint32_t F = 1u << BITS, NG = NT / kGran;
     constexpr uint32_t CS = kGran - 1;
+    constexpr uint32_t TB = EXT == 1 ? 0xFFFFu : ~0u;  // tile offset bits of meta.x
 #ifdef SGXAMD_ABLATE_NOSORT
     return;
 #endif
     const uint32_t tid = threadIdx.x;
     // D. whole granules, 16 lanes (one 128-B line) per granule
     const uint32_t lane = tid & (kGran - 1), grp = tid / kGran;
+    if constexpr (EXT == 1) {
+        // pooled: every granule is whole (the digit's writes start granule-aligned); the
+        // first g0 of d go to its current block, the rest to its fresh blocks
+        for (uint32_t j = grp; j < gtot; j += NG) {
+            const uint32_t d = L.desc[j];
+            const uint2 m = L.meta[d];
+            const uint2 ga = L.gaddr[d];
+            const uint32_t jj = j - L.gbase[d], g0 = m.x >> 16, cd = m.y & 0xFFu;
+            const uint32_t gran = jj < g0 ? ga.x + jj : ga.y + (jj - g0);
+            const uint64_t a = (uint64_t)gran * kGran + lane;
+            const uint32_t q = jj * kGran + lane;
+            const uint64_t x = q < cd ? L.carry[d * CS + q] : L.tile[(m.x & TB) + q - cd];
+            st_nt(out + a, x);
+            if (SIDE) side[a] = (uint8_t)(((uint32_t)x >> shift2) & mask2);
+        }
+    } else
     for (uint32_t j = grp; j < gtot; j += NG) {
         const uint32_t d = L.desc[j];
         const uint2 m = L.meta[d];
@@ -586,9 +642,9 @@ __device__ __forceinline__ void scatter_tile_write(ScatterLds<BITS, ITEMS, NT> &
         const uint2 m = L.meta[d];
         const uint32_t cd = m.y & 0xFFu, rd = (m.y >> 8) & 0xFFu, wd = m.y >> 16;
         if (wd > 0) {
-            if (lane < rd) L.carry[d * CS + lane] = L.tile[m.x + wd - cd + lane];
+            if (lane < rd) L.carry[d * CS + lane] = L.tile[(m.x & TB) + wd - cd + lane];
         } else if (lane < rd - cd) {
-            L.carry[d * CS + cd + lane] = L.tile[m.x + lane];
+            L.carry[d * CS + cd + lane] = L.tile[(m.x & TB) + lane];
         }
     }
 }
@@ -784,6 +840,329 @@ hipError_t launch_scatter(const row_t *in, row_t *out, const SegMap &m, uint32_t
     uint64_t *o64 = reinterpret_cast<uint64_t *>(out);
     return launch_scatter_items<kScatterItems, kScatterThreads>(i64, o64, m, grid, shift, bits, cursors, layout,
                                                                 nseg_stride, digit_base, s, ds);
+}
+
+// ------------------------------------------------ pooled pass 1, block-list pass 2 ---
+// Two-pass plans without a pass-1 histogram (rho_internal.hpp PoolOut).  Pass 1
+// (EXT 1): the same tile sort and write combining, but a digit's granules go to a chain
+// of kBlk-tuple blocks taken from the workgroup's own pool (one LDS atomic per new
+// block) instead of to cursors from a histogram + scan, so the relation is read once.
+// Pass 2 (EXT 2): a segment is up to kPass2Ents blocks of one region; a tile is
+// TILE / kBlk whole blocks, item k of thread t being tuple (t mod kBlk) of block
+// k * NT / kBlk + t / kBlk — uniform per wave, so each item loads through a buffer
+// resource over its block (lanes past the block's fill read 0 and are masked out).
+
+// Tile loads of a block-list segment (entries staged in LDS); returns the valid mask.
+template <int ITEMS, int NT, int BITS>
+__device__ __forceinline__ uint32_t load_tile_blk(const uint64_t *__restrict__ in,
+                                                  const ScatterLds<BITS, ITEMS, NT, 2> &L, uint32_t nent, uint32_t e0,
+                                                  uint64_t (&dst)[ITEMS]) {
+    static_assert(NT % kBlk == 0, "a wave reads inside one block");
+    const uint32_t o = threadIdx.x & (kBlk - 1);
+    const uint32_t h = __builtin_amdgcn_readfirstlane(threadIdx.x >> kBlkShift);
+    uint32_t vm = 0;
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {
+        const uint32_t j = e0 + (uint32_t)k * (NT / kBlk) + h;
+        const uint64_t en = j < nent ? L.ents[j] : 0ull;
+        const uint32_t phys = __builtin_amdgcn_readfirstlane((uint32_t)en);
+        const uint32_t fill = __builtin_amdgcn_readfirstlane((uint32_t)(en >> 32));
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(in + (uint64_t)phys * kBlk, fill * 8u);
+        dst[k] = buf_ld_nt_u64(rs, o * 8u, 0u);
+        vm |= (o < fill ? 1u : 0u) << k;
+    }
+    return vm;
+}
+
+// EXT 1: contiguous segment g of `in` -> pooled output (po), digit side stream.
+// EXT 2: block-list segment g (list) -> `out` at the segment-major cursors cur_init.
+template <int BITS, int ITEMS, int NT, int EXT>
+__device__ __forceinline__ void scatter_segment_ext(ScatterLds<BITS, ITEMS, NT, EXT> &L, uint32_t g,
+                                                    const uint64_t *__restrict__ in, uint64_t *__restrict__ out,
+                                                    const SegMap &m, uint32_t shift,
+                                                    const uint64_t *__restrict__ cur_init,
+                                                    const uint64_t *__restrict__ list, const PoolOut &po,
+                                                    uint8_t *__restrict__ side, uint32_t shift2, uint32_t mask2) {
+    constexpr uint32_t TILE = NT * ITEMS, BPT = TILE / kBlk;
+    constexpr uint32_t F = 1u << BITS, NG = NT / kGran, CS = kGran - 1;
+    constexpr bool SIDE = EXT == 1;
+    static_assert(F <= NT, "one owner thread per digit");
+    uint32_t r;
+    uint64_t b, e;
+    if (!seg_lookup(m, g, L.sbase, r, b, e)) return;
+    uint64_t pend = 0;
+    uint32_t carried = 0;
+    const uint32_t tid = threadIdx.x;
+    PoolState ps{0u, 0u, EXT == 1 ? g * po.pool_blocks : 0u, po.binfo};
+    if (tid < F) {
+        if constexpr (EXT == 2) pend = cur_init[(uint64_t)g * F + tid];
+        L.cnt[tid] = 0;
+    }
+    if (tid == 0) L.pool_next = 0;
+    uint32_t nent = 0;
+    if constexpr (EXT == 2) {
+        nent = (uint32_t)(e - b);  // <= kPass2Ents (the plan's segment size)
+        for (uint32_t i = tid; i < nent; i += NT) L.ents[i] = list[b + i];
+    }
+    __syncthreads();  // sbase (aliased with tile) is dead from here on
+    const uint32_t ntiles = EXT == 2 ? (nent + BPT - 1) / BPT : (uint32_t)((e - b + TILE - 1) / TILE);
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(in + b, EXT == 2 ? 0u : (uint32_t)((e - b) * sizeof(uint64_t)));
+    const auto load = [&](uint32_t ti, uint64_t(&dst)[ITEMS]) -> uint32_t {
+        if constexpr (EXT == 2) {
+            return load_tile_blk<ITEMS, NT, BITS>(in, L, nent, ti * BPT, dst);
+        } else {
+            load_tile<ITEMS, NT>(rs, ti * TILE * 8u, dst);
+            return 0u;
+        }
+    };
+    const auto tn_of = [&](uint32_t ti, uint32_t vm) -> uint32_t {
+        if constexpr (EXT == 2) return vm;
+        return (uint32_t)min<uint64_t>(TILE, e - b - (uint64_t)ti * TILE);
+    };
+    // the two-tiles-in-flight pipeline of scatter_segment
+    uint64_t va[ITEMS], vb[ITEMS];
+    uint32_t ma = load(0, va);
+    uint32_t mb = load(1, vb);
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) asm volatile("" ::"v"(va[k]));
+    uint32_t gt = scatter_tile_sort<BITS, ITEMS, NT, EXT>(L, pend, carried, va, out, tn_of(0, ma), shift, 0, &ps);
+    for (uint32_t ti = 0;; ti += 2) {
+        ma = load(ti + 2, va);
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) asm volatile("" ::"v"(vb[k]));
+        scatter_tile_write<BITS, ITEMS, NT, SIDE, EXT>(L, out, gt, side, shift2, mask2);
+        if (ti + 1 >= ntiles) break;
+        gt = scatter_tile_sort<BITS, ITEMS, NT, EXT>(L, pend, carried, vb, out, tn_of(ti + 1, mb), shift, 0, &ps);
+        mb = load(ti + 3, vb);
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) asm volatile("" ::"v"(va[k]));
+        scatter_tile_write<BITS, ITEMS, NT, SIDE, EXT>(L, out, gt, side, shift2, mask2);
+        if (ti + 2 >= ntiles) break;
+        gt = scatter_tile_sort<BITS, ITEMS, NT, EXT>(L, pend, carried, va, out, tn_of(ti + 2, ma), shift, 0, &ps);
+    }
+    // flush the carried (partial) granules; pooled: close every chain
+    __syncthreads();
+    if (tid < F) {
+        if constexpr (EXT == 1) {
+            uint32_t gran = 0;
+            if (carried) {
+                const uint32_t off = (uint32_t)(pend / kGran) & (kGPB - 1);
+                if (off == 0) {  // the chain is empty or its block is full
+                    ps.cur = ps.pool0 + atomicAdd(&L.pool_next, 1u);
+                    ++ps.nb;
+                }
+                gran = ps.cur * kGPB + off;
+            }
+            const uint64_t T = pend + carried;  // tuples of digit tid in this segment
+            if (ps.nb) po.binfo[ps.cur] = tid | ((uint32_t)(T - (uint64_t)(ps.nb - 1) * kBlk) << 16);
+            po.cnt[(uint64_t)tid * po.nseg + g] = ((uint64_t)ps.nb << 40) | T;
+            L.pend[tid] = (uint64_t)gran * kGran;
+        } else {
+            L.pend[tid] = pend;
+        }
+        L.cnt[tid] = carried;
+    }
+    __syncthreads();
+    if (EXT == 1 && tid == 0) po.used[g] = L.pool_next;
+    const uint32_t lane = tid & (kGran - 1);
+    for (uint32_t d = tid / kGran; d < F; d += NG) {
+        if (lane < L.cnt[d]) {
+            const uint64_t x = L.carry[d * CS + lane];
+            out[L.pend[d] + lane] = x;
+            if (SIDE) side[L.pend[d] + lane] = (uint8_t)(((uint32_t)x >> shift2) & mask2);
+        }
+    }
+}
+
+template <int BITS, int ITEMS, int NT>
+__global__ __launch_bounds__(NT, (scatter_waves_per_simd<BITS, ITEMS, NT, 1>())) void k_scatter_pool(
+    const uint64_t *__restrict__ in, uint64_t *__restrict__ out, SegMap m, uint32_t shift, PoolOut po,
+    uint8_t *__restrict__ side, uint32_t shift2, uint32_t mask2) {
+    __shared__ ScatterLds<BITS, ITEMS, NT, 1> L;
+    scatter_segment_ext<BITS, ITEMS, NT, 1>(L, xcd_contiguous(blockIdx.x, gridDim.x), in, out, m, shift, nullptr,
+                                            nullptr, po, side, shift2, mask2);
+}
+
+template <int BITS, int ITEMS, int NT>
+__global__ __launch_bounds__(NT, (scatter_waves_per_simd<BITS, ITEMS, NT, 2>())) void k_scatter_blk(
+    const uint64_t *__restrict__ in, const uint64_t *__restrict__ list, uint64_t *__restrict__ out, SegMap m,
+    uint32_t shift, const uint64_t *__restrict__ cursors) {
+    __shared__ ScatterLds<BITS, ITEMS, NT, 2> L;
+    const PoolOut none{};
+    scatter_segment_ext<BITS, ITEMS, NT, 2>(L, blockIdx.x, in, out, m, shift, cursors, list, none, nullptr, 0, 0);
+}
+
+hipError_t launch_scatter_pool(const row_t *in, row_t *out, const SegMap &m, uint32_t grid, uint32_t shift,
+                               uint32_t bits, const PoolOut &po, const DigitSide &ds, hipStream_t s) {
+    if (grid == 0) return hipSuccess;
+    constexpr int ITEMS = kScatterItems, NT = kScatterThreads;
+    const uint64_t *i64 = reinterpret_cast<const uint64_t *>(in);
+    uint64_t *o64 = reinterpret_cast<uint64_t *>(out);
+    const uint32_t mask2 = (1u << ds.bits2) - 1u;
+#define POOL_CASE(B)                                                                                          \
+    case B:                                                                                                   \
+        if constexpr (sizeof(ScatterLds<B, ITEMS, NT, 1>) <= 160 * 1024 && (1 << B) <= NT) {                   \
+            hipLaunchKernelGGL((k_scatter_pool<B, ITEMS, NT>), dim3(grid), dim3(NT), 0, s, i64, o64, m, shift, \
+                               po, ds.side, ds.shift2, mask2);                                                \
+            break;                                                                                            \
+        } else {                                                                                              \
+            return hipErrorInvalidValue;                                                                      \
+        }
+    switch (bits) {
+        POOL_CASE(1)
+        POOL_CASE(2)
+        POOL_CASE(3)
+        POOL_CASE(4)
+        POOL_CASE(5)
+        POOL_CASE(6)
+        POOL_CASE(7)
+        POOL_CASE(8)
+        POOL_CASE(9)
+        default:
+            return hipErrorInvalidValue;
+    }
+#undef POOL_CASE
+    return hipGetLastError();
+}
+
+hipError_t launch_scatter_blk(const row_t *in, const uint64_t *list, row_t *out, const SegMap &m, uint32_t grid,
+                              uint32_t shift, uint32_t bits, const uint64_t *cursors, hipStream_t s) {
+    if (grid == 0) return hipSuccess;
+    constexpr int ITEMS = kScatterItems, NT = kScatterThreads;
+    const uint64_t *i64 = reinterpret_cast<const uint64_t *>(in);
+    uint64_t *o64 = reinterpret_cast<uint64_t *>(out);
+#define BLK_CASE(B)                                                                                             \
+    case B:                                                                                                     \
+        hipLaunchKernelGGL((k_scatter_blk<B, ITEMS, NT>), dim3(grid), dim3(NT), 0, s, i64, list, o64, m, shift, \
+                           cursors);                                                                            \
+        break;
+    switch (bits) {
+        BLK_CASE(1)
+        BLK_CASE(2)
+        BLK_CASE(3)
+        BLK_CASE(4)
+        BLK_CASE(5)
+        BLK_CASE(6)
+        BLK_CASE(7)
+        BLK_CASE(8)
+        default:
+            return hipErrorInvalidValue;
+    }
+#undef BLK_CASE
+    return hipGetLastError();
+}
+
+// One block: from the column-scanned chain records (totals[d] = blocks << 40 | tuples)
+// the pass-2 output layout of every region (tuple starts / counts), its block-list
+// base / length and the pass-2 segment table (kPass2Ents blocks per segment).
+__global__ __launch_bounds__(1024) void k_pool_layout(const uint64_t *__restrict__ totals, uint32_t F,
+                                                      uint64_t *__restrict__ start, uint64_t *__restrict__ count,
+                                                      uint64_t *__restrict__ lbase, uint64_t *__restrict__ lcount,
+                                                      uint32_t *__restrict__ seg_base) {
+    __shared__ uint64_t scratch[1024 / kWave + 1];
+    const uint32_t d = threadIdx.x;
+    const uint64_t v = d < F ? totals[d] : 0;
+    const uint64_t tup = v & ((1ull << 40) - 1), blk = v >> 40;
+    uint64_t tot;
+    const uint64_t ex_t = block_excl_scan_u64(tup, scratch, &tot);
+    const uint64_t ex_b = block_excl_scan_u64(blk, scratch, &tot);
+    const uint64_t ns = (blk + kPass2Ents - 1) / kPass2Ents;
+    const uint64_t ex_s = block_excl_scan_u64(ns, scratch, &tot);
+    if (d < F) {
+        start[d] = ex_t;
+        count[d] = tup;
+        lbase[d] = ex_b;
+        lcount[d] = blk;
+        seg_base[d] = (uint32_t)ex_s;
+    }
+    if (d == 0) seg_base[F] = (uint32_t)tot;
+}
+
+hipError_t launch_pool_layout(uint64_t *cnt, uint32_t nseg, uint32_t bits, uint64_t *totals, uint64_t *start,
+                              uint64_t *count, uint64_t *lbase, uint64_t *lcount, uint32_t *seg_base, hipStream_t s) {
+    const uint32_t F = 1u << bits;
+    hipLaunchKernelGGL(k_scan_cols, dim3(F), dim3(kBlock), 0, s, cnt, nseg, totals);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const uint32_t threads = F < 64 ? 64 : F;
+    hipLaunchKernelGGL(k_pool_layout, dim3(1), dim3(threads), 0, s, totals, F, start, count, lbase, lcount, seg_base);
+    return hipGetLastError();
+}
+
+// One workgroup per pass-1 segment: its pool's blocks into the regions' block lists
+// (position = the region's base + the segment's prefix of blocks in that region + a
+// rank taken with an LDS atomic; the order inside a region does not matter).
+__global__ __launch_bounds__(kBlock) void k_block_list(PoolOut po, const uint64_t *__restrict__ lbase,
+                                                       uint64_t *__restrict__ list) {
+    __shared__ uint32_t rank[kMaxF];
+    const uint32_t g = blockIdx.x;
+    for (uint32_t d = threadIdx.x; d < kMaxF; d += kBlock) rank[d] = 0;
+    __syncthreads();
+    const uint32_t used = po.used[g], base = g * po.pool_blocks;
+    for (uint32_t k = threadIdx.x; k < used; k += kBlock) {
+        const uint32_t info = po.binfo[base + k];
+        const uint32_t d = info & 0xFFFFu;
+        const uint32_t rk = atomicAdd(&rank[d], 1u);
+        const uint64_t pos = lbase[d] + (po.cnt[(uint64_t)d * po.nseg + g] >> 40) + rk;
+        list[pos] = (uint64_t)(base + k) | ((uint64_t)(info >> 16) << 32);
+    }
+}
+
+hipError_t launch_block_list(const PoolOut &po, const uint64_t *lbase, uint64_t *list, hipStream_t s) {
+    if (po.nseg == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_block_list, dim3(po.nseg), dim3(kBlock), 0, s, po, lbase, list);
+    return hipGetLastError();
+}
+
+// Pass-2 histogram of a block-list segment from the digit side stream: 16 lanes per
+// block (16 B each: a block's kBlk digit bytes), 16 blocks per step, 4 steps in flight.
+__global__ __launch_bounds__(kBlock) void k_hist_side_blk(const uint8_t *__restrict__ side,
+                                                          const uint64_t *__restrict__ list, SegMap m, uint32_t bits,
+                                                          uint64_t *__restrict__ hist) {
+    static_assert(kBlk == 256, "16 lanes x 16 B per block");
+    __shared__ uint32_t h[kMaxF];
+    __shared__ uint32_t sbase[kMaxF + 1];
+    const uint32_t g = blockIdx.x;
+    uint32_t r;
+    uint64_t b, e;
+    if (!seg_lookup(m, g, sbase, r, b, e)) return;
+    const uint32_t F = 1u << bits;
+    for (uint32_t d = threadIdx.x; d < F; d += kBlock) h[d] = 0;
+    __syncthreads();
+    const uint32_t grp = threadIdx.x / 16, l = threadIdx.x % 16;
+    constexpr int U = 4;
+    for (uint64_t i0 = b; i0 < e; i0 += 16 * U) {
+        uint4 q[U];
+        uint32_t nv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = i0 + grp + 16 * u;
+            nv[u] = 0;
+            q[u] = make_uint4(0, 0, 0, 0);
+            if (i < e) {
+                const uint64_t en = list[i];
+                const uint32_t fill = (uint32_t)(en >> 32), lo = l * 16;
+                nv[u] = fill > lo ? min(16u, fill - lo) : 0u;
+                if (nv[u]) q[u] = ld_nt(reinterpret_cast<const uint4 *>(side + (uint64_t)(uint32_t)en * kBlk) + l);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t w[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+                if ((uint32_t)j < nv[u]) atomicAdd(&h[__builtin_amdgcn_ubfe(w[j >> 2], (j & 3) * 8, 8)], 1u);
+        }
+    }
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < F; d += kBlock) hist[(uint64_t)g * F + d] = h[d];
+}
+
+hipError_t launch_hist_side_blk(const uint8_t *side, const uint64_t *list, const SegMap &m, uint32_t grid,
+                                uint32_t bits, uint64_t *hist, hipStream_t s) {
+    if (grid == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_hist_side_blk, dim3(grid), dim3(kBlock), 0, s, side, list, m, bits, hist);
+    return hipGetLastError();
 }
 
 // ------------------------------------------------------------ build+probe ---

@@ -96,6 +96,36 @@ def test_big_table_partitions(sgx, orc, gpu, bits, kmax):
         assert np.array_equal(sorted_triples(got), sorted_triples(orc.rho_join_triples(R, S, 4)))
 
 
+@pytest.mark.parametrize("case", ["one_region", "hot_s", "ragged", "dense_dups"])
+def test_pooled_two_pass_layouts(sgx, orc, gpu, case):
+    """Two-pass plans take the pooled pass 1 (per-workgroup block chains, no pass-1
+    histogram) and the block-list pass 2: every tuple of one pass-1 digit (one region,
+    chains of thousands of blocks), a hot S key (one region far above the rest), ragged
+    sizes (partial tiles, chains ending inside a block) and dense duplicates, over the
+    plans 10 = 5 + 5, 14 = 7 + 7 and 17 = 9 + 8 bits, counts and materialised triples."""
+    rng = np.random.default_rng(11)
+    if case == "one_region":  # low 9 bits zero: one digit in pass 1 of every plan
+        R = rel(rng.integers(0, 1 << 20, 300_000).astype(np.uint32) << 9)
+        S = rel(rng.integers(0, 1 << 20, 400_000).astype(np.uint32) << 9)
+    elif case == "hot_s":
+        R = rel(rng.permutation(np.arange(1, 200_001, dtype=np.uint32)))
+        S = rel(np.concatenate([np.full(150_000, 4242, np.uint32),
+                                rng.integers(1, 200_001, 250_000).astype(np.uint32)]))
+    elif case == "ragged":
+        R = rel(rng.integers(0, 2**32, 123_457, dtype=np.uint64).astype(np.uint32) % 1_000_003)
+        S = rel(rng.integers(0, 2**32, 98_765, dtype=np.uint64).astype(np.uint32) % 1_000_003)
+    else:
+        R = rel(rng.integers(0, 5000, 70_001).astype(np.uint32))
+        S = rel(rng.integers(0, 5000, 65_537).astype(np.uint32))
+    exp = orc.count_join_sort(R, S)
+    for bits in (10, 14, 17):
+        res = gpu_join(sgx, R, S, radix_bits=bits, passes=2)
+        assert res.matches == exp, (case, bits, res.matches, exp)
+    if case != "dense_dups":
+        got = gpu_triples(sgx, R, S, radix_bits=14, passes=2)
+        assert np.array_equal(sorted_triples(got), sorted_triples(orc.rho_join_triples(R, S, 4)))
+
+
 def test_extreme_keys(sgx, orc, gpu):
     # 0 and 0xFFFFFFFF (the LDS empty marker) must join like any other key
     keys = np.array([0, 0xFFFFFFFF, 0xFFFFFFFF, 1, 0x80000000, 0xFFFFFFFE] * 50, dtype=np.uint32)
