@@ -130,6 +130,18 @@ inline bool pool_enabled() {
     }();
     return on;
 }
+// Counting RHO joins (no materialisation, bucket chaining) move keys only after the
+// input read: the build/probe of a count reads nothing else (radix_join.cpp:429-436
+// compares keys; the payloads are never read), so the pooled pass 1 writes the key
+// word of every tuple and pass 2 and the build/probe run on 4-byte keys.
+// SGXAMD_KEYS=0 keeps whole tuples (development A/B switch; results are identical).
+inline bool keys_enabled() {
+    static const bool on = [] {
+        const char *e = std::getenv("SGXAMD_KEYS");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return on;
+}
 constexpr uint32_t kPoolSegs = 512;  // two 512-thread workgroups per CU: one wave of workgroups
 inline uint32_t pool_segs() {
     static const uint32_t v = [] {
@@ -154,6 +166,7 @@ struct RelPlan {
     uint64_t seg2;
     uint32_t grid2;
     bool pooled;           // pooled pass 1 + block-list pass 2
+    bool keys;             // pooled, and the partitions hold 4-byte keys (counting joins)
     uint32_t pool_blocks;  // blocks per pass-1 segment pool
     uint64_t t1_tuples;    // capacity of the pass-1 output (and side stream) in tuples
     // scratch offsets (pooled: hist1 holds the chain records, tot1 their column totals)
@@ -188,7 +201,8 @@ int partition_relation_pooled(Context *ctx, hipStream_t s, Timer &tm, const std:
                          rp.nseg1};
         const DigitSide ds{side, key_shift + pol.b1, pol.b2};
         tm.mark((t + "pass1_scatter").c_str());
-        RHO_HIP(launch_scatter_pool(in, t1, m1, rp.nseg1, key_shift, pol.b1, po, ds, s));
+        RHO_HIP(launch_scatter_pool(in, sizeof(row_t), t1, rp.keys ? 4u : 8u, m1, rp.nseg1, key_shift, pol.b1, po, ds,
+                                    s));
         tm.mark((t + "pass1_scan").c_str());
         RHO_HIP(launch_pool_layout(po.cnt, rp.nseg1, pol.b1, A.at<uint64_t>(rp.tot1), start1, cnt1, lbase, lcount,
                                    segbase2, s));
@@ -207,7 +221,7 @@ int partition_relation_pooled(Context *ctx, hipStream_t s, Timer &tm, const std:
     tm.mark((t + "pass2_scan").c_str());
     RHO_HIP(launch_scan_regions(hist2, segbase2, start1, F1, pol.b2, ps, pc, s));
     tm.mark((t + "pass2_scatter").c_str());
-    RHO_HIP(launch_scatter_blk(t1, list, t2, m2, rp.grid2, key_shift + pol.b1, pol.b2, hist2, s));
+    RHO_HIP(launch_scatter_blk(t1, list, t2, rp.keys ? 4u : 8u, m2, rp.grid2, key_shift + pol.b1, pol.b2, hist2, s));
     *final_rel = t2;
     *pstart = ps;
     *pcnt = pc;
@@ -268,7 +282,22 @@ int partition_relation(Context *ctx, hipStream_t s, Timer &tm, const char *tag, 
     return MI355_OK;
 }
 
-void plan_relation(Arena &A, RelPlan &rp, uint64_t n, const Policy &pol) {
+// Pass-1 segment size of a pooled plan: whole tiles, about pool_segs() segments.
+inline uint64_t pool_seg_size(uint64_t n) {
+    const uint64_t seg = (n + pool_segs() - 1) / pool_segs();
+    return std::max<uint64_t>((seg + kTile - 1) / kTile * kTile, kTile);
+}
+// Whether a relation of n tuples can take the pooled plan: a two-pass plan with the
+// digit side stream, and block counts that fit the 24-bit chain records.
+inline bool pool_fits(uint64_t n, const Policy &pol) {
+    if (!(pol.passes == 2 && uses_digit_side(pol) && pool_enabled())) return false;
+    const uint64_t seg = pool_seg_size(n), nseg = (n + seg - 1) / seg;
+    const uint64_t pb = (seg + kBlk - 1) / kBlk + (1u << pol.b1);
+    return n / kBlk + nseg * (1u << pol.b1) < (1ull << 24) && nseg * pb < (1ull << 27);
+}
+enum PoolMode : int { kNoPool = 0, kPoolTuples = 1, kPoolKeys = 2 };
+
+void plan_relation(Arena &A, RelPlan &rp, uint64_t n, const Policy &pol, int pool = kNoPool) {
     rp.n = n;
     rp.seg1 = seg_size_for(n);
     rp.nseg1 = (uint32_t)((n + rp.seg1 - 1) / rp.seg1);
@@ -277,23 +306,22 @@ void plan_relation(Arena &A, RelPlan &rp, uint64_t n, const Policy &pol) {
     rp.grid2 = (uint32_t)((n + rp.seg2 - 1) / rp.seg2) + F1;
     rp.t1_tuples = n;
     rp.pooled = false;
-    if (pol.passes == 2 && uses_digit_side(pol) && pool_enabled() && n > 0) {
+    rp.keys = false;
+    if (pool != kNoPool) {
         // pass-1 segments of whole tiles, about pool_segs() of them; every digit of a
-        // segment fills ceil(tuples / kBlk) blocks, so a pool of ceil(seg1 / kBlk) + F1
-        // blocks always suffices.  Chain records pack blocks << 40 | tuples.
-        uint64_t seg = (n + pool_segs() - 1) / pool_segs();
-        seg = std::max<uint64_t>((seg + kTile - 1) / kTile * kTile, kTile);
+        // segment fills ceil(elements / kBlk) blocks, so a pool of ceil(seg1 / kBlk) + F1
+        // blocks always suffices.  Chain records pack blocks << 40 | elements.
+        const uint64_t seg = pool_seg_size(n);
         const uint32_t nseg = (uint32_t)((n + seg - 1) / seg);
         const uint64_t pb = (seg + kBlk - 1) / kBlk + F1;
         const uint64_t max_blocks = n / kBlk + (uint64_t)nseg * F1;
-        if (max_blocks < (1ull << 24) && (uint64_t)nseg * pb < (1ull << 27)) {
-            rp.pooled = true;
-            rp.seg1 = seg;
-            rp.nseg1 = nseg;
-            rp.pool_blocks = (uint32_t)pb;
-            rp.t1_tuples = (uint64_t)nseg * pb * kBlk;
-            rp.grid2 = (uint32_t)(max_blocks / kPass2Ents) + F1 + 1;
-        }
+        rp.pooled = true;
+        rp.keys = pool == kPoolKeys;
+        rp.seg1 = seg;
+        rp.nseg1 = nseg;
+        rp.pool_blocks = (uint32_t)pb;
+        rp.t1_tuples = (uint64_t)nseg * pb * kBlk;
+        rp.grid2 = (uint32_t)(max_blocks / kPass2Ents) + F1 + 1;
     }
     rp.hist1 = A.reserve(sizeof(uint64_t) * (size_t)F1 * std::max<uint32_t>(rp.nseg1, 1));
     rp.tot1 = A.reserve(sizeof(uint64_t) * F1);
@@ -366,8 +394,13 @@ int plan_join(Context *ctx, hipStream_t s, uint64_t nR, uint64_t nS, const mi355
     }
     Arena &A = ctx->scratch;
     A.reset();
-    plan_relation(A, pj.pr, nR, pol);
-    plan_relation(A, pj.ps, nS, pol);
+    // both relations take the same layout (the build/probe reads both alike)
+    const bool counting_rho = !pj.materialize && pj.algo == kAlgoChaining;
+    const int pool = !(pool_fits(nR, pol) && pool_fits(nS, pol)) ? kNoPool
+                     : (counting_rho && keys_enabled())          ? kPoolKeys
+                                                                  : kPoolTuples;
+    plan_relation(A, pj.pr, nR, pol, pool);
+    plan_relation(A, pj.ps, nS, pol, pool);
     const uint64_t c1R = pj.pr.t1_tuples, c1S = pj.ps.t1_tuples;  // pooled pass 1 needs room for its pools
     RHO_HIP(ctx->t1R.ensure(std::max<uint64_t>(c1R, 1) * sizeof(row_t)));
     RHO_HIP(ctx->t1S.ensure(std::max<uint64_t>(c1S, 1) * sizeof(row_t)));
@@ -531,7 +564,8 @@ int join_finish(Context *ctx, PendingJoin &pj, const row_t *dS, uint64_t nS, mi3
     if (!pj.materialize) {
         tm.mark("join_build_probe");
         RHO_HIP(launch_join(fR, fS, psR, pcR, psS, pcS, P, over, n_over, hash_shift, pol.rcap, pj.s_chunk, join_grid,
-                            kJoinCount, algo, counts, nullptr, nullptr, cyc, s));
+                            kJoinCount, algo, counts, nullptr, nullptr, cyc, s, nullptr,
+                            pj.pr.keys ? 1 : 2));
         tm.mark("join_reduce");
         RHO_HIP(launch_reduce(counts, join_grid, result, cyc, join_grid, s));
     } else {

@@ -89,7 +89,7 @@ hipError_t launch_hist_side(const uint8_t *side, const SegMap &m, uint32_t grid,
 // blocks, so the pass-1 scatter needs no cursors and the relation is read once in pass 1
 // instead of twice (histogram + scatter).
 constexpr uint32_t kBlkShift = 8;
-constexpr uint32_t kBlk = 1u << kBlkShift;          // tuples per block (2 KiB)
+constexpr uint32_t kBlk = 1u << kBlkShift;          // elements per block (2 KiB of tuples, 1 KiB of keys)
 constexpr uint32_t kPass2Ents = 512;                // blocks per pass-2 segment (LDS list copy)
 struct PoolOut {
     uint32_t *binfo;       // per pool block: digit | fill << 16
@@ -99,9 +99,12 @@ struct PoolOut {
     uint32_t nseg;
 };
 // Pass 1 of a pooled plan: contiguous input segments (m), pooled output in out, digit
-// side stream ds (required) beside every stored tuple.
-hipError_t launch_scatter_pool(const row_t *in, row_t *out, const SegMap &m, uint32_t grid, uint32_t shift,
-                               uint32_t bits, const PoolOut &po, const DigitSide &ds, hipStream_t s);
+// side stream ds (required) beside every stored element.  Elements: in_size-byte input
+// (8: row_t, 4: keys), out_size-byte output (8: row_t; 4: the key words only — counting
+// joins, whose build/probe reads nothing but keys).
+hipError_t launch_scatter_pool(const void *in, uint32_t in_size, void *out, uint32_t out_size, const SegMap &m,
+                               uint32_t grid, uint32_t shift, uint32_t bits, const PoolOut &po, const DigitSide &ds,
+                               hipStream_t s);
 // After launch_scan_single-style column scans of po.cnt (k_scan_cols, in place): region
 // tuple starts / counts (the pass-2 output layout), region block-list bases / lengths
 // and the pass-2 segment table (kPass2Ents blocks per segment).
@@ -114,8 +117,8 @@ hipError_t launch_block_list(const PoolOut &po, const uint64_t *lbase, uint64_t 
 // reg_count = lcount, seg_size = kPass2Ents).
 hipError_t launch_hist_side_blk(const uint8_t *side, const uint64_t *list, const SegMap &m, uint32_t grid,
                                 uint32_t bits, uint64_t *hist, hipStream_t s);
-hipError_t launch_scatter_blk(const row_t *in, const uint64_t *list, row_t *out, const SegMap &m, uint32_t grid,
-                              uint32_t shift, uint32_t bits, const uint64_t *cursors, hipStream_t s);
+hipError_t launch_scatter_blk(const void *in, const uint64_t *list, void *out, uint32_t elem_size, const SegMap &m,
+                              uint32_t grid, uint32_t shift, uint32_t bits, const uint64_t *cursors, hipStream_t s);
 
 // Stable scatter of every segment into `out` at the cursors of the scan.
 // digit_base (nullable) is added to the cursors: base[r * F + d].
@@ -159,7 +162,9 @@ hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, 
                        const uint64_t *s_start, const uint64_t *s_count, uint64_t P, const uint64_t *over,
                        const uint32_t *n_over, uint32_t hash_shift, uint32_t rcap, uint64_t s_chunk, uint32_t grid,
                        int mode, int algo, uint64_t *counts, const uint64_t *task_off, output_triple_t *out,
-                       uint64_t *cyc, hipStream_t s, const JoinReduce *reduce = nullptr);
+                       uint64_t *cyc, hipStream_t s, const JoinReduce *reduce = nullptr, int key_stride = 2);
+// key_stride 2: R / S are row_t partitions; 1: packed u32 keys (counting RHO only —
+// the partitions of a counting join carry keys only after the input read).
 // One-block exclusive scan of n_base + *n_extra values; *total = their sum.
 hipError_t launch_excl_scan(const uint64_t *in, const uint32_t *n_extra, uint64_t n_base, uint64_t *out,
                             uint64_t *total, hipStream_t s);

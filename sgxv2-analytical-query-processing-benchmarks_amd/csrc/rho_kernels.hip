@@ -414,17 +414,20 @@ constexpr uint32_t kGran = 16;  // tuples per output granule = one 128-B line
 
 // EXT: 0 = cursor output, contiguous input; 1 = pooled output (PoolOut); 2 = block-list
 // input (the segment's list entries staged in ents).
-template <int BITS, int ITEMS, int NT, int EXT = 0>
+// T: the element moved (uint64_t tuple, or uint32_t key of a count-only join).
+template <int BITS, int ITEMS, int NT, int EXT = 0, typename T = uint64_t>
 struct ScatterLds {
     static constexpr uint32_t F = 1u << BITS;
     static constexpr uint32_t TILE = NT * ITEMS;
     static constexpr uint32_t NW = NT / kWave;
-    static constexpr uint32_t MAXDESC = (TILE + (kGran - 1) * F) / kGran + F;
+    static constexpr uint32_t G = 128 / sizeof(T);  // elements per 128-B granule
+    static constexpr uint32_t GPB = kBlk / G;       // granules per pool block
+    static constexpr uint32_t MAXDESC = (TILE + (G - 1) * F) / G + F;
     union {
         uint32_t sbase[kMaxF + 1];  // segment table (only before the first tile)
-        uint64_t tile[TILE];        // this tile's tuples, digit-sorted
+        T tile[TILE];               // this tile's elements, digit-sorted
     };
-    uint64_t carry[F * (kGran - 1)];  // digit d: slots [d*(kGran-1), (d+1)*(kGran-1))
+    T carry[F * (G - 1)];             // digit d: slots [d*(G-1), (d+1)*(G-1))
     uint64_t pend[F];                 // global position of d's first pending (carried) tuple
     uint2 meta[F];                    // {tbase, c | r << 8 | w << 16} of the current tile
     uint32_t cnt[F];                  // tile histogram (phase A), zero between tiles
@@ -445,14 +448,13 @@ struct PoolState {
     uint32_t pool0;  // first block of the segment's pool
     uint32_t *binfo;
 };
-constexpr uint32_t kGPB = kBlk / kGran;  // granules per pool block
 
 // Waves per SIMD that the LDS footprint allows (__launch_bounds__ second argument:
 // k workgroups per CU of NT threads <=> k * NT / 256 waves per SIMD), so the
 // register allocation never becomes the tighter occupancy limit.
-template <int BITS, int ITEMS, int NT, int EXT = 0>
+template <int BITS, int ITEMS, int NT, int EXT = 0, typename T = uint64_t>
 constexpr int scatter_waves_per_simd() {
-    constexpr int k = (160 * 1024) / (int)sizeof(ScatterLds<BITS, ITEMS, NT, EXT>);
+    constexpr int k = (160 * 1024) / (int)sizeof(ScatterLds<BITS, ITEMS, NT, EXT, T>);
     constexpr int w = (k < 1 ? 1 : k) * NT / 256;
     // at most 4 waves/SIMD (128 VGPRs): fewer registers spill, and a scratch reload is
     // a vector-memory op whose wait would also wait for every store in flight
@@ -465,6 +467,25 @@ template <int ITEMS, int NT>
 __device__ __forceinline__ void load_tile(__amdgpu_buffer_rsrc_t rs, uint32_t soff, uint64_t (&dst)[ITEMS]) {
 #pragma unroll
     for (int k = 0; k < ITEMS; ++k) dst[k] = buf_ld_nt_u64(rs, threadIdx.x * 8u, soff + (uint32_t)(k * NT * 8));
+}
+
+// Element loads of T from an input of IS-byte elements (IS = 8 and T = uint32_t: the
+// key word of each tuple; the cache lines fetched are the same).
+template <typename T>
+__device__ __forceinline__ T buf_ld_nt_t(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff);
+template <>
+__device__ __forceinline__ uint64_t buf_ld_nt_t<uint64_t>(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    return buf_ld_nt_u64(r, voff, soff);
+}
+template <>
+__device__ __forceinline__ uint32_t buf_ld_nt_t<uint32_t>(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 2);
+}
+template <typename T, int IS, int ITEMS, int NT>
+__device__ __forceinline__ void load_tile_t(__amdgpu_buffer_rsrc_t rs, uint32_t soff, T (&dst)[ITEMS]) {
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k)
+        dst[k] = buf_ld_nt_t<T>(rs, threadIdx.x * (uint32_t)IS, soff + (uint32_t)(k * NT * IS));
 }
 
 // Block-wide exclusive scan of two u32 counters at once (one __syncthreads).
@@ -498,12 +519,13 @@ __device__ __forceinline__ void block_scan2(uint32_t a, uint32_t b, uint32_t (&w
 // Phases A-C of one tile: the tile ends up digit-sorted in L.tile (v is dead after).
 // tn: valid tuples of the tile (items tid + k * NT < tn); with block-list input (EXT 2)
 // a bit mask instead, bit k = item k valid.  ps: the owner thread's chain (EXT 1).
-template <int BITS, int ITEMS, int NT, int EXT = 0>
-__device__ __forceinline__ uint32_t scatter_tile_sort(ScatterLds<BITS, ITEMS, NT, EXT> &L, uint64_t &pend,
-                                                      uint32_t &carried, const uint64_t (&v)[ITEMS],
-                                                      uint64_t *__restrict__ out, uint32_t tn, uint32_t shift,
+template <int BITS, int ITEMS, int NT, int EXT = 0, typename T = uint64_t>
+__device__ __forceinline__ uint32_t scatter_tile_sort(ScatterLds<BITS, ITEMS, NT, EXT, T> &L, uint64_t &pend,
+                                                      uint32_t &carried, const T (&v)[ITEMS],
+                                                      T *__restrict__ out, uint32_t tn, uint32_t shift,
                                                       uint64_t tbase_global, PoolState *ps = nullptr) {
     constexpr uint32_t F = 1u << BITS, mask = F - 1, NW = NT / kWave;
+    constexpr uint32_t G = ScatterLds<BITS, ITEMS, NT, EXT, T>::G, GPB = ScatterLds<BITS, ITEMS, NT, EXT, T>::GPB;
     const uint32_t tid = threadIdx.x;
     const auto valid = [&](int k) { return EXT == 2 ? ((tn >> k) & 1u) != 0 : tid + k * NT < tn; };
 #ifdef SGXAMD_ABLATE_NOSORT  // development ablation (tools/part_bench): the memory pipeline alone
@@ -528,10 +550,10 @@ __device__ __forceinline__ uint32_t scatter_tile_sort(ScatterLds<BITS, ITEMS, NT
         L.cnt[tid] = 0;
         c = carried;
         p0 = pend;
-        const uint64_t aligned = (p0 + c + t) & ~uint64_t(kGran - 1);
+        const uint64_t aligned = (p0 + c + t) & ~uint64_t(G - 1);
         if (aligned > p0) {
             w = (uint32_t)(aligned - p0);
-            g = (uint32_t)(aligned / kGran - p0 / kGran);
+            g = (uint32_t)(aligned / G - p0 / G);
         }
         r = c + t - w;
     }
@@ -544,15 +566,15 @@ __device__ __forceinline__ uint32_t scatter_tile_sort(ScatterLds<BITS, ITEMS, NT
             // pooled: pend is granule-aligned (only whole granules are written before the
             // segment's end).  g0 granules fill the current block, the rest go to nnew
             // fresh blocks of the pool, taken together (consecutive, so contiguous).
-            const uint32_t off = (uint32_t)(p0 / kGran) & (kGPB - 1);
-            const uint32_t g0 = off ? min(g, kGPB - off) : 0u;
-            const uint32_t nnew = (g - g0 + kGPB - 1) / kGPB;
+            const uint32_t off = (uint32_t)(p0 / G) & (GPB - 1);
+            const uint32_t g0 = off ? min(g, GPB - off) : 0u;
+            const uint32_t nnew = (g - g0 + GPB - 1) / GPB;
             uint32_t nb0 = 0;
             if (nnew) {
                 nb0 = ps->pool0 + atomicAdd(&L.pool_next, nnew);
                 for (uint32_t j = 0; j < nnew; ++j) ps->binfo[nb0 + j] = tid | (kBlk << 16);
             }
-            L.gaddr[tid] = make_uint2(ps->cur * kGPB + off, nb0 * kGPB);
+            L.gaddr[tid] = make_uint2(ps->cur * GPB + off, nb0 * GPB);
             mx |= g0 << 16;
             if (nnew) {
                 ps->cur = nb0 + nnew - 1;
@@ -583,20 +605,61 @@ __device__ __forceinline__ uint32_t scatter_tile_sort(ScatterLds<BITS, ITEMS, NT
 // Phases D-E of the tile sorted by scatter_tile_sort (gtot = its granule count).
 // SIDE: every stored tuple's next-pass digit also goes to side[a] (a 16-lane group
 // writes 16 consecutive bytes next to its 128-B granule).
-template <int BITS, int ITEMS, int NT, bool SIDE, int EXT = 0>
-__device__ __forceinline__ void scatter_tile_write(ScatterLds<BITS, ITEMS, NT, EXT> &L, uint64_t *__restrict__ out,
+template <int BITS, int ITEMS, int NT, bool SIDE, int EXT = 0, typename T = uint64_t>
+__device__ __forceinline__ void scatter_tile_write(ScatterLds<BITS, ITEMS, NT, EXT, T> &L, T *__restrict__ out,
                                                    uint32_t gtot, uint8_t *__restrict__ side, uint32_t shift2,
                                                    uint32_t mask2) {
-    constexpr uint32_t F = 1u << BITS, NG = NT / kGran;
-    constexpr uint32_t CS = kGran - 1;
+    constexpr uint32_t G = ScatterLds<BITS, ITEMS, NT, EXT, T>::G;
+    constexpr uint32_t F = 1u << BITS, NG = NT / G;
+    constexpr uint32_t CS = G - 1;
     constexpr uint32_t TB = EXT == 1 ? 0xFFFFu : ~0u;  // tile offset bits of meta.x
 #ifdef SGXAMD_ABLATE_NOSORT
     return;
 #endif
     const uint32_t tid = threadIdx.x;
-    // D. whole granules, 16 lanes (one 128-B line) per granule
-    const uint32_t lane = tid & (kGran - 1), grp = tid / kGran;
-    if constexpr (EXT == 1) {
+    // D. whole granules, G lanes (one 128-B line) per granule
+    const uint32_t lane = tid & (G - 1), grp = tid / G;
+    if constexpr (sizeof(T) == 4) {
+        // keys: 16 lanes per granule, two consecutive keys per lane (one 8-byte store and
+        // one 2-byte side store), half the rounds and metadata reads of one key per lane
+        constexpr uint32_t NG2 = NT / 16;
+        const uint32_t l2 = 2 * (tid & 15), grp2 = tid / 16;
+        const auto elem = [&](uint32_t d, uint32_t q, uint32_t cd, uint32_t tbx) -> uint32_t {
+            return q < cd ? (uint32_t)L.carry[d * CS + q] : (uint32_t)L.tile[tbx + q - cd];
+        };
+        for (uint32_t j = grp2; j < gtot; j += NG2) {
+            const uint32_t d = L.desc[j];
+            const uint2 m = L.meta[d];
+            const uint32_t jj = j - L.gbase[d], cd = m.y & 0xFFu, tbx = m.x & TB;
+            uint64_t a;
+            uint32_t q, wd = ~0u;
+            if constexpr (EXT == 1) {
+                const uint2 ga = L.gaddr[d];
+                const uint32_t g0 = m.x >> 16;
+                a = (uint64_t)(jj < g0 ? ga.x + jj : ga.y + (jj - g0)) * G + l2;
+                q = jj * G + l2;
+            } else {
+                const uint64_t pd = L.pend[d];
+                wd = m.y >> 16;
+                a = (pd / G + jj) * G + l2;
+                q = (uint32_t)(a - pd);  // wraps when a < pd
+            }
+            const bool v0 = (EXT == 1) || (a >= L.pend[d] && q < wd);
+            const bool v1 = (EXT == 1) || (a + 1 >= L.pend[d] && q + 1 < wd);
+            if (v0 && v1) {
+                const uint32_t x0 = elem(d, q, cd, tbx), x1 = elem(d, q + 1, cd, tbx);
+                st_nt(reinterpret_cast<uint64_t *>(out + a), (uint64_t)x0 | ((uint64_t)x1 << 32));
+                if (SIDE)
+                    *reinterpret_cast<uint16_t *>(side + a) =
+                        (uint16_t)(((x0 >> shift2) & mask2) | (((x1 >> shift2) & mask2) << 8));
+            } else if (v0 || v1) {
+                const uint32_t o = v0 ? 0u : 1u;
+                const uint32_t x = elem(d, q + o, cd, tbx);
+                st_nt(reinterpret_cast<uint32_t *>(out + a + o), x);
+                if (SIDE) side[a + o] = (uint8_t)((x >> shift2) & mask2);
+            }
+        }
+    } else if constexpr (EXT == 1) {
         // pooled: every granule is whole (the digit's writes start granule-aligned); the
         // first g0 of d go to its current block, the rest to its fresh blocks
         for (uint32_t j = grp; j < gtot; j += NG) {
@@ -605,9 +668,9 @@ __device__ __forceinline__ void scatter_tile_write(ScatterLds<BITS, ITEMS, NT, E
             const uint2 ga = L.gaddr[d];
             const uint32_t jj = j - L.gbase[d], g0 = m.x >> 16, cd = m.y & 0xFFu;
             const uint32_t gran = jj < g0 ? ga.x + jj : ga.y + (jj - g0);
-            const uint64_t a = (uint64_t)gran * kGran + lane;
-            const uint32_t q = jj * kGran + lane;
-            const uint64_t x = q < cd ? L.carry[d * CS + q] : L.tile[(m.x & TB) + q - cd];
+            const uint64_t a = (uint64_t)gran * G + lane;
+            const uint32_t q = jj * G + lane;
+            const T x = q < cd ? L.carry[d * CS + q] : L.tile[(m.x & TB) + q - cd];
             st_nt(out + a, x);
             if (SIDE) side[a] = (uint8_t)(((uint32_t)x >> shift2) & mask2);
         }
@@ -617,14 +680,14 @@ __device__ __forceinline__ void scatter_tile_write(ScatterLds<BITS, ITEMS, NT, E
         const uint2 m = L.meta[d];
         const uint64_t pd = L.pend[d];
         const uint32_t cd = m.y & 0xFFu, wd = m.y >> 16;
-        const uint64_t a = (pd / kGran + (j - L.gbase[d])) * kGran + lane;
+        const uint64_t a = (pd / G + (j - L.gbase[d])) * G + lane;
         const uint64_t q = a - pd;  // sequence position inside d (wraps when a < pd)
         const bool valid = a >= pd && q < wd;
-        uint64_t x = 0;
+        T x = 0;
         if (valid) {
             x = q < cd ? L.carry[d * CS + q] : L.tile[m.x + q - cd];
 #ifdef SGXAMD_ABLATE_NOSTORE  // development ablation: everything but the global stores
-            if (x == ~0ull) out[0] = x;
+            if (x == (T)~0ull) out[0] = x;
 #elif defined(SGXAMD_PLAIN_STORE)
             out[a] = x;
 #else
@@ -853,10 +916,11 @@ hipError_t launch_scatter(const row_t *in, row_t *out, const SegMap &m, uint32_t
 // resource over its block (lanes past the block's fill read 0 and are masked out).
 
 // Tile loads of a block-list segment (entries staged in LDS); returns the valid mask.
-template <int ITEMS, int NT, int BITS>
-__device__ __forceinline__ uint32_t load_tile_blk(const uint64_t *__restrict__ in,
-                                                  const ScatterLds<BITS, ITEMS, NT, 2> &L, uint32_t nent, uint32_t e0,
-                                                  uint64_t (&dst)[ITEMS]) {
+// in: the pass-1 output, IS-byte elements.
+template <typename T, int IS, int ITEMS, int NT, int BITS>
+__device__ __forceinline__ uint32_t load_tile_blk(const char *__restrict__ in,
+                                                  const ScatterLds<BITS, ITEMS, NT, 2, T> &L, uint32_t nent,
+                                                  uint32_t e0, T (&dst)[ITEMS]) {
     static_assert(NT % kBlk == 0, "a wave reads inside one block");
     const uint32_t o = threadIdx.x & (kBlk - 1);
     const uint32_t h = __builtin_amdgcn_readfirstlane(threadIdx.x >> kBlkShift);
@@ -867,8 +931,8 @@ __device__ __forceinline__ uint32_t load_tile_blk(const uint64_t *__restrict__ i
         const uint64_t en = j < nent ? L.ents[j] : 0ull;
         const uint32_t phys = __builtin_amdgcn_readfirstlane((uint32_t)en);
         const uint32_t fill = __builtin_amdgcn_readfirstlane((uint32_t)(en >> 32));
-        const __amdgpu_buffer_rsrc_t rs = make_rsrc(in + (uint64_t)phys * kBlk, fill * 8u);
-        dst[k] = buf_ld_nt_u64(rs, o * 8u, 0u);
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(in + (uint64_t)phys * (kBlk * IS), fill * (uint32_t)IS);
+        dst[k] = buf_ld_nt_t<T>(rs, o * (uint32_t)IS, 0u);
         vm |= (o < fill ? 1u : 0u) << k;
     }
     return vm;
@@ -876,17 +940,20 @@ __device__ __forceinline__ uint32_t load_tile_blk(const uint64_t *__restrict__ i
 
 // EXT 1: contiguous segment g of `in` -> pooled output (po), digit side stream.
 // EXT 2: block-list segment g (list) -> `out` at the segment-major cursors cur_init.
-template <int BITS, int ITEMS, int NT, int EXT>
-__device__ __forceinline__ void scatter_segment_ext(ScatterLds<BITS, ITEMS, NT, EXT> &L, uint32_t g,
-                                                    const uint64_t *__restrict__ in, uint64_t *__restrict__ out,
+// T: the element written (tuple or key); IS: the input element size in bytes.
+template <int BITS, int ITEMS, int NT, int EXT, typename T, int IS>
+__device__ __forceinline__ void scatter_segment_ext(ScatterLds<BITS, ITEMS, NT, EXT, T> &L, uint32_t g,
+                                                    const char *__restrict__ in, T *__restrict__ out,
                                                     const SegMap &m, uint32_t shift,
                                                     const uint64_t *__restrict__ cur_init,
                                                     const uint64_t *__restrict__ list, const PoolOut &po,
                                                     uint8_t *__restrict__ side, uint32_t shift2, uint32_t mask2) {
+    using LdsT = ScatterLds<BITS, ITEMS, NT, EXT, T>;
     constexpr uint32_t TILE = NT * ITEMS, BPT = TILE / kBlk;
-    constexpr uint32_t F = 1u << BITS, NG = NT / kGran, CS = kGran - 1;
+    constexpr uint32_t F = 1u << BITS, G = LdsT::G, GPB = LdsT::GPB, NG = NT / G, CS = G - 1;
     constexpr bool SIDE = EXT == 1;
     static_assert(F <= NT, "one owner thread per digit");
+    static_assert(sizeof(T) <= IS, "elements are the input elements or their key words");
     uint32_t r;
     uint64_t b, e;
     if (!seg_lookup(m, g, L.sbase, r, b, e)) return;
@@ -906,12 +973,13 @@ __device__ __forceinline__ void scatter_segment_ext(ScatterLds<BITS, ITEMS, NT, 
     }
     __syncthreads();  // sbase (aliased with tile) is dead from here on
     const uint32_t ntiles = EXT == 2 ? (nent + BPT - 1) / BPT : (uint32_t)((e - b + TILE - 1) / TILE);
-    const __amdgpu_buffer_rsrc_t rs = make_rsrc(in + b, EXT == 2 ? 0u : (uint32_t)((e - b) * sizeof(uint64_t)));
-    const auto load = [&](uint32_t ti, uint64_t(&dst)[ITEMS]) -> uint32_t {
+    // (EXT 1) segments hold far fewer than 2^29 elements, so byte offsets fit 32 bits
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(in + b * IS, EXT == 2 ? 0u : (uint32_t)((e - b) * IS));
+    const auto load = [&](uint32_t ti, T(&dst)[ITEMS]) -> uint32_t {
         if constexpr (EXT == 2) {
-            return load_tile_blk<ITEMS, NT, BITS>(in, L, nent, ti * BPT, dst);
+            return load_tile_blk<T, IS, ITEMS, NT, BITS>(in, L, nent, ti * BPT, dst);
         } else {
-            load_tile<ITEMS, NT>(rs, ti * TILE * 8u, dst);
+            load_tile_t<T, IS, ITEMS, NT>(rs, ti * TILE * (uint32_t)IS, dst);
             return 0u;
         }
     };
@@ -920,25 +988,25 @@ __device__ __forceinline__ void scatter_segment_ext(ScatterLds<BITS, ITEMS, NT, 
         return (uint32_t)min<uint64_t>(TILE, e - b - (uint64_t)ti * TILE);
     };
     // the two-tiles-in-flight pipeline of scatter_segment
-    uint64_t va[ITEMS], vb[ITEMS];
+    T va[ITEMS], vb[ITEMS];
     uint32_t ma = load(0, va);
     uint32_t mb = load(1, vb);
 #pragma unroll
     for (int k = 0; k < ITEMS; ++k) asm volatile("" ::"v"(va[k]));
-    uint32_t gt = scatter_tile_sort<BITS, ITEMS, NT, EXT>(L, pend, carried, va, out, tn_of(0, ma), shift, 0, &ps);
+    uint32_t gt = scatter_tile_sort<BITS, ITEMS, NT, EXT, T>(L, pend, carried, va, out, tn_of(0, ma), shift, 0, &ps);
     for (uint32_t ti = 0;; ti += 2) {
         ma = load(ti + 2, va);
 #pragma unroll
         for (int k = 0; k < ITEMS; ++k) asm volatile("" ::"v"(vb[k]));
-        scatter_tile_write<BITS, ITEMS, NT, SIDE, EXT>(L, out, gt, side, shift2, mask2);
+        scatter_tile_write<BITS, ITEMS, NT, SIDE, EXT, T>(L, out, gt, side, shift2, mask2);
         if (ti + 1 >= ntiles) break;
-        gt = scatter_tile_sort<BITS, ITEMS, NT, EXT>(L, pend, carried, vb, out, tn_of(ti + 1, mb), shift, 0, &ps);
+        gt = scatter_tile_sort<BITS, ITEMS, NT, EXT, T>(L, pend, carried, vb, out, tn_of(ti + 1, mb), shift, 0, &ps);
         mb = load(ti + 3, vb);
 #pragma unroll
         for (int k = 0; k < ITEMS; ++k) asm volatile("" ::"v"(va[k]));
-        scatter_tile_write<BITS, ITEMS, NT, SIDE, EXT>(L, out, gt, side, shift2, mask2);
+        scatter_tile_write<BITS, ITEMS, NT, SIDE, EXT, T>(L, out, gt, side, shift2, mask2);
         if (ti + 2 >= ntiles) break;
-        gt = scatter_tile_sort<BITS, ITEMS, NT, EXT>(L, pend, carried, va, out, tn_of(ti + 2, ma), shift, 0, &ps);
+        gt = scatter_tile_sort<BITS, ITEMS, NT, EXT, T>(L, pend, carried, va, out, tn_of(ti + 2, ma), shift, 0, &ps);
     }
     // flush the carried (partial) granules; pooled: close every chain
     __syncthreads();
@@ -946,17 +1014,17 @@ __device__ __forceinline__ void scatter_segment_ext(ScatterLds<BITS, ITEMS, NT, 
         if constexpr (EXT == 1) {
             uint32_t gran = 0;
             if (carried) {
-                const uint32_t off = (uint32_t)(pend / kGran) & (kGPB - 1);
+                const uint32_t off = (uint32_t)(pend / G) & (GPB - 1);
                 if (off == 0) {  // the chain is empty or its block is full
                     ps.cur = ps.pool0 + atomicAdd(&L.pool_next, 1u);
                     ++ps.nb;
                 }
-                gran = ps.cur * kGPB + off;
+                gran = ps.cur * GPB + off;
             }
-            const uint64_t T = pend + carried;  // tuples of digit tid in this segment
-            if (ps.nb) po.binfo[ps.cur] = tid | ((uint32_t)(T - (uint64_t)(ps.nb - 1) * kBlk) << 16);
-            po.cnt[(uint64_t)tid * po.nseg + g] = ((uint64_t)ps.nb << 40) | T;
-            L.pend[tid] = (uint64_t)gran * kGran;
+            const uint64_t Tn = pend + carried;  // elements of digit tid in this segment
+            if (ps.nb) po.binfo[ps.cur] = tid | ((uint32_t)(Tn - (uint64_t)(ps.nb - 1) * kBlk) << 16);
+            po.cnt[(uint64_t)tid * po.nseg + g] = ((uint64_t)ps.nb << 40) | Tn;
+            L.pend[tid] = (uint64_t)gran * G;
         } else {
             L.pend[tid] = pend;
         }
@@ -964,49 +1032,64 @@ __device__ __forceinline__ void scatter_segment_ext(ScatterLds<BITS, ITEMS, NT, 
     }
     __syncthreads();
     if (EXT == 1 && tid == 0) po.used[g] = L.pool_next;
-    const uint32_t lane = tid & (kGran - 1);
-    for (uint32_t d = tid / kGran; d < F; d += NG) {
+    const uint32_t lane = tid & (G - 1);
+    for (uint32_t d = tid / G; d < F; d += NG) {
         if (lane < L.cnt[d]) {
-            const uint64_t x = L.carry[d * CS + lane];
+            const T x = L.carry[d * CS + lane];
             out[L.pend[d] + lane] = x;
             if (SIDE) side[L.pend[d] + lane] = (uint8_t)(((uint32_t)x >> shift2) & mask2);
         }
     }
 }
 
-template <int BITS, int ITEMS, int NT>
-__global__ __launch_bounds__(NT, (scatter_waves_per_simd<BITS, ITEMS, NT, 1>())) void k_scatter_pool(
-    const uint64_t *__restrict__ in, uint64_t *__restrict__ out, SegMap m, uint32_t shift, PoolOut po,
+template <int BITS, int ITEMS, int NT, typename T, int IS>
+__global__ __launch_bounds__(NT, (scatter_waves_per_simd<BITS, ITEMS, NT, 1, T>())) void k_scatter_pool(
+    const char *__restrict__ in, T *__restrict__ out, SegMap m, uint32_t shift, PoolOut po,
     uint8_t *__restrict__ side, uint32_t shift2, uint32_t mask2) {
-    __shared__ ScatterLds<BITS, ITEMS, NT, 1> L;
-    scatter_segment_ext<BITS, ITEMS, NT, 1>(L, xcd_contiguous(blockIdx.x, gridDim.x), in, out, m, shift, nullptr,
-                                            nullptr, po, side, shift2, mask2);
+    __shared__ ScatterLds<BITS, ITEMS, NT, 1, T> L;
+    scatter_segment_ext<BITS, ITEMS, NT, 1, T, IS>(L, xcd_contiguous(blockIdx.x, gridDim.x), in, out, m, shift,
+                                                   nullptr, nullptr, po, side, shift2, mask2);
 }
 
-template <int BITS, int ITEMS, int NT>
-__global__ __launch_bounds__(NT, (scatter_waves_per_simd<BITS, ITEMS, NT, 2>())) void k_scatter_blk(
-    const uint64_t *__restrict__ in, const uint64_t *__restrict__ list, uint64_t *__restrict__ out, SegMap m,
-    uint32_t shift, const uint64_t *__restrict__ cursors) {
-    __shared__ ScatterLds<BITS, ITEMS, NT, 2> L;
+template <int BITS, int ITEMS, int NT, typename T>
+__global__ __launch_bounds__(NT, (scatter_waves_per_simd<BITS, ITEMS, NT, 2, T>())) void k_scatter_blk(
+    const char *__restrict__ in, const uint64_t *__restrict__ list, T *__restrict__ out, SegMap m, uint32_t shift,
+    const uint64_t *__restrict__ cursors) {
+    __shared__ ScatterLds<BITS, ITEMS, NT, 2, T> L;
     const PoolOut none{};
-    scatter_segment_ext<BITS, ITEMS, NT, 2>(L, blockIdx.x, in, out, m, shift, cursors, list, none, nullptr, 0, 0);
+    scatter_segment_ext<BITS, ITEMS, NT, 2, T, (int)sizeof(T)>(L, blockIdx.x, in, out, m, shift, cursors, list, none,
+                                                               nullptr, 0, 0);
 }
 
-hipError_t launch_scatter_pool(const row_t *in, row_t *out, const SegMap &m, uint32_t grid, uint32_t shift,
-                               uint32_t bits, const PoolOut &po, const DigitSide &ds, hipStream_t s) {
-    if (grid == 0) return hipSuccess;
-    constexpr int ITEMS = kScatterItems, NT = kScatterThreads;
-    const uint64_t *i64 = reinterpret_cast<const uint64_t *>(in);
-    uint64_t *o64 = reinterpret_cast<uint64_t *>(out);
+// Elements per thread per tile: 8 tuples (32 KiB tiles); keys: 12 in the pooled pass 1
+// (24 KiB tiles; 16 spill 17-19 VGPRs at the 128-register cap), 16 in the block-list
+// pass 2 (larger tiles amortise the per-tile work: 0.75 -> 0.69 ms per 2^28 keys).
+#ifndef SGXAMD_KEY_ITEMS
+#define SGXAMD_KEY_ITEMS 12
+#endif
+#ifndef SGXAMD_KEY_ITEMS_BLK
+#define SGXAMD_KEY_ITEMS_BLK 16
+#endif
+template <typename T, int EXT>
+constexpr int items_of() {
+    return sizeof(T) == 8 ? kScatterItems : (EXT == 2 ? SGXAMD_KEY_ITEMS_BLK : SGXAMD_KEY_ITEMS);
+}
+
+template <typename T, int IS>
+hipError_t launch_scatter_pool_t(const void *in, void *out, const SegMap &m, uint32_t grid, uint32_t shift,
+                                 uint32_t bits, const PoolOut &po, const DigitSide &ds, hipStream_t s) {
+    constexpr int ITEMS = items_of<T, 1>(), NT = kScatterThreads;
+    const char *ib = static_cast<const char *>(in);
+    T *o = static_cast<T *>(out);
     const uint32_t mask2 = (1u << ds.bits2) - 1u;
-#define POOL_CASE(B)                                                                                          \
-    case B:                                                                                                   \
-        if constexpr (sizeof(ScatterLds<B, ITEMS, NT, 1>) <= 160 * 1024 && (1 << B) <= NT) {                   \
-            hipLaunchKernelGGL((k_scatter_pool<B, ITEMS, NT>), dim3(grid), dim3(NT), 0, s, i64, o64, m, shift, \
-                               po, ds.side, ds.shift2, mask2);                                                \
-            break;                                                                                            \
-        } else {                                                                                              \
-            return hipErrorInvalidValue;                                                                      \
+#define POOL_CASE(B)                                                                                             \
+    case B:                                                                                                      \
+        if constexpr (sizeof(ScatterLds<B, ITEMS, NT, 1, T>) <= 160 * 1024 && (1 << B) <= NT) {                   \
+            hipLaunchKernelGGL((k_scatter_pool<B, ITEMS, NT, T, IS>), dim3(grid), dim3(NT), 0, s, ib, o, m, shift, \
+                               po, ds.side, ds.shift2, mask2);                                                   \
+            break;                                                                                               \
+        } else {                                                                                                 \
+            return hipErrorInvalidValue;                                                                         \
         }
     switch (bits) {
         POOL_CASE(1)
@@ -1025,16 +1108,26 @@ hipError_t launch_scatter_pool(const row_t *in, row_t *out, const SegMap &m, uin
     return hipGetLastError();
 }
 
-hipError_t launch_scatter_blk(const row_t *in, const uint64_t *list, row_t *out, const SegMap &m, uint32_t grid,
-                              uint32_t shift, uint32_t bits, const uint64_t *cursors, hipStream_t s) {
+hipError_t launch_scatter_pool(const void *in, uint32_t in_size, void *out, uint32_t out_size, const SegMap &m,
+                               uint32_t grid, uint32_t shift, uint32_t bits, const PoolOut &po, const DigitSide &ds,
+                               hipStream_t s) {
     if (grid == 0) return hipSuccess;
-    constexpr int ITEMS = kScatterItems, NT = kScatterThreads;
-    const uint64_t *i64 = reinterpret_cast<const uint64_t *>(in);
-    uint64_t *o64 = reinterpret_cast<uint64_t *>(out);
-#define BLK_CASE(B)                                                                                             \
-    case B:                                                                                                     \
-        hipLaunchKernelGGL((k_scatter_blk<B, ITEMS, NT>), dim3(grid), dim3(NT), 0, s, i64, list, o64, m, shift, \
-                           cursors);                                                                            \
+    if (in_size == 8 && out_size == 8) return launch_scatter_pool_t<uint64_t, 8>(in, out, m, grid, shift, bits, po, ds, s);
+    if (in_size == 8 && out_size == 4) return launch_scatter_pool_t<uint32_t, 8>(in, out, m, grid, shift, bits, po, ds, s);
+    if (in_size == 4 && out_size == 4) return launch_scatter_pool_t<uint32_t, 4>(in, out, m, grid, shift, bits, po, ds, s);
+    return hipErrorInvalidValue;
+}
+
+template <typename T>
+hipError_t launch_scatter_blk_t(const void *in, const uint64_t *list, void *out, const SegMap &m, uint32_t grid,
+                                uint32_t shift, uint32_t bits, const uint64_t *cursors, hipStream_t s) {
+    constexpr int ITEMS = items_of<T, 2>(), NT = kScatterThreads;
+    const char *ib = static_cast<const char *>(in);
+    T *o = static_cast<T *>(out);
+#define BLK_CASE(B)                                                                                                \
+    case B:                                                                                                        \
+        hipLaunchKernelGGL((k_scatter_blk<B, ITEMS, NT, T>), dim3(grid), dim3(NT), 0, s, ib, list, o, m, shift, \
+                           cursors);                                                                               \
         break;
     switch (bits) {
         BLK_CASE(1)
@@ -1050,6 +1143,14 @@ hipError_t launch_scatter_blk(const row_t *in, const uint64_t *list, row_t *out,
     }
 #undef BLK_CASE
     return hipGetLastError();
+}
+
+hipError_t launch_scatter_blk(const void *in, const uint64_t *list, void *out, uint32_t elem_size, const SegMap &m,
+                              uint32_t grid, uint32_t shift, uint32_t bits, const uint64_t *cursors, hipStream_t s) {
+    if (grid == 0) return hipSuccess;
+    if (elem_size == 8) return launch_scatter_blk_t<uint64_t>(in, list, out, m, grid, shift, bits, cursors, s);
+    if (elem_size == 4) return launch_scatter_blk_t<uint32_t>(in, list, out, m, grid, shift, bits, cursors, s);
+    return hipErrorInvalidValue;
 }
 
 // One block: from the column-scanned chain records (totals[d] = blocks << 40 | tuples)
@@ -1255,7 +1356,8 @@ struct JoinLds<RCAP, kJoinWrite, NW> {
     uint32_t cursor;
 };
 
-template <int RCAP, int MODE, int BLOCK = kBlock>
+// KS: u32 words per partitioned element (2: row_t tuples; 1: packed keys, counting only).
+template <int RCAP, int MODE, int BLOCK = kBlock, int KS = 2>
 __global__ __launch_bounds__(BLOCK) void k_join(const uint64_t *__restrict__ R, const uint64_t *__restrict__ S,
                                                  const uint64_t *__restrict__ r_start,
                                                  const uint64_t *__restrict__ r_count,
@@ -1268,7 +1370,9 @@ __global__ __launch_bounds__(BLOCK) void k_join(const uint64_t *__restrict__ R, 
                                                  output_triple_t *__restrict__ out, uint64_t *__restrict__ cyc,
                                                  uint64_t *__restrict__ red_result, uint64_t *__restrict__ red_ticket) {
     constexpr int U = RCAP / BLOCK, NW = BLOCK / kWave;
+    static_assert(KS == 2 || MODE != kJoinWrite, "materialisation needs the payloads");
     __shared__ JoinLds<RCAP, MODE, NW> L;
+    const uint32_t *Rk = reinterpret_cast<const uint32_t *>(R), *Sk = reinterpret_cast<const uint32_t *>(S);
     const uint32_t tid = threadIdx.x, lane = __lane_id();
     const uint64_t T = P + *n_over;
     uint64_t matches = 0;
@@ -1296,7 +1400,10 @@ __global__ __launch_bounds__(BLOCK) void k_join(const uint64_t *__restrict__ R, 
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     const uint32_t i = tid + u * BLOCK;
-                    kr[u] = i < nrc ? ld_nt(rp + rc + i) : 0ull;
+                    if constexpr (KS == 1)
+                        kr[u] = i < nrc ? __builtin_nontemporal_load(Rk + r_start[p] + rc + i) : 0u;
+                    else
+                        kr[u] = i < nrc ? ld_nt(rp + rc + i) : 0ull;
                 }
                 for (uint32_t i = tid; i < (N + 3) / 4; i += BLOCK)
                     reinterpret_cast<uint4 *>(L.head)[i] = make_uint4(0, 0, 0, 0);
@@ -1330,7 +1437,10 @@ __global__ __launch_bounds__(BLOCK) void k_join(const uint64_t *__restrict__ R, 
 #pragma unroll
                         for (int u = 0; u < U; ++u) {
                             const uint64_t i = s0 + tid + u * BLOCK;
-                            ks[u] = i < nS ? __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(sp + i)) : 0u;
+                            if constexpr (KS == 1)
+                                ks[u] = i < nS ? __builtin_nontemporal_load(Sk + s_start[p] + s_lo + i) : 0u;
+                            else
+                                ks[u] = i < nS ? __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(sp + i)) : 0u;
                         }
                     }
 #pragma unroll
@@ -1450,7 +1560,7 @@ __device__ __forceinline__ uint32_t key_tag(uint32_t k, uint32_t tshift) {
 }
 
 // Each thread builds and probes in strips of UP tuples (UP chain walks in lock step).
-template <int RCAP, int BLOCK, int UP>
+template <int RCAP, int BLOCK, int UP, int KS = 2>
 __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_join_tag(
     const uint64_t *__restrict__ R, const uint64_t *__restrict__ S, const uint64_t *__restrict__ r_start,
     const uint64_t *__restrict__ r_count, const uint64_t *__restrict__ s_start, const uint64_t *__restrict__ s_count,
@@ -1471,8 +1581,9 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_join_tag(
         const uint64_t s_lo = chunk * s_chunk;
         const uint64_t nS = (nR == 0 || s_lo >= nSp) ? 0 : min<uint64_t>(nSp - s_lo, s_chunk);
         if (nS == 0) continue;
-        const uint32_t *rk = reinterpret_cast<const uint32_t *>(R + r_start[p]);  // key = low word of a tuple
-        const uint32_t *sk = reinterpret_cast<const uint32_t *>(S + s_start[p] + s_lo);
+        // key = low word of a tuple (KS 2) or a packed key (KS 1)
+        const uint32_t *rk = reinterpret_cast<const uint32_t *>(R) + r_start[p] * KS;
+        const uint32_t *sk = reinterpret_cast<const uint32_t *>(S) + (s_start[p] + s_lo) * KS;
         for (uint64_t rc = 0; rc < nR; rc += RCAP) {
             const uint64_t c_build = wall_clock64();
             const uint32_t nrc = (uint32_t)((nR - rc) < RCAP ? (nR - rc) : RCAP);
@@ -1481,7 +1592,7 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_join_tag(
             const uint32_t hmask = (1u << lgN) - 1;
             const uint32_t tshift = hash_shift + lgN;
             const bool exact = tshift + 8 >= 32;
-            const uint32_t *rkc = rk + 2 * rc;
+            const uint32_t *rkc = rk + KS * rc;
             for (uint32_t i = tid; i < ((1u << lgN) + 7) / 8; i += BLOCK)
                 reinterpret_cast<uint4 *>(L.head2)[i] = make_uint4(0, 0, 0, 0);
             __syncthreads();
@@ -1490,7 +1601,7 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_join_tag(
 #pragma unroll
                 for (int u = 0; u < UP; ++u) {
                     const uint32_t i = r0 + tid + u * BLOCK;
-                    kr[u] = i < nrc ? __builtin_nontemporal_load(rkc + 2 * i) : 0u;
+                    kr[u] = i < nrc ? __builtin_nontemporal_load(rkc + KS * i) : 0u;
                 }
 #pragma unroll
                 for (int u = 0; u < UP; ++u) {
@@ -1520,7 +1631,7 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_join_tag(
 #pragma unroll
                 for (int u = 0; u < UP; ++u) {
                     const uint64_t i = s0 + tid + u * BLOCK;
-                    ks[u] = i < nS ? __builtin_nontemporal_load(sk + 2 * i) : 0u;
+                    ks[u] = i < nS ? __builtin_nontemporal_load(sk + KS * i) : 0u;
                 }
 #pragma unroll
                 for (int u = 0; u < UP; ++u) {
@@ -1536,7 +1647,7 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_join_tag(
                         if (cur[u] != 0) {
                             const uint32_t e = cur[u] - 1;
                             if (L.tag[e] == key_tag(ks[u], tshift))
-                                tmatch_add(matches, exact || rkc[2 * e] == ks[u]);
+                                tmatch_add(matches, exact || rkc[KS * e] == ks[u]);
                             cur[u] = L.next[e];
                             more |= cur[u] != 0;
                         }
@@ -1760,11 +1871,53 @@ __global__ __launch_bounds__(kBlock) void k_join_hist(const uint64_t *__restrict
     }
 }
 
+// Counting build/probe over packed keys (key-only partitions, KS = 1).
+hipError_t launch_join_keys(const void *R, const void *S, const uint64_t *r_start, const uint64_t *r_count,
+                            const uint64_t *s_start, const uint64_t *s_count, uint64_t P, const uint64_t *over,
+                            const uint32_t *n_over, uint32_t hash_shift, uint32_t rcap, uint64_t s_chunk,
+                            uint32_t grid, int mode, int algo, uint64_t *counts, uint64_t *cyc, hipStream_t s,
+                            const JoinReduce *reduce) {
+    if (mode != kJoinCount || algo != kAlgoChaining) return hipErrorInvalidValue;
+    const uint64_t *R64 = static_cast<const uint64_t *>(R);
+    const uint64_t *S64 = static_cast<const uint64_t *>(S);
+    uint64_t *rres = reduce ? reduce->result : nullptr;
+    uint64_t *rtick = reduce ? reduce->ticket : nullptr;
+    if (rcap == kBigRcap) {
+        static const int tag_block = [] {
+            const char *e = std::getenv("SGXAMD_TAG_JOIN");
+            return e ? std::atoi(e) : 1024;
+        }();
+        if (tag_block == 512)
+            hipLaunchKernelGGL((k_join_tag<kBigRcap, 512, 16, 1>), dim3(grid), dim3(512), 0, s, R64, S64, r_start,
+                               r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts, cyc, rres, rtick);
+        else if (tag_block == 1024)
+            hipLaunchKernelGGL((k_join_tag<kBigRcap, 1024, 8, 1>), dim3(grid), dim3(1024), 0, s, R64, S64, r_start,
+                               r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts, cyc, rres, rtick);
+        else
+            hipLaunchKernelGGL((k_join<kBigRcap, kJoinCount, kBigJoinBlock, 1>), dim3(grid), dim3(kBigJoinBlock), 0, s,
+                               R64, S64, r_start, r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk,
+                               counts, nullptr, nullptr, cyc, rres, rtick);
+        return hipGetLastError();
+    }
+#define KEYS_CASE(RC)                                                                                                   case RC:                                                                                                                hipLaunchKernelGGL((k_join<RC, kJoinCount, kBlock, 1>), dim3(grid), dim3(kBlock), 0, s, R64, S64, r_start,                            r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts, nullptr, nullptr,                             cyc, rres, rtick);                                                                               break;
+    switch (rcap) {
+        KEYS_CASE(2048)
+        KEYS_CASE(4096)
+        KEYS_CASE(8192)
+        default:
+            return hipErrorInvalidValue;
+    }
+#undef KEYS_CASE
+    return hipGetLastError();
+}
+
 hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, const uint64_t *r_count,
                        const uint64_t *s_start, const uint64_t *s_count, uint64_t P, const uint64_t *over,
                        const uint32_t *n_over, uint32_t hash_shift, uint32_t rcap, uint64_t s_chunk, uint32_t grid,
                        int mode, int algo, uint64_t *counts, const uint64_t *task_off, output_triple_t *out,
-                       uint64_t *cyc, hipStream_t s, const JoinReduce *reduce) {
+                       uint64_t *cyc, hipStream_t s, const JoinReduce *reduce, int key_stride) {
+    if (key_stride == 1) return launch_join_keys(R, S, r_start, r_count, s_start, s_count, P, over, n_over, hash_shift,
+                                                 rcap, s_chunk, grid, mode, algo, counts, cyc, s, reduce);
     const uint64_t *R64 = reinterpret_cast<const uint64_t *>(R);
     const uint64_t *S64 = reinterpret_cast<const uint64_t *>(S);
     uint64_t *rres = (reduce && mode == kJoinCount) ? reduce->result : nullptr;

@@ -17,7 +17,8 @@ import os
 from dataclasses import dataclass
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-LIB_PATH = os.path.join(PKG_DIR, "libsgxamd.so")
+# SGXAMD_LIB_PATH: a development build of the same library (scripts/build_variant.sh)
+LIB_PATH = os.environ.get("SGXAMD_LIB_PATH") or os.path.join(PKG_DIR, "libsgxamd.so")
 
 MI355_OK = 0
 MI355_ERR_INVALID = -1
