@@ -29,7 +29,7 @@ sys.path.insert(0, os.path.join(PKG, "python"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 METRIC = "M probed tuples/sec (RHO join) + scan GB/s vs HBM roofline, 1/2/4/8 MI355X"
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic_r02j.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic_r02o.json")
 
 
 def log(*a):
@@ -153,23 +153,35 @@ class cpu_affinity:
         return False
 
 
-def algorithmic_bytes(kernel: str, nR: int, nS: int, passes: int = 2, pass2_bits: int = 8) -> int:
+# mi355_rho_stats.layout (sgxamd/rho.h)
+LAYOUTS = {
+    0: "8-byte tuples, pass-1 histogram + cursors",
+    1: "8-byte tuples, pooled pass 1 (per-workgroup block chains, no pass-1 histogram)",
+    2: "pooled pass 1; a counting join moves 4-byte keys after reading the 8-byte input tuples "
+       "(the payloads are never read by the count; SGXAMD_KEYS=0 moves whole tuples)",
+}
+
+
+def algorithmic_bytes(kernel: str, nR: int, nS: int, passes: int = 2, pass2_bits: int = 8, elem: int = 8) -> int:
     """Bytes a kernel must move per launch (DESIGN.md 'Kernels and their rooflines').
 
     Two-pass plans: the pass-1 scatter also writes one pass-2 digit byte per tuple (the
-    digit side stream) and the pass-2 histogram reads those bytes, not the tuples."""
+    digit side stream) and the pass-2 histogram reads those bytes, not the tuples.
+    elem: bytes per partitioned element after the input read — 8 (row_t tuples) or 4
+    (counting RHO joins move keys only: the pass-1 scatter reads 8-byte tuples and
+    writes 4-byte keys, pass 2 and the build/probe read and write keys)."""
     n = nR if kernel.startswith("R_") else nS
     side = passes == 2 and pass2_bits <= 8 and os.environ.get("SGXAMD_DIGIT_SIDE", "1") != "0"  # uses_digit_side()
     if kernel.endswith("pass2_hist") and side:
         return n              # one digit byte per tuple
     if kernel.endswith("_hist"):
         return 8 * n          # read every tuple once (key only used, AoS line read)
-    if kernel.endswith("pass1_scatter") and side:
-        return 17 * n         # read + write every tuple, + its pass-2 digit byte
+    if kernel.endswith("pass1_scatter"):
+        return (8 + elem + (1 if side else 0)) * n  # read the tuple, write the element (+ its digit byte)
     if kernel.endswith("_scatter"):
-        return 16 * n         # read + write every tuple
+        return 2 * elem * n   # read + write every element
     if kernel == "join_build_probe":
-        return 8 * (nR + nS)  # every partitioned tuple read once
+        return elem * (nR + nS)  # every partitioned element read once
     return 0
 
 
@@ -367,7 +379,8 @@ def main():
     nR = results[-1].recv_r
     nS = results[-1].recv_s
     avg = {k: statistics.mean(v) for k, v in per_kernel.items()}
-    plan = (results[-1].local_stats.get("passes") or 2, results[-1].local_stats.get("pass2_bits") or 0)
+    plan = (results[-1].local_stats.get("passes") or 2, results[-1].local_stats.get("pass2_bits") or 0,
+            results[-1].local_stats.get("elem_bytes") or 8)
     byte_kernels = {k: v for k, v in avg.items() if algorithmic_bytes(k, nR, nS, *plan) > 0}
     dom = max(byte_kernels, key=byte_kernels.get)
     achieved = algorithmic_bytes(dom, nR, nS, *plan) / (avg[dom] * 1e-3) / 1e9
@@ -383,7 +396,7 @@ def main():
     roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "avg_ms": round(avg[dom], 4), "algorithmic_bytes": algorithmic_bytes(dom, nR, nS, *plan)}
-    probe_gbs = algorithmic_bytes("join_build_probe", nR, nS) / (avg["join_build_probe"] * 1e-3) / 1e9
+    probe_gbs = algorithmic_bytes("join_build_probe", nR, nS, *plan) / (avg["join_build_probe"] * 1e-3) / 1e9
     phase = {k: round(v, 4) for k, v in sorted(avg.items())}
     ls = results[-1].local_stats
     rho_info = {
@@ -395,6 +408,7 @@ def main():
         "kernel_ms_avg": phase, "kernel_times_from": kernel_times,
         "partition_overlap": bool(args.partition_overlap),
         "radix_bits": ls.get("radix_bits"), "passes": ls.get("passes"),
+        "partition_layout": LAYOUTS.get(ls.get("layout"), "unknown"),
         "step_ms_breakdown": {k: round(v, 3) for k, v in results[-1].ms.items()},
     }
     if args.workload == "c5":
@@ -417,7 +431,9 @@ def main():
             res_w, pk_w, el_w = measure_rho(wl, Rw, Sw, gRw, gSw)
             avg_w = {k: statistics.mean(v) for k, v in pk_w.items()}
             nRw, nSw = res_w[-1].recv_r, res_w[-1].recv_s
-            pb = algorithmic_bytes("join_build_probe", nRw, nSw) / (avg_w["join_build_probe"] * 1e-3) / 1e9
+            ls_w = res_w[-1].local_stats
+            plan_w = (ls_w.get("passes") or 2, ls_w.get("pass2_bits") or 0, ls_w.get("elem_bytes") or 8)
+            pb = algorithmic_bytes("join_build_probe", nRw, nSw, *plan_w) / (avg_w["join_build_probe"] * 1e-3) / 1e9
             configs_info[wl] = {
                 "workload": desc_w, "generator": gen_w, "scaling": "strong", "global_R": gRw, "global_S": gSw,
                 "matches": res_w[-1].matches, "matches_ok": True,
@@ -747,6 +763,7 @@ def main():
                     + " relations, 8-byte {key, payload} tuples",
             "config": {"workload": workload, "algorithm": args.algorithm, "global_R": gR, "global_S": gS,
                        "parallelism": f"radix-shard{world}",
+                       "partition_layout": rho_info["partition_layout"],
                        **({"exchange": results[-1].ms.get("impl", "torch.distributed all_to_all_single (sgxamd.dist)")}
                           if world > 1 else {}),
                        **({"dist_backend": "gloo (single-GPU rehearsal, not a scaling number)"}

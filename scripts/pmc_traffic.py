@@ -22,6 +22,10 @@ import sys
 ALIASES = {
     "k_hist": ["R_pass1_hist", "S_pass1_hist"],
     "k_hist_side": ["R_pass2_hist", "S_pass2_hist"],
+    # pooled two-pass plans (one kernel per pass; listed after BY_GRID, so they win)
+    "k_scatter_pool": ["R_pass1_scatter", "S_pass1_scatter"],
+    "k_scatter_blk": ["R_pass2_scatter", "S_pass2_scatter"],
+    "k_hist_side_blk": ["R_pass2_hist", "S_pass2_hist"],
     "k_join": ["join_build_probe"],
     "k_join_tag": ["join_build_probe"],
     "k_predicate": ["scan_count", "scan_bitvector"],

@@ -476,6 +476,8 @@ void fill_join_stats(const Context *ctx, const PendingJoin &pj, const Timer &tm,
         st->passes = pol.passes;
         st->pass1_bits = pol.b1;
         st->pass2_bits = pol.b2;
+        st->layout = pj.pr.keys ? 2u : (pj.pr.pooled ? 1u : 0u);
+        st->elem_bytes = pj.pr.keys ? 4u : 8u;
         st->num_partitions = P;
         st->num_tasks = P + (uint32_t)ctx->host_result[3];
         st->max_part_r = ctx->host_result[1];

@@ -116,6 +116,8 @@ class rho_stats(C.Structure):
         ("ms_pass2_copy", C.c_double),
         ("ms_build", C.c_double),
         ("ms_probe", C.c_double),
+        ("layout", C.c_uint32),
+        ("elem_bytes", C.c_uint32),
     ]
 
     def as_dict(self) -> dict:
