@@ -409,7 +409,7 @@ def main():
         "partition_overlap": bool(args.partition_overlap),
         "radix_bits": ls.get("radix_bits"), "passes": ls.get("passes"),
         "partition_layout": LAYOUTS.get(ls.get("layout"), "unknown"),
-        "step_ms_breakdown": {k: round(v, 3) for k, v in results[-1].ms.items()},
+        "step_ms_breakdown": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in results[-1].ms.items()},
     }
     if args.workload == "c5":
         rho_info["load_report"] = load_report(results[-1], nS)
@@ -443,7 +443,8 @@ def main():
                 "probe_roofline": {"achieved": round(pb, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                    "frac": round(pb / HBM_PEAK_GBS, 4)},
                 "kernel_ms_avg": {k: round(v, 4) for k, v in sorted(avg_w.items())},
-                "step_ms_breakdown": {k: round(v, 3) for k, v in res_w[-1].ms.items()},
+                "step_ms_breakdown": {k: (round(v, 3) if isinstance(v, float) else v)
+                                      for k, v in res_w[-1].ms.items()},
                 "load_report": load_report(res_w[-1], nSw),
             }
             del Rw, Sw

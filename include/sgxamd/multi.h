@@ -59,6 +59,8 @@ typedef struct mi355_multi_stats {
     double ms_local;           /* from the last piece posted to the local join's end */
     double ms_allreduce;       /* final match-count all-reduce */
     mi355_rho_stats local;     /* the local join of rank 0 (or of the calling rank) */
+    uint32_t elem_bytes;       /* bytes per exchanged element: 8 (tuples) or 4 (keys only: a
+                                  counting join whose local join reads keys) */
 } mi355_multi_stats;
 
 /* Single process, `ngpus` ranks driven by one host thread each.  R and S are host or

@@ -170,8 +170,9 @@ class Transport {
     // collective: after `ready` (the piece's partition on the compute stream), move the
     // piece: the run for destination d starts at send + sum_{d'<d} send_counts[d'];
     // rank q's run lands at recv + sum_{q'<q} recv_counts[q'].  Enqueued on c.
-    virtual int post_exchange(int rank, hipStream_t c, hipEvent_t ready, const row_t *send,
-                              const uint64_t *send_counts, row_t *recv, const uint64_t *recv_counts) = 0;
+    // elem: bytes per element (8: row_t tuples; 4: keys of a keys-only exchange).
+    virtual int post_exchange(int rank, hipStream_t c, hipEvent_t ready, const void *send,
+                              const uint64_t *send_counts, void *recv, const uint64_t *recv_counts, size_t elem) = 0;
     // collective: *v = sum / max of every rank's *v
     virtual int allreduce(int rank, hipStream_t s, uint64_t *v, ReduceOp op) = 0;
     virtual void abort() {}
@@ -211,19 +212,22 @@ class RcclTransport final : public Transport {
         return MI355_OK;
     }
 
-    int post_exchange(int rank, hipStream_t c, hipEvent_t ready, const row_t *send, const uint64_t *send_counts,
-                      row_t *recv, const uint64_t *recv_counts) override {
+    int post_exchange(int rank, hipStream_t c, hipEvent_t ready, const void *send_v, const uint64_t *send_counts,
+                      void *recv_v, const uint64_t *recv_counts, size_t elem) override {
         const int i = rank - first_;
         const auto so = prefix(send_counts, world_), ro = prefix(recv_counts, world_);
+        const char *send = static_cast<const char *>(send_v);
+        char *recv = static_cast<char *>(recv_v);
+        const ncclDataType_t type = elem == 8 ? ncclUint64 : ncclUint32;
         MH_HIP(hipStreamWaitEvent(c, ready, 0));
         if (send_counts[rank])  // this rank's own run: a local copy
-            MH_HIP(hipMemcpyAsync(recv + ro[rank], send + so[rank], send_counts[rank] * sizeof(row_t),
+            MH_HIP(hipMemcpyAsync(recv + ro[rank] * elem, send + so[rank] * elem, send_counts[rank] * elem,
                                   hipMemcpyDeviceToDevice, c));
         MH_NCCL(rccl().GroupStart());
         for (int p = 0; p < world_; ++p) {
             if (p == rank) continue;
-            if (send_counts[p]) MH_NCCL(rccl().Send(send + so[p], send_counts[p], ncclUint64, p, comms_[i], c));
-            if (recv_counts[p]) MH_NCCL(rccl().Recv(recv + ro[p], recv_counts[p], ncclUint64, p, comms_[i], c));
+            if (send_counts[p]) MH_NCCL(rccl().Send(send + so[p] * elem, send_counts[p], type, p, comms_[i], c));
+            if (recv_counts[p]) MH_NCCL(rccl().Recv(recv + ro[p] * elem, recv_counts[p], type, p, comms_[i], c));
         }
         MH_NCCL(rccl().GroupEnd());
         return MI355_OK;
@@ -278,9 +282,10 @@ class RehearsalTransport final : public Transport {
         return MI355_OK;
     }
 
-    int post_exchange(int rank, hipStream_t c, hipEvent_t ready, const row_t *send, const uint64_t *send_counts,
-                      row_t *recv, const uint64_t *recv_counts) override {
-        posts_[rank] = Post{send, prefix(send_counts, world_), ready};
+    int post_exchange(int rank, hipStream_t c, hipEvent_t ready, const void *send, const uint64_t *send_counts,
+                      void *recv_v, const uint64_t *recv_counts, size_t elem) override {
+        char *recv = static_cast<char *>(recv_v);
+        posts_[rank] = Post{static_cast<const char *>(send), prefix(send_counts, world_), ready};
         if (!bar_.wait()) return aborted();
         uint64_t off = 0;
         int rc = MI355_OK;
@@ -288,7 +293,7 @@ class RehearsalTransport final : public Transport {
             if (!recv_counts[q]) continue;
             const Post &p = posts_[q];
             if (hipStreamWaitEvent(c, p.ready, 0) != hipSuccess ||
-                hipMemcpyAsync(recv + off, p.send + p.off[rank], recv_counts[q] * sizeof(row_t),
+                hipMemcpyAsync(recv + off * elem, p.send + p.off[rank] * elem, recv_counts[q] * elem,
                                hipMemcpyDeviceToDevice, c) != hipSuccess) {
                 set_last_error("rehearsal exchange copy failed");
                 rc = MI355_ERR_HIP;
@@ -317,7 +322,7 @@ class RehearsalTransport final : public Transport {
         return MI355_ERR_INVALID;
     }
     struct Post {
-        const row_t *send = nullptr;
+        const char *send = nullptr;
         std::vector<uint64_t> off;
         hipEvent_t ready = nullptr;
     };
@@ -354,6 +359,7 @@ int rank_streams(Context *ctx, int nev, RankStreams **out) {
 
 struct RankOut {
     uint64_t global = 0, local = 0, recv_r = 0, recv_s = 0, sent = 0;
+    bool keys = false;  // the exchange moved keys only
     double ms_post = 0, ms_local = 0, ms_allreduce = 0, ms_total = 0;
     mi355_rho_stats st{};
 };
@@ -395,36 +401,44 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
     hipStream_t c = rs->comm;
 
     // receive buffers for the worst case: every rank's piece i comes to this rank
-    uint64_t mR = nR, mS = nS;
+    uint64_t mR = nR, mS = nS, sumR = nR, sumS = nS;
     MH_RC(T.allreduce(rank, s, &mR, kMax));
     MH_RC(T.allreduce(rank, s, &mS, kMax));
+    MH_RC(T.allreduce(rank, s, &sumR, kSum));
+    MH_RC(T.allreduce(rank, s, &sumS, kSum));
     const uint64_t capR = (uint64_t)G * K * ((mR + K - 1) / K), capS = (uint64_t)G * K * ((mS + K - 1) / K);
-    MH_HIP(ctx->xsendR.ensure(std::max<uint64_t>(nR, 1) * sizeof(row_t)));
-    MH_HIP(ctx->xsendS.ensure(std::max<uint64_t>(nS, 1) * sizeof(row_t)));
-    MH_HIP(ctx->xrecvR.ensure(std::max<uint64_t>(capR, 1) * sizeof(row_t)));
-    MH_HIP(ctx->xrecvS.ensure(std::max<uint64_t>(capS, 1) * sizeof(row_t)));
+    // a counting join exchanges keys only (4 of the 8 bytes per tuple on xGMI) when its
+    // local join, planned from the mean local sizes on every rank alike, reads keys
+    o.keys = rho::keys_exchange_plan(sumR / G, sumS / G, capR, capS, &lo);
+    const size_t elem = o.keys ? sizeof(uint32_t) : sizeof(row_t);
+    MH_HIP(ctx->xsendR.ensure(std::max<uint64_t>(nR, 1) * elem));
+    MH_HIP(ctx->xsendS.ensure(std::max<uint64_t>(nS, 1) * elem));
+    MH_HIP(ctx->xrecvR.ensure(std::max<uint64_t>(capR, 1) * elem));
+    MH_HIP(ctx->xrecvS.ensure(std::max<uint64_t>(capS, 1) * elem));
 
     std::vector<uint64_t> sc(G), rc(G);
     uint64_t total[2] = {0, 0};
     for (int rel = 0; rel < 2; ++rel) {
         const row_t *in = rel ? S : R;
         const uint64_t n = rel ? nS : nR;
-        row_t *snd = (rel ? ctx->xsendS : ctx->xsendR).as<row_t>();
-        row_t *rcv = (rel ? ctx->xrecvS : ctx->xrecvR).as<row_t>();
+        char *snd = (rel ? ctx->xsendS : ctx->xsendR).as<char>();
+        char *rcv = (rel ? ctx->xrecvS : ctx->xrecvR).as<char>();
         const uint64_t per = (n + K - 1) / K;
         for (int i = 0; i < K; ++i) {
             const uint64_t a = std::min(n, i * per), b = std::min(n, (i + 1) * per);
             if (b > a)
-                MH_RC(rho::shard_partition_device(ctx, s, in + a, b - a, 0, dest_bits, snd + a, sc.data()));
+                MH_RC(rho::shard_partition_device(ctx, s, in + a, b - a, 0, dest_bits, snd + a * elem, sc.data(),
+                                                  (uint32_t)elem));
             else
                 std::fill(sc.begin(), sc.end(), 0);
             MH_RC(T.exchange_counts(rank, s, sc.data(), rc.data()));
             hipEvent_t ready = rs->ev[rel * K + i];
             MH_HIP(hipEventRecord(ready, s));
-            MH_RC(T.post_exchange(rank, c, ready, snd + a, sc.data(), rcv + total[rel], rc.data()));
+            MH_RC(T.post_exchange(rank, c, ready, snd + a * elem, sc.data(), rcv + total[rel] * elem, rc.data(),
+                                  elem));
             for (int q = 0; q < G; ++q) {
                 total[rel] += rc[q];
-                if (q != rank) o.sent += sc[q] * sizeof(row_t);
+                if (q != rank) o.sent += sc[q] * elem;
             }
         }
         MH_HIP(hipEventRecord(rs->ev[2 * K + rel], c));
@@ -437,9 +451,9 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
     // local join: R's passes once R has landed, S's passes and build/probe once S has
     MH_HIP(hipStreamWaitEvent(s, rs->ev[2 * K], 0));
     if (total[0] && total[1]) {
-        MH_RC(rho::join_pipelined_begin(ctx, s, ctx->xrecvR.as<row_t>(), total[0], total[1], &lo));
+        MH_RC(rho::join_pipelined_begin(ctx, s, ctx->xrecvR.ptr, total[0], total[1], &lo, (uint32_t)elem));
         MH_HIP(hipStreamWaitEvent(s, rs->ev[2 * K + 1], 0));
-        MH_RC(rho::join_pipelined_finish(ctx, ctx->xrecvS.as<row_t>(), total[1], &o.st));
+        MH_RC(rho::join_pipelined_finish(ctx, ctx->xrecvS.ptr, total[1], &o.st));
         o.local = o.st.matches;
     } else {
         MH_HIP(hipStreamWaitEvent(s, rs->ev[2 * K + 1], 0));
@@ -522,6 +536,7 @@ void fill_stats(mi355_multi_stats *st, const std::vector<RankOut> &outs, int G, 
     if (!outs.empty()) {
         st->local_matches = outs[0].local;
         st->local = outs[0].st;
+        st->elem_bytes = outs[0].keys ? 4u : 8u;
     }
 }
 

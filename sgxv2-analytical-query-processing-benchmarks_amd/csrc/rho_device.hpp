@@ -19,11 +19,18 @@ int join_device(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const
 // the stable shard partition by destination (host counts; synchronises s), and the
 // two halves of the pipelined local join (begin enqueues R's passes on s and returns;
 // finish runs S's passes and the build/probe on the same stream and waits).
+// out_elem 8: out holds the tuples; 4: only their key words (a keys-only exchange).
 int shard_partition_device(Context *ctx, hipStream_t s, const row_t *in, uint64_t n, uint32_t key_shift,
-                           uint32_t dest_bits, row_t *out, uint64_t *dest_counts);
-int join_pipelined_begin(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, uint64_t nS,
-                         const mi355_rho_opts *opts);
-int join_pipelined_finish(Context *ctx, const row_t *dS, uint64_t nS, mi355_rho_stats *st);
+                           uint32_t dest_bits, void *out, uint64_t *dest_counts, uint32_t out_elem = 8);
+// in_elem 8: dR / dS are row_t relations; 4: packed keys (needs keys_exchange_plan's plan).
+int join_pipelined_begin(Context *ctx, hipStream_t s, const void *dR, uint64_t nR, uint64_t nS,
+                         const mi355_rho_opts *opts, uint32_t in_elem = 8);
+int join_pipelined_finish(Context *ctx, const void *dS, uint64_t nS, mi355_rho_stats *st);
+// Whether a multi-GPU counting join can exchange keys only: fixes lo's local policy
+// (radix bits / passes) from the expected local sizes nR / nS when the caller left it
+// open, and checks that this policy takes the pooled keys layout for any local size up
+// to cap_r / cap_s (the receive capacities).  SGXAMD_KEYS=0 disables it.
+bool keys_exchange_plan(uint64_t nR, uint64_t nS, uint64_t cap_r, uint64_t cap_s, mi355_rho_opts *lo);
 // What mi355_last_join_stats reports for this thread's last join (multi-GPU calls).
 void set_last_join_stats(const mi355_rho_stats &st);
 

@@ -166,7 +166,8 @@ struct RelPlan {
     uint64_t seg2;
     uint32_t grid2;
     bool pooled;           // pooled pass 1 + block-list pass 2
-    bool keys;             // pooled, and the partitions hold 4-byte keys (counting joins)
+    bool keys;             // the partitions hold 4-byte keys (counting joins; pooled, or a shard pass)
+    uint32_t in_size;      // bytes per input element: 8 (row_t) or 4 (keys, a keys-only exchange)
     uint32_t pool_blocks;  // blocks per pass-1 segment pool
     uint64_t t1_tuples;    // capacity of the pass-1 output (and side stream) in tuples
     // scratch offsets (pooled: hist1 holds the chain records, tot1 their column totals)
@@ -201,7 +202,7 @@ int partition_relation_pooled(Context *ctx, hipStream_t s, Timer &tm, const std:
                          rp.nseg1};
         const DigitSide ds{side, key_shift + pol.b1, pol.b2};
         tm.mark((t + "pass1_scatter").c_str());
-        RHO_HIP(launch_scatter_pool(in, sizeof(row_t), t1, rp.keys ? 4u : 8u, m1, rp.nseg1, key_shift, pol.b1, po, ds,
+        RHO_HIP(launch_scatter_pool(in, rp.in_size, t1, rp.keys ? 4u : 8u, m1, rp.nseg1, key_shift, pol.b1, po, ds,
                                     s));
         tm.mark((t + "pass1_scan").c_str());
         RHO_HIP(launch_pool_layout(po.cnt, rp.nseg1, pol.b1, A.at<uint64_t>(rp.tot1), start1, cnt1, lbase, lcount,
@@ -254,8 +255,12 @@ int partition_relation(Context *ctx, hipStream_t s, Timer &tm, const char *tag, 
                                    pol.passes == 2 ? segbase2 : nullptr, rp.seg2, s));
         tm.mark((t + "pass1_scatter").c_str());
         const DigitSide ds{side, key_shift + pol.b1, pol.b2};
-        RHO_HIP(launch_scatter(in, t1, m1, rp.nseg1, key_shift, pol.b1, hist1, kDigitMajor, rp.nseg1, start1,
-                               use_side ? &ds : nullptr, s));
+        if (rp.keys)  // one pass writing key words (the keys-only shard partition)
+            RHO_HIP(launch_scatter_keys(in, reinterpret_cast<uint32_t *>(t1), m1, rp.nseg1, key_shift, pol.b1, hist1,
+                                        kDigitMajor, rp.nseg1, start1, s));
+        else
+            RHO_HIP(launch_scatter(in, t1, m1, rp.nseg1, key_shift, pol.b1, hist1, kDigitMajor, rp.nseg1, start1,
+                                   use_side ? &ds : nullptr, s));
         *final_rel = t1;
         *pstart = start1;
         *pcnt = cnt1;
@@ -307,6 +312,7 @@ void plan_relation(Arena &A, RelPlan &rp, uint64_t n, const Policy &pol, int poo
     rp.t1_tuples = n;
     rp.pooled = false;
     rp.keys = false;
+    rp.in_size = sizeof(row_t);
     if (pool != kNoPool) {
         // pass-1 segments of whole tiles, about pool_segs() of them; every digit of a
         // segment fills ceil(elements / kBlk) blocks, so a pool of ceil(seg1 / kBlk) + F1
@@ -437,9 +443,16 @@ int plan_join(Context *ctx, hipStream_t s, uint64_t nR, uint64_t nS, const mi355
 // may start after S has been produced later in the stream order of s (multi-GPU:
 // R's local passes run while S is still being exchanged).  Caller holds ctx->mu.
 int join_begin(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, uint64_t nS, const mi355_rho_opts *opts,
-               PendingJoin &pj) {
+               PendingJoin &pj, uint32_t in_elem = sizeof(row_t)) {
     int prc = plan_join(ctx, s, nR, nS, opts, pj);
     if (prc) return prc;
+    if (in_elem != sizeof(row_t)) {  // key input: only the pooled keys layout reads it
+        if (!(pj.pr.keys && pj.ps.keys)) {
+            set_last_error("key-only input needs a counting two-pass plan with the pooled layout");
+            return MI355_ERR_INVALID;
+        }
+        pj.pr.in_size = pj.ps.in_size = in_elem;
+    }
     const Policy &pol = pj.pol;
     Timer &tm = thread_timer();
     // the call's device time is always recorded (throughput in result_t); per kernel
@@ -709,25 +722,36 @@ int join_device(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const
     return join_finish(ctx, pj, dS, nS, st, out, out_cap, grow, false);
 }
 
-int join_pipelined_begin(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, uint64_t nS,
-                         const mi355_rho_opts *opts) {
+int join_pipelined_begin(Context *ctx, hipStream_t s, const void *dR, uint64_t nR, uint64_t nS,
+                         const mi355_rho_opts *opts, uint32_t in_elem) {
     PendingJoin &pj = pending_of(ctx);
     if (pj.active) {
         set_last_error("a pipelined join is already pending on this context");
         return MI355_ERR_INVALID;
     }
-    const int rc = join_begin(ctx, s, dR, nR, nS, opts, pj);
+    const int rc = join_begin(ctx, s, static_cast<const row_t *>(dR), nR, nS, opts, pj, in_elem);
     if (rc) pj.active = false;
     return rc;
 }
 
-int join_pipelined_finish(Context *ctx, const row_t *dS, uint64_t nS, mi355_rho_stats *st) {
-    return join_finish(ctx, pending_of(ctx), dS, nS, st, nullptr, 0, nullptr, true);
+int join_pipelined_finish(Context *ctx, const void *dS, uint64_t nS, mi355_rho_stats *st) {
+    return join_finish(ctx, pending_of(ctx), static_cast<const row_t *>(dS), nS, st, nullptr, 0, nullptr, true);
+}
+
+bool keys_exchange_plan(uint64_t nR, uint64_t nS, uint64_t cap_r, uint64_t cap_s, mi355_rho_opts *lo) {
+    if (!keys_enabled() || lo->materialize || lo->algorithm == MI355_ALGO_RHT) return false;
+    if (lo->radix_bits <= 0) {  // fix the local policy now: the received sizes are not known yet
+        const Policy p = choose_policy(nR, nS, lo);
+        lo->radix_bits = (int)p.bits;
+        lo->passes = (int)p.passes;
+    }
+    const Policy p = choose_policy(nR, nS, lo);
+    return pool_fits(cap_r, p) && pool_fits(cap_s, p) && lo->key_shift + p.bits <= 31;
 }
 
 // Stable partition by destination shard (multi-GPU exchange step).
 int shard_partition_device(Context *ctx, hipStream_t s, const row_t *in, uint64_t n, uint32_t key_shift,
-                           uint32_t dest_bits, row_t *out, uint64_t *dest_counts) {
+                           uint32_t dest_bits, void *out, uint64_t *dest_counts, uint32_t out_elem) {
     if (pending_of(ctx).active) {  // the arena holds the pending join's R partitions
         set_last_error("shard_partition while a pipelined join is pending on this device");
         return MI355_ERR_INVALID;
@@ -739,13 +763,14 @@ int shard_partition_device(Context *ctx, hipStream_t s, const row_t *in, uint64_
     A.reset();
     RelPlan rp{};
     plan_relation(A, rp, n, pol);
+    rp.keys = out_elem == 4;
     RHO_HIP(A.buf.ensure(A.used));
     Timer &tm = thread_timer();
     tm.begin_call(s, thread_timing_enabled());
     const row_t *f;
     const uint64_t *pst, *pcn;
-    int rc = partition_relation(ctx, s, tm, "shard_", in, out, nullptr, nullptr, rp, pol, key_shift, &f, &pst, &pcn,
-                                false);
+    int rc = partition_relation(ctx, s, tm, "shard_", in, static_cast<row_t *>(out), nullptr, nullptr, rp, pol,
+                                key_shift, &f, &pst, &pcn, false);
     if (rc) return rc;
     tm.end_call();
     const uint32_t F = 1u << dest_bits;

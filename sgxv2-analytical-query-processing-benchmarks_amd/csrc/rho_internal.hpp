@@ -119,6 +119,11 @@ hipError_t launch_hist_side_blk(const uint8_t *side, const uint64_t *list, const
                                 uint32_t bits, uint64_t *hist, hipStream_t s);
 hipError_t launch_scatter_blk(const void *in, const uint64_t *list, void *out, uint32_t elem_size, const SegMap &m,
                               uint32_t grid, uint32_t shift, uint32_t bits, const uint64_t *cursors, hipStream_t s);
+// launch_scatter's one-pass cursor scatter writing only the key word of every tuple
+// (the multi-GPU shard partition of a counting join, whose exchange moves keys).
+hipError_t launch_scatter_keys(const row_t *in, uint32_t *out, const SegMap &m, uint32_t grid, uint32_t shift,
+                               uint32_t bits, const uint64_t *cursors, HistLayout layout, uint32_t nseg_stride,
+                               const uint64_t *digit_base, hipStream_t s);
 
 // Stable scatter of every segment into `out` at the cursors of the scan.
 // digit_base (nullable) is added to the cursors: base[r * F + d].

@@ -938,6 +938,8 @@ __device__ __forceinline__ uint32_t load_tile_blk(const char *__restrict__ in,
     return vm;
 }
 
+// EXT 0: contiguous segment g of `in` -> `out` at the cursors cur_init (layout, stride,
+//        + digit_base), as scatter_segment (the keys-only shard partition).
 // EXT 1: contiguous segment g of `in` -> pooled output (po), digit side stream.
 // EXT 2: block-list segment g (list) -> `out` at the segment-major cursors cur_init.
 // T: the element written (tuple or key); IS: the input element size in bytes.
@@ -947,7 +949,9 @@ __device__ __forceinline__ void scatter_segment_ext(ScatterLds<BITS, ITEMS, NT, 
                                                     const SegMap &m, uint32_t shift,
                                                     const uint64_t *__restrict__ cur_init,
                                                     const uint64_t *__restrict__ list, const PoolOut &po,
-                                                    uint8_t *__restrict__ side, uint32_t shift2, uint32_t mask2) {
+                                                    uint8_t *__restrict__ side, uint32_t shift2, uint32_t mask2,
+                                                    HistLayout layout = kSegMajor, uint32_t nseg_stride = 0,
+                                                    const uint64_t *__restrict__ digit_base = nullptr) {
     using LdsT = ScatterLds<BITS, ITEMS, NT, EXT, T>;
     constexpr uint32_t TILE = NT * ITEMS, BPT = TILE / kBlk;
     constexpr uint32_t F = 1u << BITS, G = LdsT::G, GPB = LdsT::GPB, NG = NT / G, CS = G - 1;
@@ -962,7 +966,9 @@ __device__ __forceinline__ void scatter_segment_ext(ScatterLds<BITS, ITEMS, NT, 
     const uint32_t tid = threadIdx.x;
     PoolState ps{0u, 0u, EXT == 1 ? g * po.pool_blocks : 0u, po.binfo};
     if (tid < F) {
-        if constexpr (EXT == 2) pend = cur_init[(uint64_t)g * F + tid];
+        if constexpr (EXT != 1)
+            pend = cur_init[hist_index(layout, g, tid, F, nseg_stride)] +
+                   (digit_base ? digit_base[(uint64_t)r * F + tid] : 0);
         L.cnt[tid] = 0;
     }
     if (tid == 0) L.pool_next = 0;
@@ -1049,6 +1055,19 @@ __global__ __launch_bounds__(NT, (scatter_waves_per_simd<BITS, ITEMS, NT, 1, T>(
     __shared__ ScatterLds<BITS, ITEMS, NT, 1, T> L;
     scatter_segment_ext<BITS, ITEMS, NT, 1, T, IS>(L, xcd_contiguous(blockIdx.x, gridDim.x), in, out, m, shift,
                                                    nullptr, nullptr, po, side, shift2, mask2);
+}
+
+// The one-pass scatter with cursors (k_scatter) writing the key words of the tuples.
+template <int BITS, int ITEMS, int NT>
+__global__ __launch_bounds__(NT, (scatter_waves_per_simd<BITS, ITEMS, NT, 0, uint32_t>())) void k_scatter_keys(
+    const char *__restrict__ in, uint32_t *__restrict__ out, SegMap m, uint32_t shift,
+    const uint64_t *__restrict__ cursors, HistLayout layout, uint32_t nseg_stride,
+    const uint64_t *__restrict__ digit_base) {
+    __shared__ ScatterLds<BITS, ITEMS, NT, 0, uint32_t> L;
+    const PoolOut none{};
+    scatter_segment_ext<BITS, ITEMS, NT, 0, uint32_t, 8>(L, xcd_contiguous(blockIdx.x, gridDim.x), in, out, m, shift,
+                                                         cursors, nullptr, none, nullptr, 0, 0, layout, nseg_stride,
+                                                         digit_base);
 }
 
 template <int BITS, int ITEMS, int NT, typename T>
@@ -1142,6 +1161,33 @@ hipError_t launch_scatter_blk_t(const void *in, const uint64_t *list, void *out,
             return hipErrorInvalidValue;
     }
 #undef BLK_CASE
+    return hipGetLastError();
+}
+
+hipError_t launch_scatter_keys(const row_t *in, uint32_t *out, const SegMap &m, uint32_t grid, uint32_t shift,
+                               uint32_t bits, const uint64_t *cursors, HistLayout layout, uint32_t nseg_stride,
+                               const uint64_t *digit_base, hipStream_t s) {
+    if (grid == 0) return hipSuccess;
+    constexpr int ITEMS = items_of<uint32_t, 0>(), NT = kScatterThreads;
+    const char *ib = reinterpret_cast<const char *>(in);
+#define KEYS_CASE(B)                                                                                            \
+    case B:                                                                                                     \
+        hipLaunchKernelGGL((k_scatter_keys<B, ITEMS, NT>), dim3(grid), dim3(NT), 0, s, ib, out, m, shift, cursors, \
+                           layout, nseg_stride, digit_base);                                                    \
+        break;
+    switch (bits) {
+        KEYS_CASE(1)
+        KEYS_CASE(2)
+        KEYS_CASE(3)
+        KEYS_CASE(4)
+        KEYS_CASE(5)
+        KEYS_CASE(6)
+        KEYS_CASE(7)
+        KEYS_CASE(8)
+        default:
+            return hipErrorInvalidValue;
+    }
+#undef KEYS_CASE
     return hipGetLastError();
 }
 

@@ -143,6 +143,7 @@ class multi_stats(C.Structure):  # sgxamd/multi.h
         ("ms_local", C.c_double),
         ("ms_allreduce", C.c_double),
         ("local", rho_stats),
+        ("elem_bytes", C.c_uint32),
     ]
 
     def as_dict(self) -> dict:

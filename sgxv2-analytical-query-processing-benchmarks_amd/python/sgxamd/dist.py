@@ -252,7 +252,10 @@ def _sharded_cxx(R: torch.Tensor, S: torch.Tensor, group, algorithm: str, chunks
     st = res.stats
     ms = {"total": (time.perf_counter() - t0) * 1e3, "shard_partition_and_post_exchange": st["ms_exchange_post"],
           "exchange_wait_and_local_join": st["ms_local"], "all_reduce": st["ms_allreduce"],
-          "impl": "cxx-rccl (mi355_rho_join_sharded)"}
+          "impl": "cxx-rccl (mi355_rho_join_sharded), "
+                  + ("keys only: 4 B per tuple on xGMI (counting join)" if st.get("elem_bytes") == 4
+                     else "8-byte tuples on xGMI"),
+          "sent_bytes": st["sent_bytes"]}
     return ShardedJoinResult(res.matches, int(st["local_matches"]), int(st["recv_r_max"]), int(st["recv_s_max"]), ms,
                              st["local"])
 

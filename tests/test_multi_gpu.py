@@ -65,6 +65,26 @@ def test_zipf_and_sel(sgx, orc, gpu):
     assert multi(sgx, R, S, 4).matches == orc.rho_join(R, S, 4)[0]
 
 
+@pytest.mark.parametrize("g,n,kw", [(2, 1 << 23, {}), (4, 1 << 23, {}), (8, 1 << 21, {"radix_bits": 14, "passes": 2}),
+                                    (4, 1 << 20, {"radix_bits": 10, "passes": 2})])
+def test_keys_only_exchange(sgx, orc, gpu, g, n, kw):
+    """Counting joins whose local plan takes the pooled keys layout exchange 4-byte keys:
+    the default policy from the mean local sizes (2^23 over 2 / 4 ranks: 10 / 9 bits, two
+    passes) or a forced two-pass plan.  Exact counts, half the bytes of the tuple
+    exchange on the wire (SGXAMD_KEYS=0 in test_paths_gpu keeps tuples)."""
+    R, S = sgx.reference_relations(n, n)  # pk / fk: every rank receives R and S tuples
+    exp = orc.count_join_sort(R, S)
+    res = multi(sgx, R, S, g, **kw)
+    assert res.matches == exp
+    st = res.stats
+    assert st["elem_bytes"] == 4 and st["local"]["layout"] == 2
+    # every key of a rank except those it keeps goes out once, 4 bytes each
+    assert 4 * (2 * n) * (g - 1) // g * 0.9 < st["sent_bytes"] <= 4 * 2 * n
+    # RHT keeps the tuple exchange
+    rht = multi(sgx, R, S, g, algorithm="RHT", **kw)
+    assert rht.matches == exp and rht.stats["elem_bytes"] == 8
+
+
 @pytest.mark.parametrize("pieces", [1, 3, 7])
 def test_pieces(sgx, orc, gpu, pieces):
     R, S = sgx.reference_relations(100_000, 150_001, selectivity=50)
