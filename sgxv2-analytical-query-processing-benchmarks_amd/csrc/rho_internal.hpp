@@ -90,7 +90,10 @@ hipError_t launch_hist_side(const uint8_t *side, const SegMap &m, uint32_t grid,
 // instead of twice (histogram + scatter).
 constexpr uint32_t kBlkShift = 8;
 constexpr uint32_t kBlk = 1u << kBlkShift;          // elements per block (2 KiB of tuples, 1 KiB of keys)
-constexpr uint32_t kPass2Ents = 512;                // blocks per pass-2 segment (LDS list copy)
+#ifndef SGXAMD_PASS2_ENTS
+#define SGXAMD_PASS2_ENTS 256
+#endif
+constexpr uint32_t kPass2Ents = SGXAMD_PASS2_ENTS;  // blocks per pass-2 segment (LDS list copy)
 struct PoolOut {
     uint32_t *binfo;       // per pool block: digit | fill << 16
     uint64_t *cnt;         // [d][g] (stride nseg): blocks << 40 | tuples of digit d in segment g
