@@ -519,7 +519,8 @@ __device__ __forceinline__ void block_scan2(uint32_t a, uint32_t b, uint32_t (&w
 // Phases A-C of one tile: the tile ends up digit-sorted in L.tile (v is dead after).
 // tn: valid tuples of the tile (items tid + k * NT < tn); with block-list input (EXT 2)
 // a bit mask instead, bit k = item k valid.  ps: the owner thread's chain (EXT 1).
-template <int BITS, int ITEMS, int NT, int EXT = 0, typename T = uint64_t>
+// FULL: every item is valid (no per-item checks; callers take it for full tiles).
+template <int BITS, int ITEMS, int NT, int EXT = 0, typename T = uint64_t, bool FULL = false>
 __device__ __forceinline__ uint32_t scatter_tile_sort(ScatterLds<BITS, ITEMS, NT, EXT, T> &L, uint64_t &pend,
                                                       uint32_t &carried, const T (&v)[ITEMS],
                                                       T *__restrict__ out, uint32_t tn, uint32_t shift,
@@ -527,7 +528,7 @@ __device__ __forceinline__ uint32_t scatter_tile_sort(ScatterLds<BITS, ITEMS, NT
     constexpr uint32_t F = 1u << BITS, mask = F - 1, NW = NT / kWave;
     constexpr uint32_t G = ScatterLds<BITS, ITEMS, NT, EXT, T>::G, GPB = ScatterLds<BITS, ITEMS, NT, EXT, T>::GPB;
     const uint32_t tid = threadIdx.x;
-    const auto valid = [&](int k) { return EXT == 2 ? ((tn >> k) & 1u) != 0 : tid + k * NT < tn; };
+    const auto valid = [&](int k) { return FULL || (EXT == 2 ? ((tn >> k) & 1u) != 0 : tid + k * NT < tn); };
 #ifdef SGXAMD_ABLATE_NOSORT  // development ablation (tools/part_bench): the memory pipeline alone
 #pragma unroll
     for (int k = 0; k < ITEMS; ++k)
@@ -648,6 +649,10 @@ __device__ __forceinline__ void scatter_tile_write(ScatterLds<BITS, ITEMS, NT, E
             const bool v1 = (EXT == 1) || (a + 1 >= L.pend[d] && q + 1 < wd);
             if (v0 && v1) {
                 const uint32_t x0 = elem(d, q, cd, tbx), x1 = elem(d, q + 1, cd, tbx);
+#ifdef SGXAMD_ABLATE_NOSTORE  // development ablation: everything but the global stores
+                if ((x0 & x1) == ~0u) out[0] = x0;
+                continue;
+#endif
                 st_nt(reinterpret_cast<uint64_t *>(out + a), (uint64_t)x0 | ((uint64_t)x1 << 32));
                 if (SIDE)
                     *reinterpret_cast<uint16_t *>(side + a) =
@@ -915,27 +920,37 @@ hipError_t launch_scatter(const row_t *in, row_t *out, const SegMap &m, uint32_t
 // k * NT / kBlk + t / kBlk — uniform per wave, so each item loads through a buffer
 // resource over its block (lanes past the block's fill read 0 and are masked out).
 
-// Tile loads of a block-list segment (entries staged in LDS); returns the valid mask.
+// Tile loads of a block-list segment (entries staged in LDS); returns the valid mask
+// (bit k: item k of this lane) and, in bit 31, whether the whole tile is full.
 // in: the pass-1 output, IS-byte elements.
 template <typename T, int IS, int ITEMS, int NT, int BITS>
 __device__ __forceinline__ uint32_t load_tile_blk(const char *__restrict__ in,
                                                   const ScatterLds<BITS, ITEMS, NT, 2, T> &L, uint32_t nent,
                                                   uint32_t e0, T (&dst)[ITEMS]) {
     static_assert(NT % kBlk == 0, "a wave reads inside one block");
-    const uint32_t o = threadIdx.x & (kBlk - 1);
+    constexpr uint32_t BPT = ITEMS * (NT / kBlk);  // blocks per tile
+    static_assert(BPT <= kWave, "one list entry per lane");
+    const uint32_t o = threadIdx.x & (kBlk - 1), lane = __lane_id();
     const uint32_t h = __builtin_amdgcn_readfirstlane(threadIdx.x >> kBlkShift);
+    // the tile's list entries, one per lane (LDS broadcast-free, one read)
+    const uint64_t en = (lane < BPT && e0 + lane < nent) ? L.ents[e0 + lane] : 0ull;
+    const uint32_t en_lo = (uint32_t)en, en_hi = (uint32_t)(en >> 32);
+    // all blocks present and full: every item valid (the common case)
+    const bool full = __ballot(lane < BPT && en_hi != kBlk) == 0;
     uint32_t vm = 0;
 #pragma unroll
     for (int k = 0; k < ITEMS; ++k) {
-        const uint32_t j = e0 + (uint32_t)k * (NT / kBlk) + h;
-        const uint64_t en = j < nent ? L.ents[j] : 0ull;
-        const uint32_t phys = __builtin_amdgcn_readfirstlane((uint32_t)en);
-        const uint32_t fill = __builtin_amdgcn_readfirstlane((uint32_t)(en >> 32));
+        const uint32_t idx = (uint32_t)k * (NT / kBlk) + h;
+        const uint32_t phys = __builtin_amdgcn_readlane(en_lo, idx);
+        const uint32_t fill = __builtin_amdgcn_readlane(en_hi, idx);
         const __amdgpu_buffer_rsrc_t rs = make_rsrc(in + (uint64_t)phys * (kBlk * IS), fill * (uint32_t)IS);
         dst[k] = buf_ld_nt_t<T>(rs, o * (uint32_t)IS, 0u);
-        vm |= (o < fill ? 1u : 0u) << k;
+        if (!full) vm |= (o < fill ? 1u : 0u) << k;
     }
-    return vm;
+    // bit 31: the whole tile is full — workgroup-uniform (every wave sees the same
+    // entries), unlike the per-lane masks, so callers may branch on it around barriers
+    static_assert(ITEMS < 31, "bit 31 is the full-tile flag");
+    return full ? (0x80000000u | ((1u << ITEMS) - 1u)) : vm;
 }
 
 // EXT 0: contiguous segment g of `in` -> `out` at the cursors cur_init (layout, stride,
@@ -993,26 +1008,42 @@ __device__ __forceinline__ void scatter_segment_ext(ScatterLds<BITS, ITEMS, NT, 
         if constexpr (EXT == 2) return vm;
         return (uint32_t)min<uint64_t>(TILE, e - b - (uint64_t)ti * TILE);
     };
+    // full tiles (all but the segment's last in pass 1; tiles without a partial block in
+    // pass 2) sort without per-item validity checks.  The test must be uniform over the
+    // workgroup (the sort has barriers): tn itself with contiguous input, the loader's
+    // full-tile bit with block-list input (the per-lane masks differ).
+    const auto is_full = [&](uint32_t tn) -> bool {
+        if constexpr (EXT == 2) return (tn >> 31) != 0;
+        return tn == TILE;
+    };
+#ifndef SGXAMD_FULL_POOL
+#define SGXAMD_FULL_POOL 0  // pass 1: the second sort copy spills 3-5 VGPRs (measured 0.01 ms slower)
+#endif
+    const auto sort = [&](T(&v)[ITEMS], uint32_t tn) -> uint32_t {
+        if ((EXT != 1 || SGXAMD_FULL_POOL) && is_full(tn))
+            return scatter_tile_sort<BITS, ITEMS, NT, EXT, T, true>(L, pend, carried, v, out, tn, shift, 0, &ps);
+        return scatter_tile_sort<BITS, ITEMS, NT, EXT, T, false>(L, pend, carried, v, out, tn, shift, 0, &ps);
+    };
     // the two-tiles-in-flight pipeline of scatter_segment
     T va[ITEMS], vb[ITEMS];
     uint32_t ma = load(0, va);
     uint32_t mb = load(1, vb);
 #pragma unroll
     for (int k = 0; k < ITEMS; ++k) asm volatile("" ::"v"(va[k]));
-    uint32_t gt = scatter_tile_sort<BITS, ITEMS, NT, EXT, T>(L, pend, carried, va, out, tn_of(0, ma), shift, 0, &ps);
+    uint32_t gt = sort(va, tn_of(0, ma));
     for (uint32_t ti = 0;; ti += 2) {
         ma = load(ti + 2, va);
 #pragma unroll
         for (int k = 0; k < ITEMS; ++k) asm volatile("" ::"v"(vb[k]));
         scatter_tile_write<BITS, ITEMS, NT, SIDE, EXT, T>(L, out, gt, side, shift2, mask2);
         if (ti + 1 >= ntiles) break;
-        gt = scatter_tile_sort<BITS, ITEMS, NT, EXT, T>(L, pend, carried, vb, out, tn_of(ti + 1, mb), shift, 0, &ps);
+        gt = sort(vb, tn_of(ti + 1, mb));
         mb = load(ti + 3, vb);
 #pragma unroll
         for (int k = 0; k < ITEMS; ++k) asm volatile("" ::"v"(va[k]));
         scatter_tile_write<BITS, ITEMS, NT, SIDE, EXT, T>(L, out, gt, side, shift2, mask2);
         if (ti + 2 >= ntiles) break;
-        gt = scatter_tile_sort<BITS, ITEMS, NT, EXT, T>(L, pend, carried, va, out, tn_of(ti + 2, ma), shift, 0, &ps);
+        gt = sort(va, tn_of(ti + 2, ma));
     }
     // flush the carried (partial) granules; pooled: close every chain
     __syncthreads();
