@@ -54,6 +54,8 @@ inline bool big_join_enabled() {
 inline bool uses_big_table(const mi355_rho_opts *o) {
     return !(o && (o->materialize || o->algorithm == MI355_ALGO_RHT)) && big_join_enabled();
 }
+// The caller left the radix bits to the planner (an explicit plan keeps its tables).
+inline bool opts_free_bits(const mi355_rho_opts *o) { return !(o && o->radix_bits > 0); }
 
 Policy choose_policy(uint64_t nR, uint64_t nS, const mi355_rho_opts *o) {
     Policy p{};
@@ -97,7 +99,13 @@ Policy choose_policy(uint64_t nR, uint64_t nS, const mi355_rho_opts *o) {
         p.b1 = p.bits;
         p.b2 = 0;
     } else {
-        p.b1 = (p.bits + 1) / 2;
+        // odd bit counts: the larger digit in pass 1, or with SGXAMD_SPLIT=2 in pass 2
+        // (development A/B switch)
+        static const bool late = [] {
+            const char *e = std::getenv("SGXAMD_SPLIT");
+            return e && std::atoi(e) == 2;
+        }();
+        p.b1 = late ? p.bits / 2 : (p.bits + 1) / 2;
         p.b2 = p.bits - p.b1;
     }
     // chain table large enough that the average partition needs one R chunk
@@ -419,7 +427,13 @@ int plan_join(Context *ctx, hipStream_t s, uint64_t nR, uint64_t nS, const mi355
         RHO_HIP(ctx->sideS.ensure(std::max<uint64_t>(c1S, 16)));
     }
     const uint64_t P = 1ull << pol.bits;
-    if (uses_big_table(opts) && pol.rcap == 8192 && (nR + P - 1) / P > 8192) {
+    // the 16,384-key counting table with 32,768-key S chunks: partitions above 8192 R
+    // keys, and plans sized for those S chunks (S much larger than R, e.g. BASELINE config
+    // 4: 4096 R and 32,768 S keys per partition read R once per partition instead of once
+    // per 8192-key S chunk); enough partitions that one task each fills the chip
+    const uint64_t avgR = (nR + P - 1) / P, avgS = (nS + P - 1) / P;
+    if (uses_big_table(opts) && ((pol.rcap == 8192 && avgR > 8192) ||
+                                 (P >= 8192 && avgS > kSChunk && avgR <= kBigRcap && opts_free_bits(opts)))) {
         pj.pol.rcap = kBigRcap;
         pj.s_chunk = kBigSChunk;
     }
