@@ -414,6 +414,27 @@ def main():
     if args.workload == "c5":
         rho_info["load_report"] = load_report(results[-1], nS)
 
+    # the same join moving whole 8-byte tuples (the reference's data movement), measured
+    # beside the headline: the probe phase's HBM fraction on the tuple layout
+    if world == 1 and args.workload == "c2" and args.algorithm == "RHO" and ls.get("elem_bytes") == 4:
+        sgxamd.set_key_layout(False)
+        try:
+            res_t, pk_t, el_t = measure_rho("c2", R, S, gR, gS)
+        finally:
+            sgxamd.set_key_layout(True)
+        avg_t = {k: statistics.mean(v) for k, v in pk_t.items()}
+        ls_t = res_t[-1].local_stats
+        plan_t = (ls_t.get("passes") or 2, ls_t.get("pass2_bits") or 0, ls_t.get("elem_bytes") or 8)
+        pb_t = algorithmic_bytes("join_build_probe", nR, nS, *plan_t) / (avg_t["join_build_probe"] * 1e-3) / 1e9
+        rho_info["tuple_layout"] = {
+            "partition_layout": LAYOUTS.get(ls_t.get("layout"), "unknown"), "timed": "untimed for value; own K steps",
+            "ms_per_step": round(el_t / args.steps * 1e3, 4),
+            "M_probed_tuples_per_s": round(N_glob * args.steps / el_t / 1e6, 1),
+            "probe_roofline": {"achieved": round(pb_t, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                               "frac": round(pb_t / HBM_PEAK_GBS, 4)},
+            "kernel_ms_avg": {k: round(v, 4) for k, v in sorted(avg_t.items())},
+        }
+
     # the CPU baseline joins the relations the GPU joined (BASELINE config 2 at N = 1):
     # one device-to-host copy, outside every timed region
     cpu_rel = None

@@ -167,6 +167,14 @@ int mi355_timing_get(const char **names, double *ms, int cap);
  */
 void mi355_set_partition_overlap(int on);
 
+/*
+ * Partition layout of this thread's counting RHO joins (default 1): 1 moves the 4-byte
+ * key of every tuple after the input read (the build/probe of a count reads keys only),
+ * 0 moves whole 8-byte tuples as the reference does.  Counts are identical; the
+ * environment switch SGXAMD_KEYS=0 forces 0 for the whole process.
+ */
+void mi355_set_key_layout(int on);
+
 /* Stream used by calls that take no explicit stream (NULL = library stream). */
 void mi355_set_stream(void *stream);
 

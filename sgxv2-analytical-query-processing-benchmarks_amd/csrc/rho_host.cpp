@@ -148,7 +148,7 @@ inline bool keys_enabled() {
         const char *e = std::getenv("SGXAMD_KEYS");
         return !(e && std::atoi(e) == 0);
     }();
-    return on;
+    return on && thread_key_layout();
 }
 constexpr uint32_t kPoolSegs = 512;  // two 512-thread workgroups per CU: one wave of workgroups
 inline uint32_t pool_segs() {

@@ -17,6 +17,7 @@ thread_local bool t_timing = false;
 thread_local void *t_stream = nullptr;
 thread_local Timer t_timer;
 thread_local bool t_overlap = false;
+thread_local bool t_keys = true;
 std::mutex g_ctx_mu;
 std::map<int, std::unique_ptr<Context>> g_ctx;
 }  // namespace
@@ -117,6 +118,7 @@ hipStream_t side_stream(Context *ctx) {
 }
 bool thread_timing_enabled() { return t_timing; }
 bool thread_partition_overlap() { return t_overlap; }
+bool thread_key_layout() { return t_keys; }
 
 bool one_pass_selection() {
     static const bool on = [] {
@@ -206,6 +208,8 @@ int mi355_device_count(void) {
 void mi355_timing_enable(int on) { sgxamd::t_timing = on != 0; }
 
 void mi355_set_partition_overlap(int on) { sgxamd::t_overlap = on != 0; }
+
+void mi355_set_key_layout(int on) { sgxamd::t_keys = on != 0; }
 
 int mi355_timing_get(const char **names, double *ms, int cap) {
     const auto &rec = sgxamd::t_timer.records();

@@ -111,6 +111,8 @@ Timer &thread_side_timer();
 hipStream_t side_stream(Context *ctx);
 bool thread_timing_enabled();
 bool thread_partition_overlap();
+// Counting joins move keys only after the input read (mi355_set_key_layout, default on).
+bool thread_key_layout();
 // Index / value / dictionary scans in one pass with a decoupled look-back;
 // SGXAMD_SCAN_ONEPASS=0 selects their two-pass form (development A/B switch, read
 // once; results are identical).

@@ -212,6 +212,7 @@ SIGNATURES = {
     "mi355_rho_join_finish": (C.c_int, [_P, C.c_uint64, C.POINTER(rho_opts), C.POINTER(rho_stats)]),
     "mi355_timing_enable": (None, [C.c_int]),
     "mi355_set_partition_overlap": (None, [C.c_int]),
+    "mi355_set_key_layout": (None, [C.c_int]),
     "mi355_timing_get": (C.c_int, [C.POINTER(C.c_char_p), C.POINTER(C.c_double), C.c_int]),
     "mi355_set_stream": (None, [_P]),
     # multi.h
@@ -495,6 +496,12 @@ def timing_enable(on: bool = True) -> None:
 def set_partition_overlap(on: bool = True) -> None:
     """R/S partition chains on two streams (default) or back to back on one."""
     lib.mi355_set_partition_overlap(1 if on else 0)
+
+
+def set_key_layout(on: bool = True) -> None:
+    """Counting joins on this thread move 4-byte keys after the input read (default) or
+    whole 8-byte tuples (the reference's data movement); counts are identical."""
+    lib.mi355_set_key_layout(1 if on else 0)
 
 
 def timings() -> list[tuple[str, float]]:

@@ -126,6 +126,26 @@ def test_pooled_two_pass_layouts(sgx, orc, gpu, case):
         assert np.array_equal(sorted_triples(got), sorted_triples(orc.rho_join_triples(R, S, 4)))
 
 
+def test_key_layout_switch(sgx, orc, gpu):
+    """mi355_set_key_layout: counting joins move 4-byte keys (layout 2) or whole tuples
+    (layout 1) after the input read; the counts are identical, materialising joins keep
+    tuples either way."""
+    rng = np.random.default_rng(21)
+    R = rel(rng.integers(0, 1 << 21, 400_001).astype(np.uint32))
+    S = rel(rng.integers(0, 1 << 21, 300_007).astype(np.uint32))
+    exp = orc.count_join_sort(R, S)
+    try:
+        for on, layout in ((True, 2), (False, 1), (True, 2)):
+            sgx.set_key_layout(on)
+            res = gpu_join(sgx, R, S, radix_bits=14, passes=2)
+            assert res.matches == exp and res.stats["layout"] == layout
+            assert res.stats["elem_bytes"] == (4 if on else 8)
+    finally:
+        sgx.set_key_layout(True)
+    got = gpu_triples(sgx, R, S, radix_bits=14, passes=2)
+    assert len(got) == exp
+
+
 def test_extreme_keys(sgx, orc, gpu):
     # 0 and 0xFFFFFFFF (the LDS empty marker) must join like any other key
     keys = np.array([0, 0xFFFFFFFF, 0xFFFFFFFF, 1, 0x80000000, 0xFFFFFFFE] * 50, dtype=np.uint32)
