@@ -29,7 +29,7 @@ sys.path.insert(0, os.path.join(PKG, "python"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 METRIC = "M probed tuples/sec (RHO join) + scan GB/s vs HBM roofline, 1/2/4/8 MI355X"
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic_r02zb.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic_r02zk.json")
 
 
 def log(*a):
@@ -207,6 +207,8 @@ def main():
                     help="config 5's Zipf stream: host mt19937_64 seed 22222 staged to HBM (BASELINE.md row 5) "
                          "or the device generator")
     ap.add_argument("--no-tpch", action="store_true")
+    ap.add_argument("--no-tuple-layout", action="store_true",
+                    help="skip the whole-tuple comparison join (profiling passes: per-kernel PMC averages stay one layout)")
     ap.add_argument("--no-paper", action="store_true",
                     help="skip the runs at the shapes of the reference's own published numbers")
     ap.add_argument("--tpch-scale-milli", type=int, default=10000, help="TPC-H scale factor x 1000 (10000 = SF10)")
@@ -416,7 +418,8 @@ def main():
 
     # the same join moving whole 8-byte tuples (the reference's data movement), measured
     # beside the headline: the probe phase's HBM fraction on the tuple layout
-    if world == 1 and args.workload == "c2" and args.algorithm == "RHO" and ls.get("elem_bytes") == 4:
+    if (world == 1 and args.workload == "c2" and args.algorithm == "RHO" and ls.get("elem_bytes") == 4
+            and not args.no_tuple_layout):
         sgxamd.set_key_layout(False)
         try:
             res_t, pk_t, el_t = measure_rho("c2", R, S, gR, gS)

@@ -22,16 +22,16 @@ cat "$OUT/bench.json"
 
 [ -n "$SKIP_PROF" ] && exit 0
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -d "$OUT/kt" -o kt --output-format csv \
-  -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-tpch --no-paper --no-configs "$@" > "$OUT/kt.log" 2>&1 \
+  -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-tpch --no-paper --no-configs --no-tuple-layout "$@" > "$OUT/kt.log" 2>&1 \
   || { echo "kernel-trace failed"; tail -30 "$OUT/kt.log"; exit 1; }
 find "$OUT/kt" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats.csv" \;
 head -30 "$OUT/kernel_stats.csv"
 
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -T -d "$OUT/fetch" -o fetch --output-format csv \
-  -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-tpch --no-paper --no-configs "$@" > "$OUT/fetch.log" 2>&1 \
+  -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-tpch --no-paper --no-configs --no-tuple-layout "$@" > "$OUT/fetch.log" 2>&1 \
   || { echo "pmc FETCH_SIZE failed"; tail -30 "$OUT/fetch.log"; exit 1; }
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -T -d "$OUT/write" -o write --output-format csv \
-  -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-tpch --no-paper --no-configs "$@" > "$OUT/write.log" 2>&1 \
+  -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-tpch --no-paper --no-configs --no-tuple-layout "$@" > "$OUT/write.log" 2>&1 \
   || { echo "pmc WRITE_SIZE failed"; tail -30 "$OUT/write.log"; exit 1; }
 find "$OUT/fetch" "$OUT/write" -name "*counter_collection.csv" | head
 echo done
