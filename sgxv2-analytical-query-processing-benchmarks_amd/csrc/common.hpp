@@ -52,6 +52,15 @@ __device__ __forceinline__ uint4 buf_ld_nt_u128(__amdgpu_buffer_rsrc_t r, uint32
 __device__ __forceinline__ void st_nt(uint64_t *p, uint64_t v) { __builtin_nontemporal_store(v, p); }
 __device__ __forceinline__ void st_nt(uint32_t *p, uint32_t v) { __builtin_nontemporal_store(v, p); }
 
+// c ? a : b as one v_cndmask_b32 (the compiler otherwise turns a select between two
+// LDS addresses into exec-masked branches); the condition is the wave's lane mask
+__device__ __forceinline__ uint32_t vsel(bool c, uint32_t a, uint32_t b) {
+    const uint64_t m = __builtin_amdgcn_ballot_w64(c);
+    uint32_t r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(a), "s"(m));
+    return r;
+}
+
 __device__ __forceinline__ uint64_t lanemask_lt() {
     const uint32_t lane = __lane_id();
     return lane == 0 ? 0ull : (~0ull >> (64 - lane));

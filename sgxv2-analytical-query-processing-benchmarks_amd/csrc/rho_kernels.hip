@@ -412,6 +412,16 @@ hipError_t launch_scan_regions(uint64_t *hist, const uint32_t *seg_base, const u
 // register sets).  The last carries of the segment are flushed at the end.
 constexpr uint32_t kGran = 16;  // tuples per output granule = one 128-B line
 
+// c ? *a : *b for two LDS elements with one read: the LDS address is selected, not the
+// loaded value (a select between two loads becomes exec-masked branches, each with its
+// own read and wait)
+template <typename T>
+__device__ __forceinline__ T lds_pick(bool c, const T *a, const T *b) {
+    typedef __attribute__((address_space(3))) const T lds_t;
+    const uint32_t pa = (uint32_t)(uintptr_t)(lds_t *)a, pb = (uint32_t)(uintptr_t)(lds_t *)b;
+    return *(lds_t *)(uintptr_t)vsel(c, pa, pb);
+}
+
 // EXT: 0 = cursor output, contiguous input; 1 = pooled output (PoolOut); 2 = block-list
 // input (the segment's list entries staged in ents).
 // T: the element moved (uint64_t tuple, or uint32_t key of a count-only join).
@@ -625,45 +635,65 @@ __device__ __forceinline__ void scatter_tile_write(ScatterLds<BITS, ITEMS, NT, E
         // one 2-byte side store), half the rounds and metadata reads of one key per lane
         constexpr uint32_t NG2 = NT / 16;
         const uint32_t l2 = 2 * (tid & 15), grp2 = tid / 16;
+        // element q of d's run: its carries, then the tile's
         const auto elem = [&](uint32_t d, uint32_t q, uint32_t cd, uint32_t tbx) -> uint32_t {
-            return q < cd ? (uint32_t)L.carry[d * CS + q] : (uint32_t)L.tile[tbx + q - cd];
+            return (uint32_t)lds_pick(q < cd, &L.carry[d * CS + q], &L.tile[tbx + q - cd]);
         };
-        for (uint32_t j = grp2; j < gtot; j += NG2) {
+        // one granule's write: destination, its two keys, which of them are written
+        struct GranW {
+            uint64_t a;
+            uint32_t x0, x1;
+            bool v0, v1;
+        };
+        const auto gran = [&](uint32_t j) -> GranW {
             const uint32_t d = L.desc[j];
             const uint2 m = L.meta[d];
             const uint32_t jj = j - L.gbase[d], cd = m.y & 0xFFu, tbx = m.x & TB;
-            uint64_t a;
-            uint32_t q, wd = ~0u;
+            GranW w;
+            uint32_t q;
             if constexpr (EXT == 1) {
-                const uint2 ga = L.gaddr[d];
+                // every granule whole; both block addresses in one 64-bit LDS read
+                const uint64_t gv = *reinterpret_cast<const uint64_t *>(&L.gaddr[d]);
                 const uint32_t g0 = m.x >> 16;
-                a = (uint64_t)(jj < g0 ? ga.x + jj : ga.y + (jj - g0)) * G + l2;
+                const uint32_t gb = jj < g0 ? (uint32_t)gv + jj : (uint32_t)(gv >> 32) + (jj - g0);
+                w.a = (uint64_t)gb * G + l2;
                 q = jj * G + l2;
+                w.v0 = w.v1 = true;
             } else {
                 const uint64_t pd = L.pend[d];
-                wd = m.y >> 16;
-                a = (pd / G + jj) * G + l2;
-                q = (uint32_t)(a - pd);  // wraps when a < pd
+                const uint32_t wd = m.y >> 16;
+                w.a = (pd / G + jj) * G + l2;
+                q = (uint32_t)(w.a - pd);  // wraps when a < pd
+                w.v0 = w.a >= pd && q < wd;
+                w.v1 = w.a + 1 >= pd && q + 1 < wd;
             }
-            const bool v0 = (EXT == 1) || (a >= L.pend[d] && q < wd);
-            const bool v1 = (EXT == 1) || (a + 1 >= L.pend[d] && q + 1 < wd);
-            if (v0 && v1) {
-                const uint32_t x0 = elem(d, q, cd, tbx), x1 = elem(d, q + 1, cd, tbx);
-#ifdef SGXAMD_ABLATE_NOSTORE  // development ablation: everything but the global stores
-                if ((x0 & x1) == ~0u) out[0] = x0;
-                continue;
-#endif
-                st_nt(reinterpret_cast<uint64_t *>(out + a), (uint64_t)x0 | ((uint64_t)x1 << 32));
+            // reads of keys not written stay inside the digit's run (q = 0)
+            w.x0 = elem(d, w.v0 ? q : 0u, cd, tbx);
+            w.x1 = elem(d, w.v1 ? q + 1 : 0u, cd, tbx);
+            return w;
+        };
+        const auto put = [&](const GranW &w) {
+            if (w.v0 && w.v1) {
+                st_nt(reinterpret_cast<uint64_t *>(out + w.a), (uint64_t)w.x0 | ((uint64_t)w.x1 << 32));
                 if (SIDE)
-                    *reinterpret_cast<uint16_t *>(side + a) =
-                        (uint16_t)(((x0 >> shift2) & mask2) | (((x1 >> shift2) & mask2) << 8));
-            } else if (v0 || v1) {
-                const uint32_t o = v0 ? 0u : 1u;
-                const uint32_t x = elem(d, q + o, cd, tbx);
-                st_nt(reinterpret_cast<uint32_t *>(out + a + o), x);
-                if (SIDE) side[a + o] = (uint8_t)((x >> shift2) & mask2);
+                    *reinterpret_cast<uint16_t *>(side + w.a) =
+                        (uint16_t)(((w.x0 >> shift2) & mask2) | (((w.x1 >> shift2) & mask2) << 8));
+            } else if (w.v0 || w.v1) {
+                const uint32_t o = w.v0 ? 0u : 1u, x = w.v0 ? w.x0 : w.x1;
+                st_nt(reinterpret_cast<uint32_t *>(out + w.a + o), x);
+                if (SIDE) side[w.a + o] = (uint8_t)((x >> shift2) & mask2);
             }
-        }
+        };
+        // pooled pass 1: two granules per group and round, so that their LDS read
+        // chains overlap (measured 1 % faster there, 0.5 % slower in the cursor pass 2)
+        uint32_t j = grp2;
+        if constexpr (EXT == 1)
+            for (; j + NG2 < gtot; j += 2 * NG2) {
+                const GranW w0 = gran(j), w1 = gran(j + NG2);
+                put(w0);
+                put(w1);
+            }
+        for (; j < gtot; j += NG2) put(gran(j));
     } else if constexpr (EXT == 1) {
         // pooled: every granule is whole (the digit's writes start granule-aligned); the
         // first g0 of d go to its current block, the rest to its fresh blocks
@@ -675,7 +705,7 @@ __device__ __forceinline__ void scatter_tile_write(ScatterLds<BITS, ITEMS, NT, E
             const uint32_t gran = jj < g0 ? ga.x + jj : ga.y + (jj - g0);
             const uint64_t a = (uint64_t)gran * G + lane;
             const uint32_t q = jj * G + lane;
-            const T x = q < cd ? L.carry[d * CS + q] : L.tile[(m.x & TB) + q - cd];
+            const T x = lds_pick(q < cd, &L.carry[d * CS + q], &L.tile[(m.x & TB) + q - cd]);
             st_nt(out + a, x);
             if (SIDE) side[a] = (uint8_t)(((uint32_t)x >> shift2) & mask2);
         }
@@ -690,7 +720,7 @@ __device__ __forceinline__ void scatter_tile_write(ScatterLds<BITS, ITEMS, NT, E
         const bool valid = a >= pd && q < wd;
         T x = 0;
         if (valid) {
-            x = q < cd ? L.carry[d * CS + q] : L.tile[m.x + q - cd];
+            x = lds_pick(q < cd, &L.carry[d * CS + q], &L.tile[m.x + q - cd]);
 #ifdef SGXAMD_ABLATE_NOSTORE  // development ablation: everything but the global stores
             if (x == (T)~0ull) out[0] = x;
 #elif defined(SGXAMD_PLAIN_STORE)
