@@ -168,7 +168,7 @@ def algorithmic_bytes(kernel: str, nR: int, nS: int, passes: int = 2, pass2_bits
     Two-pass plans: the pass-1 scatter also writes one pass-2 digit byte per tuple (the
     digit side stream) and the pass-2 histogram reads those bytes, not the tuples.
     elem: bytes per partitioned element after the input read — 8 (row_t tuples) or 4
-    (counting RHO joins move keys only: the pass-1 scatter reads 8-byte tuples and
+    (counting joins move keys only: the pass-1 scatter reads 8-byte tuples and
     writes 4-byte keys, pass 2 and the build/probe read and write keys)."""
     n = nR if kernel.startswith("R_") else nS
     side = passes == 2 and pass2_bits <= 8 and os.environ.get("SGXAMD_DIGIT_SIDE", "1") != "0"  # uses_digit_side()

@@ -79,7 +79,7 @@ typedef struct mi355_rho_stats {
     double ms_build;          /* "Build": ms_join split by the build/probe wall-clock ticks the */
     double ms_probe;          /* "Join":   fused build+probe kernel measures per workgroup */
     /* partition layout: 0 = tuples, pass-1 histogram + cursors; 1 = pooled pass 1 (no
-     * pass-1 histogram), tuples; 2 = pooled pass 1, 4-byte keys (counting RHO joins) */
+     * pass-1 histogram), tuples; 2 = pooled pass 1, 4-byte keys (counting joins, RHO and RHT) */
     uint32_t layout;
     uint32_t elem_bytes;      /* bytes per partitioned element after the input read (8 or 4) */
 } mi355_rho_stats;
@@ -168,7 +168,7 @@ int mi355_timing_get(const char **names, double *ms, int cap);
 void mi355_set_partition_overlap(int on);
 
 /*
- * Partition layout of this thread's counting RHO joins (default 1): 1 moves the 4-byte
+ * Partition layout of this thread's counting joins (RHO and RHT) (default 1): 1 moves the 4-byte
  * key of every tuple after the input read (the build/probe of a count reads keys only),
  * 0 moves whole 8-byte tuples as the reference does.  Counts are identical; the
  * environment switch SGXAMD_KEYS=0 forces 0 for the whole process.

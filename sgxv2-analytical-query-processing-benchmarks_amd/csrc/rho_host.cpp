@@ -409,9 +409,10 @@ int plan_join(Context *ctx, hipStream_t s, uint64_t nR, uint64_t nS, const mi355
     Arena &A = ctx->scratch;
     A.reset();
     // both relations take the same layout (the build/probe reads both alike)
-    const bool counting_rho = !pj.materialize && pj.algo == kAlgoChaining;
+    // counting joins (RHO and RHT) move 4-byte keys after the input read
+    const bool counting = !pj.materialize;
     const int pool = !(pool_fits(nR, pol) && pool_fits(nS, pol)) ? kNoPool
-                     : (counting_rho && keys_enabled())          ? kPoolKeys
+                     : (counting && keys_enabled())              ? kPoolKeys
                                                                   : kPoolTuples;
     plan_relation(A, pj.pr, nR, pol, pool);
     plan_relation(A, pj.ps, nS, pol, pool);
@@ -753,7 +754,7 @@ int join_pipelined_finish(Context *ctx, const void *dS, uint64_t nS, mi355_rho_s
 }
 
 bool keys_exchange_plan(uint64_t nR, uint64_t nS, uint64_t cap_r, uint64_t cap_s, mi355_rho_opts *lo) {
-    if (!keys_enabled() || lo->materialize || lo->algorithm == MI355_ALGO_RHT) return false;
+    if (!keys_enabled() || lo->materialize) return false;
     if (lo->radix_bits <= 0) {  // fix the local policy now: the received sizes are not known yet
         const Policy p = choose_policy(nR, nS, lo);
         lo->radix_bits = (int)p.bits;

@@ -1801,7 +1801,15 @@ struct HistJoinLds {
     uint64_t red[kWaves + 2];
 };
 
-template <int RCAP, int MODE>
+// Element i of a partitioned relation: an 8-byte tuple (KS 2) or a 4-byte key (KS 1,
+// counting joins over key partitions; the payload half reads as 0).
+template <int KS>
+__device__ __forceinline__ uint64_t ld_elem_nt(const uint64_t *base, uint64_t i) {
+    if constexpr (KS == 2) return ld_nt(base + i);
+    else return __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(base) + i);
+}
+
+template <int RCAP, int MODE, int KS = 2>
 __global__ __launch_bounds__(kBlock) void k_join_hist(const uint64_t *__restrict__ R, const uint64_t *__restrict__ S,
                                                       const uint64_t *__restrict__ r_start,
                                                       const uint64_t *__restrict__ r_count,
@@ -1814,6 +1822,7 @@ __global__ __launch_bounds__(kBlock) void k_join_hist(const uint64_t *__restrict
                                                       output_triple_t *__restrict__ out, uint64_t *__restrict__ cyc,
                                                       uint64_t *__restrict__ red_result,
                                                       uint64_t *__restrict__ red_ticket) {
+    static_assert(KS == 2 || MODE == kJoinCount, "key partitions carry no payloads");
     constexpr int U = RCAP / kBlock;
     constexpr int NB = HistJoinLds<RCAP, MODE>::NB;
     __shared__ HistJoinLds<RCAP, MODE> L;
@@ -1833,8 +1842,7 @@ __global__ __launch_bounds__(kBlock) void k_join_hist(const uint64_t *__restrict
             if (tid == 0) L.cursor = 0;
         }
         if (nS > 0) {
-            const uint64_t *rp = R + r_start[p];
-            const uint64_t *sp = S + s_start[p] + s_lo;
+            const uint64_t r0 = r_start[p], sb = s_start[p] + s_lo;
             for (uint64_t rc = 0; rc < nR; rc += RCAP) {
                 const uint64_t c_build = wall_clock64();
                 const uint32_t nrc = (uint32_t)((nR - rc) < RCAP ? (nR - rc) : RCAP);
@@ -1847,7 +1855,7 @@ __global__ __launch_bounds__(kBlock) void k_join_hist(const uint64_t *__restrict
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     const uint32_t i = tid + u * kBlock;
-                    kr[u] = i < nrc ? ld_nt(rp + rc + i) : 0ull;
+                    kr[u] = i < nrc ? ld_elem_nt<KS>(R, r0 + rc + i) : 0ull;
                 }
                 for (uint32_t i = tid; i <= nh; i += kBlock) L.off[i] = 0;
                 __syncthreads();
@@ -1895,7 +1903,7 @@ __global__ __launch_bounds__(kBlock) void k_join_hist(const uint64_t *__restrict
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
                         const uint64_t i = s0 + tid + u * kBlock;
-                        const uint64_t x = i < nS ? ld_nt(sp + i) : 0ull;
+                        const uint64_t x = i < nS ? ld_elem_nt<KS>(S, sb + i) : 0ull;
                         ks[u] = (uint32_t)x;
                         if constexpr (MODE == kJoinWrite) sv[u] = (uint32_t)(x >> 32);
                     }
@@ -1984,11 +1992,29 @@ hipError_t launch_join_keys(const void *R, const void *S, const uint64_t *r_star
                             const uint32_t *n_over, uint32_t hash_shift, uint32_t rcap, uint64_t s_chunk,
                             uint32_t grid, int mode, int algo, uint64_t *counts, uint64_t *cyc, hipStream_t s,
                             const JoinReduce *reduce) {
-    if (mode != kJoinCount || algo != kAlgoChaining) return hipErrorInvalidValue;
+    if (mode != kJoinCount) return hipErrorInvalidValue;
     const uint64_t *R64 = static_cast<const uint64_t *>(R);
     const uint64_t *S64 = static_cast<const uint64_t *>(S);
     uint64_t *rres = reduce ? reduce->result : nullptr;
     uint64_t *rtick = reduce ? reduce->ticket : nullptr;
+    if (algo == kAlgoHistogram) {
+#define HIST_KEYS_CASE(RC)                                                                                   \
+    case RC:                                                                                                 \
+        hipLaunchKernelGGL((k_join_hist<RC, kJoinCount, 1>), dim3(grid), dim3(kBlock), 0, s, R64, S64,      \
+                           r_start, r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts, \
+                           nullptr, nullptr, cyc, rres, rtick);                                              \
+        break;
+        switch (rcap) {
+            HIST_KEYS_CASE(2048)
+            HIST_KEYS_CASE(4096)
+            HIST_KEYS_CASE(8192)
+            default:
+                return hipErrorInvalidValue;
+        }
+#undef HIST_KEYS_CASE
+        return hipGetLastError();
+    }
+    if (algo != kAlgoChaining) return hipErrorInvalidValue;
     if (rcap == kBigRcap) {
         static const int tag_block = [] {
             const char *e = std::getenv("SGXAMD_TAG_JOIN");

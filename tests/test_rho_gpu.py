@@ -121,15 +121,18 @@ def test_pooled_two_pass_layouts(sgx, orc, gpu, case):
     for bits in (10, 14, 17):
         res = gpu_join(sgx, R, S, radix_bits=bits, passes=2)
         assert res.matches == exp, (case, bits, res.matches, exp)
+        # RHT counts over the same key partitions (histogram build/probe with KS = 1)
+        rht = gpu_join(sgx, R, S, radix_bits=bits, passes=2, algorithm="RHT")
+        assert rht.matches == exp and rht.stats["layout"] == 2, (case, bits, rht.matches, exp)
     if case != "dense_dups":
         got = gpu_triples(sgx, R, S, radix_bits=14, passes=2)
         assert np.array_equal(sorted_triples(got), sorted_triples(orc.rho_join_triples(R, S, 4)))
 
 
 def test_key_layout_switch(sgx, orc, gpu):
-    """mi355_set_key_layout: counting joins move 4-byte keys (layout 2) or whole tuples
-    (layout 1) after the input read; the counts are identical, materialising joins keep
-    tuples either way."""
+    """mi355_set_key_layout: counting joins (RHO and RHT) move 4-byte keys (layout 2) or
+    whole tuples (layout 1) after the input read; the counts are identical, materialising
+    joins keep tuples either way."""
     rng = np.random.default_rng(21)
     R = rel(rng.integers(0, 1 << 21, 400_001).astype(np.uint32))
     S = rel(rng.integers(0, 1 << 21, 300_007).astype(np.uint32))
@@ -137,9 +140,10 @@ def test_key_layout_switch(sgx, orc, gpu):
     try:
         for on, layout in ((True, 2), (False, 1), (True, 2)):
             sgx.set_key_layout(on)
-            res = gpu_join(sgx, R, S, radix_bits=14, passes=2)
-            assert res.matches == exp and res.stats["layout"] == layout
-            assert res.stats["elem_bytes"] == (4 if on else 8)
+            for alg in ("RHO", "RHT"):
+                res = gpu_join(sgx, R, S, radix_bits=14, passes=2, algorithm=alg)
+                assert res.matches == exp and res.stats["layout"] == layout, alg
+                assert res.stats["elem_bytes"] == (4 if on else 8)
     finally:
         sgx.set_key_layout(True)
     got = gpu_triples(sgx, R, S, radix_bits=14, passes=2)
