@@ -73,7 +73,10 @@ Policy choose_policy(uint64_t nR, uint64_t nS, const mi355_rho_opts *o) {
         // partition would exceed two tables.
         // Counting joins with the 16,384-tuple table size partitions for that table
         // once there are enough of them to fill the chip (>= 2^13 tasks): fewer digits
-        // per partition pass, one task per partition.
+        // per partition pass; S-driven bits aim at two 32,768-key chunks per partition
+        // (BASELINE config 4, 2^27 x 2^30: 14 bits = 7 + 7, R's table built twice per
+        // partition, 7.71-7.94 ms per join vs 8.04-8.28 at 15 bits = 8 + 7 with one chunk:
+        // an 8-bit pass over 2^30 keys costs more than R's second build).
         // scripts/size_sweep.py, DESIGN.md §3 (|R| = |S|, ms): 2^28: 14 / 15 / 16 bits
         // 5.53 / 5.58 / 5.71; 2^30: 16 / 17 / 18 bits 23.2 / 30.4 / 41.3; 2^31: 16 / 17
         // / 18 bits 47.2 / 60.7 / 83.5.
@@ -87,7 +90,7 @@ Policy choose_policy(uint64_t nR, uint64_t nS, const mi355_rho_opts *o) {
         uint32_t bits_s = std::min<uint32_t>(clog2(nS, kSChunk), 16);
         if (big && clog2(nR, kBigRcap) >= 13) {
             bits_r = std::min(clog2(nR, kBigRcap), cap_r);
-            bits_s = std::min<uint32_t>(clog2(nS, kBigSChunk), 16);
+            bits_s = std::min<uint32_t>(clog2(nS, 2 * kBigSChunk), 16);
         }
         p.bits = std::min(std::max(bits_r, bits_s), kMaxBits);
     }

@@ -239,9 +239,10 @@ def test_full_size_config2_property(sgx, gpu):
 def test_config4_full_size(sgx, gpu):
     """BASELINE config 4 at its size on one GPU: pk(2^27, seed 11111) join fk(2^30,
     maxid 2^27, seed 22222) = 8 shuffled copies of 1..2^27 (native.cpp:62-101 shapes,
-    device generators).  matches == |S|; the planner sizes partitions for S
-    (ceil(log2(2^30 / 32,768)) = 15 bits, 8 + 7): every R partition then holds exactly
-    2^27 / 2^15 = 4096 keys and every S partition its 8 copies, 32,768 tuples."""
+    device generators).  matches == |S|; the planner sizes partitions for two 32,768-key
+    S chunks (ceil(log2(2^30 / 65,536)) = 14 bits, 7 + 7): every R partition then holds
+    exactly 2^27 / 2^14 = 8192 keys and every S partition its 8 copies, 65,536 tuples,
+    probed in two tasks."""
     import torch
 
     nR, nS = 1 << 27, 1 << 30
@@ -252,9 +253,9 @@ def test_config4_full_size(sgx, gpu):
     res = sgx.rho_join(R, nR, S, nS)
     assert res.matches == nS
     st = res.stats
-    assert (st["radix_bits"], st["passes"], st["num_partitions"]) == (15, 2, 1 << 15)
-    assert st["max_part_r"] == 4096 and st["max_part_s"] == 32768
-    assert (1 << 15) <= st["num_tasks"] <= (1 << 17)  # whole S chunks per partition
+    assert (st["radix_bits"], st["passes"], st["num_partitions"]) == (14, 2, 1 << 14)
+    assert st["max_part_r"] == 8192 and st["max_part_s"] == 65536
+    assert st["num_tasks"] == 1 << 15  # two 32,768-key S chunks per partition
     del R, S
     torch.cuda.empty_cache()
 
