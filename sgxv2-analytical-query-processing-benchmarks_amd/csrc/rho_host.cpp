@@ -73,10 +73,11 @@ Policy choose_policy(uint64_t nR, uint64_t nS, const mi355_rho_opts *o) {
         // partition would exceed two tables.
         // Counting joins with the 16,384-tuple table size partitions for that table
         // once there are enough of them to fill the chip (>= 2^13 tasks): fewer digits
-        // per partition pass; S-driven bits aim at two 32,768-key chunks per partition
-        // (BASELINE config 4, 2^27 x 2^30: 14 bits = 7 + 7, R's table built twice per
-        // partition, 7.71-7.94 ms per join vs 8.04-8.28 at 15 bits = 8 + 7 with one chunk:
-        // an 8-bit pass over 2^30 keys costs more than R's second build).
+        // per partition pass; S-driven bits aim at 65,536 S keys per partition
+        // (BASELINE config 4, 2^27 x 2^30: 14 bits = 7 + 7, 7.71-7.94 ms per join even
+        // with R's table built twice per partition, vs 8.04-8.28 at 15 bits = 8 + 7 with
+        // 32,768 per partition: an 8-bit pass over 2^30 keys costs more than that build;
+        // 13 bits = 7 + 6, 131,072 per partition: 7.77-7.79).
         // scripts/size_sweep.py, DESIGN.md §3 (|R| = |S|, ms): 2^28: 14 / 15 / 16 bits
         // 5.53 / 5.58 / 5.71; 2^30: 16 / 17 / 18 bits 23.2 / 30.4 / 41.3; 2^31: 16 / 17
         // / 18 bits 47.2 / 60.7 / 83.5.
@@ -90,7 +91,7 @@ Policy choose_policy(uint64_t nR, uint64_t nS, const mi355_rho_opts *o) {
         uint32_t bits_s = std::min<uint32_t>(clog2(nS, kSChunk), 16);
         if (big && clog2(nR, kBigRcap) >= 13) {
             bits_r = std::min(clog2(nR, kBigRcap), cap_r);
-            bits_s = std::min<uint32_t>(clog2(nS, 2 * kBigSChunk), 16);
+            bits_s = std::min<uint32_t>(clog2(nS, kBigSPart), 16);
         }
         p.bits = std::min(std::max(bits_r, bits_s), kMaxBits);
     }
@@ -439,7 +440,11 @@ int plan_join(Context *ctx, hipStream_t s, uint64_t nR, uint64_t nS, const mi355
     if (uses_big_table(opts) && ((pol.rcap == 8192 && avgR > 8192) ||
                                  (P >= 8192 && avgS > kSChunk && avgR <= kBigRcap && opts_free_bits(opts)))) {
         pj.pol.rcap = kBigRcap;
-        pj.s_chunk = kBigSChunk;
+        // S-heavy plans (BASELINE config 4: 65,536 S keys per partition) probe a
+        // partition in one task: 7.24-7.35 vs 7.46-7.52 ms per join with two 32,768-key
+        // tasks that build the R table twice; at 16,384 S keys per partition (configs 2
+        // and 5) the 32,768-key chunks split hot partitions finer (Zipf: 0.544 vs 0.56 ms)
+        pj.s_chunk = avgS >= kBigSPart ? kBigSPart : kBigSChunk;
     }
     pj.over_cap = (uint32_t)(nS / pj.s_chunk + 1);
     // one workgroup per task up to 2048 (few partitions with a large S — a tiny build

@@ -153,6 +153,9 @@ constexpr uint64_t kSChunk = 8192;
 constexpr uint32_t kBigRcap = 16384;
 constexpr int kBigJoinBlock = 1024;
 constexpr uint64_t kBigSChunk = 32768;
+// S tuples per partition the planner aims at with the big table; partitions that large
+// on average are probed in chunks of this size (one task per partition when uniform)
+constexpr uint64_t kBigSPart = 65536;
 enum JoinMode : int { kJoinCount = 0, kJoinTaskCount = 1, kJoinWrite = 2 };
 // Build/probe algorithm of one task: RHO's bucket chaining or RHT's histogram join.
 enum JoinAlgo : int { kAlgoChaining = 0, kAlgoHistogram = 1 };

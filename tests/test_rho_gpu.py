@@ -242,7 +242,7 @@ def test_config4_full_size(sgx, gpu):
     device generators).  matches == |S|; the planner sizes partitions for two 32,768-key
     S chunks (ceil(log2(2^30 / 65,536)) = 14 bits, 7 + 7): every R partition then holds
     exactly 2^27 / 2^14 = 8192 keys and every S partition its 8 copies, 65,536 tuples,
-    probed in two tasks."""
+    probed in one task."""
     import torch
 
     nR, nS = 1 << 27, 1 << 30
@@ -255,7 +255,7 @@ def test_config4_full_size(sgx, gpu):
     st = res.stats
     assert (st["radix_bits"], st["passes"], st["num_partitions"]) == (14, 2, 1 << 14)
     assert st["max_part_r"] == 8192 and st["max_part_s"] == 65536
-    assert st["num_tasks"] == 1 << 15  # two 32,768-key S chunks per partition
+    assert st["num_tasks"] == 1 << 14  # one 65,536-key S chunk per partition
     del R, S
     torch.cuda.empty_cache()
 
