@@ -1322,6 +1322,60 @@ hipError_t launch_block_list(const PoolOut &po, const uint64_t *lbase, uint64_t 
     return hipGetLastError();
 }
 
+// Pass-2 histogram of up to 128 digits with one private counter row per lane: the two
+// u16 counts of digits 2p and 2p+1 for lane l sit in word p * 64 + l, so the lanes of
+// an atomic hit distinct words in distinct banks (4-byte LDS atomics bank on (a/4) mod 32
+// per 32-lane group); lane l of the four waves shares a row.  A row counts at most
+// 4 waves x 16 keys per block x (segment blocks / 16) per lane (1024 at kPass2Ents = 256,
+// 8192 at 2048), inside a u16.  A shared 128-bin histogram spent 70 % of its LDS cycles
+// in bank conflicts (SQ counters, r02t); the private rows take 5-10 % off the kernel
+// (0.096 -> 0.087 ms per 2^28 keys), which is bound by its two dependent loads (list
+// entry, then the digit bytes) more than by the LDS.
+constexpr uint32_t kLaneHistF = 128;
+__device__ __forceinline__ void hist_side_lanes(const uint8_t *__restrict__ side, const uint64_t *__restrict__ list,
+                                                uint64_t b, uint64_t e, uint32_t F, uint64_t *__restrict__ out) {
+    static_assert(kPass2Ents <= 4096, "u16 lane counters");
+    constexpr uint32_t W = kLaneHistF / 2 * kWave;
+    __shared__ uint32_t hp[W];
+    const uint32_t tid = threadIdx.x, lane = __lane_id();
+    for (uint32_t i = tid; i < W; i += kBlock) hp[i] = 0;
+    __syncthreads();
+    const uint32_t grp = tid / 16, l = tid % 16;
+    constexpr int U = 4;  // blocks in flight per 16-lane group (8: same, 16: 20 % slower)
+    for (uint64_t i0 = b; i0 < e; i0 += 16 * U) {
+        uint4 q[U];
+        uint32_t nv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = i0 + grp + 16 * u;
+            nv[u] = 0;
+            q[u] = make_uint4(0, 0, 0, 0);
+            if (i < e) {
+                const uint64_t en = list[i];
+                const uint32_t fill = (uint32_t)(en >> 32), lo = l * 16;
+                nv[u] = fill > lo ? min(16u, fill - lo) : 0u;
+                if (nv[u]) q[u] = ld_nt(reinterpret_cast<const uint4 *>(side + (uint64_t)(uint32_t)en * kBlk) + l);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t w[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const uint32_t d = __builtin_amdgcn_ubfe(w[j >> 2], (j & 3) * 8, 8);
+                if ((uint32_t)j < nv[u]) atomicAdd(&hp[(d >> 1) * kWave + lane], 1u << ((d & 1u) * 16u));
+            }
+        }
+    }
+    __syncthreads();
+    for (uint32_t d = tid; d < F; d += kBlock) {
+        uint32_t c = 0;
+        for (uint32_t k = 0; k < kWave; ++k)  // rotated rows: the 32 lanes of a read hit 32 banks
+            c += (hp[(d >> 1) * kWave + ((k + d) & (kWave - 1))] >> ((d & 1u) * 16u)) & 0xFFFFu;
+        out[d] = c;
+    }
+}
+
 // Pass-2 histogram of a block-list segment from the digit side stream: 16 lanes per
 // block (16 B each: a block's kBlk digit bytes), 16 blocks per step, 4 steps in flight.
 __global__ __launch_bounds__(kBlock) void k_hist_side_blk(const uint8_t *__restrict__ side,
@@ -1335,10 +1389,14 @@ __global__ __launch_bounds__(kBlock) void k_hist_side_blk(const uint8_t *__restr
     uint64_t b, e;
     if (!seg_lookup(m, g, sbase, r, b, e)) return;
     const uint32_t F = 1u << bits;
-    for (uint32_t d = threadIdx.x; d < F; d += kBlock) h[d] = 0;
-    __syncthreads();
     const uint32_t grp = threadIdx.x / 16, l = threadIdx.x % 16;
     constexpr int U = 4;
+    if (F <= kLaneHistF) {  // workgroup-uniform
+        hist_side_lanes(side, list, b, e, F, hist + (uint64_t)g * F);
+        return;
+    }
+    for (uint32_t d = threadIdx.x; d < F; d += kBlock) h[d] = 0;
+    __syncthreads();
     for (uint64_t i0 = b; i0 < e; i0 += 16 * U) {
         uint4 q[U];
         uint32_t nv[U];
