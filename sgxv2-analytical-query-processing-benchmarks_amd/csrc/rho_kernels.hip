@@ -1329,34 +1329,40 @@ hipError_t launch_block_list(const PoolOut &po, const uint64_t *lbase, uint64_t 
 // 4 waves x 16 keys per block x (segment blocks / 16) per lane (1024 at kPass2Ents = 256,
 // 8192 at 2048), inside a u16.  A shared 128-bin histogram spent 70 % of its LDS cycles
 // in bank conflicts (SQ counters, r02t); the private rows take 5-10 % off the kernel
-// (0.096 -> 0.087 ms per 2^28 keys), which is bound by its two dependent loads (list
-// entry, then the digit bytes) more than by the LDS.
+// (0.096 -> 0.087 ms per 2^28 keys), the list entries staged in LDS with the next
+// step's digit bytes in flight another 18-20 % (0.087 -> 0.071): the kernel was bound
+// by its two dependent loads per step more than by the LDS.
 constexpr uint32_t kLaneHistF = 128;
 __device__ __forceinline__ void hist_side_lanes(const uint8_t *__restrict__ side, const uint64_t *__restrict__ list,
                                                 uint64_t b, uint64_t e, uint32_t F, uint64_t *__restrict__ out) {
     static_assert(kPass2Ents <= 4096, "u16 lane counters");
     constexpr uint32_t W = kLaneHistF / 2 * kWave;
     __shared__ uint32_t hp[W];
+    __shared__ uint64_t ents[kPass2Ents];  // the segment's list entries, one coalesced read
     const uint32_t tid = threadIdx.x, lane = __lane_id();
+    const uint32_t ne = (uint32_t)(e - b);  // <= kPass2Ents (pass-2 segments)
     for (uint32_t i = tid; i < W; i += kBlock) hp[i] = 0;
+    for (uint32_t i = tid; i < ne; i += kBlock) ents[i] = list[b + i];
     __syncthreads();
     const uint32_t grp = tid / 16, l = tid % 16;
-    constexpr int U = 4;  // blocks in flight per 16-lane group (8: same, 16: 20 % slower)
-    for (uint64_t i0 = b; i0 < e; i0 += 16 * U) {
-        uint4 q[U];
-        uint32_t nv[U];
+    constexpr int U = 4;  // blocks per 16-lane group and step
+    constexpr uint32_t SPAN = 16 * U;
+    // one step: the 16-B digit pieces of U blocks per group (entries past ne load nothing)
+    const auto load_step = [&](uint32_t i0, uint4 (&q)[U], uint32_t (&nv)[U]) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint64_t i = i0 + grp + 16 * u;
+            const uint32_t i = i0 + grp + 16 * u;
             nv[u] = 0;
             q[u] = make_uint4(0, 0, 0, 0);
-            if (i < e) {
-                const uint64_t en = list[i];
+            if (i < ne) {
+                const uint64_t en = ents[i];
                 const uint32_t fill = (uint32_t)(en >> 32), lo = l * 16;
                 nv[u] = fill > lo ? min(16u, fill - lo) : 0u;
                 if (nv[u]) q[u] = ld_nt(reinterpret_cast<const uint4 *>(side + (uint64_t)(uint32_t)en * kBlk) + l);
             }
         }
+    };
+    const auto count_step = [&](const uint4 (&q)[U], const uint32_t (&nv)[U]) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t w[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
@@ -1366,6 +1372,16 @@ __device__ __forceinline__ void hist_side_lanes(const uint8_t *__restrict__ side
                 if ((uint32_t)j < nv[u]) atomicAdd(&hp[(d >> 1) * kWave + lane], 1u << ((d & 1u) * 16u));
             }
         }
+    };
+    // two register sets: the next step's loads are in flight while a step is counted
+    uint4 q0[U], q1[U];
+    uint32_t n0[U], n1[U];
+    load_step(0, q0, n0);
+    for (uint32_t i0 = 0; i0 < ne; i0 += 2 * SPAN) {
+        load_step(i0 + SPAN, q1, n1);
+        count_step(q0, n0);
+        load_step(i0 + 2 * SPAN, q0, n0);
+        count_step(q1, n1);
     }
     __syncthreads();
     for (uint32_t d = tid; d < F; d += kBlock) {
@@ -1391,7 +1407,7 @@ __global__ __launch_bounds__(kBlock) void k_hist_side_blk(const uint8_t *__restr
     const uint32_t F = 1u << bits;
     const uint32_t grp = threadIdx.x / 16, l = threadIdx.x % 16;
     constexpr int U = 4;
-    if (F <= kLaneHistF) {  // workgroup-uniform
+    if (F <= kLaneHistF && e - b <= kPass2Ents) {  // workgroup-uniform
         hist_side_lanes(side, list, b, e, F, hist + (uint64_t)g * F);
         return;
     }
