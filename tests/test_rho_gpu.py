@@ -256,7 +256,15 @@ def test_config4_full_size(sgx, gpu):
     assert (st["radix_bits"], st["passes"], st["num_partitions"]) == (14, 2, 1 << 14)
     assert st["max_part_r"] == 8192 and st["max_part_s"] == 65536
     assert st["num_tasks"] == 1 << 14  # one 65,536-key S chunk per partition
-    del R, S
+    # a hot S key: 2^23 tuples of S take R key 12345 (still one R match each), so its
+    # partition holds > 2^23 tuples and is split into 65,536-key tasks
+    hot = S[: 1 << 23]
+    hot.copy_((hot & ~0xFFFFFFFF) | 12345)
+    res = sgx.rho_join(R, nR, S, nS)
+    assert res.matches == nS
+    st = res.stats
+    assert st["max_part_s"] > 1 << 23 and st["num_tasks"] >= (1 << 14) + (1 << 23) // 65536 - 1
+    del R, S, hot
     torch.cuda.empty_cache()
 
 
