@@ -8,12 +8,18 @@
  * exchange step moves every tuple to its owner:
  *   1. per relation, in pieces: stable shard partition of the local slice by
  *      d = key & (G - 1) (the pass-1 machinery of radix_join.cpp:851-931 with G bins);
- *   2. the G x G piece counts (RCCL all-gather of the per-destination counts);
+ *   2. the G x G piece counts: a host table between the rank threads of one process,
+ *      or an RCCL all-gather on a second communicator (never queued behind the
+ *      previous piece's tuples on the tuple communicator);
  *   3. the tuples (RCCL send/recv per peer, on a communication stream, while the next
  *      piece is partitioned), into a contiguous receive buffer per relation;
  *   4. the local join of the received relations with key_shift = log2(G) (R's local
  *      passes while S is still on the wire);
- *   5. an RCCL all-reduce of the match counts.
+ *   5. an all-reduce of the match counts.
+ * Every rank issues the same collectives whether or not it failed: a rank whose
+ * allocation, shard pass or local join fails flags it in the next count exchange or in
+ * the final all-reduce, and every rank returns an error at that step (the first-hand
+ * error on the failed rank, MI355_ERR_COMM "another rank failed" on the others).
  * The caller, native.cpp:137 -> run_join -> RHO, is unchanged: RHO() (joins.hpp)
  * takes this path when SGXAMD_GPUS > 1 (joinconfig_t has no spare field for a GPU
  * count).
@@ -93,6 +99,17 @@ int mi355_last_multi_stats(mi355_multi_stats *out);
 
 /* Pieces each relation is exchanged in (default 4; 1..64); applies to later calls. */
 void mi355_multi_set_pieces(int pieces);
+
+/* Frees the workspaces (exchange and join buffers) of the rehearsal transport's
+ * logical ranks, which are otherwise kept for the process: call it between large
+ * rehearsal joins that do not reuse them.  The calling thread's device must be the
+ * rehearsal's. */
+int mi355_multi_release(void);
+
+/* Test hook: rank `rank` fails at `step` of every later multi-GPU join (1: exchange
+ * buffer allocation, 2: a shard pass of S, 3: the local join) as an allocation or
+ * kernel error would; step 0 clears it. */
+void mi355_multi_inject_failure(int rank, int step);
 
 #ifdef __cplusplus
 } /* extern "C" */

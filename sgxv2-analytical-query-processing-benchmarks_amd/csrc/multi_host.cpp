@@ -18,6 +18,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -66,6 +67,8 @@ struct Rccl {
     decltype(&ncclCommInitRank) CommInitRank = nullptr;
     decltype(&ncclCommInitAll) CommInitAll = nullptr;
     decltype(&ncclCommDestroy) CommDestroy = nullptr;
+    decltype(&ncclCommAbort) CommAbort = nullptr;
+    decltype(&ncclCommSplit) CommSplit = nullptr;
     decltype(&ncclGroupStart) GroupStart = nullptr;
     decltype(&ncclGroupEnd) GroupEnd = nullptr;
     decltype(&ncclSend) Send = nullptr;
@@ -94,6 +97,8 @@ const Rccl &rccl() {
         sym(r.CommInitRank, "ncclCommInitRank");
         sym(r.CommInitAll, "ncclCommInitAll");
         sym(r.CommDestroy, "ncclCommDestroy");
+        sym(r.CommAbort, "ncclCommAbort");
+        sym(r.CommSplit, "ncclCommSplit");
         sym(r.GroupStart, "ncclGroupStart");
         sym(r.GroupEnd, "ncclGroupEnd");
         sym(r.Send, "ncclSend");
@@ -158,23 +163,32 @@ class Barrier {
 
 // ---------------------------------------------------------------- transports
 enum ReduceOp { kSum, kMax };
+constexpr int kMaxReduce = 4;  // values per all-reduce
 
+// Every collective a rank issues is reached by every rank, failed or not: a rank that
+// failed (an allocation, a kernel) says so in the next collective instead of leaving
+// it, so all ranks see the failure at the same step and return together (no peer is
+// left waiting in a collective the failed rank never posts).
 class Transport {
    public:
     virtual ~Transport() = default;
     virtual int world() const = 0;
     virtual int kind() const = 0;
-    // collective: send[d] = tuples this rank sends to rank d in this piece;
-    // recv[q] = tuples rank q sends to this rank (host arrays of world() entries)
-    virtual int exchange_counts(int rank, hipStream_t s, const uint64_t *send, uint64_t *recv) = 0;
+    // collective: send[d] = tuples this rank sends to rank d in this piece, fail = this
+    // rank has failed; recv[q] = tuples rank q sends to this rank, *any_fail = some rank
+    // has failed (then nothing of this piece is posted, by any rank)
+    virtual int exchange_counts(int rank, hipStream_t s, const uint64_t *send, bool fail, uint64_t *recv,
+                                bool *any_fail) = 0;
     // collective: after `ready` (the piece's partition on the compute stream), move the
     // piece: the run for destination d starts at send + sum_{d'<d} send_counts[d'];
     // rank q's run lands at recv + sum_{q'<q} recv_counts[q'].  Enqueued on c.
     // elem: bytes per element (8: row_t tuples; 4: keys of a keys-only exchange).
     virtual int post_exchange(int rank, hipStream_t c, hipEvent_t ready, const void *send,
                               const uint64_t *send_counts, void *recv, const uint64_t *recv_counts, size_t elem) = 0;
-    // collective: *v = sum / max of every rank's *v
-    virtual int allreduce(int rank, hipStream_t s, uint64_t *v, ReduceOp op) = 0;
+    // collective: v[0..n) = element-wise sum / max over the ranks (n <= kMaxReduce)
+    virtual int allreduce(int rank, hipStream_t s, uint64_t *v, int n, ReduceOp op) = 0;
+    // a rank's transport call failed (the transport itself is broken): release the
+    // host-side waiters; communicators are torn down by the owner afterwards
     virtual void abort() {}
 };
 
@@ -184,31 +198,95 @@ std::vector<uint64_t> prefix(const uint64_t *c, int n) {
     return p;
 }
 
-// RCCL over xGMI.  One communicator per local rank: all G of them (one process, one
-// thread per GPU, ncclCommInitAll) or this process's one (ncclCommInitRank).
+// Counts, flags and reductions of the ranks of ONE process (threads): shared host
+// tables between barriers.  No device round trip, and nothing queued behind the tuple
+// traffic of a communicator.
+class HostCollectives {
+   public:
+    explicit HostCollectives(int world)
+        : world_(world), bar_(world), counts_(world, std::vector<uint64_t>(world + 1)), red_(world) {}
+    int world() const { return world_; }
+    bool wait() { return bar_.wait(); }
+    void abort() { bar_.abort(); }
+
+    int exchange_counts(int rank, const uint64_t *send, bool fail, uint64_t *recv, bool *any_fail) {
+        std::copy(send, send + world_, counts_[rank].begin());
+        counts_[rank][world_] = fail ? 1 : 0;
+        if (!bar_.wait()) return aborted();
+        bool f = false;
+        for (int q = 0; q < world_; ++q) {
+            recv[q] = counts_[q][rank];
+            f = f || counts_[q][world_];
+        }
+        *any_fail = f;
+        if (!bar_.wait()) return aborted();  // the table is reused by the next piece
+        return MI355_OK;
+    }
+
+    int allreduce(int rank, uint64_t *v, int n, ReduceOp op) {
+        std::copy(v, v + n, red_[rank].begin());
+        if (!bar_.wait()) return aborted();
+        for (int j = 0; j < n; ++j) {
+            uint64_t r = op == kSum ? 0 : red_[0][j];
+            for (int q = 0; q < world_; ++q) r = op == kSum ? r + red_[q][j] : std::max(r, red_[q][j]);
+            v[j] = r;
+        }
+        if (!bar_.wait()) return aborted();
+        return MI355_OK;
+    }
+
+   private:
+    int aborted() {
+        set_last_error("another rank's transport failed");
+        return MI355_ERR_COMM;
+    }
+    int world_;
+    Barrier bar_;
+    std::vector<std::vector<uint64_t>> counts_;  // [rank][G counts + fail flag]
+    std::vector<std::array<uint64_t, kMaxReduce>> red_;
+};
+
+// RCCL over xGMI.  Tuples (keys) go through `comms` with grouped send/recv on each
+// rank's communication stream.  Counts, flags and reductions never share a
+// communicator with the tuples: RCCL orders every operation of one communicator, so a
+// piece's count all-gather on the tuple communicator would wait for the previous
+// piece's transfer (and the host, which needs the counts to post the next piece, with
+// it).  They go through a host table between the threads of one process
+// (ncclCommInitAll mode), or through a second communicator per rank (ncclCommSplit of
+// the tuple communicator, one process per GPU).
 class RcclTransport final : public Transport {
    public:
-    RcclTransport(int world, int first_rank, std::vector<ncclComm_t> comms, std::vector<int> devices)
-        : world_(world), first_(first_rank), comms_(std::move(comms)), devices_(std::move(devices)),
-          buf_(comms_.size()), host_(comms_.size(), nullptr) {}
+    RcclTransport(int world, int first_rank, std::vector<ncclComm_t> comms, std::vector<ncclComm_t> ccomms,
+                  std::shared_ptr<HostCollectives> host)
+        : world_(world), first_(first_rank), comms_(std::move(comms)), ccomms_(std::move(ccomms)),
+          host_(std::move(host)), buf_(comms_.size()), pinned_(comms_.size(), nullptr) {}
     ~RcclTransport() override {
         for (auto &b : buf_) b.release();
-        for (auto *h : host_)
+        for (auto *h : pinned_)
             if (h) (void)hipHostFree(h);
     }
     int world() const override { return world_; }
     int kind() const override { return MI355_TRANSPORT_RCCL; }
 
-    int exchange_counts(int rank, hipStream_t s, const uint64_t *send, uint64_t *recv) override {
+    int exchange_counts(int rank, hipStream_t s, const uint64_t *send, bool fail, uint64_t *recv,
+                        bool *any_fail) override {
+        if (host_) return host_->exchange_counts(rank, send, fail, recv, any_fail);
         const int i = rank - first_;
+        const size_t w1 = world_ + 1;  // G counts + the fail flag
         uint64_t *d = nullptr, *h = nullptr;
         MH_RC(scratch(i, &d, &h));
         std::memcpy(h, send, sizeof(uint64_t) * world_);
-        MH_HIP(hipMemcpyAsync(d, h, sizeof(uint64_t) * world_, hipMemcpyHostToDevice, s));
-        MH_NCCL(rccl().AllGather(d, d + world_, world_, ncclUint64, comms_[i], s));
-        MH_HIP(hipMemcpyAsync(h + world_, d + world_, sizeof(uint64_t) * world_ * world_, hipMemcpyDeviceToHost, s));
+        h[world_] = fail ? 1 : 0;
+        MH_HIP(hipMemcpyAsync(d, h, sizeof(uint64_t) * w1, hipMemcpyHostToDevice, s));
+        MH_NCCL(rccl().AllGather(d, d + w1, w1, ncclUint64, ccomms_[i], s));
+        MH_HIP(hipMemcpyAsync(h + w1, d + w1, sizeof(uint64_t) * w1 * world_, hipMemcpyDeviceToHost, s));
         MH_HIP(hipStreamSynchronize(s));
-        for (int q = 0; q < world_; ++q) recv[q] = h[world_ + (size_t)q * world_ + rank];
+        bool f = false;
+        for (int q = 0; q < world_; ++q) {
+            recv[q] = h[w1 + q * w1 + rank];
+            f = f || h[w1 + q * w1 + world_];
+        }
+        *any_fail = f;
         return MI355_OK;
     }
 
@@ -233,63 +311,65 @@ class RcclTransport final : public Transport {
         return MI355_OK;
     }
 
-    int allreduce(int rank, hipStream_t s, uint64_t *v, ReduceOp op) override {
+    int allreduce(int rank, hipStream_t s, uint64_t *v, int n, ReduceOp op) override {
+        if (host_) return host_->allreduce(rank, v, n, op);
         const int i = rank - first_;
         uint64_t *d = nullptr, *h = nullptr;
         MH_RC(scratch(i, &d, &h));
-        h[0] = *v;
-        MH_HIP(hipMemcpyAsync(d, h, sizeof(uint64_t), hipMemcpyHostToDevice, s));
-        MH_NCCL(rccl().AllReduce(d, d, 1, ncclUint64, op == kSum ? ncclSum : ncclMax, comms_[i], s));
-        MH_HIP(hipMemcpyAsync(h, d, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+        std::memcpy(h, v, sizeof(uint64_t) * n);
+        MH_HIP(hipMemcpyAsync(d, h, sizeof(uint64_t) * n, hipMemcpyHostToDevice, s));
+        MH_NCCL(rccl().AllReduce(d, d, n, ncclUint64, op == kSum ? ncclSum : ncclMax, ccomms_[i], s));
+        MH_HIP(hipMemcpyAsync(h, d, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, s));
         MH_HIP(hipStreamSynchronize(s));
-        *v = h[0];
+        std::memcpy(v, h, sizeof(uint64_t) * n);
         return MI355_OK;
+    }
+
+    void abort() override {
+        if (host_) host_->abort();
     }
 
    private:
-    // per local rank: device [world + world^2] u64 and its pinned host mirror
+    // per local rank: device [(G+1) + G(G+1)] u64 and its pinned host mirror
     int scratch(int i, uint64_t **d, uint64_t **h) {
-        const size_t bytes = sizeof(uint64_t) * (world_ + (size_t)world_ * world_);
+        const size_t bytes = sizeof(uint64_t) * std::max<size_t>((world_ + 1) * (size_t)(world_ + 1), kMaxReduce);
         MH_HIP(buf_[i].ensure(bytes));
-        if (!host_[i]) MH_HIP(hipHostMalloc(reinterpret_cast<void **>(&host_[i]), bytes));
+        if (!pinned_[i]) MH_HIP(hipHostMalloc(reinterpret_cast<void **>(&pinned_[i]), bytes));
         *d = buf_[i].as<uint64_t>();
-        *h = host_[i];
+        *h = pinned_[i];
         return MI355_OK;
     }
     int world_, first_;
-    std::vector<ncclComm_t> comms_;
-    std::vector<int> devices_;
+    std::vector<ncclComm_t> comms_, ccomms_;
+    std::shared_ptr<HostCollectives> host_;
     std::vector<DeviceBuffer> buf_;
-    std::vector<uint64_t *> host_;
+    std::vector<uint64_t *> pinned_;
 };
 
-// G logical ranks on one GPU, one host thread each: counts and reductions through
-// shared host tables, tuples by device-to-device copies that the receiver enqueues on
-// its communication stream after the sender's partition event.  Same collective
-// sequence and receive layout as the RCCL transport.
+// G logical ranks on one GPU, one host thread each: counts and reductions through the
+// host tables, tuples by device-to-device copies that the receiver enqueues on its
+// communication stream after the sender's partition event.  Same collective sequence
+// and receive layout as the RCCL transport.
 class RehearsalTransport final : public Transport {
    public:
-    explicit RehearsalTransport(int world)
-        : world_(world), bar_(world), counts_(world, std::vector<uint64_t>(world)), posts_(world), red_(world) {}
-    int world() const override { return world_; }
+    explicit RehearsalTransport(int world) : host_(world), posts_(world) {}
+    int world() const override { return host_.world(); }
     int kind() const override { return MI355_TRANSPORT_REHEARSAL; }
 
-    int exchange_counts(int rank, hipStream_t, const uint64_t *send, uint64_t *recv) override {
-        std::copy(send, send + world_, counts_[rank].begin());
-        if (!bar_.wait()) return aborted();
-        for (int q = 0; q < world_; ++q) recv[q] = counts_[q][rank];
-        if (!bar_.wait()) return aborted();
-        return MI355_OK;
+    int exchange_counts(int rank, hipStream_t, const uint64_t *send, bool fail, uint64_t *recv,
+                        bool *any_fail) override {
+        return host_.exchange_counts(rank, send, fail, recv, any_fail);
     }
 
     int post_exchange(int rank, hipStream_t c, hipEvent_t ready, const void *send, const uint64_t *send_counts,
                       void *recv_v, const uint64_t *recv_counts, size_t elem) override {
+        const int G = host_.world();
         char *recv = static_cast<char *>(recv_v);
-        posts_[rank] = Post{static_cast<const char *>(send), prefix(send_counts, world_), ready};
-        if (!bar_.wait()) return aborted();
+        posts_[rank] = Post{static_cast<const char *>(send), prefix(send_counts, G), ready};
+        if (!host_.wait()) return aborted();
         uint64_t off = 0;
         int rc = MI355_OK;
-        for (int q = 0; q < world_ && rc == MI355_OK; ++q) {
+        for (int q = 0; q < G && rc == MI355_OK; ++q) {
             if (!recv_counts[q]) continue;
             const Post &p = posts_[q];
             if (hipStreamWaitEvent(c, p.ready, 0) != hipSuccess ||
@@ -300,37 +380,28 @@ class RehearsalTransport final : public Transport {
             }
             off += recv_counts[q];
         }
-        if (!bar_.wait()) return aborted();  // the posts table is reused by the next piece
+        if (!host_.wait()) return aborted();  // the posts table is reused by the next piece
         return rc;
     }
 
-    int allreduce(int rank, hipStream_t, uint64_t *v, ReduceOp op) override {
-        red_[rank] = *v;
-        if (!bar_.wait()) return aborted();
-        uint64_t r = op == kSum ? 0 : red_[0];
-        for (uint64_t x : red_) r = op == kSum ? r + x : std::max(r, x);
-        if (!bar_.wait()) return aborted();
-        *v = r;
-        return MI355_OK;
+    int allreduce(int rank, hipStream_t, uint64_t *v, int n, ReduceOp op) override {
+        return host_.allreduce(rank, v, n, op);
     }
 
-    void abort() override { bar_.abort(); }
+    void abort() override { host_.abort(); }
 
    private:
     int aborted() {
-        set_last_error("another rank of the rehearsal failed");
-        return MI355_ERR_INVALID;
+        set_last_error("another rank's transport failed");
+        return MI355_ERR_COMM;
     }
     struct Post {
         const char *send = nullptr;
         std::vector<uint64_t> off;
         hipEvent_t ready = nullptr;
     };
-    int world_;
-    Barrier bar_;
-    std::vector<std::vector<uint64_t>> counts_;
+    HostCollectives host_;
     std::vector<Post> posts_;
-    std::vector<uint64_t> red_;
 };
 
 // ---------------------------------------------------------------- one rank's join
@@ -359,7 +430,8 @@ int rank_streams(Context *ctx, int nev, RankStreams **out) {
 
 struct RankOut {
     uint64_t global = 0, local = 0, recv_r = 0, recv_s = 0, sent = 0;
-    bool keys = false;  // the exchange moved keys only
+    bool keys = false;       // the exchange moved keys only
+    bool peer_fail = false;  // the call failed because another rank did
     double ms_post = 0, ms_local = 0, ms_allreduce = 0, ms_total = 0;
     mi355_rho_stats st{};
 };
@@ -370,10 +442,30 @@ uint32_t log2_exact(int g) {
     return b;
 }
 
+// Test hook (mi355_multi_inject_failure): rank `g_fail_rank` fails at step
+// `g_fail_step` of its next multi-GPU join, as an allocation or kernel error would.
+std::atomic<int> g_fail_rank{-1}, g_fail_step{0};
+enum FailStep { kFailBuffers = 1, kFailPiece = 2, kFailLocal = 3 };
+bool injected(int rank, int step) {
+    if (g_fail_rank.load() != rank || g_fail_step.load() != step) return false;
+    set_last_error("injected failure (mi355_multi_inject_failure)");
+    return true;
+}
+
 // The pipeline of the file comment for rank `rank` on its context (device current,
 // ctx->mu held).  R / S: this rank's device-resident slices.
+//
+// Collectives, identical on every rank whatever fails: two all-reduces (sizes, element
+// format), then per piece a count exchange and its post, then one final all-reduce
+// (matches, failures).  A rank whose buffers, shard pass or local join fail keeps
+// issuing them with its fail flag set; the first count exchange or the final
+// all-reduce that carries a flag ends the call on every rank with an error.  Only a
+// failing transport call itself (MI355_ERR_COMM) leaves the sequence.
+//
+// pre_fail != MI355_OK: the rank failed before its join (no context, staging); it
+// takes part in the collectives with its flag set (ctx may be null then).
 int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *R, uint64_t nR, const row_t *S,
-              uint64_t nS, const mi355_rho_opts *opts, RankOut &o) {
+              uint64_t nS, const mi355_rho_opts *opts, RankOut &o, int pre_fail = MI355_OK) {
     const auto t0 = Clock::now();
     const int G = T.world();
     const uint32_t dest_bits = log2_exact(G);
@@ -386,6 +478,7 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
     lo.out = nullptr;
     lo.out_capacity = 0;
     if (G == 1) {  // nothing to exchange
+        if (pre_fail != MI355_OK) return pre_fail;
         if (nR && nS) {
             MH_RC(rho::join_pipelined_begin(ctx, s, R, nR, nS, &lo));
             MH_RC(rho::join_pipelined_finish(ctx, S, nS, &o.st));
@@ -397,28 +490,57 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
         return MI355_OK;
     }
     RankStreams *rs = nullptr;
-    MH_RC(rank_streams(ctx, 2 * K + 2, &rs));
-    hipStream_t c = rs->comm;
+    // this rank's first error, kept until the next collective reports it
+    int fail_rc = pre_fail != MI355_OK ? pre_fail : rank_streams(ctx, 2 * K + 2, &rs);
+    std::string fail_msg = fail_rc ? last_error() : "";
+    auto fail = [&](int rc) {
+        if (rc != MI355_OK && fail_rc == MI355_OK) {
+            fail_rc = rc;
+            fail_msg = last_error();
+        }
+    };
+    auto peer_failed = [&]() {
+        if (fail_rc != MI355_OK) {
+            set_last_error(fail_msg);
+            return fail_rc;
+        }
+        o.peer_fail = true;
+        set_last_error("another rank failed; every rank left the multi-GPU join at the same step");
+        return MI355_ERR_COMM;
+    };
 
-    // receive buffers for the worst case: every rank's piece i comes to this rank
-    uint64_t mR = nR, mS = nS, sumR = nR, sumS = nS;
-    MH_RC(T.allreduce(rank, s, &mR, kMax));
-    MH_RC(T.allreduce(rank, s, &mS, kMax));
-    MH_RC(T.allreduce(rank, s, &sumR, kSum));
-    MH_RC(T.allreduce(rank, s, &sumS, kSum));
-    const uint64_t capR = (uint64_t)G * K * ((mR + K - 1) / K), capS = (uint64_t)G * K * ((mS + K - 1) / K);
-    // a counting join exchanges keys only (4 of the 8 bytes per tuple on xGMI) when its
-    // local join, planned from the mean local sizes on every rank alike, reads keys
-    o.keys = rho::keys_exchange_plan(sumR / G, sumS / G, capR, capS, &lo);
+    // global sizes: the mean local sizes plan the local join, the largest slices size
+    // the receive buffers for the worst case (every rank's piece i comes to this rank)
+    uint64_t sum[2] = {nR, nS}, mx[2] = {nR, nS};
+    MH_RC(T.allreduce(rank, s, sum, 2, kSum));
+    MH_RC(T.allreduce(rank, s, mx, 2, kMax));
+    const uint64_t cR = (uint64_t)G * K * ((mx[0] + K - 1) / K), cS = (uint64_t)G * K * ((mx[1] + K - 1) / K);
+    // the element format must be the same on every rank (the SGXAMD_KEYS switch and the
+    // calling thread's key layout are per process / per thread): keys only when every
+    // rank's plan, from the same global sizes, takes the pooled keys layout
+    mi355_rho_opts kl = lo;
+    uint64_t notkeys = rho::keys_exchange_plan(sum[0] / G, sum[1] / G, cR, cS, &kl) ? 0 : 1;
+    MH_RC(T.allreduce(rank, s, &notkeys, 1, kMax));
+    o.keys = notkeys == 0;
+    if (o.keys) lo = kl;  // the local policy fixed from the global sizes
     const size_t elem = o.keys ? sizeof(uint32_t) : sizeof(row_t);
-    MH_HIP(ctx->xsendR.ensure(std::max<uint64_t>(nR, 1) * elem));
-    MH_HIP(ctx->xsendS.ensure(std::max<uint64_t>(nS, 1) * elem));
-    MH_HIP(ctx->xrecvR.ensure(std::max<uint64_t>(capR, 1) * elem));
-    MH_HIP(ctx->xrecvS.ensure(std::max<uint64_t>(capS, 1) * elem));
+    if (fail_rc == MI355_OK) {
+        hipError_t e = ctx->xsendR.ensure(std::max<uint64_t>(nR, 1) * elem);
+        if (e == hipSuccess) e = ctx->xsendS.ensure(std::max<uint64_t>(nS, 1) * elem);
+        if (e == hipSuccess) e = ctx->xrecvR.ensure(std::max<uint64_t>(cR, 1) * elem);
+        if (e == hipSuccess) e = ctx->xrecvS.ensure(std::max<uint64_t>(cS, 1) * elem);
+        if (e != hipSuccess) {
+            set_last_error(std::string("exchange buffers (") + std::to_string((2 * (nR + nS) + cR + cS) * elem) +
+                           " bytes): " + hipGetErrorString(e));
+            fail(e == hipErrorOutOfMemory ? MI355_ERR_OOM : MI355_ERR_HIP);
+        }
+        if (injected(rank, kFailBuffers)) fail(MI355_ERR_OOM);
+    }
 
     std::vector<uint64_t> sc(G), rc(G);
     uint64_t total[2] = {0, 0};
-    for (int rel = 0; rel < 2; ++rel) {
+    bool any_fail = false;
+    for (int rel = 0; rel < 2 && !any_fail; ++rel) {
         const row_t *in = rel ? S : R;
         const uint64_t n = rel ? nS : nR;
         char *snd = (rel ? ctx->xsendS : ctx->xsendR).as<char>();
@@ -426,22 +548,29 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
         const uint64_t per = (n + K - 1) / K;
         for (int i = 0; i < K; ++i) {
             const uint64_t a = std::min(n, i * per), b = std::min(n, (i + 1) * per);
-            if (b > a)
-                MH_RC(rho::shard_partition_device(ctx, s, in + a, b - a, 0, dest_bits, snd + a * elem, sc.data(),
-                                                  (uint32_t)elem));
-            else
-                std::fill(sc.begin(), sc.end(), 0);
-            MH_RC(T.exchange_counts(rank, s, sc.data(), rc.data()));
+            std::fill(sc.begin(), sc.end(), 0);
+            if (fail_rc == MI355_OK && b > a) {
+                fail(rho::shard_partition_device(ctx, s, in + a, b - a, 0, dest_bits, snd + a * elem, sc.data(),
+                                                 (uint32_t)elem));
+                if (rel == 1 && i == K / 2 && injected(rank, kFailPiece)) fail(MI355_ERR_HIP);
+            }
+            if (fail_rc != MI355_OK) std::fill(sc.begin(), sc.end(), 0);
+            MH_RC(T.exchange_counts(rank, s, sc.data(), fail_rc != MI355_OK, rc.data(), &any_fail));
+            if (any_fail) break;  // every rank sees the same flags: none posts this piece
             hipEvent_t ready = rs->ev[rel * K + i];
             MH_HIP(hipEventRecord(ready, s));
-            MH_RC(T.post_exchange(rank, c, ready, snd + a * elem, sc.data(), rcv + total[rel] * elem, rc.data(),
-                                  elem));
+            MH_RC(T.post_exchange(rank, rs->comm, ready, snd + a * elem, sc.data(), rcv + total[rel] * elem,
+                                  rc.data(), elem));
             for (int q = 0; q < G; ++q) {
                 total[rel] += rc[q];
                 if (q != rank) o.sent += sc[q] * elem;
             }
         }
-        MH_HIP(hipEventRecord(rs->ev[2 * K + rel], c));
+        if (!any_fail) MH_HIP(hipEventRecord(rs->ev[2 * K + rel], rs->comm));
+    }
+    if (any_fail) {  // the pieces posted so far were posted by every rank: let them land
+        if (rs) MH_HIP(hipStreamSynchronize(rs->comm));
+        return peer_failed();
     }
     o.recv_r = total[0];
     o.recv_s = total[1];
@@ -451,20 +580,24 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
     // local join: R's passes once R has landed, S's passes and build/probe once S has
     MH_HIP(hipStreamWaitEvent(s, rs->ev[2 * K], 0));
     if (total[0] && total[1]) {
-        MH_RC(rho::join_pipelined_begin(ctx, s, ctx->xrecvR.ptr, total[0], total[1], &lo, (uint32_t)elem));
+        int lrc = injected(rank, kFailLocal) ? MI355_ERR_OOM
+                                             : rho::join_pipelined_begin(ctx, s, ctx->xrecvR.ptr, total[0], total[1],
+                                                                         &lo, (uint32_t)elem);
         MH_HIP(hipStreamWaitEvent(s, rs->ev[2 * K + 1], 0));
-        MH_RC(rho::join_pipelined_finish(ctx, ctx->xrecvS.ptr, total[1], &o.st));
-        o.local = o.st.matches;
+        if (lrc == MI355_OK) lrc = rho::join_pipelined_finish(ctx, ctx->xrecvS.ptr, total[1], &o.st);
+        fail(lrc);
+        o.local = lrc == MI355_OK ? o.st.matches : 0;
     } else {
         MH_HIP(hipStreamWaitEvent(s, rs->ev[2 * K + 1], 0));
-        MH_HIP(hipStreamSynchronize(s));
     }
-    MH_HIP(hipStreamSynchronize(c));
+    MH_HIP(hipStreamSynchronize(s));
+    MH_HIP(hipStreamSynchronize(rs->comm));
     const auto t2 = Clock::now();
     o.ms_local = std::chrono::duration<double, std::milli>(t2 - t1).count();
-    uint64_t m = o.local;
-    MH_RC(T.allreduce(rank, s, &m, kSum));
-    o.global = m;
+    uint64_t m[2] = {o.local, fail_rc != MI355_OK ? 1u : 0u};
+    MH_RC(T.allreduce(rank, s, m, 2, kSum));
+    if (m[1]) return peer_failed();
+    o.global = m[0];
     o.ms_allreduce = ms_since(t2);
     o.ms_total = ms_since(t0);
     return MI355_OK;
@@ -510,6 +643,18 @@ int comms_all(int G, std::vector<ncclComm_t> *out) {
     }
     *out = it->second;
     return MI355_OK;
+}
+
+// A transport call failed on some rank (every rank thread has returned): the
+// communicators may hold unmatched operations, so they are aborted and dropped from the
+// cache; the next call creates new ones.
+void drop_comms_all(int G) {
+    std::lock_guard<std::mutex> lk(g_all_mu);
+    auto it = g_all.find(G);
+    if (it == g_all.end()) return;
+    for (ncclComm_t c : it->second)
+        if (c && rccl().CommAbort) (void)rccl().CommAbort(c);
+    g_all.erase(it);
 }
 
 void fill_stats(mi355_multi_stats *st, const std::vector<RankOut> &outs, int G, int kind, int rank) {
@@ -569,39 +714,57 @@ int join_multi(const row_t *R, uint64_t nR, const row_t *S, uint64_t nS, int G, 
     if (kind == MI355_TRANSPORT_RCCL) {
         std::vector<ncclComm_t> comms;
         MH_RC(comms_all(G, &comms));
-        std::vector<int> devs(G);
-        for (int g = 0; g < G; ++g) devs[g] = g;
-        T = std::make_unique<RcclTransport>(G, 0, comms, devs);
+        T = std::make_unique<RcclTransport>(G, 0, comms, std::vector<ncclComm_t>{},
+                                            std::make_shared<HostCollectives>(G));
     } else {
         T = std::make_unique<RehearsalTransport>(G);
     }
+    // the rank threads run with the caller's per-thread settings (key layout, timing)
+    const bool keys = thread_key_layout(), timing = thread_timing_enabled();
     const bool dR = is_device_pointer(R), dS = is_device_pointer(S);
     std::vector<RankOut> outs(G);
     std::vector<int> rcs(G, MI355_OK);
     std::vector<std::string> errs(G);
     auto body = [&](int g) -> int {
+        mi355_set_key_layout(keys ? 1 : 0);
+        mi355_timing_enable(timing ? 1 : 0);
         const int dev = kind == MI355_TRANSPORT_RCCL ? g : cur;
-        MH_HIP(hipSetDevice(dev));
         int status = MI355_OK;
-        Context *ctx = kind == MI355_TRANSPORT_RCCL ? current_context(&status) : rehearsal_context(dev, g, &status);
-        if (!ctx) return status;
-        std::lock_guard<std::mutex> lk(ctx->mu);
+        Context *ctx = nullptr;
+        if (hipSetDevice(dev) != hipSuccess) {
+            set_last_error("hipSetDevice(" + std::to_string(dev) + ") failed");
+            status = MI355_ERR_HIP;
+        } else {
+            ctx = kind == MI355_TRANSPORT_RCCL ? current_context(&status) : rehearsal_context(dev, g, &status);
+        }
         // this rank's slices (radix_join.cpp:1488-1499: floor(n/T) each, the last the rest)
         const uint64_t pr = nR / G, ps = nS / G;
         const uint64_t r0 = pr * g, s0 = ps * g;
         const uint64_t rn = g == G - 1 ? nR - r0 : pr, sn = g == G - 1 ? nS - s0 : ps;
         const row_t *lR = R + r0, *lS = S + s0;
-        if (!(dR && dev == cur)) {  // stage into this rank's device (H2D, or peer D2D)
-            MH_HIP(ctx->inR.ensure(std::max<uint64_t>(rn, 1) * sizeof(row_t)));
-            MH_HIP(hipMemcpyAsync(ctx->inR.ptr, lR, rn * sizeof(row_t), hipMemcpyDefault, ctx->stream));
-            lR = ctx->inR.as<row_t>();
+        // without a context the rank still takes part in the collectives, flagged as failed
+        if (!ctx) return rank_join(*T, g, nullptr, nullptr, nullptr, 0, nullptr, 0, opts, outs[g], status);
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        int src = MI355_OK;
+        auto stage = [&](DeviceBuffer &buf, const row_t *&p, uint64_t n) {
+            if (src != MI355_OK) return;
+            const hipError_t e1 = buf.ensure(std::max<uint64_t>(n, 1) * sizeof(row_t));
+            const hipError_t e2 =
+                e1 == hipSuccess ? hipMemcpyAsync(buf.ptr, p, n * sizeof(row_t), hipMemcpyDefault, ctx->stream) : e1;
+            if (e2 != hipSuccess) {
+                set_last_error(std::string("staging a slice: ") + hipGetErrorString(e2));
+                src = e2 == hipErrorOutOfMemory ? MI355_ERR_OOM : MI355_ERR_HIP;
+                return;
+            }
+            p = buf.as<row_t>();
+        };
+        if (!(dR && dev == cur)) stage(ctx->inR, lR, rn);  // H2D, or peer D2D
+        if (!(dS && dev == cur)) stage(ctx->inS, lS, sn);
+        if (src == MI355_OK && hipStreamSynchronize(ctx->stream) != hipSuccess) {
+            set_last_error("staging the slices failed");
+            src = MI355_ERR_HIP;
         }
-        if (!(dS && dev == cur)) {
-            MH_HIP(ctx->inS.ensure(std::max<uint64_t>(sn, 1) * sizeof(row_t)));
-            MH_HIP(hipMemcpyAsync(ctx->inS.ptr, lS, sn * sizeof(row_t), hipMemcpyDefault, ctx->stream));
-            lS = ctx->inS.as<row_t>();
-        }
-        MH_HIP(hipStreamSynchronize(ctx->stream));
+        if (src != MI355_OK) return rank_join(*T, g, ctx, ctx->stream, nullptr, 0, nullptr, 0, opts, outs[g], src);
         return rank_join(*T, g, ctx, ctx->stream, lR, rn, lS, sn, opts, outs[g]);
     };
     std::vector<std::thread> th;
@@ -610,16 +773,26 @@ int join_multi(const row_t *R, uint64_t nR, const row_t *S, uint64_t nS, int G, 
             rcs[g] = body(g);
             if (rcs[g] != MI355_OK) {
                 errs[g] = last_error();
-                T->abort();
+                // a failed transport call leaves the sequence of collectives: release the
+                // other ranks' host waits (flagged failures keep it and need nothing)
+                if (rcs[g] == MI355_ERR_COMM && !outs[g].peer_fail) T->abort();
             }
         });
     for (auto &t : th) t.join();
     (void)hipSetDevice(cur);
-    for (int g = 0; g < G; ++g) {
-        if (rcs[g] != MI355_OK) {
-            set_last_error("rank " + std::to_string(g) + ": " + errs[g]);
-            return rcs[g];
-        }
+    bool comm_broken = false;
+    for (int g = 0; g < G; ++g) comm_broken = comm_broken || (rcs[g] == MI355_ERR_COMM && !outs[g].peer_fail);
+    if (comm_broken && kind == MI355_TRANSPORT_RCCL) {
+        T.reset();
+        drop_comms_all(G);
+    }
+    // report the rank that failed first-hand, not the peers that followed it
+    int first = -1;
+    for (int g = 0; g < G; ++g)
+        if (rcs[g] != MI355_OK && (first < 0 || (outs[first].peer_fail && !outs[g].peer_fail))) first = g;
+    if (first >= 0) {
+        set_last_error("rank " + std::to_string(first) + ": " + errs[first]);
+        return rcs[first];
     }
     fill_stats(st, outs, G, kind, 0);
     return MI355_OK;
@@ -628,10 +801,22 @@ int join_multi(const row_t *R, uint64_t nR, const row_t *S, uint64_t nS, int G, 
 thread_local mi355_multi_stats t_last_multi{};
 
 // ---------------------------------------------------------------- one process per GPU
+// comm carries the tuples, ccomm (ncclCommSplit of comm, same ranks) the counts, flags
+// and reductions.  broken: a transport call failed; both were aborted.
 struct CommHandle {
     int world = 0, rank = 0, device = 0;
-    ncclComm_t comm = nullptr;
+    ncclComm_t comm = nullptr, ccomm = nullptr;
+    bool broken = false;
     std::unique_ptr<RcclTransport> T;
+    void abort_comms() {
+        T.reset();
+        for (ncclComm_t *c : {&comm, &ccomm})
+            if (*c && rccl().CommAbort) {
+                (void)rccl().CommAbort(*c);
+                *c = nullptr;
+            }
+        broken = true;
+    }
 };
 
 }  // namespace multi
@@ -692,6 +877,30 @@ int mi355_rho_join_multi(const table_t *relR, const table_t *relS, const joincon
 
 void mi355_multi_set_pieces(int pieces) { multi::g_pieces = std::max(1, std::min(64, pieces)); }
 
+int mi355_multi_release(void) {
+    std::lock_guard<std::mutex> lk(multi::g_reh_mu);
+    int cur = 0;
+    MH_HIP(hipGetDevice(&cur));
+    int rc = MI355_OK;
+    for (auto &kv : multi::g_reh) {
+        Context *ctx = kv.second.get();
+        std::lock_guard<std::mutex> ck(ctx->mu);
+        if (hipSetDevice(ctx->device) != hipSuccess || hipStreamSynchronize(ctx->stream) != hipSuccess) {
+            set_last_error("mi355_multi_release: device synchronisation failed");
+            rc = MI355_ERR_HIP;
+            break;
+        }
+        release_workspace(ctx);
+    }
+    (void)hipSetDevice(cur);
+    return rc;
+}
+
+void mi355_multi_inject_failure(int rank, int step) {
+    multi::g_fail_step = step;
+    multi::g_fail_rank = step > 0 ? rank : -1;
+}
+
 int mi355_multi_unique_id(void *id128) {
     if (!id128) return MI355_ERR_INVALID;
     MH_RC(multi::require_rccl());
@@ -714,8 +923,14 @@ int mi355_multi_comm_init(const void *id128, int nranks, int rank, void **comm) 
     ncclUniqueId id;
     std::memcpy(&id, id128, sizeof(id));
     MH_NCCL(multi::rccl().CommInitRank(&h->comm, nranks, id, rank));
+    const ncclResult_t sr = multi::rccl().CommSplit(h->comm, 0, rank, &h->ccomm, nullptr);
+    if (sr != ncclSuccess) {
+        set_last_error(std::string("ncclCommSplit (count communicator): ") + multi::rccl().ErrorString(sr));
+        h->abort_comms();
+        return MI355_ERR_COMM;
+    }
     h->T = std::make_unique<multi::RcclTransport>(nranks, rank, std::vector<ncclComm_t>{h->comm},
-                                                  std::vector<int>{h->device});
+                                                  std::vector<ncclComm_t>{h->ccomm}, nullptr);
     *comm = h.release();
     return MI355_OK;
 }
@@ -724,7 +939,8 @@ int mi355_multi_comm_destroy(void *comm) {
     auto *h = static_cast<multi::CommHandle *>(comm);
     if (!h) return MI355_OK;
     h->T.reset();
-    if (h->comm && multi::rccl().CommDestroy) (void)multi::rccl().CommDestroy(h->comm);
+    for (ncclComm_t c : {h->ccomm, h->comm})
+        if (c && multi::rccl().CommDestroy) (void)multi::rccl().CommDestroy(c);
     delete h;
     return MI355_OK;
 }
@@ -744,15 +960,33 @@ int mi355_rho_join_sharded(void *comm, const row_t *R, uint64_t nR, const row_t 
         set_last_error("mi355_rho_join_sharded: key_shift and materialize must be 0");
         return MI355_ERR_INVALID;
     }
+    if (h->broken) {
+        set_last_error("mi355_rho_join_sharded: the communicator was aborted after a failed RCCL call");
+        return MI355_ERR_COMM;
+    }
     MH_HIP(hipSetDevice(h->device));
     int status = MI355_OK;
     Context *ctx = current_context(&status);
-    if (!ctx) return status;
-    std::lock_guard<std::mutex> lk(ctx->mu);
     std::vector<multi::RankOut> outs(1);
-    // the caller's stream (opts->stream or mi355_set_stream): R and S were produced there
-    hipStream_t s = thread_stream(ctx, opts ? opts->stream : nullptr);
-    MH_RC(multi::rank_join(*h->T, h->rank, ctx, s, R, nR, S, nS, opts, outs[0]));
+    int rc;
+    if (!ctx) {  // take part in the collectives, flagged as failed
+        rc = multi::rank_join(*h->T, h->rank, nullptr, nullptr, nullptr, 0, nullptr, 0, opts, outs[0], status);
+    } else {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        // the caller's stream (opts->stream or mi355_set_stream): R and S were produced there
+        hipStream_t s = thread_stream(ctx, opts ? opts->stream : nullptr);
+        rc = multi::rank_join(*h->T, h->rank, ctx, s, R, nR, S, nS, opts, outs[0]);
+    }
+    if (rc != MI355_OK) {
+        // a failed RCCL call leaves unmatched operations behind: abort this rank's
+        // communicators (the peers' calls fail or are torn down with the job)
+        if (rc == MI355_ERR_COMM && !outs[0].peer_fail) {
+            const std::string e = last_error();
+            h->abort_comms();
+            set_last_error(e);
+        }
+        return rc;
+    }
     mi355_multi_stats local{};
     mi355_multi_stats *st = stats ? stats : &local;
     multi::fill_stats(st, outs, h->world, MI355_TRANSPORT_RCCL, h->rank);

@@ -172,6 +172,17 @@ std::unique_ptr<Context> make_context(int device, int *status) {
     return ctx;
 }
 
+void release_workspace(Context *ctx) {
+    for (DeviceBuffer *b : {&ctx->inR, &ctx->inS, &ctx->t1R, &ctx->t1S, &ctx->t2R, &ctx->t2S, &ctx->sideR, &ctx->sideS,
+                            &ctx->scratch.buf, &ctx->mat, &ctx->tp_mask, &ctx->tp_blk, &ctx->tp_trip, &ctx->scan_in,
+                            &ctx->scan_out, &ctx->scan_aux, &ctx->scan_dict, &ctx->xsendR, &ctx->xsendS, &ctx->xrecvR,
+                            &ctx->xrecvS})
+        b->release();
+    for (DeviceBuffer &b : ctx->tp_cols) b.release();
+    for (DeviceBuffer &b : ctx->tp_rel) b.release();
+    ctx->scratch.reset();
+}
+
 hipStream_t thread_stream(Context *ctx, void *explicit_stream) {
     if (explicit_stream) return static_cast<hipStream_t>(explicit_stream);
     if (t_stream) return static_cast<hipStream_t>(t_stream);

@@ -105,6 +105,10 @@ Context *current_context(int *status);
 // The caller keeps it for the process lifetime.  nullptr (last error set) on failure.
 std::unique_ptr<Context> make_context(int device, int *status);
 
+// Frees every workspace buffer of ctx (the caller holds ctx->mu and no work is pending
+// on its streams); later calls allocate again.
+void release_workspace(Context *ctx);
+
 Timer &thread_timer();
 Timer &thread_side_timer();
 // Lazily created side stream and fork/join/total events of ctx (nullptr on failure).

@@ -227,6 +227,8 @@ SIGNATURES = {
                                          C.POINTER(multi_stats)]),
     "mi355_last_multi_stats": (C.c_int, [C.POINTER(multi_stats)]),
     "mi355_multi_set_pieces": (None, [C.c_int]),
+    "mi355_multi_inject_failure": (None, [C.c_int, C.c_int]),
+    "mi355_multi_release": (C.c_int, []),
     # scan.h
     "mi355_scan_count_u8": (C.c_int, [C.c_uint8, C.c_uint8, _P, C.c_size_t, _U64P]),
     "mi355_scan_count_i32": (C.c_int, [C.c_int32, C.c_int32, _P, C.c_size_t, _U64P]),
@@ -432,6 +434,17 @@ def rho_join_sharded(handle: int, R, nR: int, S, nS: int, *, algorithm: str = "R
 
 def multi_set_pieces(pieces: int) -> None:
     lib.mi355_multi_set_pieces(pieces)
+
+
+def multi_release() -> None:
+    """Free the rehearsal ranks' workspaces (mi355_multi_release)."""
+    _check(lib.mi355_multi_release())
+
+
+def multi_inject_failure(rank: int, step: int) -> None:
+    """Test hook: `rank` fails at `step` (1 buffers, 2 a shard pass, 3 the local join) of
+    every later multi-GPU join; step 0 clears it."""
+    lib.mi355_multi_inject_failure(rank, step)
 
 
 def rho_join_tables(R, nR: int, S, nS: int, nthreads: int = 1, materialize: bool = False,

@@ -37,9 +37,11 @@ HIP library; tests inject CPU restatements to run the exchange logic on gloo.
 With the "nccl" backend (RCCL) and device tensors the whole pipeline runs in C++
 (sgxamd/multi.h, mi355_rho_join_sharded): this module only hands rank 0's RCCL unique
 id to the other ranks and calls the library, whose rank pipeline is the one above
-(pieced shard partition, all-gather of the piece counts, send/recv of the tuples on a
-communication stream, pipelined local join, all-reduce).  SGXAMD_DIST_IMPL=python keeps
-the torch.distributed implementation below, which the gloo tests also exercise.
+(pieced shard partition, all-gather of the piece counts on a second communicator,
+send/recv of the tuples on a communication stream, pipelined local join, all-reduce).
+If it fails, every rank raises (there is no silent fallback).  SGXAMD_DIST_IMPL=python
+selects the torch.distributed implementation below explicitly; the gloo tests
+exercise it.
 """
 from __future__ import annotations
 
@@ -222,23 +224,51 @@ def _post_exchange(dst: torch.Tensor, src: torch.Tensor, send_counts: list[int],
 
 
 _comms: dict = {}
-_cxx_failed: list = []
+
+
+def _agree_ok(ok: bool, group) -> bool:
+    """True on every rank iff `ok` on every rank (a MAX all-reduce of the failure flag on
+    the host-side count group)."""
+    flag = torch.tensor([0 if ok else 1], dtype=torch.int64)
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=_count_group(group))
+    return int(flag.item()) == 0
 
 
 def _cxx_comm(group) -> int:
-    """This rank's RCCL communicator of the C++ path for `group` (collective on first use)."""
+    """This rank's RCCL communicator of the C++ path for `group` (collective on first use).
+
+    Rank 0's unique id travels with its error, if any, so a failure there ends the call
+    on every rank; after the communicator init every rank agrees on the outcome before
+    any rank returns a handle (a rank that raised alone would leave its peers waiting in
+    the join's first collective)."""
     key = id(group)
     if key not in _comms:
         rank = dist.get_rank(group)
-        obj = [multi_unique_id() if rank == 0 else None]
+        obj = [None]
+        if rank == 0:
+            try:
+                obj[0] = ("ok", multi_unique_id())
+            except Mi355Error as e:
+                obj[0] = ("error", str(e))
         src = dist.get_global_rank(group, 0) if group is not None else 0
         dist.broadcast_object_list(obj, src=src, group=group)
-        _comms[key] = multi_comm_init(obj[0], dist.get_world_size(group), rank)
+        status, payload = obj[0]
+        if status != "ok":
+            raise Mi355Error(f"sgxamd.dist: rank 0 could not create the RCCL unique id: {payload}")
+        handle, err = None, None
+        try:
+            handle = multi_comm_init(payload, dist.get_world_size(group), rank)
+        except Mi355Error as e:
+            err = e
+        if not _agree_ok(err is None, group):
+            raise Mi355Error(f"sgxamd.dist: RCCL communicator init failed on some rank"
+                             + (f" (this rank: {err})" if err else ""))
+        _comms[key] = handle
     return _comms[key]
 
 
 def _use_cxx(R: torch.Tensor, group, partition_fn, local_join_fn) -> bool:
-    return (R.is_cuda and partition_fn is None and local_join_fn is None and not _cxx_failed
+    return (R.is_cuda and partition_fn is None and local_join_fn is None
             and dist.get_backend(group) == "nccl" and os.environ.get("SGXAMD_DIST_IMPL", "cxx") == "cxx")
 
 
@@ -283,13 +313,12 @@ def sharded_rho_join(R: torch.Tensor, S: torch.Tensor, *, group=None, partition_
 
     if _use_cxx(R, group, partition_fn, local_join_fn):
         # RCCL through the C++ library; torch's stream is synchronised first (the library
-        # runs on its own streams unless mi355_set_stream named torch's)
+        # runs on its own streams unless mi355_set_stream named torch's).  A failure
+        # raises: the library fails every rank at the same collective step, so no rank
+        # is left inside a collective, and a failing product path never yields a number
+        # from a different implementation.
         torch.cuda.current_stream(R.device).synchronize()
-        try:
-            return _sharded_cxx(R, S, group, algorithm, chunks)
-        except Mi355Error as e:  # keep running on the torch.distributed path, and say so
-            print(f"sgxamd.dist: C++ RCCL path failed ({e}); using the torch.distributed path", file=sys.stderr)
-            _cxx_failed.append(str(e))
+        return _sharded_cxx(R, S, group, algorithm, chunks)
     cgroup = _count_group(group)
     # R piece by piece: each piece's exchange is in flight on the RCCL stream while the
     # next pieces (and then S) are shard-partitioned on the compute stream

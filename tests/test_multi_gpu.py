@@ -167,3 +167,97 @@ def test_rccl_comm_single_rank(sgx, orc, gpu):
         assert res.stats["transport"] == "rccl" and res.stats["world"] == 1
     finally:
         sgx.multi_comm_destroy(h)
+
+
+@pytest.mark.parametrize("step", [1, 2, 3])
+def test_failure_on_one_rank(sgx, orc, gpu, step):
+    """A rank that fails (exchange buffers, a shard pass of S, its local join) flags it in
+    the next collective: every rank leaves the join at the same step, the call returns
+    the failed rank's own error (no rank is left waiting in a collective), and the next
+    join on the same transport is exact."""
+    R, S = sgx.reference_relations(1 << 17, (1 << 17) + 5)
+    exp = orc.rho_join(R, S, 4)[0]
+    sgx.multi_inject_failure(2, step)
+    try:
+        with pytest.raises(sgx.Mi355Error, match="rank 2: injected failure"):
+            multi(sgx, R, S, 4)
+    finally:
+        sgx.multi_inject_failure(-1, 0)
+    assert multi(sgx, R, S, 4).matches == exp
+
+
+def _slices_sent(keys, g, elem):
+    """Bytes a rank-sliced relation sends to other ranks: per slice (radix_join.cpp:1488-1499
+    slicing), every element whose low log2(g) key bits name another rank."""
+    import torch
+
+    n = keys.numel()
+    per = n // g
+    kept = 0
+    for r in range(g):
+        a, b = r * per, (n if r == g - 1 else (r + 1) * per)
+        kept += int(((keys[a:b] & (g - 1)) == r).sum().item())
+    return (n - kept) * elem
+
+
+def test_config4_rehearsal_full_size(sgx, gpu):
+    """BASELINE config 4 at its size through the 8-rank pipeline (rehearsal transport on one
+    MI355X): pk(2^27) join fk(2^30, maxid 2^27), device generators (native.cpp:62-101
+    shapes).  Exercises the receive capacity G*K*ceil(m/K) = 2^30 keys per rank (4 GiB,
+    byte offsets past 2^32), the keys-only plan decision and the local S-heavy plan with
+    key_shift 3.  matches == |S|; every rank receives exactly 2^24 R and 2^27 S keys (8
+    copies of its 1/8 of 1..2^27); 4-byte keys on the wire, the exact bytes."""
+    import torch
+
+    nR, nS, g = 1 << 27, 1 << 30, 8
+    R = torch.empty(nR, dtype=torch.int64, device=gpu)
+    S = torch.empty(nS, dtype=torch.int64, device=gpu)
+    sgx.gen_pk_dev(R, nR, 0, nR, 11111)
+    sgx.gen_fk_dev(S, nS, 0, nR, 22222)
+    try:
+        res = sgx.rho_join_multi(R, nR, S, nS, g, transport="rehearsal")
+        st = res.stats
+        assert res.matches == nS
+        assert st["world"] == g and st["elem_bytes"] == 4 and st["local"]["layout"] == 2
+        assert st["recv_r_max"] == st["recv_r_min"] == nR // g
+        assert st["recv_s_max"] == st["recv_s_min"] == nS // g
+        sent = _slices_sent(R & 0xFFFFFFFF, g, 4) + _slices_sent(S & 0xFFFFFFFF, g, 4)
+        assert st["sent_bytes"] == sent
+        assert abs(sent - 4 * (nR + nS) * 7 / 8) < 4 * (nR + nS) * 0.001
+        print(f"c4 rehearsal G=8: {st['ms_total']:.2f} ms, local plan {st['local']['radix_bits']} bits, "
+              f"sent {st['sent_bytes'] / 1e9:.3f} GB")
+    finally:
+        del R, S
+        sgx.multi_release()
+        torch.cuda.empty_cache()
+
+
+def test_config5_rehearsal_full_size(sgx, gpu):
+    """BASELINE config 5 at its size through the 8-rank pipeline: pk(2^28) join the host
+    mt19937_64 seed-22222 Zipf(0.75) stream over 1..2^28 (generator.cpp restating
+    genzipf.cpp:87-144), staged once to HBM.  matches == |S| (every Zipf key is an R key);
+    the load report: the hot keys land where their low 3 bits say, so the received S
+    per rank is uneven (reported as max / mean)."""
+    import torch
+
+    n, g = 1 << 28, 8
+    R = torch.empty(n, dtype=torch.int64, device=gpu)
+    sgx.gen_pk_dev(R, n, 0, n, 11111)
+    host = np.empty(n, dtype=np.int64)
+    sgx.gen_zipf(host, n, n, 0.75, 22222, 16)
+    S = torch.from_numpy(host).to(gpu)
+    del host
+    try:
+        res = sgx.rho_join_multi(R, n, S, n, g, transport="rehearsal")
+        st = res.stats
+        assert res.matches == n
+        assert st["elem_bytes"] == 4
+        assert st["recv_r_max"] == st["recv_r_min"] == n // g
+        per_rank = torch.bincount((S & (g - 1)).to(torch.int64), minlength=g)
+        assert st["recv_s_max"] == int(per_rank.max()) and st["recv_s_min"] == int(per_rank.min())
+        print(f"c5 rehearsal G=8: {st['ms_total']:.2f} ms, recv_s max/mean "
+              f"{st['recv_s_max'] / (n / g):.3f}, max S partition {st['max_part_s']}")
+    finally:
+        del R, S
+        sgx.multi_release()
+        torch.cuda.empty_cache()
