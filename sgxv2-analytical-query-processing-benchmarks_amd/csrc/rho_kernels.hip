@@ -1855,6 +1855,279 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_join_tag(
     if (red_ticket) join_reduce_last(counts, cyc, red_result, red_ticket, L.red);
 }
 
+// ------------------------------ 16,384-key counting table with exchange links (X) ---
+// bucket_chaining_join (:359-458) for counting joins with one LDS word per bucket and
+// one per R key, each a link that carries the tag of the entry it points to:
+//   head[b]  = (i + 1) | tag(i) << 16 for the last R key i inserted into bucket b, 0 = empty;
+//   link[i]  = head[b] as it was before i was inserted (the next entry and its tag).
+// The build is one LDS exchange and one LDS store per R key (no compare-and-swap
+// retries: a 32-bit head is swapped whole); a chain step of the probe is one LDS read,
+// which yields the next entry's index and tag together, so a probe costs 1 + chain
+// length reads (the 80 KiB tagged table reads head, tag and next: 1 + 2 x chain).
+// link is indexed by the 1-based entry, so a finished walk (w = 0) reads link[0] = 0 and
+// every chain step is branch-free.
+// Tags are the 16 key bits above the bucket bits: with hash_shift + log2 N + 16 >= 32
+// they are all remaining key bits and tag equality is key equality; otherwise a tag
+// match is confirmed against the R key (an L2 hit).  128 KiB per table: one 1,024-thread
+// workgroup per CU, so the keys stream in strips of UP per thread with the next strip's
+// buffer loads in flight while one is inserted or probed, across task boundaries (the
+// 80 KiB table instead overlaps two workgroups' phases).
+template <int RCAP, int NW>
+struct JoinLdsX {
+    uint32_t head[RCAP];
+    uint32_t link[RCAP + 1];  // 1-based: link[0] = 0, the end of every chain, is never written
+    uint64_t red[NW + 2];
+};
+
+__device__ __forceinline__ uint32_t key_tag16(uint32_t k, uint32_t tshift) {
+    return tshift >= 32 ? 0u : ((k >> tshift) & 0xFFFFu);
+}
+
+// Workgroup-uniform position in the workgroup's stream of key strips: task t (grid
+// stride), its R chunk rc, phase 0 (R keys, build) or 1 (S keys, probe), strip offset;
+// r_base / s_base: the element index of the task's R chunk / S range.
+struct XCursor {
+    uint64_t t, nR, nS, rc, off, r_base, s_base;
+    uint32_t phase;
+};
+
+__device__ __forceinline__ uint64_t uni_u64(uint64_t v) {  // a uniform value kept in SGPRs
+    return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+           __builtin_amdgcn_readfirstlane((uint32_t)v);
+}
+
+struct XTasks {
+    const uint64_t *r_start, *r_count, *s_start, *s_count, *over;
+    uint64_t P, T, s_chunk;
+};
+
+template <int RCAP>
+__device__ __forceinline__ uint32_t x_nrc(const XCursor &c) {
+    const uint64_t d = c.nR - c.rc;
+    return d < (uint64_t)RCAP ? (uint32_t)d : (uint32_t)RCAP;
+}
+
+// the first task at or after c.t with work (c.t >= T: none)
+__device__ __forceinline__ void x_seek(XCursor &c, const XTasks &k) {
+    for (; c.t < k.T; c.t += gridDim.x) {
+        uint64_t p, chunk;
+        decode_task(uni_u64(c.t), k.P, k.over, p, chunk);
+        p = uni_u64(p);
+        chunk = uni_u64(chunk);
+        const uint64_t nR = uni_u64(k.r_count[p]), nSp = uni_u64(k.s_count[p]);
+        const uint64_t s_lo = chunk * k.s_chunk;
+        const uint64_t rem = nSp > s_lo ? nSp - s_lo : 0;
+        const uint64_t nS = nR == 0 ? 0 : (rem < k.s_chunk ? rem : k.s_chunk);
+        if (nS) {
+            c.nR = nR;
+            c.nS = nS;
+            c.rc = 0;
+            c.off = 0;
+            c.phase = 0;
+            c.r_base = uni_u64(k.r_start[p]);
+            c.s_base = uni_u64(k.s_start[p]) + s_lo;
+            return;
+        }
+    }
+}
+
+template <int RCAP, uint32_t STRIP>
+__device__ __forceinline__ void x_advance(XCursor &c, const XTasks &k) {
+    c.off += STRIP;
+    if (c.phase == 0) {
+        if (c.off >= x_nrc<RCAP>(c)) {
+            c.phase = 1;
+            c.off = 0;
+        }
+    } else if (c.off >= c.nS) {
+        c.rc += RCAP;
+        c.off = 0;
+        c.phase = 0;
+        if (c.rc >= c.nR) {
+            c.t += gridDim.x;
+            x_seek(c, k);
+        }
+    }
+}
+
+// The strip's keys through a buffer resource over exactly its elements: lanes past the
+// end read 0 (hardware bounds check), so every load is issued unconditionally and the
+// wait for a strip never covers the loads of the strip after it.
+template <int RCAP, int BLOCK, int UP, int KS>
+__device__ __forceinline__ void x_load(const XCursor &c, const XTasks &k, const uint32_t *rkeys,
+                                       const uint32_t *skeys, uint32_t (&v)[UP]) {
+    constexpr uint32_t STRIP = BLOCK * UP;
+    uint64_t base = 0, n = 0;
+    const uint32_t *src = rkeys;
+    if (c.t < k.T) {
+        if (c.phase == 0) {
+            base = c.r_base + c.rc + c.off;
+            n = x_nrc<RCAP>(c) - c.off;
+        } else {
+            src = skeys;
+            base = c.s_base + c.off;
+            n = c.nS - c.off;
+        }
+    }
+    const uint32_t cnt = n < STRIP ? (uint32_t)n : STRIP;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(src + base * KS, cnt * 4u * KS);
+#pragma unroll
+    for (int u = 0; u < UP; ++u)
+        v[u] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)((threadIdx.x + u * BLOCK) * 4u * KS), 0, 2);
+}
+
+// One strip: clear the table at a chunk's first R strip, insert (phase 0) or probe
+// (phase 1) the strip's keys; a barrier after a chunk's last R strip (nx: the strip
+// after this one).  Returns the strip's matches (this thread).
+template <int RCAP, int BLOCK, int UP, int KS>
+__device__ __forceinline__ uint32_t x_step(JoinLdsX<RCAP, BLOCK / kWave> &L, const XCursor &c, const XCursor &nx,
+                                           const uint32_t (&k)[UP], const uint32_t *rkeys, uint32_t hash_shift,
+                                           uint64_t &cyc2) {
+    const uint32_t tid = threadIdx.x;
+    const uint64_t c0 = wall_clock64();
+    const uint32_t nrc = x_nrc<RCAP>(c);
+    const uint32_t lgN = nrc <= 1 ? 0u : 32u - __builtin_clz(nrc - 1);  // N = NEXT_POW_2(numR)
+    const uint32_t hmask = (1u << lgN) - 1;
+    const uint32_t tshift = hash_shift + lgN;
+    uint32_t m = 0;
+    if (c.phase == 0) {  // BUILD-LOOP (:407-411)
+        if (c.off == 0) {
+            __syncthreads();  // the previous chunk's probe is done with the table
+            for (uint32_t i = tid; i < ((1u << lgN) + 3) / 4; i += BLOCK)
+                reinterpret_cast<uint4 *>(L.head)[i] = make_uint4(0, 0, 0, 0);
+            __syncthreads();
+        }
+        const uint32_t lim = nrc - (uint32_t)c.off;
+        if (lim >= BLOCK * UP) {  // a full strip: every exchange in flight before the link stores
+            uint32_t old[UP];
+#pragma unroll
+            for (int u = 0; u < UP; ++u) {
+                const uint32_t i = (uint32_t)c.off + tid + u * BLOCK;
+                old[u] = atomicExch(&L.head[(k[u] >> hash_shift) & hmask], (i + 1) | (key_tag16(k[u], tshift) << 16));
+            }
+#pragma unroll
+            for (int u = 0; u < UP; ++u) L.link[(uint32_t)c.off + tid + u * BLOCK + 1] = old[u];
+        } else {
+#pragma unroll
+            for (int u = 0; u < UP; ++u) {
+                const uint32_t j = tid + u * BLOCK;
+                if (j < lim) {
+                    const uint32_t i = (uint32_t)c.off + j;
+                    const uint32_t b = (k[u] >> hash_shift) & hmask;
+                    L.link[i + 1] = atomicExch(&L.head[b], (i + 1) | (key_tag16(k[u], tshift) << 16));
+                }
+            }
+        }
+        if (nx.phase != 0 || nx.t != c.t || nx.rc != c.rc) __syncthreads();  // the chunk's table is complete
+    } else {  // PROBE-LOOP (:429-436)
+        const uint64_t lim = c.nS - c.off;
+        uint32_t w[UP];
+#pragma unroll
+        for (int u = 0; u < UP; ++u) {
+            const uint32_t h = L.head[(k[u] >> hash_shift) & hmask];
+            w[u] = vsel(tid + u * BLOCK < lim, h, 0u);
+        }
+        if (tshift + 16 >= 32) {
+            // the tag is every remaining key bit: chain steps without branches, all UP link
+            // reads in flight at once (a finished walk re-reads link[0], a broadcast)
+            bool more = true;
+            while (more) {
+                more = false;
+#pragma unroll
+                for (int u = 0; u < UP; ++u) {
+                    const uint32_t x = w[u];
+                    m += (x != 0 && (x >> 16) == key_tag16(k[u], tshift)) ? 1u : 0u;
+                    w[u] = L.link[x & 0xFFFFu];
+                    more |= w[u] != 0;
+                }
+            }
+        } else {  // a tag match is confirmed against the R key (an L2 hit)
+            const uint32_t *rkc = rkeys + (c.r_base + c.rc) * KS;
+            bool more = true;
+            while (more) {
+                more = false;
+#pragma unroll
+                for (int u = 0; u < UP; ++u) {
+                    if (w[u] != 0) {
+                        const uint32_t e = w[u] & 0xFFFFu;
+                        if ((w[u] >> 16) == key_tag16(k[u], tshift) && rkc[KS * (e - 1)] == k[u]) ++m;
+                        w[u] = L.link[e];
+                        more |= w[u] != 0;
+                    }
+                }
+            }
+        }
+    }
+    cyc2 = wall_clock64() - c0;
+    return m;
+}
+
+template <int RCAP, int BLOCK, int UP, int KS = 1>
+__global__ __launch_bounds__(BLOCK, 1) void k_join_x(
+    const uint64_t *__restrict__ R, const uint64_t *__restrict__ S, const uint64_t *__restrict__ r_start,
+    const uint64_t *__restrict__ r_count, const uint64_t *__restrict__ s_start, const uint64_t *__restrict__ s_count,
+    uint64_t P, const uint64_t *__restrict__ over, const uint32_t *__restrict__ n_over, uint32_t hash_shift,
+    uint64_t s_chunk, uint64_t *__restrict__ counts, uint64_t *__restrict__ cyc, uint64_t *__restrict__ red_result,
+    uint64_t *__restrict__ red_ticket, uint32_t ncounts) {
+    constexpr int NW = BLOCK / kWave;
+    constexpr uint32_t STRIP = BLOCK * UP;
+    __shared__ JoinLdsX<RCAP, NW> L;
+    const uint32_t tid = threadIdx.x, lane = __lane_id();
+    const XTasks tk{r_start, r_count, s_start, s_count, over, P, uni_u64(P + *n_over), s_chunk};
+    const uint32_t *rkeys = reinterpret_cast<const uint32_t *>(R);
+    const uint32_t *skeys = reinterpret_cast<const uint32_t *>(S);
+    uint64_t matches = 0, bcyc = 0, pcyc = 0;
+    if (tid == 0) L.link[0] = 0;  // visible after the first build strip's barriers
+
+    XCursor ca{(uint64_t)blockIdx.x, 0, 0, 0, 0, 0, 0, 0}, cb{};
+    x_seek(ca, tk);
+    uint32_t ka[UP], kb[UP];
+    x_load<RCAP, BLOCK, UP, KS>(ca, tk, rkeys, skeys, ka);
+    // two register sets, the loop unrolled by two so that no set is ever copied (a copy
+    // of a set still in flight would wait for it); the empty asm uses wait for a set
+    // right after the next set's loads are issued, in straight-line code, where the
+    // compiler's wait count is exactly UP
+    while (ca.t < tk.T) {
+        cb = ca;
+        x_advance<RCAP, STRIP>(cb, tk);
+        x_load<RCAP, BLOCK, UP, KS>(cb, tk, rkeys, skeys, kb);
+#pragma unroll
+        for (int u = 0; u < UP; ++u) asm volatile("" ::"v"(ka[u]));
+        uint64_t dt;
+        matches += x_step<RCAP, BLOCK, UP, KS>(L, ca, cb, ka, rkeys, hash_shift, dt);
+        bcyc += ca.phase == 0 ? dt : 0;
+        pcyc += ca.phase == 0 ? 0 : dt;
+        if (cb.t >= tk.T) break;
+        ca = cb;
+        x_advance<RCAP, STRIP>(ca, tk);
+        x_load<RCAP, BLOCK, UP, KS>(ca, tk, rkeys, skeys, ka);
+#pragma unroll
+        for (int u = 0; u < UP; ++u) asm volatile("" ::"v"(kb[u]));
+        matches += x_step<RCAP, BLOCK, UP, KS>(L, cb, ca, kb, rkeys, hash_shift, dt);
+        bcyc += cb.phase == 0 ? dt : 0;
+        pcyc += cb.phase == 0 ? 0 : dt;
+    }
+    matches = wave_sum_u64(matches);
+    __syncthreads();
+    if (lane == 0) L.red[tid / kWave] = matches;
+    __syncthreads();
+    if (tid == 0) {
+        uint64_t acc = 0;
+        for (int w = 0; w < NW; ++w) acc += L.red[w];
+        counts[blockIdx.x] = acc;
+    }
+    if (cyc && tid == 0) {
+        cyc[2 * blockIdx.x] = bcyc;
+        cyc[2 * blockIdx.x + 1] = pcyc;
+    }
+    // the grid is one workgroup per CU; the caller's count slots past it read as 0
+    for (uint32_t i = gridDim.x + blockIdx.x * BLOCK + tid; i < ncounts; i += gridDim.x * BLOCK) {
+        counts[i] = 0;
+        if (cyc) cyc[2 * i] = cyc[2 * i + 1] = 0;
+    }
+    if (red_ticket) join_reduce_last(counts, cyc, red_result, red_ticket, L.red);
+}
+
 // ------------------------------------------------------- histogram join (RHT) ---
 // histogram_join (radix_join.cpp:463-612), the build/probe of RHT (:1645-1648), per
 // task in LDS.  For an R chunk of nrc tuples: Nhist = max(nextpow2(nrc) / 4, 4)
@@ -2060,6 +2333,27 @@ __global__ __launch_bounds__(kBlock) void k_join_hist(const uint64_t *__restrict
     }
 }
 
+// SGXAMD_XJOIN (development A/B switch, read once): strip width UP of the exchange-link
+// table k_join_x (8 or 16 keys per thread); 0 = the 80 KiB tagged table.
+int x_join_up() {
+    static const int up = [] {
+        const char *e = std::getenv("SGXAMD_XJOIN");
+        const int v = e ? std::atoi(e) : 0;
+        return v == 8 || v == 16 ? v : 0;
+    }();
+    return up;
+}
+uint32_t cu_count() {
+    static const uint32_t n = [] {
+        int dev = 0, v = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+            v = 256;
+        return (uint32_t)v;
+    }();
+    return n;
+}
+
 // Counting build/probe over packed keys (key-only partitions, KS = 1).
 hipError_t launch_join_keys(const void *R, const void *S, const uint64_t *r_start, const uint64_t *r_count,
                             const uint64_t *s_start, const uint64_t *s_count, uint64_t P, const uint64_t *over,
@@ -2089,6 +2383,16 @@ hipError_t launch_join_keys(const void *R, const void *S, const uint64_t *r_star
         return hipGetLastError();
     }
     if (algo != kAlgoChaining) return hipErrorInvalidValue;
+    if (rcap == kBigRcap && x_join_up()) {
+        const uint32_t g = std::min<uint32_t>(grid, cu_count());
+        if (x_join_up() == 16)
+            hipLaunchKernelGGL((k_join_x<kBigRcap, 1024, 16, 1>), dim3(g), dim3(1024), 0, s, R64, S64, r_start, r_count,
+                               s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts, cyc, rres, rtick, grid);
+        else
+            hipLaunchKernelGGL((k_join_x<kBigRcap, 1024, 8, 1>), dim3(g), dim3(1024), 0, s, R64, S64, r_start, r_count,
+                               s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts, cyc, rres, rtick, grid);
+        return hipGetLastError();
+    }
     if (rcap == kBigRcap) {
         static const int tag_block = [] {
             const char *e = std::getenv("SGXAMD_TAG_JOIN");
@@ -2150,6 +2454,18 @@ hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, 
         // one 16,384-tuple chain table per 1,024-thread workgroup: all 160 KiB of LDS
         // (plain counting only; the materialising table carries 4 B more per tuple)
         if (mode != kJoinCount) return hipErrorInvalidValue;
+        if (x_join_up()) {
+            const uint32_t g = std::min<uint32_t>(grid, cu_count());
+            if (x_join_up() == 16)
+                hipLaunchKernelGGL((k_join_x<kBigRcap, 1024, 16, 2>), dim3(g), dim3(1024), 0, s, R64, S64, r_start,
+                                   r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts, cyc, rres,
+                                   rtick, grid);
+            else
+                hipLaunchKernelGGL((k_join_x<kBigRcap, 1024, 8, 2>), dim3(g), dim3(1024), 0, s, R64, S64, r_start,
+                                   r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts, cyc, rres,
+                                   rtick, grid);
+            return hipGetLastError();
+        }
         // SGXAMD_TAG_JOIN (development A/B switch, read once): 1024 (default) / 512 = the
         // 80 KiB tagged table (two workgroups per CU) with that many threads; 0 = the
         // 160 KiB table, one 1,024-thread workgroup per CU.  2^28 build/probe, one box,
