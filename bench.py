@@ -473,6 +473,33 @@ def main():
             }
             del Rw, Sw
             torch.cuda.empty_cache()
+        # config 2 on the reference's own relations (native.cpp:62-101: glibc rand() Knuth
+        # shuffles, seeds 11111 / 22222, generated on the host by the restated generator
+        # and staged to HBM), beside the device-generated headline: untimed for value
+        if world == 1:
+            n2 = 1 << args.log2n
+            t_gen = time.perf_counter()
+            Rh, Sh = sgxamd.reference_relations(n2, n2)
+            gen_s = time.perf_counter() - t_gen
+            Rr = torch.from_numpy(Rh.view(np.int64)).to(dev)
+            Sr = torch.from_numpy(Sh.view(np.int64)).to(dev)
+            del Rh, Sh
+            res_r, pk_r, el_r = measure_rho("c2", Rr, Sr, n2, n2)
+            avg_r = {k: statistics.mean(v) for k, v in pk_r.items()}
+            ls_r = res_r[-1].local_stats
+            configs_info["c2_reference_relations"] = {
+                "workload": f"RHO join |R|=|S|=2^{args.log2n}, the reference's generators (BASELINE config 2)",
+                "generator": f"host glibc-rand Knuth shuffles restated (generator.cpp:100-153), seeds 11111 / "
+                             f"22222, {gen_s:.1f} s, staged to HBM",
+                "timed": "untimed for value; own K steps", "matches": res_r[-1].matches, "matches_ok": True,
+                "ms_per_step": round(el_r / args.steps * 1e3, 4),
+                "M_probed_tuples_per_s": round(n2 * args.steps / el_r / 1e6, 1),
+                "radix_bits": ls_r.get("radix_bits"), "passes": ls_r.get("passes"),
+                "partition_layout": LAYOUTS.get(ls_r.get("layout"), "unknown"),
+                "kernel_ms_avg": {k: round(v, 4) for k, v in sorted(avg_r.items())},
+            }
+            del Rr, Sr
+            torch.cuda.empty_cache()
     # BASELINE config 1's shape (|R| = |S| = 2^20, reference generators) on one GPU: the
     # small-join latency next to the CPU number of the same config (cpu_baseline.rho.config1)
     c1_gpu = None
@@ -637,16 +664,30 @@ def main():
             for _ in range(max(1, args.warmup)):
                 run()
             barrier()
+            kt = {}
             t1 = time.perf_counter()
             for _ in range(args.steps):
                 run()
+                for name, ms in sgxamd.timings():
+                    kt.setdefault(name, []).append(ms)
             barrier()
             el = (time.perf_counter() - t1) / args.steps
             gib = nu / el / 2**30
+            k_avg = {k: round(statistics.mean(v), 4) for k, v in kt.items()}
+            # the dominant kernel's roofline: column bytes + its output (bitvector n/8 B,
+            # index list 8 B per match), over its HIP-event time
+            main = "scan_bitvector" if kind.startswith("bitvector") else max(k_avg, key=k_avg.get, default=None)
+            out_b = nu // 8 if kind.startswith("bitvector") else 8 * k10
+            kroof = None
+            if main and k_avg.get(main):
+                gbs = (nu + out_b) / (k_avg[main] * 1e-3) / 1e9
+                kroof = {"kernel": main, "bytes": nu + out_b, "ms": k_avg[main], "achieved": round(gbs, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4)}
             paper_info[f"scan_u8_{kind}"] = {"entries": nu, "predicate": [0, hi], "GiB_per_s": round(gib, 1),
                                              "ms": round(el * 1e3, 4), "reference_GiB_per_s": ref,
                                              "reference": f"Xeon Gold 6326, 16 threads, native ({src})",
-                                             "ratio": round(gib / ref, 1)}
+                                             "ratio": round(gib / ref, 1), "kernel_ms_avg": k_avg,
+                                             "kernel_roofline": kroof}
         del col, bvu, idxu
         torch.cuda.empty_cache()
 

@@ -593,3 +593,29 @@ def test_golden_join_counts(sgx, gpu):
     R = relation(sgx, f"pk_{z['n']}_11111")
     assert gpu_join(sgx, R, Z).matches == z["pk_join_matches"]
     assert gpu_join(sgx, Z, Z).matches == z["self_join_matches"]
+
+
+def test_config2_reference_relations_full_size(sgx, gpu):
+    """BASELINE config 2 on the reference's own relations at full size: pk(2^28, seed
+    11111) and fk(2^28, seed 22222) from the restated glibc rand() Knuth shuffles
+    (native.cpp:62-101, generator.cpp:100-153), generated on the host and staged to HBM.
+    matches == |S|, and the plan is the device relations' one: 14 radix bits in two
+    passes, key partitions, every R and S partition exactly 2^14 keys (pk 1..2^28 and a
+    permutation of it: each key's low 14 bits once per 2^14)."""
+    import torch
+
+    n = 1 << 28
+    Rh, Sh = sgx.reference_relations(n, n)
+    assert int(Rh["key"][:8].min()) >= 1 and int(Rh["key"].max()) == n
+    R = torch.from_numpy(Rh.view(np.int64)).to(gpu)
+    S = torch.from_numpy(Sh.view(np.int64)).to(gpu)
+    del Rh, Sh
+    try:
+        res = sgx.rho_join(R, n, S, n)
+        st = res.stats
+        assert res.matches == n
+        assert (st["radix_bits"], st["passes"], st["layout"]) == (14, 2, 2)
+        assert st["max_part_r"] == st["max_part_s"] == 1 << 14
+    finally:
+        del R, S
+        torch.cuda.empty_cache()
