@@ -28,6 +28,7 @@ ALIASES = {
     "k_hist_side_blk": ["R_pass2_hist", "S_pass2_hist"],
     "k_join": ["join_build_probe"],
     "k_join_tag": ["join_build_probe"],
+    "k_join_x": ["join_build_probe"],
     "k_predicate": ["scan_count", "scan_bitvector"],
     "k_expand": ["scan_expand_index"],
     "k_select": ["scan_select_index"],

@@ -151,7 +151,6 @@ constexpr uint64_t kSChunk = 8192;
 // 1,024-thread workgroup (160 KiB of LDS) and 32,768-tuple S chunks, so that neither
 // side is read twice at the 2^30-tuple sizes.
 constexpr uint32_t kBigRcap = 16384;
-constexpr int kBigJoinBlock = 1024;
 constexpr uint64_t kBigSChunk = 32768;
 // S tuples per partition the planner aims at with the big table; partitions that large
 // on average are probed in chunks of this size (one task per partition when uniform)

@@ -1711,150 +1711,6 @@ __global__ __launch_bounds__(BLOCK) void k_join(const uint64_t *__restrict__ R, 
     }
 }
 
-// ------------------------------------------- 16,384-tuple counting table in 80 KiB ---
-// The counting join of bucket_chaining_join (:359-458) with the chain table of one R
-// chunk packed into half a CU's LDS, so that two workgroups share a CU and overlap
-// each other's phases (R load, head clear, build, probe), which a single 160 KiB
-// table per CU leaves serial:
-//   head[N]  u16, 1-based (0 = empty), two per 32-bit word; the build links tuple i
-//            with a compare-and-swap on its bucket's word (LDS has no 16-bit exchange);
-//   next[i]  u16, 1-based;
-//   tag[i]   u8 = the key bits [hash_shift + log2 N, +8).
-// Inside a task every key agrees on the bits below hash_shift (the radix partition,
-// and the rank bits of a shard exchange) and inside a chain on the bucket bits
-// [hash_shift, hash_shift + log2 N), so with hash_shift + log2 N + 8 >= 32 the tag
-// holds all remaining key bits and tag equality is key equality (2^28 tuples at 14
-// radix bits: 14 + 14 + 4).  Otherwise a tag match is confirmed against the R key,
-// re-read from the partitioned relation (an L2 hit).
-template <int RCAP, int NW>
-struct JoinLdsTag {
-    union {
-        __attribute__((aligned(16))) uint32_t head2[RCAP / 2];
-        uint64_t red[NW + 2];
-    };
-    uint16_t next[RCAP];
-    uint8_t tag[RCAP];
-};
-
-__device__ __forceinline__ uint32_t key_tag(uint32_t k, uint32_t tshift) {
-    return tshift >= 32 ? 0u : ((k >> tshift) & 0xFFu);
-}
-
-// Each thread builds and probes in strips of UP tuples (UP chain walks in lock step).
-template <int RCAP, int BLOCK, int UP, int KS = 2>
-__global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_join_tag(
-    const uint64_t *__restrict__ R, const uint64_t *__restrict__ S, const uint64_t *__restrict__ r_start,
-    const uint64_t *__restrict__ r_count, const uint64_t *__restrict__ s_start, const uint64_t *__restrict__ s_count,
-    uint64_t P, const uint64_t *__restrict__ over, const uint32_t *__restrict__ n_over, uint32_t hash_shift,
-    uint64_t s_chunk, uint64_t *__restrict__ counts, uint64_t *__restrict__ cyc, uint64_t *__restrict__ red_result,
-    uint64_t *__restrict__ red_ticket) {
-    constexpr int NW = BLOCK / kWave;
-    constexpr uint32_t STRIP = BLOCK * UP;
-    __shared__ JoinLdsTag<RCAP, NW> L;
-    const uint32_t tid = threadIdx.x, lane = __lane_id();
-    const uint64_t T = P + *n_over;
-    uint64_t matches = 0;
-    uint64_t bcyc = 0, pcyc = 0;
-    for (uint64_t t = blockIdx.x; t < T; t += gridDim.x) {
-        uint64_t p, chunk;
-        decode_task(t, P, over, p, chunk);
-        const uint64_t nR = r_count[p], nSp = s_count[p];
-        const uint64_t s_lo = chunk * s_chunk;
-        const uint64_t nS = (nR == 0 || s_lo >= nSp) ? 0 : min<uint64_t>(nSp - s_lo, s_chunk);
-        if (nS == 0) continue;
-        // key = low word of a tuple (KS 2) or a packed key (KS 1)
-        const uint32_t *rk = reinterpret_cast<const uint32_t *>(R) + r_start[p] * KS;
-        const uint32_t *sk = reinterpret_cast<const uint32_t *>(S) + (s_start[p] + s_lo) * KS;
-        for (uint64_t rc = 0; rc < nR; rc += RCAP) {
-            const uint64_t c_build = wall_clock64();
-            const uint32_t nrc = (uint32_t)((nR - rc) < RCAP ? (nR - rc) : RCAP);
-            uint32_t lgN = 0;
-            while ((1u << lgN) < nrc) ++lgN;  // N = NEXT_POW_2(numR)
-            const uint32_t hmask = (1u << lgN) - 1;
-            const uint32_t tshift = hash_shift + lgN;
-            const bool exact = tshift + 8 >= 32;
-            const uint32_t *rkc = rk + KS * rc;
-            for (uint32_t i = tid; i < ((1u << lgN) + 7) / 8; i += BLOCK)
-                reinterpret_cast<uint4 *>(L.head2)[i] = make_uint4(0, 0, 0, 0);
-            __syncthreads();
-            for (uint32_t r0 = 0; r0 < nrc; r0 += STRIP) {  // BUILD-LOOP (:407-411)
-                uint32_t kr[UP];
-#pragma unroll
-                for (int u = 0; u < UP; ++u) {
-                    const uint32_t i = r0 + tid + u * BLOCK;
-                    kr[u] = i < nrc ? __builtin_nontemporal_load(rkc + KS * i) : 0u;
-                }
-#pragma unroll
-                for (int u = 0; u < UP; ++u) {
-                    const uint32_t i = r0 + tid + u * BLOCK;
-                    if (i < nrc) {
-                        const uint32_t k = kr[u];
-                        L.tag[i] = (uint8_t)key_tag(k, tshift);
-                        const uint32_t b = (k >> hash_shift) & hmask;
-                        const uint32_t sh = (b & 1u) * 16u;
-                        uint32_t *w = &L.head2[b >> 1];
-                        uint32_t old = *w;
-                        while (true) {
-                            const uint32_t nw = (old & ~(0xFFFFu << sh)) | ((i + 1) << sh);
-                            const uint32_t prev = atomicCAS(w, old, nw);
-                            if (prev == old) break;
-                            old = prev;
-                        }
-                        L.next[i] = (uint16_t)(old >> sh);
-                    }
-                }
-            }
-            __syncthreads();
-            const uint64_t c_probe = wall_clock64();
-            bcyc += c_probe - c_build;
-            for (uint64_t s0 = 0; s0 < nS; s0 += STRIP) {  // PROBE-LOOP (:429-436)
-                uint32_t ks[UP], cur[UP];
-#pragma unroll
-                for (int u = 0; u < UP; ++u) {
-                    const uint64_t i = s0 + tid + u * BLOCK;
-                    ks[u] = i < nS ? __builtin_nontemporal_load(sk + KS * i) : 0u;
-                }
-#pragma unroll
-                for (int u = 0; u < UP; ++u) {
-                    const uint64_t i = s0 + tid + u * BLOCK;
-                    const uint32_t b = (ks[u] >> hash_shift) & hmask;
-                    cur[u] = i < nS ? (L.head2[b >> 1] >> ((b & 1u) * 16u)) & 0xFFFFu : 0u;
-                }
-                bool more = true;
-                while (more) {
-                    more = false;
-#pragma unroll
-                    for (int u = 0; u < UP; ++u) {
-                        if (cur[u] != 0) {
-                            const uint32_t e = cur[u] - 1;
-                            if (L.tag[e] == key_tag(ks[u], tshift))
-                                tmatch_add(matches, exact || rkc[KS * e] == ks[u]);
-                            cur[u] = L.next[e];
-                            more |= cur[u] != 0;
-                        }
-                    }
-                }
-            }
-            __syncthreads();
-            pcyc += wall_clock64() - c_probe;
-        }
-    }
-    matches = wave_sum_u64(matches);
-    __syncthreads();
-    if (lane == 0) L.red[tid / kWave] = matches;
-    __syncthreads();
-    if (tid == 0) {
-        uint64_t acc = 0;
-        for (int w = 0; w < NW; ++w) acc += L.red[w];
-        counts[blockIdx.x] = acc;
-    }
-    if (cyc && tid == 0) {
-        cyc[2 * blockIdx.x] = bcyc;
-        cyc[2 * blockIdx.x + 1] = pcyc;
-    }
-    if (red_ticket) join_reduce_last(counts, cyc, red_result, red_ticket, L.red);
-}
-
 // ------------------------------ 16,384-key counting table with exchange links (X) ---
 // bucket_chaining_join (:359-458) for counting joins with one LDS word per bucket and
 // one per R key, each a link that carries the tag of the entry it points to:
@@ -2333,16 +2189,7 @@ __global__ __launch_bounds__(kBlock) void k_join_hist(const uint64_t *__restrict
     }
 }
 
-// SGXAMD_XJOIN (development A/B switch, read once): strip width UP of the exchange-link
-// table k_join_x (8 or 16 keys per thread); 0 = the 80 KiB tagged table.
-int x_join_up() {
-    static const int up = [] {
-        const char *e = std::getenv("SGXAMD_XJOIN");
-        const int v = e ? std::atoi(e) : 0;
-        return v == 8 || v == 16 ? v : 0;
-    }();
-    return up;
-}
+// Multiprocessors of the current device: k_join_x runs one workgroup per CU.
 uint32_t cu_count() {
     static const uint32_t n = [] {
         int dev = 0, v = 0;
@@ -2383,31 +2230,10 @@ hipError_t launch_join_keys(const void *R, const void *S, const uint64_t *r_star
         return hipGetLastError();
     }
     if (algo != kAlgoChaining) return hipErrorInvalidValue;
-    if (rcap == kBigRcap && x_join_up()) {
-        const uint32_t g = std::min<uint32_t>(grid, cu_count());
-        if (x_join_up() == 16)
-            hipLaunchKernelGGL((k_join_x<kBigRcap, 1024, 16, 1>), dim3(g), dim3(1024), 0, s, R64, S64, r_start, r_count,
-                               s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts, cyc, rres, rtick, grid);
-        else
-            hipLaunchKernelGGL((k_join_x<kBigRcap, 1024, 8, 1>), dim3(g), dim3(1024), 0, s, R64, S64, r_start, r_count,
-                               s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts, cyc, rres, rtick, grid);
-        return hipGetLastError();
-    }
-    if (rcap == kBigRcap) {
-        static const int tag_block = [] {
-            const char *e = std::getenv("SGXAMD_TAG_JOIN");
-            return e ? std::atoi(e) : 1024;
-        }();
-        if (tag_block == 512)
-            hipLaunchKernelGGL((k_join_tag<kBigRcap, 512, 16, 1>), dim3(grid), dim3(512), 0, s, R64, S64, r_start,
-                               r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts, cyc, rres, rtick);
-        else if (tag_block == 1024)
-            hipLaunchKernelGGL((k_join_tag<kBigRcap, 1024, 8, 1>), dim3(grid), dim3(1024), 0, s, R64, S64, r_start,
-                               r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts, cyc, rres, rtick);
-        else
-            hipLaunchKernelGGL((k_join<kBigRcap, kJoinCount, kBigJoinBlock, 1>), dim3(grid), dim3(kBigJoinBlock), 0, s,
-                               R64, S64, r_start, r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk,
-                               counts, nullptr, nullptr, cyc, rres, rtick);
+    if (rcap == kBigRcap) {  // one workgroup per CU (128 KiB table), strips of 8 keys per thread
+        hipLaunchKernelGGL((k_join_x<kBigRcap, 1024, 8, 1>), dim3(std::min<uint32_t>(grid, cu_count())), dim3(1024), 0,
+                           s, R64, S64, r_start, r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts,
+                           cyc, rres, rtick, grid);
         return hipGetLastError();
     }
 #define KEYS_CASE(RC)                                                                                                   case RC:                                                                                                                hipLaunchKernelGGL((k_join<RC, kJoinCount, kBlock, 1>), dim3(grid), dim3(kBlock), 0, s, R64, S64, r_start,                            r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts, nullptr, nullptr,                             cyc, rres, rtick);                                                                               break;
@@ -2451,39 +2277,12 @@ hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, 
                 return hipErrorInvalidValue;
         }
     } else if (rcap == kBigRcap) {
-        // one 16,384-tuple chain table per 1,024-thread workgroup: all 160 KiB of LDS
-        // (plain counting only; the materialising table carries 4 B more per tuple)
+        // the 16,384-tuple counting table (k_join_x: 128 KiB, one workgroup per CU;
+        // plain counting only, the materialising table carries 4 B more per tuple)
         if (mode != kJoinCount) return hipErrorInvalidValue;
-        if (x_join_up()) {
-            const uint32_t g = std::min<uint32_t>(grid, cu_count());
-            if (x_join_up() == 16)
-                hipLaunchKernelGGL((k_join_x<kBigRcap, 1024, 16, 2>), dim3(g), dim3(1024), 0, s, R64, S64, r_start,
-                                   r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts, cyc, rres,
-                                   rtick, grid);
-            else
-                hipLaunchKernelGGL((k_join_x<kBigRcap, 1024, 8, 2>), dim3(g), dim3(1024), 0, s, R64, S64, r_start,
-                                   r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts, cyc, rres,
-                                   rtick, grid);
-            return hipGetLastError();
-        }
-        // SGXAMD_TAG_JOIN (development A/B switch, read once): 1024 (default) / 512 = the
-        // 80 KiB tagged table (two workgroups per CU) with that many threads; 0 = the
-        // 160 KiB table, one 1,024-thread workgroup per CU.  2^28 build/probe, one box,
-        // alternating: 0.849-0.851 ms (0), 0.794-0.796 (512), 0.696-0.698 (1024)
-        static const int tag_block = [] {
-            const char *e = std::getenv("SGXAMD_TAG_JOIN");
-            return e ? std::atoi(e) : 1024;
-        }();
-        if (tag_block == 512)
-            hipLaunchKernelGGL((k_join_tag<kBigRcap, 512, 16>), dim3(grid), dim3(512), 0, s, R64, S64, r_start, r_count,
-                               s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts, cyc, rres, rtick);
-        else if (tag_block == 1024)
-            hipLaunchKernelGGL((k_join_tag<kBigRcap, 1024, 8>), dim3(grid), dim3(1024), 0, s, R64, S64, r_start, r_count,
-                               s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts, cyc, rres, rtick);
-        else
-            hipLaunchKernelGGL((k_join<kBigRcap, kJoinCount, kBigJoinBlock>), dim3(grid), dim3(kBigJoinBlock), 0, s,
-                               R64, S64, r_start, r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk,
-                               counts, task_off, out, cyc, rres, rtick);
+        hipLaunchKernelGGL((k_join_x<kBigRcap, 1024, 8, 2>), dim3(std::min<uint32_t>(grid, cu_count())), dim3(1024), 0,
+                           s, R64, S64, r_start, r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts,
+                           cyc, rres, rtick, grid);
     } else if (mode == kJoinCount && grid <= 512 && rcap <= 4096) {
         // few tasks (small joins: one workgroup per CU at most): 1,024 threads per table
         // instead of 256, so that a CU holds 16 waves to hide the load latencies

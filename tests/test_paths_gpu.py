@@ -3,15 +3,12 @@ SGXAMD_DIGIT_SIDE=0 (pass-2 histograms over the tuples instead of the digit side
 stream), SGXAMD_BIG_JOIN=0 (R partitions above 8192 tuples in 8192-tuple chain tables
 instead of the 16,384-tuple counting table; the 5-bit plan below has 32,768-tuple
 partitions) and SGXAMD_SCAN_ONEPASS=0 (index / value / dictionary scans as bitvector
-pass + expand pass instead of the one-pass look-back selection), SGXAMD_TAG_JOIN=0 / 512
-(the 16,384-tuple counting table as one 160 KiB table per CU, or the 80 KiB tagged
-table with 512 threads, instead of the tagged table with 1,024), SGXAMD_SMALL_JOIN=0
+pass + expand pass instead of the one-pass look-back selection), SGXAMD_SMALL_JOIN=0
 (small one-pass joins on the regular launch sequence instead of the three-launch path:
 the (5, 1) plan and the full-range cases below take it), SGXAMD_POOL=0 (two-pass plans
 with a pass-1 histogram and cursors instead of the pooled pass 1 and block-list pass 2;
 SGXAMD_POOL_SEGS sets the pooled pass-1 workgroups: 3 gives large pools, 100000 one
-tile per segment), SGXAMD_KEYS=0 (counting joins move whole tuples instead of keys),
-SGXAMD_XJOIN=8 / 16 (the exchange-link counting table, 8 or 16 keys per thread and strip).  The switches are read
+tile per segment), SGXAMD_KEYS=0 (counting joins move whole tuples instead of keys).  The switches are read
 once per process, so each setting runs in a child process against the oracle (the
 TPC-H selections ride along: they share the library's workspace)."""
 import os
@@ -68,10 +65,9 @@ print("paths ok")
 
 @pytest.mark.parametrize("env", [{"SGXAMD_DIGIT_SIDE": "0", "SGXAMD_SCAN_ONEPASS": "0", "SGXAMD_BIG_JOIN": "0"},
                                  {"SGXAMD_DIGIT_SIDE": "1", "SGXAMD_SCAN_ONEPASS": "1", "SGXAMD_BIG_JOIN": "1"},
-                                 {"SGXAMD_TAG_JOIN": "0"}, {"SGXAMD_TAG_JOIN": "512"}, {"SGXAMD_SMALL_JOIN": "0"},
+                                 {"SGXAMD_SMALL_JOIN": "0"},
                                  {"SGXAMD_POOL": "0"}, {"SGXAMD_POOL_SEGS": "3"}, {"SGXAMD_POOL_SEGS": "100000"},
-                                 {"SGXAMD_KEYS": "0"}, {"SGXAMD_XJOIN": "8"}, {"SGXAMD_XJOIN": "16"},
-                                 {"SGXAMD_XJOIN": "8", "SGXAMD_KEYS": "0"}])
+                                 {"SGXAMD_KEYS": "0"}])
 def test_switch_paths_match_oracle(env):
     e = dict(os.environ, **env)
     e["PYTHONPATH"] = os.pathsep.join([os.path.join(PKG, "python"), os.path.join(ROOT, "oracle"),
