@@ -178,6 +178,12 @@ void mi355_set_key_layout(int on);
 /* Stream used by calls that take no explicit stream (NULL = library stream). */
 void mi355_set_stream(void *stream);
 
+/* Frees the current device's workspace (partition buffers, scratch, staging, scan and
+ * TPC-H buffers) after the work queued on its library stream has finished; the next
+ * call allocates again.  The workspace is otherwise grow-only and kept for the
+ * process.  MI355_ERR_INVALID while a pipelined join is pending. */
+int mi355_release_workspace(void);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

@@ -49,11 +49,10 @@ inline bool big_join_enabled() {
     return on;
 }
 
-// Counting RHO joins (no materialisation) build partitions above 8192 R tuples in
-// kBigRcap-tuple LDS tables; the other modes in 8192-tuple chunks.
-inline bool uses_big_table(const mi355_rho_opts *o) {
-    return !(o && (o->materialize || o->algorithm == MI355_ALGO_RHT)) && big_join_enabled();
-}
+// Counting joins (no materialisation; RHO's chain table k_join_x, RHT's bucket table
+// k_join_hist<kBigRcap>) build partitions above 8192 R tuples in kBigRcap-tuple LDS
+// tables; materialising joins in 8192-tuple chunks.
+inline bool uses_big_table(const mi355_rho_opts *o) { return !(o && o->materialize) && big_join_enabled(); }
 // The caller left the radix bits to the planner (an explicit plan keeps its tables).
 inline bool opts_free_bits(const mi355_rho_opts *o) { return !(o && o->radix_bits > 0); }
 
@@ -815,6 +814,20 @@ thread_local mi355_rho_stats g_last_stats{};
 void rho::set_last_join_stats(const mi355_rho_stats &st) { g_last_stats = st; }
 
 extern "C" {
+
+int mi355_release_workspace(void) {
+    int status = MI355_OK;
+    Context *ctx = current_context(&status);
+    if (!ctx) return status;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (rho::pending_of(ctx).active) {
+        set_last_error("mi355_release_workspace: a pipelined join is pending");
+        return MI355_ERR_INVALID;
+    }
+    RHO_HIP(hipStreamSynchronize(ctx->stream));
+    release_workspace(ctx);
+    return MI355_OK;
+}
 
 int mi355_last_join_stats(mi355_rho_stats *out) {
     if (!out) return MI355_ERR_INVALID;

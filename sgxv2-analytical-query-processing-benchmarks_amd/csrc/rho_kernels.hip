@@ -10,6 +10,8 @@
 // Radix digits are taken as (key >> shift) & (F - 1) with the pass-1 digit in the
 // low bits, exactly like HASH_BIT_MODULO(key, MASK, R) (:47) with R = shift.
 // All work is integer; HBM bandwidth is the roofline.
+#include <type_traits>
+
 #include "common.hpp"
 #include "rho_internal.hpp"
 
@@ -1747,9 +1749,13 @@ struct XCursor {
     uint32_t phase;
 };
 
-__device__ __forceinline__ uint64_t uni_u64(uint64_t v) {  // a uniform value kept in SGPRs
-    return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
-           __builtin_amdgcn_readfirstlane((uint32_t)v);
+// A uniform value kept in SGPRs.  readfirstlane returns int: each half goes through
+// uint32_t, or a low word >= 2^31 would sign-extend over the high word (element
+// indices past 2^31: test_max_size_pk_fk).
+__device__ __forceinline__ uint64_t uni_u64(uint64_t v) {
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+    return ((uint64_t)hi << 32) | lo;
 }
 
 struct XTasks {
@@ -1807,8 +1813,9 @@ __device__ __forceinline__ void x_advance(XCursor &c, const XTasks &k) {
 }
 
 // The strip's keys through a buffer resource over exactly its elements: lanes past the
-// end read 0 (hardware bounds check), so every load is issued unconditionally and the
-// wait for a strip never covers the loads of the strip after it.
+// end read 0 (hardware bounds check, applied to the VGPR offset, which therefore holds
+// the whole offset), so every load is issued unconditionally and the wait for a strip
+// never covers the loads of the strip after it.
 template <int RCAP, int BLOCK, int UP, int KS>
 __device__ __forceinline__ void x_load(const XCursor &c, const XTasks &k, const uint32_t *rkeys,
                                        const uint32_t *skeys, uint32_t (&v)[UP]) {
@@ -1994,14 +2001,14 @@ __global__ __launch_bounds__(BLOCK, 1) void k_join_x(
 // with its bucket's contiguous run [off[b], off[b+1]) (:574-600).  The reference's
 // unrolled re-order tail drops the "+ 1" of the bucket index (:556-560); that slip
 // is not restated here, every R tuple lands in its own bucket.
-template <int RCAP, int MODE>
+template <int RCAP, int MODE, int NW = kWaves>
 struct HistJoinLds {
     static constexpr int NB = RCAP / 4;  // max buckets of one chunk
     uint32_t off[NB + 1];
     uint32_t keys[RCAP];
     uint32_t rpay[MODE == kJoinWrite ? RCAP : 1];
     uint32_t cursor;
-    uint64_t red[kWaves + 2];
+    uint64_t red[NW + 2];
 };
 
 // Element i of a partitioned relation: an 8-byte tuple (KS 2) or a 4-byte key (KS 1,
@@ -2012,8 +2019,11 @@ __device__ __forceinline__ uint64_t ld_elem_nt(const uint64_t *base, uint64_t i)
     else return __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(base) + i);
 }
 
-template <int RCAP, int MODE, int KS = 2>
-__global__ __launch_bounds__(kBlock) void k_join_hist(const uint64_t *__restrict__ R, const uint64_t *__restrict__ S,
+// BLOCK threads per table: kBlock (256) for tables up to 8192 tuples; 1024 for the
+// 16,384-key counting table (80 KiB: keys + 4,097 bucket offsets, two workgroups per CU),
+// which probes in strips of 8 S keys per thread to stay within 64 VGPRs.
+template <int RCAP, int MODE, int KS = 2, int BLOCK = kBlock>
+__global__ __launch_bounds__(BLOCK) void k_join_hist(const uint64_t *__restrict__ R, const uint64_t *__restrict__ S,
                                                       const uint64_t *__restrict__ r_start,
                                                       const uint64_t *__restrict__ r_count,
                                                       const uint64_t *__restrict__ s_start,
@@ -2026,10 +2036,14 @@ __global__ __launch_bounds__(kBlock) void k_join_hist(const uint64_t *__restrict
                                                       uint64_t *__restrict__ red_result,
                                                       uint64_t *__restrict__ red_ticket) {
     static_assert(KS == 2 || MODE == kJoinCount, "key partitions carry no payloads");
-    constexpr int U = RCAP / kBlock;
-    constexpr int NB = HistJoinLds<RCAP, MODE>::NB;
-    __shared__ HistJoinLds<RCAP, MODE> L;
-    __shared__ uint64_t scan_scratch[kWaves + 1];
+    constexpr int NW = BLOCK / kWave;
+    constexpr int U = RCAP / BLOCK;
+    constexpr int UP = (BLOCK == kBlock || U < 8) ? U : 8;  // S keys per thread and probe strip
+    constexpr int NB = HistJoinLds<RCAP, MODE, NW>::NB;
+    // R elements held across the histogram scan: the key (and the payload when writing)
+    using RT = typename std::conditional<MODE == kJoinWrite, uint64_t, uint32_t>::type;
+    __shared__ HistJoinLds<RCAP, MODE, NW> L;
+    __shared__ uint64_t scan_scratch[NW + 1];
     const uint32_t tid = threadIdx.x, lane = __lane_id();
     const uint64_t T = P + *n_over;
     uint64_t matches = 0;
@@ -2054,24 +2068,24 @@ __global__ __launch_bounds__(kBlock) void k_join_hist(const uint64_t *__restrict
                 uint32_t nh = N >> 2;
                 if (nh < 4) nh = 4;  // get_hist_size
                 const uint32_t hmask = nh - 1;
-                uint64_t kr[U];
+                RT kr[U];
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
-                    const uint32_t i = tid + u * kBlock;
-                    kr[u] = i < nrc ? ld_elem_nt<KS>(R, r0 + rc + i) : 0ull;
+                    const uint32_t i = tid + u * BLOCK;
+                    kr[u] = i < nrc ? (RT)ld_elem_nt<KS>(R, r0 + rc + i) : (RT)0;
                 }
-                for (uint32_t i = tid; i <= nh; i += kBlock) L.off[i] = 0;
+                for (uint32_t i = tid; i <= nh; i += BLOCK) L.off[i] = 0;
                 __syncthreads();
                 uint32_t slot[U];
 #pragma unroll
                 for (int u = 0; u < U; ++u) {  // HISTOGRAM CREATION (:489-517)
-                    const uint32_t i = tid + u * kBlock;
+                    const uint32_t i = tid + u * BLOCK;
                     if (i < nrc) slot[u] = atomicAdd(&L.off[((uint32_t)kr[u] >> hash_shift) & hmask], 1u);
                 }
                 __syncthreads();
                 {  // prefix sum on histogram (:520-524): thread tid owns buckets [tid*E, tid*E + E)
-                    const uint32_t E = (nh + kBlock - 1) / kBlock;
-                    uint32_t loc[NB / kBlock > 0 ? NB / kBlock : 1];
+                    const uint32_t E = (nh + BLOCK - 1) / BLOCK;
+                    uint32_t loc[NB / BLOCK > 0 ? NB / BLOCK : 1];
                     uint32_t sum = 0;
                     for (uint32_t j = 0; j < E; ++j) {
                         const uint32_t b = tid * E + j;
@@ -2090,7 +2104,7 @@ __global__ __launch_bounds__(kBlock) void k_join_hist(const uint64_t *__restrict
                 __syncthreads();
 #pragma unroll
                 for (int u = 0; u < U; ++u) {  // BUILD PHASE: re-order (:527-561)
-                    const uint32_t i = tid + u * kBlock;
+                    const uint32_t i = tid + u * BLOCK;
                     if (i < nrc) {
                         const uint32_t pos = L.off[((uint32_t)kr[u] >> hash_shift) & hmask] + slot[u];
                         L.keys[pos] = (uint32_t)kr[u];
@@ -2100,19 +2114,19 @@ __global__ __launch_bounds__(kBlock) void k_join_hist(const uint64_t *__restrict
                 __syncthreads();
                 const uint64_t c_probe = wall_clock64();
                 bcyc += c_probe - c_build;
-                for (uint64_t s0 = 0; s0 < nS; s0 += RCAP) {  // PROBE PHASE (:570-600)
-                    uint32_t ks[U], j[U], end[U];
-                    uint32_t sv[MODE == kJoinWrite ? U : 1];
+                for (uint64_t s0 = 0; s0 < nS; s0 += (uint64_t)UP * BLOCK) {  // PROBE PHASE (:570-600)
+                    uint32_t ks[UP], j[UP], end[UP];
+                    uint32_t sv[MODE == kJoinWrite ? UP : 1];
 #pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        const uint64_t i = s0 + tid + u * kBlock;
+                    for (int u = 0; u < UP; ++u) {
+                        const uint64_t i = s0 + tid + u * BLOCK;
                         const uint64_t x = i < nS ? ld_elem_nt<KS>(S, sb + i) : 0ull;
                         ks[u] = (uint32_t)x;
                         if constexpr (MODE == kJoinWrite) sv[u] = (uint32_t)(x >> 32);
                     }
 #pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        const uint64_t i = s0 + tid + u * kBlock;
+                    for (int u = 0; u < UP; ++u) {
+                        const uint64_t i = s0 + tid + u * BLOCK;
                         const uint32_t b = (ks[u] >> hash_shift) & hmask;
                         j[u] = i < nS ? L.off[b] : 0u;
                         end[u] = i < nS ? L.off[b + 1] : 0u;
@@ -2121,7 +2135,7 @@ __global__ __launch_bounds__(kBlock) void k_join_hist(const uint64_t *__restrict
                     while (more) {
                         more = false;
 #pragma unroll
-                        for (int u = 0; u < U; ++u) {
+                        for (int u = 0; u < UP; ++u) {
                             if constexpr (MODE == kJoinWrite) {
                                 const bool live = j[u] < end[u];
                                 const bool m = live && L.keys[j[u]] == ks[u];
@@ -2161,7 +2175,7 @@ __global__ __launch_bounds__(kBlock) void k_join_hist(const uint64_t *__restrict
             __syncthreads();
             if (tid == 0) {
                 uint64_t acc = 0;
-                for (int w = 0; w < kWaves; ++w) acc += L.red[w];
+                for (int w = 0; w < NW; ++w) acc += L.red[w];
                 counts[t] = acc;
             }
             __syncthreads();
@@ -2176,7 +2190,7 @@ __global__ __launch_bounds__(kBlock) void k_join_hist(const uint64_t *__restrict
         __syncthreads();
         if (tid == 0) {
             uint64_t acc = 0;
-            for (int w = 0; w < kWaves; ++w) acc += L.red[w];
+            for (int w = 0; w < NW; ++w) acc += L.red[w];
             counts[blockIdx.x] = acc;
         }
     }
@@ -2187,6 +2201,161 @@ __global__ __launch_bounds__(kBlock) void k_join_hist(const uint64_t *__restrict
     if constexpr (MODE == kJoinCount) {
         if (red_ticket) join_reduce_last(counts, cyc, red_result, red_ticket, L.red);
     }
+}
+
+// RHT counting join (histogram_join :463-612) with 16,384-key tables in 72 KiB, two
+// 1,024-thread workgroups per CU: the R keys of a chunk re-ordered bucket-contiguous
+// (keys[16384], 64 KiB), bucket offsets as u16 (<= 16,384; 8 KiB), and the histogram's
+// u32 counters in the keys' space until the scan has turned them into offsets.  The
+// planner then gives RHT the same 14-bit plan as RHO at 2^28 with one table per
+// partition (the 8192-tuple table builds each partition in two chunks and probes every
+// S key twice).  8 waves per SIMD (64 VGPRs).  Each thread keeps its 16 R keys and their in-bucket ranks (two u16 per
+// register) across the scan; the probe walks strips of 8 S keys per thread.
+template <int KS>
+__global__ __launch_bounds__(1024, 8) void k_join_hist_big(
+    const uint64_t *__restrict__ R, const uint64_t *__restrict__ S, const uint64_t *__restrict__ r_start,
+    const uint64_t *__restrict__ r_count, const uint64_t *__restrict__ s_start, const uint64_t *__restrict__ s_count,
+    uint64_t P, const uint64_t *__restrict__ over, const uint32_t *__restrict__ n_over, uint32_t hash_shift,
+    uint64_t s_chunk, uint64_t *__restrict__ counts, uint64_t *__restrict__ cyc, uint64_t *__restrict__ red_result,
+    uint64_t *__restrict__ red_ticket) {
+    constexpr int RCAP = kBigRcap, BLOCK = 1024, NW = BLOCK / kWave, U = RCAP / BLOCK, UP = 8, NB = RCAP / 4;
+    struct Lds {
+        union {
+            uint32_t hist[NB];  // bucket counters (histogram creation, :489-517)
+            uint32_t keys[RCAP];
+        };
+        uint16_t off[NB + 1];
+        uint64_t red[NW + 2];  // block scan scratch, then the reduction
+    };
+    __shared__ Lds L;
+    const uint32_t tid = threadIdx.x, lane = __lane_id();
+    const uint64_t T = P + *n_over;
+    uint64_t matches = 0, bcyc = 0, pcyc = 0;
+    for (uint64_t t = blockIdx.x; t < T; t += gridDim.x) {
+        uint64_t p, chunk;
+        decode_task(uni_u64(t), P, over, p, chunk);
+        p = uni_u64(p);
+        chunk = uni_u64(chunk);
+        const uint64_t nR = uni_u64(r_count[p]), nSp = uni_u64(s_count[p]);
+        const uint64_t s_lo = chunk * s_chunk;
+        const uint64_t nS = (nR == 0 || s_lo >= nSp) ? 0 : min<uint64_t>(nSp - s_lo, s_chunk);
+        if (nS == 0) continue;
+        const uint64_t r0 = uni_u64(r_start[p]), sb = uni_u64(s_start[p]) + s_lo;
+        for (uint64_t rc = 0; rc < nR; rc += RCAP) {
+            const uint64_t c_build = wall_clock64();
+            const uint32_t nrc = (uint32_t)((nR - rc) < RCAP ? (nR - rc) : RCAP);
+            uint32_t N = 1;
+            while (N < nrc) N <<= 1;
+            const uint32_t nh = N >> 2 < 4 ? 4u : N >> 2;  // get_hist_size
+            const uint32_t hmask = nh - 1;
+            // buffer loads over the chunk: the whole offset in the VGPR (the hardware range
+            // check covers the VGPR offset, not the SGPR one), 0 past the chunk's end
+            const __amdgpu_buffer_rsrc_t rr =
+                make_rsrc(reinterpret_cast<const uint32_t *>(R) + (r0 + rc) * KS, nrc * 4u * KS);
+            uint32_t kr[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                kr[u] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rr, (int)((tid + u * BLOCK) * 4u * KS), 0, 2);
+            __syncthreads();  // the previous chunk's probe is done with keys / off
+            for (uint32_t i = tid; i < nh; i += BLOCK) L.hist[i] = 0;
+            __syncthreads();
+            uint32_t slot2[U / 2];  // in-bucket ranks, two u16 per register
+            const auto ranks = [&](auto full) {  // HISTOGRAM CREATION (:489-517)
+#pragma unroll
+                for (int u = 0; u < U; u += 2) {
+                    const uint32_t i = tid + u * BLOCK;
+                    const uint32_t a =
+                        (full || i < nrc) ? atomicAdd(&L.hist[(kr[u] >> hash_shift) & hmask], 1u) : 0u;
+                    const uint32_t b =
+                        (full || i + BLOCK < nrc) ? atomicAdd(&L.hist[(kr[u + 1] >> hash_shift) & hmask], 1u) : 0u;
+                    slot2[u / 2] = a | (b << 16);
+                }
+            };
+            // a full chunk (every chunk at 2^28) without per-item exec masks
+            if (nrc == (uint32_t)RCAP) ranks(std::true_type{});
+            else ranks(std::false_type{});
+            __syncthreads();
+            {  // prefix sum on histogram (:520-524): thread tid owns buckets [tid*E, tid*E + E)
+                const uint32_t E = (nh + BLOCK - 1) / BLOCK;
+                uint32_t loc[NB / BLOCK];
+                uint32_t sum = 0;
+#pragma unroll
+                for (uint32_t j = 0; j < (uint32_t)(NB / BLOCK); ++j) {
+                    const uint32_t b = tid * E + j;
+                    const uint32_t c = (j < E && b < nh) ? L.hist[b] : 0u;
+                    loc[j] = sum;
+                    sum += c;
+                }
+                uint64_t tot;
+                const uint32_t base = (uint32_t)block_excl_scan_u64(sum, L.red, &tot);
+#pragma unroll
+                for (uint32_t j = 0; j < (uint32_t)(NB / BLOCK); ++j) {
+                    const uint32_t b = tid * E + j;
+                    if (j < E && b < nh) L.off[b] = (uint16_t)(base + loc[j]);
+                }
+                if (tid == 0) L.off[nh] = (uint16_t)nrc;
+            }
+            __syncthreads();  // hist is dead: its space takes the keys
+            // the bucket addresses are recomputed here rather than kept from the histogram
+            // atomics across the scan (16 more live registers: spills at 64 VGPRs)
+#pragma unroll
+            for (int u = 0; u < U; ++u) asm volatile("" : "+v"(kr[u]));
+#pragma unroll
+            for (int u = 0; u < U; ++u) {  // BUILD PHASE: re-order (:527-561)
+                const uint32_t i = tid + u * BLOCK;
+                if (i < nrc) {
+                    const uint32_t sl = (slot2[u / 2] >> ((u & 1) * 16)) & 0xFFFFu;
+                    L.keys[L.off[(kr[u] >> hash_shift) & hmask] + sl] = kr[u];
+                }
+            }
+            __syncthreads();
+            const uint64_t c_probe = wall_clock64();
+            bcyc += c_probe - c_build;
+            for (uint64_t s0 = 0; s0 < nS; s0 += (uint64_t)UP * BLOCK) {  // PROBE PHASE (:570-600)
+                const uint32_t lim = (uint32_t)min<uint64_t>(nS - s0, (uint64_t)UP * BLOCK);
+                const __amdgpu_buffer_rsrc_t rs =
+                    make_rsrc(reinterpret_cast<const uint32_t *>(S) + (sb + s0) * KS, lim * 4u * KS);
+                uint32_t ks[UP], j[UP], end[UP];
+#pragma unroll
+                for (int u = 0; u < UP; ++u)
+                    ks[u] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)((tid + u * BLOCK) * 4u * KS), 0, 2);
+#pragma unroll
+                for (int u = 0; u < UP; ++u) {
+                    const uint32_t i = tid + u * BLOCK;
+                    const uint32_t b = (ks[u] >> hash_shift) & hmask;
+                    j[u] = i < lim ? L.off[b] : 0u;
+                    end[u] = i < lim ? L.off[b + 1] : 0u;
+                }
+                bool more = true;
+                while (more) {
+                    more = false;
+#pragma unroll
+                    for (int u = 0; u < UP; ++u) {
+                        if (j[u] < end[u]) {
+                            matches += (L.keys[j[u]] == ks[u]);
+                            ++j[u];
+                            more |= j[u] < end[u];
+                        }
+                    }
+                }
+            }
+            pcyc += wall_clock64() - c_probe;
+        }
+    }
+    matches = wave_sum_u64(matches);
+    __syncthreads();
+    if (lane == 0) L.red[tid / kWave] = matches;
+    __syncthreads();
+    if (tid == 0) {
+        uint64_t acc = 0;
+        for (int w = 0; w < NW; ++w) acc += L.red[w];
+        counts[blockIdx.x] = acc;
+    }
+    if (cyc && tid == 0) {
+        cyc[2 * blockIdx.x] = bcyc;
+        cyc[2 * blockIdx.x + 1] = pcyc;
+    }
+    if (red_ticket) join_reduce_last(counts, cyc, red_result, red_ticket, L.red);
 }
 
 // Multiprocessors of the current device: k_join_x runs one workgroup per CU.
@@ -2223,6 +2392,10 @@ hipError_t launch_join_keys(const void *R, const void *S, const uint64_t *r_star
             HIST_KEYS_CASE(2048)
             HIST_KEYS_CASE(4096)
             HIST_KEYS_CASE(8192)
+            case kBigRcap:
+                hipLaunchKernelGGL(k_join_hist_big<1>, dim3(grid), dim3(1024), 0, s, R64, S64, r_start, r_count,
+                                   s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts, cyc, rres, rtick);
+                break;
             default:
                 return hipErrorInvalidValue;
         }
@@ -2273,6 +2446,11 @@ hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, 
             JOIN_MODES(k_join_hist, 2048)
             JOIN_MODES(k_join_hist, 4096)
             JOIN_MODES(k_join_hist, 8192)
+            case kBigRcap:  // the 16,384-tuple table: counting only
+                if (mode != kJoinCount) return hipErrorInvalidValue;
+                hipLaunchKernelGGL(k_join_hist_big<2>, dim3(grid), dim3(1024), 0, s, R64, S64, r_start, r_count,
+                                   s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts, cyc, rres, rtick);
+                break;
             default:
                 return hipErrorInvalidValue;
         }

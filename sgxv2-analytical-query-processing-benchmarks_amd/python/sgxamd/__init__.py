@@ -229,6 +229,7 @@ SIGNATURES = {
     "mi355_multi_set_pieces": (None, [C.c_int]),
     "mi355_multi_inject_failure": (None, [C.c_int, C.c_int]),
     "mi355_multi_release": (C.c_int, []),
+    "mi355_release_workspace": (C.c_int, []),
     # scan.h
     "mi355_scan_count_u8": (C.c_int, [C.c_uint8, C.c_uint8, _P, C.c_size_t, _U64P]),
     "mi355_scan_count_i32": (C.c_int, [C.c_int32, C.c_int32, _P, C.c_size_t, _U64P]),
@@ -434,6 +435,11 @@ def rho_join_sharded(handle: int, R, nR: int, S, nS: int, *, algorithm: str = "R
 
 def multi_set_pieces(pieces: int) -> None:
     lib.mi355_multi_set_pieces(pieces)
+
+
+def release_workspace() -> None:
+    """Free the current device's workspace (mi355_release_workspace)."""
+    _check(lib.mi355_release_workspace())
 
 
 def multi_release() -> None:

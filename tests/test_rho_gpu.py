@@ -77,8 +77,8 @@ def test_random_with_duplicates(sgx, orc, gpu, seed, nR, nS, kmax):
 
 @pytest.mark.parametrize("bits,kmax", [(6, 1 << 22), (5, 2**32 - 1), (4, 1 << 19), (1, 1 << 12)])
 def test_big_table_partitions(sgx, orc, gpu, bits, kmax):
-    """Partitions above 8192 R tuples take the 16,384-tuple counting table (one
-    1,024-thread workgroup per CU, 32,768-tuple S chunks): |R| = 2^20 over 2^bits
+    """Partitions above 8192 R tuples take the 16,384-tuple counting tables (RHO's chain
+    table k_join_x, RHT's bucket table k_join_hist_big; 32,768-tuple S chunks): |R| = 2^20 over 2^bits
     partitions gives 16,384 (one table, ragged), 32,768 (two), 65,536 (four, duplicate
     keys) and 2^19 (32 tables, long chains, 16 S chunks per partition) R tuples per
     partition; the materialising join of the same plan keeps 8192-tuple chunks."""
@@ -91,6 +91,8 @@ def test_big_table_partitions(sgx, orc, gpu, bits, kmax):
     res = gpu_join(sgx, R, S, radix_bits=bits, passes=passes)
     assert res.matches == exp
     assert res.stats["max_part_r"] > 8192
+    # RHT's 16,384-key bucket table (k_join_hist_big): full and ragged chunks
+    assert gpu_join(sgx, R, S, radix_bits=bits, passes=passes, algorithm="RHT").matches == exp
     if bits == 6:
         got = gpu_triples(sgx, R, S, radix_bits=bits, passes=passes)
         assert np.array_equal(sorted_triples(got), sorted_triples(orc.rho_join_triples(R, S, 4)))
@@ -485,7 +487,7 @@ def test_rht_matches_oracle(sgx, orc, gpu, case):
         S = rel(np.concatenate([np.full(30_000, 3, np.uint32), rng.integers(0, 50_000, 40_000).astype(np.uint32)]))
     exp = orc.rht_join(R, S, 4)
     assert exp == orc.count_join_sort(R, S)
-    for bits, passes in [(0, 0), (5, 1), (13, 2)]:
+    for bits, passes in [(0, 0), (5, 1), (13, 2), (2, 1), (1, 1)]:  # (2, 1) / (1, 1): 16,384-key tables
         assert gpu_join(sgx, R, S, radix_bits=bits, passes=passes, algorithm="RHT").matches == exp
     if len(R) <= 1 << 16:
         got = gpu_triples(sgx, R, S, algorithm="RHT")
