@@ -1143,6 +1143,139 @@ __global__ __launch_bounds__(NT, (scatter_waves_per_simd<BITS, ITEMS, NT, 2, T>(
                                                                nullptr, 0, 0);
 }
 
+// ----------------------------------------- pass 2 of key partitions as an LDS sort ---
+// radix_cluster (:715-761) / the pass-2 partition_copy over the block list of a
+// segment, for 4-byte keys: each tile of TILE keys is counting-sorted by its pass-2
+// digit in LDS and written straight to the final partitions at the segment's cursors
+// (the pass-2 histogram + scan: cursors[g * F + d]).  Per key: one LDS atomic (rank),
+// one LDS read + write (placement), one LDS read of the sorted key and one 8-byte
+// read of its digit's offset, one 4-byte store; no carries and no granule
+// descriptors (k_scatter_blk's write combining).  The consecutive tiles of a segment
+// continue the same digit runs, so a line split between two tiles is completed by the
+// same workgroup moments later (in its XCD's L2); only the runs' ends at segment
+// boundaries are written as partial lines by two workgroups.  The next tile's keys
+// load while a tile is sorted and written (two register sets).
+template <int BITS, int NT, int ITEMS>
+struct SortBlkLds {
+    static constexpr uint32_t F = 1u << BITS, TILE = NT * ITEMS;
+    union {
+        uint32_t sbase[kMaxF + 1];  // segment table (seg_lookup, before the first tile)
+        uint32_t sorted[TILE];      // the tile's keys, digit-sorted
+    };
+    uint64_t ents[kPass2Ents];  // the segment's block list: physical block | fill << 32
+    uint64_t dbase[F];          // next output position of digit d in this segment
+    uint64_t off[F];            // destination of sorted position q with digit d: off[d] + q
+    uint32_t cnt[F];            // tile histogram (phase A), zero between tiles
+    uint32_t start[F];          // digit-sorted tile offset of d
+    uint32_t wsum[NT / kWave + 1];
+};
+
+// 6 waves per SIMD (84 VGPRs): three 512-thread workgroups per CU
+template <int BITS, int NT, int ITEMS>
+__global__ __launch_bounds__(NT, NT * 3 / 256) void k_sort_blk(const uint32_t *__restrict__ in, const uint64_t *__restrict__ list,
+                                                    uint32_t *__restrict__ out, SegMap m, uint32_t shift,
+                                                    const uint64_t *__restrict__ cursors) {
+    using LdsT = SortBlkLds<BITS, NT, ITEMS>;
+    constexpr uint32_t F = LdsT::F, TILE = LdsT::TILE, BPT = TILE / kBlk, mask = F - 1, NW = NT / kWave;
+    constexpr uint32_t WPB = kBlk / kWave;  // waves per block row: item u of wave w reads block u * (NT / kBlk) + w / WPB
+    static_assert(TILE % kBlk == 0 && NT % kBlk == 0 && F <= NT && ITEMS <= 16, "tile geometry");
+    __shared__ LdsT L;
+    const uint32_t tid = threadIdx.x, lane = __lane_id(), wave = tid / kWave;
+    const uint32_t g = blockIdx.x;
+    uint32_t r;
+    uint64_t b, e;
+    if (!seg_lookup(m, g, L.sbase, r, b, e)) return;
+    const uint32_t nent = (uint32_t)(e - b);  // <= kPass2Ents (the plan's segment size)
+    for (uint32_t i = tid; i < nent; i += NT) L.ents[i] = list[b + i];
+    if (tid < F) {
+        L.dbase[tid] = cursors[(uint64_t)g * F + tid];
+        L.cnt[tid] = 0;
+    }
+    __syncthreads();  // sbase (aliased with sorted) is dead from here on
+    const uint32_t ntiles = (nent + BPT - 1) / BPT;
+    const uint32_t o = tid & (kBlk - 1);
+    const uint32_t h = __builtin_amdgcn_readfirstlane(wave / WPB);
+    // tile ti's keys: item u = element o of block u * (NT / kBlk) + h of the tile
+    // (one block per wave and item, through a buffer resource over its fill: lanes past
+    // it read 0 and are masked out); returns the valid mask (bit u: item u)
+    const auto load = [&](uint32_t ti, uint32_t(&k)[ITEMS]) -> uint32_t {
+        uint32_t vm = 0;
+#pragma unroll
+        for (int u = 0; u < (int)ITEMS; ++u) {
+            const uint32_t idx = ti * BPT + (uint32_t)u * (NT / kBlk) + h;
+            const uint64_t en = idx < nent ? L.ents[idx] : 0ull;  // one address per wave: a broadcast
+            const uint32_t phys = __builtin_amdgcn_readfirstlane((uint32_t)en);
+            const uint32_t fill = __builtin_amdgcn_readfirstlane((uint32_t)(en >> 32));
+            const __amdgpu_buffer_rsrc_t rs = make_rsrc(in + (uint64_t)phys * kBlk, fill * 4u);
+            k[u] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)(o * 4u), 0, 2);
+            vm |= (o < fill ? 1u : 0u) << u;
+        }
+        return vm;
+    };
+    const auto sort_write = [&](const uint32_t(&k)[ITEMS], uint32_t vm) {
+        // A. rank of every key inside its digit (tile histogram at once)
+        uint32_t rd[ITEMS];
+#pragma unroll
+        for (int u = 0; u < (int)ITEMS; ++u) {
+            const uint32_t d = (k[u] >> shift) & mask;
+            rd[u] = ((vm >> u) & 1u) ? (atomicAdd(&L.cnt[d], 1u) | (d << 16)) : 0u;
+        }
+        __syncthreads();
+        // B. digit starts (block scan over F counters), destinations, next cursors
+        uint32_t c = 0, incl = 0;
+        if (tid < F) {
+            c = L.cnt[tid];
+            incl = wave_incl_scan_u32(c);
+            if (lane == kWave - 1 || tid == F - 1) L.wsum[wave] = incl;
+        }
+        __syncthreads();
+        if (tid < F) {
+            uint32_t pre = 0;
+            for (uint32_t w = 0; w < wave; ++w) pre += L.wsum[w];
+            const uint32_t st = pre + incl - c;
+            L.start[tid] = st;
+            const uint64_t db = L.dbase[tid];
+            L.off[tid] = db - st;
+            L.dbase[tid] = db + c;
+            L.cnt[tid] = 0;
+            if (tid == F - 1) L.wsum[NW] = st + c;  // the tile's valid keys
+        }
+        __syncthreads();
+        // C. the tile, digit-sorted
+#pragma unroll
+        for (int u = 0; u < (int)ITEMS; ++u)
+            if ((vm >> u) & 1u) L.sorted[L.start[rd[u] >> 16] + (rd[u] & 0xFFFFu)] = k[u];
+        __syncthreads();
+        // D. sorted position q -> off[d] + q: consecutive lanes, consecutive addresses
+        const uint32_t tn = L.wsum[NW];
+#pragma unroll 2  // (fully unrolled, the 64-bit destinations of all items stay live: 125 VGPRs)
+        for (int u = 0; u < (int)ITEMS; ++u) {
+            const uint32_t q = tid + (uint32_t)u * NT;
+            if (q < tn) {
+                const uint32_t x = L.sorted[q];
+                // a plain (write-back) store: the lines a store leaves partial are
+                // completed in L2 by the next wave or tile, not sent to HBM in pieces
+                out[L.off[(x >> shift) & mask] + q] = x;
+            }
+        }
+        // the next tile's phase A touches only cnt (zeroed in B); its C comes after a barrier
+    };
+    uint32_t ka[ITEMS], kb[ITEMS];
+    uint32_t ma = load(0, ka);
+    for (uint32_t ti = 0;; ti += 2) {
+        const uint32_t mb = load(ti + 1, kb);  // past the last tile: no blocks, all masked
+#pragma unroll
+        for (int u = 0; u < (int)ITEMS; ++u) asm volatile("" ::"v"(ka[u]));
+        sort_write(ka, ma);
+        if (ti + 1 >= ntiles) break;
+        ma = load(ti + 2, ka);
+#pragma unroll
+        for (int u = 0; u < (int)ITEMS; ++u) asm volatile("" ::"v"(kb[u]));
+        sort_write(kb, mb);
+        if (ti + 2 >= ntiles) break;
+    }
+}
+
 // Elements per thread per tile: 8 tuples (32 KiB tiles); keys: 12 in the pooled pass 1
 // (24 KiB tiles; 16 spill 17-19 VGPRs at the 128-register cap), 16 in the block-list
 // pass 2 (larger tiles amortise the per-tile work: 0.75 -> 0.69 ms per 2^28 keys).
@@ -1200,9 +1333,44 @@ hipError_t launch_scatter_pool(const void *in, uint32_t in_size, void *out, uint
     return hipErrorInvalidValue;
 }
 
+// SGXAMD_SORT2 (development A/B switch, read once): 1 (default) = key partitions' pass 2
+// as the LDS counting sort k_sort_blk; 0 = the write-combining k_scatter_blk.
+// 2^28 keys, alternating on one box: 0.569-0.578 ms per relation vs 0.583-0.599 (k_scatter_blk).
+bool sort2_enabled() {
+    static const bool on = [] {
+        const char *e = std::getenv("SGXAMD_SORT2");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return on;
+}
+
 template <typename T>
 hipError_t launch_scatter_blk_t(const void *in, const uint64_t *list, void *out, const SegMap &m, uint32_t grid,
                                 uint32_t shift, uint32_t bits, const uint64_t *cursors, hipStream_t s) {
+    if constexpr (sizeof(T) == 4) {
+        if (sort2_enabled()) {
+            const uint32_t *ik = static_cast<const uint32_t *>(in);
+            uint32_t *ok = static_cast<uint32_t *>(out);
+#define SORT_CASE(B)                                                                                              \
+    case B:                                                                                                       \
+        hipLaunchKernelGGL((k_sort_blk<B, 512, 16>), dim3(grid), dim3(512), 0, s, ik, list, ok, m, shift, cursors); \
+        break;
+            switch (bits) {
+                SORT_CASE(1)
+                SORT_CASE(2)
+                SORT_CASE(3)
+                SORT_CASE(4)
+                SORT_CASE(5)
+                SORT_CASE(6)
+                SORT_CASE(7)
+                SORT_CASE(8)
+                default:
+                    return hipErrorInvalidValue;
+            }
+#undef SORT_CASE
+            return hipGetLastError();
+        }
+    }
     constexpr int ITEMS = items_of<T, 2>(), NT = kScatterThreads;
     const char *ib = static_cast<const char *>(in);
     T *o = static_cast<T *>(out);

@@ -8,7 +8,9 @@ pass + expand pass instead of the one-pass look-back selection), SGXAMD_SMALL_JO
 the (5, 1) plan and the full-range cases below take it), SGXAMD_POOL=0 (two-pass plans
 with a pass-1 histogram and cursors instead of the pooled pass 1 and block-list pass 2;
 SGXAMD_POOL_SEGS sets the pooled pass-1 workgroups: 3 gives large pools, 100000 one
-tile per segment), SGXAMD_KEYS=0 (counting joins move whole tuples instead of keys).  The switches are read
+tile per segment), SGXAMD_KEYS=0 (counting joins move whole tuples instead of keys),
+SGXAMD_SORT2=0 (pass 2 of key partitions with the write-combining scatter instead of
+the LDS counting sort).  The switches are read
 once per process, so each setting runs in a child process against the oracle (the
 TPC-H selections ride along: they share the library's workspace)."""
 import os
@@ -43,6 +45,15 @@ for n in (1, 1000, 65536, 65537, (1 << 20) + 37):
     col = rng.integers(0, 256, n).astype(np.int32)
     for lo, hi in [(0, 26), (0, 255), (7, 7), (200, 100)]:
         cnt = oracle.scan("count", "i32", lo, hi, col)
+        assert sgxamd.scan_count(lo, hi, col, n) == cnt
+        bv = np.zeros((n + 63) // 64, dtype=np.uint64)
+        sgxamd.scan_bitvector(lo, hi, col, n, bv)
+        assert np.array_equal(bv, oracle.scan("bitvector", "i32", lo, hi, col)), (n, lo, hi)
+        c8 = col.astype(np.uint8)
+        assert sgxamd.scan_count(lo, hi, c8, n, "u8") == oracle.scan("count", "u8", lo, hi, c8)
+        bv8 = np.zeros((n + 63) // 64, dtype=np.uint64)
+        sgxamd.scan_bitvector(lo, hi, c8, n, bv8, "u8")
+        assert np.array_equal(bv8, oracle.scan("bitvector", "u8", lo, hi, c8)), (n, lo, hi)
         idx = np.zeros(max(cnt, 1), dtype=np.uint64)
         assert sgxamd.scan_index(lo, hi, col, n, idx, cnt) == cnt
         assert np.array_equal(idx[:cnt], oracle.scan("index", "i32", lo, hi, col)), (n, lo, hi)
@@ -67,7 +78,7 @@ print("paths ok")
                                  {"SGXAMD_DIGIT_SIDE": "1", "SGXAMD_SCAN_ONEPASS": "1", "SGXAMD_BIG_JOIN": "1"},
                                  {"SGXAMD_SMALL_JOIN": "0"},
                                  {"SGXAMD_POOL": "0"}, {"SGXAMD_POOL_SEGS": "3"}, {"SGXAMD_POOL_SEGS": "100000"},
-                                 {"SGXAMD_KEYS": "0"}])
+                                 {"SGXAMD_KEYS": "0"}, {"SGXAMD_SORT2": "0"}])
 def test_switch_paths_match_oracle(env):
     e = dict(os.environ, **env)
     e["PYTHONPATH"] = os.pathsep.join([os.path.join(PKG, "python"), os.path.join(ROOT, "oracle"),
