@@ -241,8 +241,8 @@ def test_full_size_config2_property(sgx, gpu):
 def test_config4_full_size(sgx, gpu):
     """BASELINE config 4 at its size on one GPU: pk(2^27, seed 11111) join fk(2^30,
     maxid 2^27, seed 22222) = 8 shuffled copies of 1..2^27 (native.cpp:62-101 shapes,
-    device generators).  matches == |S|; the planner sizes partitions for two 32,768-key
-    S chunks (ceil(log2(2^30 / 65,536)) = 14 bits, 7 + 7): every R partition then holds
+    device generators).  matches == |S|; the planner sizes partitions for one 65,536-key
+    S task each (ceil(log2(2^30 / 65,536)) = 14 bits, 7 + 7): every R partition then holds
     exactly 2^27 / 2^14 = 8192 keys and every S partition its 8 copies, 65,536 tuples,
     probed in one task."""
     import torch
