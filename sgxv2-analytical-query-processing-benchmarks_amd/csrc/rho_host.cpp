@@ -673,6 +673,16 @@ int join_small(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const 
     if (!ctx->sync.ptr) {  // hand-off words: zero once, every kernel leaves them zero
         RHO_HIP(ctx->sync.ensure(kSyncWords * sizeof(uint64_t)));
         RHO_HIP(hipMemsetAsync(ctx->sync.ptr, 0, kSyncWords * sizeof(uint64_t), s));
+        // the mapped host result block and its device address in sync[kSyncHostResult]
+        if (!ctx->host_join)
+            RHO_HIP(hipHostMalloc(reinterpret_cast<void **>(&ctx->host_join), 8 * sizeof(uint64_t),
+                                  hipHostMallocMapped | hipHostMallocCoherent));
+        void *dp = nullptr;
+        RHO_HIP(hipHostGetDevicePointer(&dp, ctx->host_join, 0));
+        ctx->host_result[8] = reinterpret_cast<uint64_t>(dp);
+        RHO_HIP(hipMemcpyAsync(ctx->sync.as<uint64_t>() + kSyncHostResult, ctx->host_result + 8, sizeof(uint64_t),
+                               hipMemcpyHostToDevice, s));
+        RHO_HIP(hipStreamSynchronize(s));
     }
     Timer &tm = thread_timer();
     const bool per_kernel = thread_timing_enabled() || (opts && opts->timing);
@@ -711,8 +721,9 @@ int join_small(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const 
                         pj.key_shift + pol.bits, pol.rcap, pj.s_chunk, pj.join_grid, kJoinCount, pj.algo,
                         A.at<uint64_t>(pj.off_counts), nullptr, nullptr, A.at<uint64_t>(pj.off_cyc), s, &red));
     tm.end_call();
-    RHO_HIP(hipMemcpyAsync(ctx->host_result, result, 6 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    // the join's last workgroup wrote the six result words into host_join: no copy back
     RHO_HIP(hipStreamSynchronize(s));
+    for (int i = 0; i < 6; ++i) ctx->host_result[i] = reinterpret_cast<volatile uint64_t *>(ctx->host_join)[i];
     tm.collect();
     fill_join_stats(ctx, pj, tm, -1.f, st);
     return MI355_OK;

@@ -52,6 +52,11 @@ hipError_t launch_scan_regions(uint64_t *hist, const uint32_t *seg_base, const u
 // them): the tickets and digit totals of the in-launch hand-offs of the one-launch
 // histogram (launch_hist_pair) and of the build/probe count reduction.
 constexpr uint32_t kSyncTicketR = 0, kSyncTicketS = 1, kSyncTicket2 = 2, kSyncTicketJoin = 3;
+// sync[kSyncTicketJoin + 1] holds the device address of the context's mapped host
+// result block (set once, never written by a kernel): the small join's last
+// workgroup stores the six result words there, so the host reads them after the
+// stream synchronises, without a device-to-host copy.
+constexpr uint32_t kSyncHostResult = kSyncTicketJoin + 1;
 constexpr uint32_t kSyncTotR = 8, kSyncTotS = kSyncTotR + kMaxF, kSyncWords = kSyncTotS + kMaxF;
 
 // Small one-pass joins: histograms of R and S, digit starts / counts and the build/probe

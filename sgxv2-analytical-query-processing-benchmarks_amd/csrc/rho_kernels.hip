@@ -1658,14 +1658,30 @@ __device__ __forceinline__ void join_reduce_last(const uint64_t *__restrict__ co
             p += cyc[2 * i + 1];
         }
     }
-    uint64_t t;
+    uint64_t t, tb = 0, tp = 0;
     (void)block_excl_scan_u64(acc, red, &t);
-    if (threadIdx.x == 0) result[0] = t;
     if (cyc) {
-        (void)block_excl_scan_u64(b, red, &t);
-        if (threadIdx.x == 0) result[4] = t;
-        (void)block_excl_scan_u64(p, red, &t);
-        if (threadIdx.x == 0) result[5] = t;
+        (void)block_excl_scan_u64(b, red, &tb);
+        (void)block_excl_scan_u64(p, red, &tp);
+    }
+    if (threadIdx.x == 0) {
+        result[0] = t;
+        if (cyc) {
+            result[4] = tb;
+            result[5] = tp;
+        }
+        // the call's result block in mapped host memory (kSyncHostResult): all six words
+        // (result[1..3] come from the launches before this one)
+        uint64_t *h = reinterpret_cast<uint64_t *>(ticket[kSyncHostResult - kSyncTicketJoin]);
+        if (h) {
+            h[0] = t;
+            h[1] = result[1];
+            h[2] = result[2];
+            h[3] = result[3];
+            h[4] = tb;
+            h[5] = tp;
+            __threadfence_system();
+        }
     }
 }
 

@@ -89,6 +89,7 @@ struct Context {
     // scan workspace
     DeviceBuffer scan_in, scan_out, scan_aux, scan_dict;
     uint64_t *host_result = nullptr;  // pinned 64 x u64
+    uint64_t *host_join = nullptr;    // coherent, mapped 8 x u64: written by the small join's kernel
     // multi-GPU exchange workspace (multi_host.cpp): shard-partitioned send buffers and
     // the receive buffers the peers' pieces land in
     DeviceBuffer xsendR, xsendS, xrecvR, xrecvS;
