@@ -7,6 +7,7 @@
 // of device-wide kernels instead of T pthreads with barriers, and partitions are
 // sized for the LDS of a CU rather than for L2 (calc_num_radix_bits :295-317).
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -656,6 +657,40 @@ int join_finish(Context *ctx, PendingJoin &pj, const row_t *dS, uint64_t nS, mi3
 // last-workgroup reduction.  SGXAMD_SMALL_JOIN=0 turns it off (A/B; results identical).
 constexpr uint64_t kSmallJoinMax = 1ull << 23;  // |R| + |S| up to which the path is taken
 
+// Waits for the small join's done flag in mapped host memory: a spin of at most 2 ms
+// (a 2^23-tuple small join takes ~0.2 ms), then the stream synchronisation, which
+// also reports a kernel fault; the flag must be set after it.
+int wait_host_flag(volatile uint64_t *flag, hipStream_t s) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t i = 1;; ++i) {
+        if (*flag) {
+            std::atomic_thread_fence(std::memory_order_acquire);
+            return MI355_OK;
+        }
+        if ((i & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
+        __builtin_ia32_pause();
+    }
+    RHO_HIP(hipStreamSynchronize(s));
+    if (!*flag) {
+        set_last_error("small join: the build/probe finished without its done flag");
+        return MI355_ERR_HIP;
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    return MI355_OK;
+}
+
+// The device's constant wall clock (wall_clock64()) in kHz, queried once.
+double wall_clock_khz() {
+    static const double khz = [] {
+        int dev = 0, v = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeWallClockRate, dev) !=
+                                                     hipSuccess || v <= 0)
+            return 100000.0;  // 100 MHz on CDNA3/4
+        return (double)v;
+    }();
+    return khz;
+}
+
 bool small_join_enabled() {
     static const bool on = [] {
         const char *e = std::getenv("SGXAMD_SMALL_JOIN");
@@ -675,7 +710,7 @@ int join_small(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const 
         RHO_HIP(hipMemsetAsync(ctx->sync.ptr, 0, kSyncWords * sizeof(uint64_t), s));
         // the mapped host result block and its device address in sync[kSyncHostResult]
         if (!ctx->host_join)
-            RHO_HIP(hipHostMalloc(reinterpret_cast<void **>(&ctx->host_join), 8 * sizeof(uint64_t),
+            RHO_HIP(hipHostMalloc(reinterpret_cast<void **>(&ctx->host_join), kHostJoinWords * sizeof(uint64_t),
                                   hipHostMallocMapped | hipHostMallocCoherent));
         void *dp = nullptr;
         RHO_HIP(hipHostGetDevicePointer(&dp, ctx->host_join, 0));
@@ -686,7 +721,9 @@ int join_small(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const 
     }
     Timer &tm = thread_timer();
     const bool per_kernel = thread_timing_enabled() || (opts && opts->timing);
-    tm.begin_call(s, true, !per_kernel);
+    tm.begin_call(s, per_kernel);  // without per-kernel events the kernels time the call
+    volatile uint64_t *hj = ctx->host_join;
+    hj[kHostJoinDone] = 0;
     // segments of at least 8192 tuples: fewer digit-total atomics per address (2^20 x 2^20:
     // 4096 / 8192 / 16384 / 32768-tuple segments 67.9 / 58.5 / 64.6 / 85.3 us per join;
     // SGXAMD_SMALL_SEG overrides, development)
@@ -721,11 +758,20 @@ int join_small(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const 
                         pj.key_shift + pol.bits, pol.rcap, pj.s_chunk, pj.join_grid, kJoinCount, pj.algo,
                         A.at<uint64_t>(pj.off_counts), nullptr, nullptr, A.at<uint64_t>(pj.off_cyc), s, &red));
     tm.end_call();
-    // the join's last workgroup wrote the six result words into host_join: no copy back
-    RHO_HIP(hipStreamSynchronize(s));
-    for (int i = 0; i < 6; ++i) ctx->host_result[i] = reinterpret_cast<volatile uint64_t *>(ctx->host_join)[i];
+    // the join's last workgroup wrote the result words into host_join: no copy back, and
+    // without per-kernel events no stream synchronisation either (a launch + synchronise
+    // round trip costs ~9 us, launch + a spin on a mapped flag ~6 us)
+    float span = -1.f;
+    if (per_kernel) {
+        RHO_HIP(hipStreamSynchronize(s));
+    } else {
+        const int rc2 = wait_host_flag(hj + kHostJoinDone, s);
+        if (rc2) return rc2;
+        span = (float)((double)hj[kHostJoinSpan] / wall_clock_khz());
+    }
+    for (int i = 0; i < 6; ++i) ctx->host_result[i] = hj[i];
     tm.collect();
-    fill_join_stats(ctx, pj, tm, -1.f, st);
+    fill_join_stats(ctx, pj, tm, span, st);
     return MI355_OK;
 }
 

@@ -54,9 +54,12 @@ hipError_t launch_scan_regions(uint64_t *hist, const uint32_t *seg_base, const u
 constexpr uint32_t kSyncTicketR = 0, kSyncTicketS = 1, kSyncTicket2 = 2, kSyncTicketJoin = 3;
 // sync[kSyncTicketJoin + 1] holds the device address of the context's mapped host
 // result block (set once, never written by a kernel): the small join's last
-// workgroup stores the six result words there, so the host reads them after the
-// stream synchronises, without a device-to-host copy.
-constexpr uint32_t kSyncHostResult = kSyncTicketJoin + 1;
+// workgroup stores the six result words there, then the device span of the call
+// (word 6, wall-clock ticks since k_hist_pair's first workgroup stored its start in
+// sync[kSyncT0]) and last the done flag (word 7), which the host spins on instead of
+// synchronising the stream.
+constexpr uint32_t kSyncHostResult = kSyncTicketJoin + 1, kSyncT0 = kSyncTicketJoin + 2;
+constexpr uint32_t kHostJoinSpan = 6, kHostJoinDone = 7, kHostJoinWords = 8;
 constexpr uint32_t kSyncTotR = 8, kSyncTotS = kSyncTotR + kMaxF, kSyncWords = kSyncTotS + kMaxF;
 
 // Small one-pass joins: histograms of R and S, digit starts / counts and the build/probe

@@ -172,6 +172,8 @@ __global__ __launch_bounds__(kBlock) void k_hist_pair(HistPairRel A, HistPairRel
     const HistPairRel &H = isB ? B : A;
     const uint32_t g = isB ? blockIdx.x - A.grid : blockIdx.x;
     const uint32_t F = 1u << bits;
+    if (blockIdx.x == 0 && threadIdx.x == 0)  // the call's start (small-join device span)
+        ticket2[kSyncT0 - kSyncTicket2] = wall_clock64();
     const bool any = hist_segment(H.in, H.m, g, H.shift, bits, h, sbase);
     for (uint32_t d = threadIdx.x; d < F; d += kBlock) {
         const uint32_t v = any ? h[d] : 0u;
@@ -1671,8 +1673,9 @@ __device__ __forceinline__ void join_reduce_last(const uint64_t *__restrict__ co
             result[5] = tp;
         }
         // the call's result block in mapped host memory (kSyncHostResult): all six words
-        // (result[1..3] come from the launches before this one)
-        uint64_t *h = reinterpret_cast<uint64_t *>(ticket[kSyncHostResult - kSyncTicketJoin]);
+        // (result[1..3] come from the launches before this one), the device span, then
+        // the done flag the host spins on -- the kernel's last memory operation
+        volatile uint64_t *h = reinterpret_cast<volatile uint64_t *>(ticket[kSyncHostResult - kSyncTicketJoin]);
         if (h) {
             h[0] = t;
             h[1] = result[1];
@@ -1680,6 +1683,9 @@ __device__ __forceinline__ void join_reduce_last(const uint64_t *__restrict__ co
             h[3] = result[3];
             h[4] = tb;
             h[5] = tp;
+            h[kHostJoinSpan] = wall_clock64() - ticket[kSyncT0 - kSyncTicketJoin];
+            __threadfence_system();
+            h[kHostJoinDone] = 1;
             __threadfence_system();
         }
     }
