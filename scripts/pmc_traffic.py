@@ -30,7 +30,6 @@ ALIASES = {
     "k_join_tag": ["join_build_probe"],
     "k_join_x": ["join_build_probe"],
     "k_predicate": ["scan_count", "scan_bitvector"],
-    "k_expand": ["scan_expand_index"],
     "k_select": ["scan_select_index"],
 }
 # kernels whose bench-size launches differ per pass, told apart by grid size (pass 2's

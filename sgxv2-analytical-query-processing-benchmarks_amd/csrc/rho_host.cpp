@@ -103,13 +103,8 @@ Policy choose_policy(uint64_t nR, uint64_t nS, const mi355_rho_opts *o) {
         p.b1 = p.bits;
         p.b2 = 0;
     } else {
-        // odd bit counts: the larger digit in pass 1, or with SGXAMD_SPLIT=2 in pass 2
-        // (development A/B switch)
-        static const bool late = [] {
-            const char *e = std::getenv("SGXAMD_SPLIT");
-            return e && std::atoi(e) == 2;
-        }();
-        p.b1 = late ? p.bits / 2 : (p.bits + 1) / 2;
+        // odd bit counts: the larger digit in pass 1
+        p.b1 = (p.bits + 1) / 2;
         p.b2 = p.bits - p.b1;
     }
     // chain table large enough that the average partition needs one R chunk

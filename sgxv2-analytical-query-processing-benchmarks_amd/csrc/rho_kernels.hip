@@ -727,8 +727,6 @@ __device__ __forceinline__ void scatter_tile_write(ScatterLds<BITS, ITEMS, NT, E
             x = lds_pick(q < cd, &L.carry[d * CS + q], &L.tile[m.x + q - cd]);
 #ifdef SGXAMD_ABLATE_NOSTORE  // development ablation: everything but the global stores
             if (x == (T)~0ull) out[0] = x;
-#elif defined(SGXAMD_PLAIN_STORE)
-            out[a] = x;
 #else
             st_nt(out + a, x);
 #endif
@@ -1050,11 +1048,9 @@ __device__ __forceinline__ void scatter_segment_ext(ScatterLds<BITS, ITEMS, NT, 
         if constexpr (EXT == 2) return (tn >> 31) != 0;
         return tn == TILE;
     };
-#ifndef SGXAMD_FULL_POOL
-#define SGXAMD_FULL_POOL 0  // pass 1: the second sort copy spills 3-5 VGPRs (measured 0.01 ms slower)
-#endif
+    // (pooled pass 1, EXT 1, keeps one sort copy: a full-tile copy spills 3-5 VGPRs there)
     const auto sort = [&](T(&v)[ITEMS], uint32_t tn) -> uint32_t {
-        if ((EXT != 1 || SGXAMD_FULL_POOL) && is_full(tn))
+        if (EXT != 1 && is_full(tn))
             return scatter_tile_sort<BITS, ITEMS, NT, EXT, T, true>(L, pend, carried, v, out, tn, shift, 0, &ps);
         return scatter_tile_sort<BITS, ITEMS, NT, EXT, T, false>(L, pend, carried, v, out, tn, shift, 0, &ps);
     };
@@ -1172,15 +1168,29 @@ struct SortBlkLds {
     uint32_t wsum[NT / kWave + 1];
 };
 
-// 6 waves per SIMD (84 VGPRs): three 512-thread workgroups per CU
+// Geometry (development: compile-time variants through scripts/build_variant.sh):
+// 512 threads x 16 keys (8192-key tiles), three workgroups per CU = 6 waves per SIMD
+// (80 VGPRs).
+#ifndef SGXAMD_SORT_NT
+#define SGXAMD_SORT_NT 512
+#endif
+#ifndef SGXAMD_SORT_ITEMS
+#define SGXAMD_SORT_ITEMS 16
+#endif
+#ifndef SGXAMD_SORT_WGS
+#define SGXAMD_SORT_WGS 3
+#endif
+#ifndef SGXAMD_SORT_UNROLL
+#define SGXAMD_SORT_UNROLL 2
+#endif
 template <int BITS, int NT, int ITEMS>
-__global__ __launch_bounds__(NT, NT * 3 / 256) void k_sort_blk(const uint32_t *__restrict__ in, const uint64_t *__restrict__ list,
+__global__ __launch_bounds__(NT, NT * SGXAMD_SORT_WGS / 256) void k_sort_blk(const uint32_t *__restrict__ in, const uint64_t *__restrict__ list,
                                                     uint32_t *__restrict__ out, SegMap m, uint32_t shift,
                                                     const uint64_t *__restrict__ cursors) {
     using LdsT = SortBlkLds<BITS, NT, ITEMS>;
     constexpr uint32_t F = LdsT::F, TILE = LdsT::TILE, BPT = TILE / kBlk, mask = F - 1, NW = NT / kWave;
     constexpr uint32_t WPB = kBlk / kWave;  // waves per block row: item u of wave w reads block u * (NT / kBlk) + w / WPB
-    static_assert(TILE % kBlk == 0 && NT % kBlk == 0 && F <= NT && ITEMS <= 16, "tile geometry");
+    static_assert(TILE % kBlk == 0 && NT % kBlk == 0 && F <= NT && ITEMS <= 32 && TILE <= 65536, "tile geometry");
     __shared__ LdsT L;
     const uint32_t tid = threadIdx.x, lane = __lane_id(), wave = tid / kWave;
     const uint32_t g = blockIdx.x;
@@ -1250,7 +1260,7 @@ __global__ __launch_bounds__(NT, NT * 3 / 256) void k_sort_blk(const uint32_t *_
         __syncthreads();
         // D. sorted position q -> off[d] + q: consecutive lanes, consecutive addresses
         const uint32_t tn = L.wsum[NW];
-#pragma unroll 2  // (fully unrolled, the 64-bit destinations of all items stay live: 125 VGPRs)
+#pragma unroll SGXAMD_SORT_UNROLL  // (fully unrolled, the 64-bit destinations of all items stay live: 125 VGPRs)
         for (int u = 0; u < (int)ITEMS; ++u) {
             const uint32_t q = tid + (uint32_t)u * NT;
             if (q < tn) {
@@ -1355,7 +1365,8 @@ hipError_t launch_scatter_blk_t(const void *in, const uint64_t *list, void *out,
             uint32_t *ok = static_cast<uint32_t *>(out);
 #define SORT_CASE(B)                                                                                              \
     case B:                                                                                                       \
-        hipLaunchKernelGGL((k_sort_blk<B, 512, 16>), dim3(grid), dim3(512), 0, s, ik, list, ok, m, shift, cursors); \
+        hipLaunchKernelGGL((k_sort_blk<B, SGXAMD_SORT_NT, SGXAMD_SORT_ITEMS>), dim3(grid), dim3(SGXAMD_SORT_NT), 0, s, \
+                           ik, list, ok, m, shift, cursors);                                                      \
         break;
             switch (bits) {
                 SORT_CASE(1)

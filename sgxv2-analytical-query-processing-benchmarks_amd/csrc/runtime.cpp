@@ -120,13 +120,6 @@ bool thread_timing_enabled() { return t_timing; }
 bool thread_partition_overlap() { return t_overlap; }
 bool thread_key_layout() { return t_keys; }
 
-bool one_pass_selection() {
-    static const bool on = [] {
-        const char *e = std::getenv("SGXAMD_SCAN_ONEPASS");
-        return !(e && std::atoi(e) == 0);
-    }();
-    return on;
-}
 
 Context *current_context(int *status) {
     int ndev = 0;

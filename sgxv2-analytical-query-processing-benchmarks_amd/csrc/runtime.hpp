@@ -118,10 +118,6 @@ bool thread_timing_enabled();
 bool thread_partition_overlap();
 // Counting joins move keys only after the input read (mi355_set_key_layout, default on).
 bool thread_key_layout();
-// Index / value / dictionary scans in one pass with a decoupled look-back;
-// SGXAMD_SCAN_ONEPASS=0 selects their two-pass form (development A/B switch, read
-// once; results are identical).
-bool one_pass_selection();
 hipStream_t thread_stream(Context *ctx, void *explicit_stream);
 
 bool is_device_pointer(const void *p);

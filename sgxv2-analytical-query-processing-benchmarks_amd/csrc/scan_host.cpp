@@ -89,19 +89,16 @@ int run(Op op, T lo, T hi, const T *in, size_t n, void *out, size_t cap, uint64_
     Arena &A = ctx->scratch;
     A.reset();
     const size_t o_counts = A.reserve(sizeof(uint64_t) * g.nchunks);
-    const size_t o_offs = A.reserve(sizeof(uint64_t) * g.nchunks);
     const size_t o_res = A.reserve(sizeof(uint64_t) * 2);
-    const bool select1 = selects && one_pass_selection();
-    const size_t o_status = A.reserve(sizeof(uint64_t) * (select1 ? select_chunks(n) : 0) + 16);
+    const size_t o_status = A.reserve(sizeof(uint64_t) * (selects ? select_chunks(n) : 0) + 16);
     SCAN_HIP(A.buf.ensure(A.used));
     uint64_t *counts = A.at<uint64_t>(o_counts);
-    uint64_t *offs = A.at<uint64_t>(o_offs);
     uint64_t *res = A.at<uint64_t>(o_res);
     uint64_t *sel_status = A.at<uint64_t>(o_status) + 2;
     uint32_t *ticket = A.at<uint32_t>(o_status);
 
     const bool out_dev = out && is_device_pointer(out);
-    if (select1) {
+    if (selects) {  // one pass: k_select with a decoupled look-back
         OutT *o = static_cast<OutT *>(out);
         if (!out_dev) {
             SCAN_HIP(ctx->scan_out.ensure(std::max<size_t>(cap, 1) * sizeof(OutT)));
@@ -152,54 +149,18 @@ int run(Op op, T lo, T hi, const T *in, size_t n, void *out, size_t cap, uint64_
     SCAN_HIP(launch_predicate<T>(din, n, lo, hi, g.rows_per_chunk, g.nchunks, bv, counts, s));
     size_t copy_bytes = 0;
     void *dev_out = nullptr;
-    if (op == Op::kCount || op == Op::kBitvector) {
-        tm.mark("scan_sum");
-        SCAN_HIP(launch_sum(counts, g.nchunks, res, s));
-        if (op == Op::kBitvector && !out_dev) {
-            dev_out = bv;
-            copy_bytes = nwords * sizeof(uint64_t);
-        }
-    } else {
-        tm.mark("scan_chunk_scan");
-        SCAN_HIP(launch_chunk_scan(counts, g.nchunks, offs, res, s));
-        OutT *o = static_cast<OutT *>(out);
-        if (!out_dev) {
-            SCAN_HIP(ctx->scan_out.ensure(std::max<size_t>(cap, 1) * sizeof(OutT)));
-            o = ctx->scan_out.as<OutT>();
-            dev_out = o;
-        }
-        tm.mark(op == Op::kIndex ? "scan_expand_index" : op == Op::kValues ? "scan_expand_values"
-                                                                              : "scan_expand_explicit");
-        if (op == Op::kIndex)
-            SCAN_HIP((launch_expand<T, OutT, 0>(bv, din, n, g.rows_per_chunk, g.nchunks, offs, o, cap, s)));
-        else if (op == Op::kValues)
-            SCAN_HIP((launch_expand<T, OutT, 1>(bv, din, n, g.rows_per_chunk, g.nchunks, offs, o, cap, s)));
-        else if constexpr (std::is_same<T, uint8_t>::value && std::is_same<OutT, uint64_t>::value) {
-            SCAN_HIP(hipMemsetAsync(ticket, 0, 2 * sizeof(uint32_t), s));
-            SCAN_HIP((launch_expand<T, OutT, 3>(bv, din, n, g.rows_per_chunk, g.nchunks, offs, o, cap, s, daux,
-                                                aux_len, ticket + 1)));
-        }
+    tm.mark("scan_sum");
+    SCAN_HIP(launch_sum(counts, g.nchunks, res, s));
+    if (op == Op::kBitvector && !out_dev) {
+        dev_out = bv;
+        copy_bytes = nwords * sizeof(uint64_t);
     }
     tm.end_call();
     SCAN_HIP(hipMemcpyAsync(ctx->host_result, res, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-    if (op == Op::kExplicit)
-        SCAN_HIP(hipMemcpyAsync(ctx->host_result + 1, ticket, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     SCAN_HIP(hipStreamSynchronize(s));
-    const uint64_t total = ctx->host_result[0];
-    if (op == Op::kExplicit && (reinterpret_cast<const uint32_t *>(ctx->host_result + 1)[1] & 2u)) {
-        set_last_error("explicit_index_scan: a match's index entry lies past the index array");
-        return MI355_ERR_INVALID;
-    }
-    if (result) *result = total;
-    if (dev_out && out) {
-        if (selects) copy_bytes = std::min<uint64_t>(total, cap) * sizeof(OutT);
-        if (copy_bytes) SCAN_HIP(hipMemcpy(out, dev_out, copy_bytes, hipMemcpyDeviceToHost));
-    }
+    if (result) *result = ctx->host_result[0];
+    if (dev_out && out && copy_bytes) SCAN_HIP(hipMemcpy(out, dev_out, copy_bytes, hipMemcpyDeviceToHost));
     tm.collect();
-    if (selects && total > cap) {
-        set_last_error("output capacity " + std::to_string(cap) + " < " + std::to_string(total) + " matches");
-        return MI355_ERR_CAPACITY;
-    }
     return MI355_OK;
 }
 
@@ -259,16 +220,11 @@ int run_dict(int64_t lo, int64_t hi, const int64_t *dict, uint64_t dict_size, co
     const CodeT *din = nullptr;
     int rc = stage_input(ctx, s, in, n, &din);
     if (rc) return rc;
-    const Geometry g = geometry(n);
-    const uint64_t nwords = (n + 63) / 64;
     Arena &A = ctx->scratch;
     A.reset();
-    const size_t o_counts = A.reserve(sizeof(uint64_t) * g.nchunks);
-    const size_t o_offs = A.reserve(sizeof(uint64_t) * g.nchunks);
     const size_t o_res = A.reserve(sizeof(uint64_t) * 2);
     const size_t o_range = A.reserve(sizeof(uint64_t) * 2);
-    const bool select1 = one_pass_selection();
-    const size_t o_status = A.reserve(sizeof(uint64_t) * (select1 ? select_chunks(n) : 0) + 16);
+    const size_t o_status = A.reserve(sizeof(uint64_t) * select_chunks(n) + 16);
     SCAN_HIP(A.buf.ensure(A.used));
     uint64_t *range = A.at<uint64_t>(o_range);
     tm.mark("dict_range");
@@ -280,35 +236,23 @@ int run_dict(int64_t lo, int64_t hi, const int64_t *dict, uint64_t dict_size, co
     const CodeT clo = (CodeT)(CastT)ctx->host_result[0];
     const CodeT chi = (CodeT)(CastT)(int64_t)(ctx->host_result[1] - 1);
 
-    uint64_t *counts = A.at<uint64_t>(o_counts), *offs = A.at<uint64_t>(o_offs), *res = A.at<uint64_t>(o_res);
+    uint64_t *res = A.at<uint64_t>(o_res);
     const bool out_dev = out && is_device_pointer(out);
     int64_t *o = out;
     if (!out_dev) {
         SCAN_HIP(ctx->scan_out.ensure(std::max<size_t>(cap, 1) * sizeof(int64_t)));
         o = ctx->scan_out.as<int64_t>();
     }
-    if (select1) {
-        tm.mark("dict_select");
-        SCAN_HIP((launch_select<CodeT, int64_t, 2>(din, n, clo, chi, A.at<uint32_t>(o_status),
-                                                   A.at<uint64_t>(o_status) + 2, o, cap, res, s, ddict)));
-    } else {
-        SCAN_HIP(ctx->scan_aux.ensure(std::max<uint64_t>(nwords, 1) * sizeof(uint64_t)));
-        uint64_t *bv = ctx->scan_aux.as<uint64_t>();
-        tm.mark("dict_bitvector");
-        SCAN_HIP(launch_predicate<CodeT>(din, n, clo, chi, g.rows_per_chunk, g.nchunks, bv, counts, s));
-        tm.mark("dict_chunk_scan");
-        SCAN_HIP(launch_chunk_scan(counts, g.nchunks, offs, res, s));
-        tm.mark("dict_decode");
-        SCAN_HIP((launch_expand<CodeT, int64_t, 2>(bv, din, n, g.rows_per_chunk, g.nchunks, offs, o, cap, s, ddict)));
-    }
+    tm.mark("dict_select");
+    SCAN_HIP((launch_select<CodeT, int64_t, 2>(din, n, clo, chi, A.at<uint32_t>(o_status),
+                                               A.at<uint64_t>(o_status) + 2, o, cap, res, s, ddict)));
     tm.end_call();
     SCAN_HIP(hipMemcpyAsync(ctx->host_result, res, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-    if (select1)
-        SCAN_HIP(hipMemcpyAsync(ctx->host_result + 1, A.at<uint32_t>(o_status), 2 * sizeof(uint32_t),
-                                hipMemcpyDeviceToHost, s));
+    SCAN_HIP(hipMemcpyAsync(ctx->host_result + 1, A.at<uint32_t>(o_status), 2 * sizeof(uint32_t),
+                            hipMemcpyDeviceToHost, s));
     SCAN_HIP(hipStreamSynchronize(s));
     const uint64_t total = ctx->host_result[0];
-    if (select1 && reinterpret_cast<const uint32_t *>(ctx->host_result + 1)[1] != 0) {
+    if (reinterpret_cast<const uint32_t *>(ctx->host_result + 1)[1] != 0) {
         set_last_error("one-pass selection: look-back poll gave up");
         return MI355_ERR_HIP;
     }

@@ -15,18 +15,6 @@ template <typename T>
 hipError_t launch_predicate(const T *in, uint64_t n, T lo, T hi, uint64_t rows_per_chunk, uint32_t nchunks,
                             uint64_t *bv, uint64_t *chunk_counts, hipStream_t s);
 
-hipError_t launch_chunk_scan(const uint64_t *counts, uint32_t nchunks, uint64_t *offsets, uint64_t *total,
-                             hipStream_t s);
-
-// MODE 0: row indexes (OutT = uint64_t); MODE 1: values (u8 -> uint32_t, i32 -> int32_t);
-// MODE 2: dictionary-decoded values dict[code] (OutT = int64_t); MODE 3: entries of the
-// explicit index array `dict` (aux_len u64 entries) as SIMD512::explicit_index_scan
-// gathers them (an entry past aux_len sets bit 2 of *err).
-template <typename T, typename OutT, int MODE>
-hipError_t launch_expand(const uint64_t *bv, const T *in, uint64_t n, uint64_t rows_per_chunk, uint32_t nchunks,
-                         const uint64_t *chunk_off, OutT *out, uint64_t cap, hipStream_t s,
-                         const int64_t *dict = nullptr, uint64_t aux_len = 0, uint32_t *err = nullptr);
-
 // One-pass index (MODE 0) / value (1) / dictionary (2) / explicit index (3) selection
 // with decoupled look-back over chunks (scan_kernels.hip k_select).  ticket: two u32
 // (after the launch, bit 0 of ticket[1] = a look-back poll gave up, bit 1 = an explicit

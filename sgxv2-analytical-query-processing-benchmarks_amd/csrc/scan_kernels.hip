@@ -3,17 +3,16 @@
 // Replaces the AVX-512 loops of Scan-Micro-Benchmarks/shared_libraries/SimdScan/src/SIMD512.cpp:
 //   count            :7-32    -> k_predicate<T, false>  (chunk counts, then a sum)
 //   bitvector_scan   :210-222 -> k_predicate<T, true>   (one 64-bit word per 64 rows)
-//   implicit_index_scan(_self_alloc) :225-287 -> k_predicate<T, true> + k_chunk_scan + k_expand<.., kIndex>
-//   scan             :91-150  -> same pipeline, k_expand<.., kValue>
+//   implicit_index_scan(_self_alloc) :225-287 -> k_select<.., 0> (one pass, decoupled look-back)
+//   scan             :91-150  -> k_select<.., 1>
 // A 512-bit compare of the reference covers 64 uint8 codes; here one wave-wide
 // 16-byte-per-lane load covers 1024 uint8 codes or 256 int32 values, and the
 // predicate mask of 64 consecutive rows is assembled across 4 (u8) or 16 (i32)
 // lanes with DPP row operations into exactly the reference's __mmask64 word layout.
-// Index/value compaction is two-phase without inter-workgroup waiting: the
-// bitvector pass also emits one match count per chunk, a one-block scan turns
-// those into chunk output offsets, and the expand pass reads only the bitvector
-// (n/8 bytes), stages each wave's matches in LDS and writes them coalesced (lane j
-// of a wave writes output j).
+// Index/value compaction is one pass (k_select): each chunk's bitvector stays in LDS,
+// its output offset comes from a decoupled look-back over the chunks before it, and
+// each wave's matches are staged in LDS and written coalesced (lane j of a wave
+// writes output j).
 #include "common.hpp"
 #include "scan_internal.hpp"
 
@@ -309,28 +308,6 @@ hipError_t launch_sum_u8(const uint8_t *in, uint64_t n, uint8_t lo, uint8_t hi, 
 template hipError_t launch_predicate<int32_t>(const int32_t *, uint64_t, int32_t, int32_t, uint64_t, uint32_t,
                                               uint64_t *, uint64_t *, hipStream_t);
 
-// One block: exclusive scan of the chunk counts -> chunk offsets, total in *total.
-__global__ __launch_bounds__(1024) void k_chunk_scan(const uint64_t *__restrict__ counts, uint32_t nchunks,
-                                                     uint64_t *__restrict__ offsets, uint64_t *__restrict__ total) {
-    __shared__ uint64_t scratch[1024 / kWave + 1];
-    uint64_t carry = 0;
-    for (uint32_t b = 0; b < nchunks; b += 1024) {
-        const uint32_t i = b + threadIdx.x;
-        const uint64_t v = i < nchunks ? counts[i] : 0;
-        uint64_t tot;
-        const uint64_t ex = block_excl_scan_u64(v, scratch, &tot);
-        if (i < nchunks) offsets[i] = carry + ex;
-        carry += tot;
-    }
-    if (threadIdx.x == 0) *total = carry;
-}
-
-hipError_t launch_chunk_scan(const uint64_t *counts, uint32_t nchunks, uint64_t *offsets, uint64_t *total,
-                             hipStream_t s) {
-    hipLaunchKernelGGL(k_chunk_scan, dim3(1), dim3(1024), 0, s, counts, nchunks, offsets, total);
-    return hipGetLastError();
-}
-
 // LDS writes of a wave made visible to the other lanes of the same wave (no block
 // barrier: the staging area below is private to its wave).
 __device__ __forceinline__ void wave_lds_sync() {
@@ -339,15 +316,6 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Expand the bitvector of one chunk into row indexes (MODE 0), values (MODE 1) or
-// dictionary-decoded values dict[code] (MODE 2, the dict_scan_* family).
-// Each wave takes 64 words (4096 rows) per step, one word per lane.  A lane writes
-// the row offsets of its set bits into the wave's LDS staging area at its exclusive
-// word-popcount prefix, then the wave streams the staged outputs to HBM with lane j
-// writing the wave's j-th, (j+64)-th, ... output: every store instruction covers 64
-// consecutive output slots.  Steps with more than kStage matches in a wave (dense
-// predicates) stage in rounds of kStage.  The word of the next step is loaded before
-// the current one is expanded.
 // SIMD512::explicit_index_scan (SIMD512.cpp:152-208) gathers the matches of row r from
 // the u64 index vector index_compressed[i + j] (block i = r / 64, sub-block j = (r % 64) / 8),
 // lane r % 8: entry 8 * (r / 64 + (r % 64) / 8) + r % 8, restated as written.
@@ -372,114 +340,6 @@ __device__ __forceinline__ OutT select_value(uint64_t row, const T *__restrict__
 
 constexpr uint32_t kStage = 1024;  // staged outputs per wave and round (u32 row offsets, 4 KiB)
 
-template <typename T, typename OutT, int MODE>
-__global__ __launch_bounds__(kBlock) void k_expand(const uint64_t *__restrict__ bv, const T *__restrict__ in,
-                                                   uint64_t n, uint64_t rows_per_chunk,
-                                                   const uint64_t *__restrict__ chunk_off, OutT *__restrict__ out,
-                                                   uint64_t cap, const int64_t *__restrict__ dict, uint64_t aux_len,
-                                                   uint32_t *__restrict__ err) {
-    __shared__ uint32_t stage_s[kWaves][kStage];
-    __shared__ uint32_t wtot_s[kWaves];
-    const uint32_t lane = __lane_id(), wave = threadIdx.x / kWave;
-    uint32_t *stage = stage_s[wave];
-    const uint64_t nwords = (n + 63) / 64;
-    const uint64_t w0 = (uint64_t)blockIdx.x * (rows_per_chunk / 64);
-    uint64_t w1 = w0 + rows_per_chunk / 64;
-    if (w1 > nwords) w1 = nwords;
-    uint64_t base = chunk_off[blockIdx.x];
-    uint64_t wi = w0 + (uint64_t)wave * 64 + lane;
-    uint64_t x_next = wi < w1 ? ld_nt(bv + wi) : 0ull;
-    for (uint64_t wb = w0; wb < w1; wb += kWaves * 64) {
-        const uint64_t x = x_next;
-        wi += kWaves * 64;
-        x_next = wi < w1 ? ld_nt(bv + wi) : 0ull;
-        const uint32_t c = __popcll(x);
-        const uint32_t incl = wave_incl_scan_u32(c);
-        const uint32_t excl = incl - c;
-        const uint32_t wtot = __shfl(incl, 63, kWave);
-        if (lane == 0) wtot_s[wave] = wtot;
-        __syncthreads();
-        uint64_t woff = base;
-        uint64_t all = 0;
-#pragma unroll
-        for (int w = 0; w < kWaves; ++w) {
-            const uint32_t t = wtot_s[w];
-            if (w < (int)wave) woff += t;
-            all += t;
-        }
-        const uint64_t row0 = (wb + (uint64_t)wave * 64) * 64;  // first row of this wave's 64 words
-        for (uint32_t r0 = 0; r0 < wtot; r0 += kStage) {
-            const uint32_t r1 = r0 + kStage;
-            if (excl < r1 && incl > r0) {
-                uint64_t y = x;
-                uint32_t p = excl;
-                while (y) {
-                    const uint32_t bit = (uint32_t)__builtin_ctzll(y);
-                    y &= y - 1;
-                    if (p >= r0 && p < r1) stage[p - r0] = lane * 64 + bit;
-                    ++p;
-                }
-            }
-            wave_lds_sync();
-            const uint32_t nr = min(kStage, wtot - r0);
-            for (uint32_t m = lane; m < nr; m += 64) {
-                const uint64_t row = row0 + stage[m];
-                const uint64_t o = woff + r0 + m;
-                if (o < cap) {
-                    const OutT v = select_value<T, OutT, MODE>(row, in, dict, aux_len, err);
-                    __builtin_nontemporal_store(v, out + o);
-                }
-            }
-            wave_lds_sync();
-        }
-        base += all;
-        __syncthreads();
-    }
-}
-
-template <typename T, typename OutT, int MODE>
-hipError_t launch_expand(const uint64_t *bv, const T *in, uint64_t n, uint64_t rows_per_chunk, uint32_t nchunks,
-                         const uint64_t *chunk_off, OutT *out, uint64_t cap, hipStream_t s, const int64_t *dict,
-                         uint64_t aux_len, uint32_t *err) {
-    if (nchunks == 0) return hipSuccess;
-    hipLaunchKernelGGL((k_expand<T, OutT, MODE>), dim3(nchunks), dim3(kBlock), 0, s, bv, in, n, rows_per_chunk,
-                       chunk_off, out, cap, dict, aux_len, err);
-    return hipGetLastError();
-}
-
-template hipError_t launch_expand<uint8_t, uint64_t, 0>(const uint64_t *, const uint8_t *, uint64_t, uint64_t,
-                                                        uint32_t, const uint64_t *, uint64_t *, uint64_t,
-                                                        hipStream_t, const int64_t *, uint64_t, uint32_t *);
-template hipError_t launch_expand<int32_t, uint64_t, 0>(const uint64_t *, const int32_t *, uint64_t, uint64_t,
-                                                        uint32_t, const uint64_t *, uint64_t *, uint64_t,
-                                                        hipStream_t, const int64_t *, uint64_t, uint32_t *);
-template hipError_t launch_expand<uint8_t, uint32_t, 1>(const uint64_t *, const uint8_t *, uint64_t, uint64_t,
-                                                        uint32_t, const uint64_t *, uint32_t *, uint64_t,
-                                                        hipStream_t, const int64_t *, uint64_t, uint32_t *);
-template hipError_t launch_expand<int32_t, int32_t, 1>(const uint64_t *, const int32_t *, uint64_t, uint64_t,
-                                                       uint32_t, const uint64_t *, int32_t *, uint64_t,
-                                                       hipStream_t, const int64_t *, uint64_t, uint32_t *);
-
-template hipError_t launch_expand<uint8_t, int64_t, 2>(const uint64_t *, const uint8_t *, uint64_t, uint64_t,
-                                                       uint32_t, const uint64_t *, int64_t *, uint64_t, hipStream_t,
-                                                       const int64_t *, uint64_t, uint32_t *);
-template hipError_t launch_expand<uint16_t, int64_t, 2>(const uint64_t *, const uint16_t *, uint64_t, uint64_t,
-                                                        uint32_t, const uint64_t *, int64_t *, uint64_t, hipStream_t,
-                                                        const int64_t *, uint64_t, uint32_t *);
-template hipError_t launch_expand<uint32_t, int64_t, 2>(const uint64_t *, const uint32_t *, uint64_t, uint64_t,
-                                                        uint32_t, const uint64_t *, int64_t *, uint64_t, hipStream_t,
-                                                        const int64_t *, uint64_t, uint32_t *);
-// named by run<T, uint64_t>'s value branch, never called
-template hipError_t launch_expand<uint8_t, uint64_t, 1>(const uint64_t *, const uint8_t *, uint64_t, uint64_t,
-                                                        uint32_t, const uint64_t *, uint64_t *, uint64_t, hipStream_t,
-                                                        const int64_t *, uint64_t, uint32_t *);
-template hipError_t launch_expand<int32_t, uint64_t, 1>(const uint64_t *, const int32_t *, uint64_t, uint64_t,
-                                                        uint32_t, const uint64_t *, uint64_t *, uint64_t, hipStream_t,
-                                                        const int64_t *, uint64_t, uint32_t *);
-template hipError_t launch_expand<uint8_t, uint64_t, 3>(const uint64_t *, const uint8_t *, uint64_t, uint64_t,
-                                                        uint32_t, const uint64_t *, uint64_t *, uint64_t, hipStream_t,
-                                                        const int64_t *, uint64_t, uint32_t *);
-
 // ------------------------------------------------------- one-pass selection ---
 // Index / value / dictionary output in ONE pass over the column (implicit_index_scan,
 // scan and dict_scan_* of SIMD512.cpp:91-150, 251-287, 289-629): the column is read
@@ -495,8 +355,12 @@ template hipError_t launch_expand<uint8_t, uint64_t, 3>(const uint64_t *, const 
 //      back to the nearest inclusive prefix, and the chunk's own inclusive prefix is
 //      published; a predecessor that has not counted yet is polled again — it is
 //      already running, so the wait ends;
-//   3. the LDS bitvector expanded exactly like k_expand (per-wave LDS staging of
-//      the matches, coalesced stores) at the chunk's exclusive prefix.
+//   3. the LDS bitvector expanded at the chunk's exclusive prefix: each wave takes 64
+//      words (4096 rows) per step, one word per lane; a lane writes the row offsets of
+//      its set bits into the wave's LDS staging area at its exclusive word-popcount
+//      prefix, then lane j writes the wave's j-th, (j+64)-th, ... output (every store
+//      instruction covers 64 consecutive output slots; dense steps stage in rounds of
+//      kStage).
 // The chunk that ends the column writes the total.
 constexpr uint32_t kSelChunk = 65536;  // rows per chunk of 32-bit values (8 KiB LDS bitvector)
 // narrower codes take proportionally more rows per chunk (the same 256 KiB of input)

@@ -2,8 +2,7 @@
 SGXAMD_DIGIT_SIDE=0 (pass-2 histograms over the tuples instead of the digit side
 stream), SGXAMD_BIG_JOIN=0 (R partitions above 8192 tuples in 8192-tuple chain tables
 instead of the 16,384-tuple counting table; the 5-bit plan below has 32,768-tuple
-partitions) and SGXAMD_SCAN_ONEPASS=0 (index / value / dictionary scans as bitvector
-pass + expand pass instead of the one-pass look-back selection), SGXAMD_SMALL_JOIN=0
+partitions), SGXAMD_SMALL_JOIN=0
 (small one-pass joins on the regular launch sequence instead of the three-launch path:
 the (5, 1) plan and the full-range cases below take it), SGXAMD_POOL=0 (two-pass plans
 with a pass-1 histogram and cursors instead of the pooled pass 1 and block-list pass 2;
@@ -74,8 +73,8 @@ print("paths ok")
 """
 
 
-@pytest.mark.parametrize("env", [{"SGXAMD_DIGIT_SIDE": "0", "SGXAMD_SCAN_ONEPASS": "0", "SGXAMD_BIG_JOIN": "0"},
-                                 {"SGXAMD_DIGIT_SIDE": "1", "SGXAMD_SCAN_ONEPASS": "1", "SGXAMD_BIG_JOIN": "1"},
+@pytest.mark.parametrize("env", [{"SGXAMD_DIGIT_SIDE": "0", "SGXAMD_BIG_JOIN": "0"},
+                                 {"SGXAMD_DIGIT_SIDE": "1", "SGXAMD_BIG_JOIN": "1"},
                                  {"SGXAMD_SMALL_JOIN": "0"},
                                  {"SGXAMD_POOL": "0"}, {"SGXAMD_POOL_SEGS": "3"}, {"SGXAMD_POOL_SEGS": "100000"},
                                  {"SGXAMD_KEYS": "0"}, {"SGXAMD_SORT2": "0"}])
