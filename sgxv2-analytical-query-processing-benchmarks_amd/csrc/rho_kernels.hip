@@ -1168,20 +1168,25 @@ struct SortBlkLds {
     uint32_t wsum[NT / kWave + 1];
 };
 
-// Geometry (development: compile-time variants through scripts/build_variant.sh):
-// 512 threads x 16 keys (8192-key tiles), three workgroups per CU = 6 waves per SIMD
-// (80 VGPRs).
+// Geometry (compile-time variants through scripts/build_variant.sh + ab_lib.sh, r03v-x):
+// 1024 threads x 16 keys = 16,384-key tiles, one workgroup per CU (4 waves per SIMD,
+// 128 VGPRs), phase D fully unrolled: 0.529-0.554 ms per 2^28 keys on three boxes
+// against 0.585-0.63 for 512 x 16 with three workgroups per CU (the longer digit runs
+// per tile -- 128 keys, 512 B -- leave fewer partial lines and per-tile steps).  Larger
+// tiles spill (24 keys per thread: 0.94 ms); two 1024-thread workgroups per CU without
+// the next-tile prefetch (64 VGPRs), or with the ranks taken by a second LDS atomic in
+// phase C, measured equal (0.52-0.55); 512-key segments (SGXAMD_PASS2_ENTS=512) 0.54-0.57.
 #ifndef SGXAMD_SORT_NT
-#define SGXAMD_SORT_NT 512
+#define SGXAMD_SORT_NT 1024
 #endif
 #ifndef SGXAMD_SORT_ITEMS
 #define SGXAMD_SORT_ITEMS 16
 #endif
 #ifndef SGXAMD_SORT_WGS
-#define SGXAMD_SORT_WGS 3
+#define SGXAMD_SORT_WGS 1
 #endif
 #ifndef SGXAMD_SORT_UNROLL
-#define SGXAMD_SORT_UNROLL 2
+#define SGXAMD_SORT_UNROLL 16
 #endif
 template <int BITS, int NT, int ITEMS>
 __global__ __launch_bounds__(NT, NT * SGXAMD_SORT_WGS / 256) void k_sort_blk(const uint32_t *__restrict__ in, const uint64_t *__restrict__ list,
@@ -1260,7 +1265,7 @@ __global__ __launch_bounds__(NT, NT * SGXAMD_SORT_WGS / 256) void k_sort_blk(con
         __syncthreads();
         // D. sorted position q -> off[d] + q: consecutive lanes, consecutive addresses
         const uint32_t tn = L.wsum[NW];
-#pragma unroll SGXAMD_SORT_UNROLL  // (fully unrolled, the 64-bit destinations of all items stay live: 125 VGPRs)
+#pragma unroll SGXAMD_SORT_UNROLL
         for (int u = 0; u < (int)ITEMS; ++u) {
             const uint32_t q = tid + (uint32_t)u * NT;
             if (q < tn) {
@@ -1347,7 +1352,8 @@ hipError_t launch_scatter_pool(const void *in, uint32_t in_size, void *out, uint
 
 // SGXAMD_SORT2 (development A/B switch, read once): 1 (default) = key partitions' pass 2
 // as the LDS counting sort k_sort_blk; 0 = the write-combining k_scatter_blk.
-// 2^28 keys, alternating on one box: 0.569-0.578 ms per relation vs 0.583-0.599 (k_scatter_blk).
+// 2^28 keys per relation: 0.53-0.55 ms (16,384-key tiles, r03v-x) vs 0.585-0.60 for
+// k_scatter_blk (alternating on one box, r03u).
 bool sort2_enabled() {
     static const bool on = [] {
         const char *e = std::getenv("SGXAMD_SORT2");
