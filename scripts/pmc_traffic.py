@@ -15,6 +15,7 @@ import collections
 import csv
 import glob
 import json
+import os
 import sys
 
 # rocprof kernel name -> bench.py timer names (|R| = |S| in the bench, so the launches
@@ -25,6 +26,7 @@ ALIASES = {
     # pooled two-pass plans (one kernel per pass; listed after BY_GRID, so they win)
     "k_scatter_pool": ["R_pass1_scatter", "S_pass1_scatter"],
     "k_scatter_blk": ["R_pass2_scatter", "S_pass2_scatter"],
+    "k_sort_blk": ["R_pass2_scatter", "S_pass2_scatter"],
     "k_hist_side_blk": ["R_pass2_hist", "S_pass2_hist"],
     "k_join": ["join_build_probe"],
     "k_join_tag": ["join_build_probe"],
@@ -97,7 +99,7 @@ def main():
         if k in per_kernel:
             for name in names:
                 bytes_per_launch[name] = per_kernel[k]["total_bytes"]
-    json.dump({"log2n": log2n, "source": run,
+    json.dump({"log2n": log2n, "source": run, "commit": os.environ.get("COMMIT", "unknown"),
                "correction": "read = 2 * FETCH_SIZE KiB (gfx950), write = WRITE_SIZE KiB; per kernel, the mean "
                              "over launches within 2x of its largest launch (the bench-size ones)",
                "bytes_per_launch": bytes_per_launch, "per_kernel": per_kernel}, open(out, "w"), indent=1)
