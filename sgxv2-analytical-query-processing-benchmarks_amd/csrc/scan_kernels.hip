@@ -355,18 +355,26 @@ constexpr uint32_t kStage = 1024;  // staged outputs per wave and round (u32 row
 //      back to the nearest inclusive prefix, and the chunk's own inclusive prefix is
 //      published; a predecessor that has not counted yet is polled again — it is
 //      already running, so the wait ends;
-//   3. the LDS bitvector expanded at the chunk's exclusive prefix: each wave takes 64
-//      words (4096 rows) per step, one word per lane; a lane writes the row offsets of
+//   3. the LDS bitvector expanded at the chunk's exclusive prefix: each wave expands a
+//      contiguous quarter of the words (one block barrier for the quarters' offsets,
+//      1.77 vs 1.82 ms at the uint8 10 % shape with the waves interleaved per 64-word
+//      step and a barrier per step), 64 words (4096 rows) per step, one word per lane;
+//      a lane writes the row offsets of
 //      its set bits into the wave's LDS staging area at its exclusive word-popcount
 //      prefix, then lane j writes the wave's j-th, (j+64)-th, ... output (every store
 //      instruction covers 64 consecutive output slots; dense steps stage in rounds of
 //      kStage).
 // The chunk that ends the column writes the total.
 constexpr uint32_t kSelChunk = 65536;  // rows per chunk of 32-bit values (8 KiB LDS bitvector)
-// narrower codes take proportionally more rows per chunk (the same 256 KiB of input)
+// uint16 codes take 131,072 rows per chunk (the same 256 KiB of input)
+// (uint8: 131,072 rows, 16 KiB of LDS bitvector, five workgroups per CU: 1.77 ms at the
+// reference's 2^32-code 10 % shape against 1.81 with 65,536 and 1.97 with 262,144 rows)
 template <typename T>
-constexpr uint32_t sel_chunk() { return kSelChunk * (uint32_t)(4 / sizeof(T)); }
+constexpr uint32_t sel_chunk() { return sizeof(T) == 1 ? 2 * kSelChunk : kSelChunk * (uint32_t)(4 / sizeof(T)); }
 
+#ifndef SGXAMD_SEL_ABLATE
+#define SGXAMD_SEL_ABLATE 0
+#endif
 template <typename T, typename OutT, int MODE>
 __global__ __launch_bounds__(kBlock) void k_select(const T *__restrict__ in, uint64_t n, T lo, T hi,
                                                    uint32_t *__restrict__ ticket, uint64_t *__restrict__ status,
@@ -375,7 +383,7 @@ __global__ __launch_bounds__(kBlock) void k_select(const T *__restrict__ in, uin
                                                    uint64_t *__restrict__ total) {
     constexpr uint32_t V = 16 / sizeof(T), LPW = 64 / V, FULL = (1u << V) - 1u;
     constexpr uint32_t CH = sel_chunk<T>(), NWORD = CH / 64;
-    constexpr int U = 8;  // 16-B loads in flight per lane
+    constexpr int U = 8;  // 16-B loads in flight per lane (uint8: 4 or 16 measured equal)
     __shared__ uint64_t bits[NWORD];
     constexpr uint32_t STG = kStage;
     __shared__ uint32_t stage_s[kWaves][STG];
@@ -450,25 +458,29 @@ __global__ __launch_bounds__(kBlock) void k_select(const T *__restrict__ in, uin
     if (r1 == n && threadIdx.x == 0) *total = excl + agg;
 
     // 3. expand the LDS bitvector at the chunk's prefix
-    uint64_t base_out = excl;
-    for (uint32_t wb = 0; wb < nw; wb += kWaves * 64) {
-        const uint32_t wi = wb + wave * 64 + lane;
-        const uint64_t x = wi < nw ? bits[wi] : 0ull;
+#if SGXAMD_SEL_ABLATE == 1  // development ablation: no expand
+    return;
+#endif
+    // each wave expands a contiguous quarter of the chunk's words on its own (one block
+    // barrier per chunk for the quarters' output offsets, wave-level syncs after it)
+    const uint32_t qw = (nw + kWaves - 1) / kWaves;
+    const uint32_t w0 = min(nw, wave * qw), w1 = min(nw, w0 + qw);
+    uint32_t qc = 0;
+    for (uint32_t wi = w0 + lane; wi < w1; wi += 64) qc += __popcll(bits[wi]);
+    qc = wave_incl_scan_u32(qc);
+    if (lane == 63) wtot_s[wave] = qc;
+    __syncthreads();
+    uint64_t woff = excl;
+    for (int w = 0; w < (int)wave; ++w) woff += wtot_s[w];
+    uint32_t *stage = stage_s[wave];
+    for (uint32_t wb = w0; wb < w1; wb += 64) {
+        const uint32_t wi = wb + lane;
+        const uint64_t x = wi < w1 ? bits[wi] : 0ull;
         const uint32_t cnt = __popcll(x);
         const uint32_t incl = wave_incl_scan_u32(cnt);
         const uint32_t ex = incl - cnt;
         const uint32_t wtot = __shfl(incl, 63, kWave);
-        if (lane == 0) wtot_s[wave] = wtot;
-        __syncthreads();
-        uint64_t woff = base_out, all = 0;
-#pragma unroll
-        for (int w = 0; w < kWaves; ++w) {
-            const uint32_t t = wtot_s[w];
-            if (w < (int)wave) woff += t;
-            all += t;
-        }
-        const uint64_t row0 = r0 + (uint64_t)(wb + wave * 64) * 64;
-        uint32_t *stage = stage_s[wave];
+        const uint64_t row0 = r0 + (uint64_t)wb * 64;
         for (uint32_t s0 = 0; s0 < wtot; s0 += STG) {
             const uint32_t s1 = s0 + STG;
             if (ex < s1 && incl > s0) {
@@ -486,17 +498,17 @@ __global__ __launch_bounds__(kBlock) void k_select(const T *__restrict__ in, uin
             for (uint32_t m = lane; m < nr; m += 64) {
                 const uint64_t row = row0 + stage[m];
                 const uint64_t o = woff + s0 + m;
-                if (o < cap) {
-                    // non-temporal: the outputs are not re-read here (measured 4 % faster
-                    // than plain stores at C3)
+                if (o < cap && SGXAMD_SEL_ABLATE != 2) {
+                    // non-temporal: the outputs are not re-read here (4 % faster than plain
+                    // stores at C3; each lane storing its own matches instead of the staged,
+                    // coalesced stores: 3.5 vs 1.8 ms at the uint8 10 % shape)
                     const OutT v = select_value<T, OutT, MODE>(row, in, dict, aux_len, &ticket[1]);
                     __builtin_nontemporal_store(v, out + o);
                 }
             }
             wave_lds_sync();
         }
-        base_out += all;
-        __syncthreads();
+        woff += wtot;
     }
 }
 
