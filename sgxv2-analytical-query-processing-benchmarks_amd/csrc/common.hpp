@@ -81,16 +81,26 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
     return v;
 }
 
-// Inclusive prefix sum over the wave.
-__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
-    const uint32_t lane = __lane_id();
-#pragma unroll
-    for (int off = 1; off < kWave; off <<= 1) {
-        uint32_t t = __shfl_up(v, off, kWave);
-        if (lane >= (uint32_t)off) v += t;
-    }
+// Inclusive prefix sum over the wave on the VALU with DPP (no LDS round trips): a
+// Kogge-Stone scan inside each 16-lane row (row_shr:1/2/4/8, lanes shifted in from
+// outside the row read 0), then row_bcast:15 adds row 0's total to row 1 and row 2's to
+// row 3, and row_bcast:31 adds lane 31's running total to rows 2 and 3 (GFX9 DPP).
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp_or0(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWS, 0xF, true);
+}
+__device__ __forceinline__ uint32_t wave_incl_scan_dpp_u32(uint32_t v) {
+    v += dpp_or0<0x111, 0xF>(v);  // row_shr:1
+    v += dpp_or0<0x112, 0xF>(v);  // row_shr:2
+    v += dpp_or0<0x114, 0xF>(v);  // row_shr:4
+    v += dpp_or0<0x118, 0xF>(v);  // row_shr:8
+    v += dpp_or0<0x142, 0xA>(v);  // row_bcast:15 into rows 1 and 3
+    v += dpp_or0<0x143, 0xC>(v);  // row_bcast:31 into rows 2 and 3
     return v;
 }
+
+// Inclusive prefix sum over the wave.
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) { return wave_incl_scan_dpp_u32(v); }
 
 __device__ __forceinline__ uint64_t wave_incl_scan_u64(uint64_t v) {
     const uint32_t lane = __lane_id();

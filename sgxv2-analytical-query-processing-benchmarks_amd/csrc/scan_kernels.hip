@@ -403,6 +403,26 @@ __global__ __launch_bounds__(kBlock) void k_select(const T *__restrict__ in, uin
     // 1. predicate -> LDS bitvector + count
     uint64_t count = 0;
     constexpr uint32_t STEP = kWaves * 64 * V;  // rows per block per load round
+    static_assert(CH % (U * STEP) == 0, "whole load rounds per chunk");
+    if (r1 - r0 == CH) {
+        // a whole chunk (every chunk but the column's last): raw buffer loads over the
+        // chunk, no per-load bounds branches
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(in + r0, CH * (uint32_t)sizeof(T));
+        const uint32_t voff = (wave * 64 * V + lane * V) * (uint32_t)sizeof(T);
+        for (uint32_t it = 0; it < CH / (U * STEP); ++it) {
+            uint4 q[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) q[u] = buf_ld_nt_u128(rs, voff, (it * U + u) * STEP * (uint32_t)sizeof(T));
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t m = match_mask<T>(q[u], lo, hi, FULL);
+                count += __popc(m);
+                const uint64_t x = group_or<LPW>((uint64_t)m << (V * (lane % LPW)));
+                const uint32_t row = (it * U + u) * STEP + wave * 64 * V + lane * V;  // chunk-relative
+                if ((lane % LPW) == 0) bits[row / 64] = x;
+            }
+        }
+    } else
     // wave-uniform loop: lanes past r1 read nothing and contribute empty masks, so every
     // lane takes part in the DPP word assembly
     for (uint64_t wbase = r0 + (uint64_t)wave * 64 * V; wbase < r1; wbase += U * STEP) {
@@ -467,8 +487,8 @@ __global__ __launch_bounds__(kBlock) void k_select(const T *__restrict__ in, uin
     const uint32_t w0 = min(nw, wave * qw), w1 = min(nw, w0 + qw);
     uint32_t qc = 0;
     for (uint32_t wi = w0 + lane; wi < w1; wi += 64) qc += __popcll(bits[wi]);
-    qc = wave_incl_scan_u32(qc);
-    if (lane == 63) wtot_s[wave] = qc;
+    qc = wave_sum_u32(qc);
+    if (lane == 0) wtot_s[wave] = qc;
     __syncthreads();
     uint64_t woff = excl;
     for (int w = 0; w < (int)wave; ++w) woff += wtot_s[w];
@@ -477,10 +497,36 @@ __global__ __launch_bounds__(kBlock) void k_select(const T *__restrict__ in, uin
         const uint32_t wi = wb + lane;
         const uint64_t x = wi < w1 ? bits[wi] : 0ull;
         const uint32_t cnt = __popcll(x);
-        const uint32_t incl = wave_incl_scan_u32(cnt);
+        const uint32_t incl = wave_incl_scan_dpp_u32(cnt);
         const uint32_t ex = incl - cnt;
-        const uint32_t wtot = __shfl(incl, 63, kWave);
+        const uint32_t wtot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
         const uint64_t row0 = r0 + (uint64_t)wb * 64;
+        if (wtot <= STG) {
+            // the step's matches fit the staging area (every step below 1/4 density):
+            // no staging rounds, and each 32-bit half of the word in its own bit loop
+            // (v_ffbl_b32 + y &= y - 1 + one LDS store per set bit)
+            uint32_t p = ex;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                uint32_t y = (uint32_t)(x >> (32 * h));
+                const uint32_t base = lane * 64 + 32 * h;
+                while (y) {
+                    stage[p++] = base + (uint32_t)__builtin_ctz(y);
+                    y &= y - 1;
+                }
+            }
+            wave_lds_sync();
+            for (uint32_t m = lane; m < wtot; m += 64) {
+                const uint64_t o = woff + m;
+                if (o < cap && SGXAMD_SEL_ABLATE != 2) {
+                    const OutT v = select_value<T, OutT, MODE>(row0 + stage[m], in, dict, aux_len, &ticket[1]);
+                    __builtin_nontemporal_store(v, out + o);
+                }
+            }
+            wave_lds_sync();
+            woff += wtot;
+            continue;
+        }
         for (uint32_t s0 = 0; s0 < wtot; s0 += STG) {
             const uint32_t s1 = s0 + STG;
             if (ex < s1 && incl > s0) {
