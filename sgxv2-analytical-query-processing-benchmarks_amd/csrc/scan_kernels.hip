@@ -26,17 +26,32 @@ constexpr int kUnroll = 4;
 template <typename T>
 __device__ __forceinline__ uint32_t match_mask(const uint4 &q, T lo, T hi, uint32_t valid);
 
-// 16 uint8 codes -> 16-bit mask (unsigned compare, _mm512_cmpge/le_epu8_mask).
+// 16 uint8 codes -> 16-bit mask (unsigned compare, _mm512_cmpge/le_epu8_mask), on packed
+// 16-bit halves: pair k holds codes k and k + 8 (one v_perm_b32 from words k/4 and
+// k/4 + 2), b + 256 - lo has bit 8 set iff b >= lo and hi + 256 - b iff b <= hi (both
+// in [1, 511]), so (b + 256 - lo) & (hi + 256 - b) & 0x100 is the predicate of code k,
+// and of code k + 8 at bit 24.  The eight pairs' flags are OR-ed in at bits 8 + k /
+// 24 + k (v_lshl_or_b32) and one v_perm_b32 takes bytes 1 and 3: 5 VALU per 2 codes,
+// against 3 VALU (two SGPR-writing compares and a select) + 1 SALU per code before.
+typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
 template <>
 __device__ __forceinline__ uint32_t match_mask<uint8_t>(const uint4 &q, uint8_t lo, uint8_t hi, uint32_t valid) {
     const uint32_t w[4] = {q.x, q.y, q.z, q.w};
-    uint32_t m = 0;
+    const unsigned short c1 = (unsigned short)(256u - lo), c2 = (unsigned short)(256u + hi);
+    const u16x2_t vc1 = {c1, c1}, vc2 = {c2, c2};
+    uint32_t acc = 0;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        const uint32_t b = __builtin_amdgcn_ubfe(w[j >> 2], (j & 3) * 8, 8);
-        m |= (uint32_t)(b >= lo && b <= hi) << j;
+    for (int k = 0; k < 8; ++k) {
+        const uint32_t sel = 0x0c000c00u | ((4u + (k & 3)) << 16) | (uint32_t)(k & 3);
+        const u16x2_t p = __builtin_bit_cast(u16x2_t, __builtin_amdgcn_perm(w[2 + (k >> 2)], w[k >> 2], sel));
+        const uint32_t t = __builtin_bit_cast(uint32_t, p + vc1);
+        const uint32_t u = __builtin_bit_cast(uint32_t, vc2 - p);
+        const uint32_t f = __builtin_amdgcn_bitop3_b32(t, u, 0x01000100u, 0x80);  // t & u & mask
+        if (k == 0) acc = f;
+        else  // one v_lshl_or_b32 (left to itself the compiler shifts, then masks, then ORs)
+            asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(acc) : "v"(f), "i"(k), "v"(acc));
     }
-    return m & valid;
+    return __builtin_amdgcn_perm(0u, acc, 0x0c0c0301u) & valid;
 }
 
 // 4 int32 values -> 4-bit mask (signed compare).
@@ -394,7 +409,9 @@ __global__ __launch_bounds__(kBlock) void k_select(const T *__restrict__ in, uin
     const uint32_t lane = __lane_id(), wave = threadIdx.x / kWave;
     if (threadIdx.x == 0) chunk_s = atomicAdd(ticket, 1u);
     __syncthreads();
-    const uint32_t c = chunk_s;
+    // uniform by construction; readfirstlane keeps the chunk's buffer resource in SGPRs
+    // (read from LDS it stayed a VGPR value, and every buffer load became a waterfall loop)
+    const uint32_t c = (uint32_t)__builtin_amdgcn_readfirstlane((int)chunk_s);
     const uint64_t r0 = (uint64_t)c * CH;
     if (r0 >= n) return;  // (the grid has exactly one workgroup per chunk)
     const uint64_t r1 = min<uint64_t>(r0 + CH, n);
@@ -505,22 +522,57 @@ __global__ __launch_bounds__(kBlock) void k_select(const T *__restrict__ in, uin
             // the step's matches fit the staging area (every step below 1/4 density):
             // no staging rounds, and each 32-bit half of the word in its own bit loop
             // (v_ffbl_b32 + y &= y - 1 + one LDS store per set bit)
+            // the set bits leave in groups of four (two ds_write2_b32 per group) after
+            // a single and a pair that make the rest a multiple of four: a lane's loop
+            // runs popcount / 4 times, and no write lands past its own slots (the
+            // next lane's first slot is taken in the first round)
             uint32_t p = ex;
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 uint32_t y = (uint32_t)(x >> (32 * h));
                 const uint32_t base = lane * 64 + 32 * h;
-                while (y) {
+                const uint32_t ch = __popc(y);
+                if (ch & 1u) {
                     stage[p++] = base + (uint32_t)__builtin_ctz(y);
                     y &= y - 1;
                 }
+                if (ch & 2u) {
+                    const uint32_t a = (uint32_t)__builtin_ctz(y);
+                    y &= y - 1;
+                    const uint32_t b = (uint32_t)__builtin_ctz(y);
+                    y &= y - 1;
+                    stage[p] = base + a;
+                    stage[p + 1] = base + b;
+                    p += 2;
+                }
+                while (y) {
+                    uint32_t s[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        s[j] = base + (uint32_t)__builtin_ctz(y);
+                        y &= y - 1;
+                    }
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) stage[p + j] = s[j];
+                    p += 4;
+                }
             }
             wave_lds_sync();
-            for (uint32_t m = lane; m < wtot; m += 64) {
-                const uint64_t o = woff + m;
-                if (o < cap && SGXAMD_SEL_ABLATE != 2) {
-                    const OutT v = select_value<T, OutT, MODE>(row0 + stage[m], in, dict, aux_len, &ticket[1]);
-                    __builtin_nontemporal_store(v, out + o);
+            // four staged offsets read per lane before their stores (one LDS wait per
+            // four outputs instead of one per output)
+            const bool fits = woff + wtot <= cap;
+            for (uint32_t m0 = 0; m0 < wtot; m0 += 4 * 64) {
+                uint32_t s[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) s[j] = stage[(m0 + j * 64 + lane) & (STG - 1)];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t m = m0 + j * 64 + lane;
+                    const uint64_t o = woff + m;
+                    if (m < wtot && (fits || o < cap) && SGXAMD_SEL_ABLATE != 2) {
+                        const OutT v = select_value<T, OutT, MODE>(row0 + s[j], in, dict, aux_len, &ticket[1]);
+                        __builtin_nontemporal_store(v, out + o);
+                    }
                 }
             }
             wave_lds_sync();
