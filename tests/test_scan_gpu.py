@@ -35,6 +35,34 @@ def test_all_outputs_match_oracle(sgx, orc, gpu, dtype, n):
             assert np.array_equal(vals[:cnt], orc.scan("values", dtype, lo, hi, col))
 
 
+def test_u8_predicate_sweep(sgx, orc, gpu):
+    """The uint8 predicate on packed 16-bit halves ((b + 256 - lo) & (hi + 256 - b) & 0x100,
+    scan_kernels.hip match_mask<uint8_t>) against the oracle for bounds on and around every
+    byte-boundary case, empty ranges (lo > hi) included, on a ragged column holding every
+    code at every lane and byte position: count and bitvector for all 196 (lo, hi) pairs,
+    index and values for every seventh pair (SIMD512.cpp:7-32, 210-222, 251-287)."""
+    import torch
+
+    n = 3 * 65536 + 77
+    col = np.random.default_rng(11).integers(0, 256, n).astype(np.uint8)
+    col[:4096] = np.arange(4096) % 256  # every code at every byte of a 16-byte lane load
+    d = torch.from_numpy(col).to(gpu)
+    bounds = [0, 1, 2, 7, 8, 15, 16, 100, 127, 128, 129, 200, 254, 255]
+    bv = torch.zeros((n + 63) // 64, dtype=torch.int64, device=gpu)
+    for i, (lo, hi) in enumerate((a, b) for a in bounds for b in bounds):
+        cnt = orc.scan("count", "u8", lo, hi, col)
+        assert sgx.scan_count(lo, hi, d, n, "u8") == cnt, (lo, hi)
+        sgx.scan_bitvector(lo, hi, d, n, bv, "u8")
+        assert np.array_equal(bv.cpu().numpy().view(np.uint64), orc.scan("bitvector", "u8", lo, hi, col)), (lo, hi)
+        if i % 7 == 0:
+            idx = torch.zeros(max(cnt, 1), dtype=torch.int64, device=gpu)
+            assert sgx.scan_index(lo, hi, d, n, idx, cnt, "u8") == cnt
+            assert np.array_equal(idx.cpu().numpy().view(np.uint64)[:cnt], orc.scan("index", "u8", lo, hi, col))
+            vals = np.zeros(max(cnt, 1), dtype=np.uint32)
+            assert sgx.scan_values(lo, hi, col, n, vals, cnt, "u8") == cnt
+            assert np.array_equal(vals[:cnt], orc.scan("values", "u8", lo, hi, col))
+
+
 def test_signed_i32_full_range(sgx, orc, gpu):
     col = np.random.default_rng(3).integers(-(2**31), 2**31, 200_003, dtype=np.int64).astype(np.int32)
     for lo, hi in [(-(2**31), -1), (-1000, 1000), (0, 2**31 - 1), (-(2**31), 2**31 - 1)]:
