@@ -29,7 +29,7 @@ sys.path.insert(0, os.path.join(PKG, "python"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 METRIC = "M probed tuples/sec (RHO join) + scan GB/s vs HBM roofline, 1/2/4/8 MI355X"
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic_r03q2.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic_r03q7.json")
 
 
 def log(*a):
@@ -519,7 +519,7 @@ def main():
         t1 = time.perf_counter()
         for _ in range(reps1):
             r1 = sgxamd.rho_join(R1, c1, S1, c1, stream=stream)
-            dev_ms.append(r1.stats["ms_total"])
+            dev_ms.append(r1.stat("ms_total"))  # one field: no stats dict in the timed loop
         barrier()
         el1 = (time.perf_counter() - t1) / reps1
         sgxamd.timing_enable(True)

@@ -364,6 +364,10 @@ class JoinResult:
             self._stats = self._raw.as_dict()
         return self._stats
 
+    def stat(self, name: str):
+        """One field of the stats, without building the dict."""
+        return self._stats[name] if self._stats is not None else getattr(self._raw, name)
+
     def __repr__(self) -> str:
         return f"JoinResult(matches={self.matches}, stats={self.stats})"
 
