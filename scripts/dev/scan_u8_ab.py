@@ -41,3 +41,6 @@ c32 = torch.empty(ns, dtype=torch.int32, device="cuda")
 sgx.gen_scan_dev(c32, ns, 0, 0, "i32")
 t = kt(lambda: sgx.scan_count(0, 26, c32, ns))
 print("i32 count", t, f"{4 * ns / (t['scan_count'] * 1e-3) / 1e12:.2f} TB/s", flush=True)
+bv32 = torch.empty(ns // 64, dtype=torch.int64, device="cuda")
+t = kt(lambda: sgx.scan_bitvector(0, 26, c32, ns, bv32))
+print("i32 bitvector", t, f"{(4 * ns + ns // 8) / (t['scan_bitvector'] * 1e-3) / 1e12:.2f} TB/s", flush=True)

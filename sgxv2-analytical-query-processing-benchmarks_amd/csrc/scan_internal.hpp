@@ -9,7 +9,10 @@ namespace sgxamd {
 namespace scan {
 
 constexpr uint64_t kChunkQuantum = 16384;  // rows; multiple of waves * 64 * V * unroll for u8 and i32
-constexpr uint64_t kChunkTarget = 2048;    // workgroups per scan
+#ifndef SGXAMD_SCAN_WGS
+#define SGXAMD_SCAN_WGS 2048
+#endif
+constexpr uint64_t kChunkTarget = SGXAMD_SCAN_WGS;  // workgroups per scan
 
 template <typename T>
 hipError_t launch_predicate(const T *in, uint64_t n, T lo, T hi, uint64_t rows_per_chunk, uint32_t nchunks,

@@ -158,7 +158,8 @@ struct PredicateTile {
     template <bool FULL_TILE>
     static __device__ __forceinline__ void process(const uint4 (&q)[kUnroll], const uint32_t (&valid)[kUnroll],
                                                    uint64_t base, uint64_t r1, uint64_t nwords, T lo, T hi,
-                                                   uint64_t *__restrict__ bv, uint64_t &count) {
+                                                   uint64_t *__restrict__ bv, uint64_t &count,
+                                                   uint64_t *win = nullptr, uint64_t win_word = 0) {
         const uint32_t lane = __lane_id();
         if constexpr (WRITE && FULL_TILE && LPW == (uint32_t)kUnroll) {
             // one word per lane (u8 codes: kUnroll rounds x 16 words = 64 words per
@@ -178,9 +179,14 @@ struct PredicateTile {
                 const uint64_t x = group_or<LPW>((uint64_t)m << (V * (lane % LPW)));
                 if (mine == (uint32_t)u) w = x;
             }
+            const uint64_t word = (base + mine * STEP) / 64 + lane / LPW;
+            if (win) {  // staged in the workgroup's LDS window (k_predicate flushes it)
+                win[word - win_word] = w;
+                return;
+            }
             // non-temporal: 0.957 vs 0.986 ms at 2^32 codes (the redundant-lane stores of
             // the loop below measured 20 % slower non-temporal)
-            __builtin_nontemporal_store(w, bv + (base + mine * STEP) / 64 + lane / LPW);
+            __builtin_nontemporal_store(w, bv + word);
             return;
         }
 #pragma unroll
@@ -193,13 +199,21 @@ struct PredicateTile {
                 const uint64_t word = (base + u * STEP) / 64 + lane / LPW;
                 // (a non-temporal word store measured 20 % slower, one lane per group
                 // storing 2 % slower)
-                if (FULL_TILE) bv[word] = x;
+                if (FULL_TILE && win) {  // staged in the workgroup's LDS window
+                    if ((lane % LPW) == 0) win[word - win_word] = x;
+                } else if (FULL_TILE) bv[word] = x;
                 else if ((lane % LPW) == 0 && word < nwords && (base + u * STEP) < r1) bv[word] = x;
             }
         }
     }
 };
 
+#ifndef SGXAMD_BV_BURST
+#define SGXAMD_BV_BURST 1
+#endif
+#ifndef SGXAMD_BV_I32
+#define SGXAMD_BV_I32 1
+#endif
 template <typename T, bool WRITE, bool SUM = false>
 __global__ __launch_bounds__(kBlock) void k_predicate(const T *__restrict__ in, uint64_t n, T lo, T hi,
                                                       uint64_t rows_per_chunk, uint64_t *__restrict__ bv,
@@ -209,6 +223,19 @@ __global__ __launch_bounds__(kBlock) void k_predicate(const T *__restrict__ in, 
     constexpr uint64_t STEP = PT::STEP;
     constexpr uint64_t ITER = STEP * kUnroll;  // rows per block iteration
     __shared__ uint64_t red[kWaves];
+    // bitvectors: the words of BW block iterations are staged in LDS and written in one
+    // burst per window (16-B non-temporal stores, consecutive lanes on consecutive
+    // addresses) instead of one store per wave and iteration between the column's
+    // reads.  uint8 at 2^32 codes, 1 %, on one box (profiles/r03q9_bitvector_window_ab.log):
+    // direct stores 0.92 ms; windows of 8 / 16 / 32 / 40 / 64 / 72 iterations 0.90 /
+    // 0.89 / 0.83 / 0.77 / 0.74 / 0.76 ms (64: 128 KiB of LDS, one workgroup per CU; with
+    // 1,024 or 4,096 workgroups 0.75-0.76 / 0.73); int32 2^30: 0.765-0.776 -> 0.748-0.759
+    constexpr bool BURST = WRITE && SGXAMD_BV_BURST && (SGXAMD_BV_I32 || PT::LPW == (uint32_t)kUnroll);
+#ifndef SGXAMD_BV_WIN
+#define SGXAMD_BV_WIN 64
+#endif
+    constexpr uint32_t BW = SGXAMD_BV_WIN, WIN = BURST ? BW * (uint32_t)(ITER / 64) : 1;
+    __shared__ uint64_t win[WIN];
     const uint32_t lane = __lane_id(), wave = threadIdx.x / kWave;
     const uint64_t r0 = (uint64_t)blockIdx.x * rows_per_chunk;
     const uint64_t r1 = (r0 + rows_per_chunk < n) ? r0 + rows_per_chunk : n;
@@ -238,6 +265,21 @@ __global__ __launch_bounds__(kBlock) void k_predicate(const T *__restrict__ in, 
             for (int u = 0; u < kUnroll; ++u) asm volatile("" ::"v"(q[u].x), "v"(q[u].y), "v"(q[u].z), "v"(q[u].w));
         };
         const uint64_t wbase = r0 + (uint64_t)wave * 64 * V;
+        uint64_t *const wp = BURST ? win : nullptr;
+        const auto win_word = [&](uint64_t it) { return (r0 + (it / BW) * BW * ITER) / 64; };
+        // after iteration it: a full window (or the last iteration) goes out in one burst
+        const auto flush = [&](uint64_t it) {
+            if constexpr (BURST) {
+                if ((it + 1) % BW != 0 && it + 1 != nfull) return;
+                __syncthreads();
+                typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
+                const uint32_t nw = (uint32_t)(it % BW + 1) * (uint32_t)(ITER / 64);
+                u64x2_t *dst = reinterpret_cast<u64x2_t *>(bv + win_word(it));
+                const u64x2_t *src = reinterpret_cast<const u64x2_t *>(win);
+                for (uint32_t i = threadIdx.x; i < nw / 2; i += kBlock) __builtin_nontemporal_store(src[i], dst + i);
+                __syncthreads();
+            }
+        };
         // iterations in pairs, no branch between a prefetch and its wait (LLVM would sink
         // a prefetch whose result is dead on an early-exit path below the next stores)
         load(qa, 0);
@@ -246,14 +288,20 @@ __global__ __launch_bounds__(kBlock) void k_predicate(const T *__restrict__ in, 
         const uint64_t npairs = nfull / 2;
         for (uint64_t p = 0; p < npairs; ++p) {
             const uint64_t it = 2 * p;
-            PT::template process<true>(qa, valid, wbase + it * ITER, r1, nwords, lo, hi, bv, count);
+            PT::template process<true>(qa, valid, wbase + it * ITER, r1, nwords, lo, hi, bv, count, wp, win_word(it));
             load(qa, it + 2);
             wait_for(qb);
-            PT::template process<true>(qb, valid, wbase + (it + 1) * ITER, r1, nwords, lo, hi, bv, count);
+            PT::template process<true>(qb, valid, wbase + (it + 1) * ITER, r1, nwords, lo, hi, bv, count, wp,
+                                       win_word(it + 1));
+            flush(it + 1);
             load(qb, it + 3);
             wait_for(qa);
         }
-        if (nfull & 1) PT::template process<true>(qa, valid, wbase + (nfull - 1) * ITER, r1, nwords, lo, hi, bv, count);
+        if (nfull & 1) {
+            PT::template process<true>(qa, valid, wbase + (nfull - 1) * ITER, r1, nwords, lo, hi, bv, count, wp,
+                                       win_word(nfull - 1));
+            flush(nfull - 1);
+        }
     }
     // ragged end of the last chunk: fewer than ITER rows, element loads at the very end
     for (uint64_t base = full_end + (uint64_t)wave * 64 * V; base < r1; base += ITER) {
