@@ -230,11 +230,17 @@ __global__ __launch_bounds__(kBlock) void k_predicate(const T *__restrict__ in, 
     // direct stores 0.92 ms; windows of 8 / 16 / 32 / 40 / 64 / 72 iterations 0.90 /
     // 0.89 / 0.83 / 0.77 / 0.74 / 0.76 ms (64: 128 KiB of LDS, one workgroup per CU; with
     // 1,024 or 4,096 workgroups 0.75-0.76 / 0.73); int32 2^30: 0.765-0.776 -> 0.748-0.759
+    // with 64 iterations (32 KiB), 0.704-0.713 with 128 (64 KiB: a 2^30-row chunk in one
+    // window; profiles/r03q12_wide_bitvector_window_ab.log)
     constexpr bool BURST = WRITE && SGXAMD_BV_BURST && (SGXAMD_BV_I32 || PT::LPW == (uint32_t)kUnroll);
 #ifndef SGXAMD_BV_WIN
 #define SGXAMD_BV_WIN 64
 #endif
-    constexpr uint32_t BW = SGXAMD_BV_WIN, WIN = BURST ? BW * (uint32_t)(ITER / 64) : 1;
+#ifndef SGXAMD_BV_WIN_WIDE
+#define SGXAMD_BV_WIN_WIDE 128
+#endif
+    constexpr uint32_t BW = sizeof(T) == 1 ? SGXAMD_BV_WIN : SGXAMD_BV_WIN_WIDE;  // iterations (16/32-bit codes)
+    constexpr uint32_t WIN = BURST ? BW * (uint32_t)(ITER / 64) : 1;
     __shared__ uint64_t win[WIN];
     const uint32_t lane = __lane_id(), wave = threadIdx.x / kWave;
     const uint64_t r0 = (uint64_t)blockIdx.x * rows_per_chunk;
