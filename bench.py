@@ -162,6 +162,91 @@ LAYOUTS = {
 }
 
 
+def visible_gpus() -> int:
+    """GPUs this process could use, counted without initialising HIP (on this image
+    torch.cuda.device_count() does not initialise the GPU)."""
+    import torch
+
+    return torch.cuda.device_count()
+
+
+def launch_ranks(cmd: list[str], n: int, grace_s: float = 60.0, env_extra: dict | None = None) -> int:
+    """Runs `cmd` as n rank processes with the torch.distributed.run environment (RANK,
+    LOCAL_RANK, WORLD_SIZE, LOCAL_WORLD_SIZE, MASTER_ADDR=127.0.0.1, a free MASTER_PORT).
+    Rank 0's stdout is relayed to this process's stdout, every other rank's to stderr.
+    When a rank fails, the others get `grace_s` seconds and are then terminated (a peer
+    may wait in a collective the failed rank never reaches).  Returns 0 if every rank
+    succeeded, else the worst status (a rank killed by signal k counts as 128 + k)."""
+    import signal
+    import socket
+    import subprocess
+    import threading
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GROUP_RANK="0", **(env_extra or {}))
+        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, start_new_session=True))
+    log(f"bench.py: started {n} rank processes (pids {[p.pid for p in procs]}, master 127.0.0.1:{port})")
+
+    def pump(r, p):
+        for line in p.stdout:
+            if r == 0:
+                sys.stdout.write(line)
+                sys.stdout.flush()
+            else:
+                log(f"[rank {r} stdout] {line.rstrip()}")
+
+    pumps = [threading.Thread(target=pump, args=(r, p), daemon=True) for r, p in enumerate(procs)]
+    for t in pumps:
+        t.start()
+    failed_at = None
+    while any(p.poll() is None for p in procs):
+        rcs = [p.poll() for p in procs]
+        if failed_at is None and any(rc not in (None, 0) for rc in rcs):
+            failed_at = time.monotonic()
+            log(f"bench.py: a rank failed (exit statuses {rcs}); the others get {grace_s:.0f} s to finish")
+        if failed_at is not None and time.monotonic() - failed_at > grace_s:
+            for sig, wait_s in ((signal.SIGTERM, 10.0), (signal.SIGKILL, 0.0)):
+                for p in procs:
+                    if p.poll() is None:
+                        os.killpg(p.pid, sig)
+                t_end = time.monotonic() + wait_s
+                while time.monotonic() < t_end and any(p.poll() is None for p in procs):
+                    time.sleep(0.1)
+            for p in procs:
+                p.wait()
+            break
+        time.sleep(0.1)
+    for t in pumps:
+        t.join(timeout=10)
+    status = [p.returncode if p.returncode >= 0 else 128 - p.returncode for p in procs]
+    if any(status):
+        log(f"bench.py: rank exit statuses {status}")
+    return max(status, default=0)
+
+
+def spawn_ranks(args, argv: list[str]) -> int:
+    """`--gpus N` without a launcher (no WORLD_SIZE in the environment): N fresh rank
+    processes of this script, one per GPU, started before this process touches a GPU --
+    the way the reference's join_init_run spawns its NTHREADS workers itself
+    (radix_join.cpp:1531-1540, driven by paper-4-scaling.py:190-199 -> native -n T).
+    With the RCCL backend every rank needs a GPU of its own: fewer visible GPUs is an
+    error (exit 2), never a line for fewer GPUs.  The gloo backend is the one-GPU
+    rehearsal of the multi-rank path (the ranks share the visible GPUs)."""
+    n = args.gpus
+    have = visible_gpus()
+    if args.dist_backend == "nccl" and have < n:
+        log(f"bench.py: --gpus {n} needs {n} visible GPUs (one RCCL rank per GPU), but {have} "
+            f"{'is' if have == 1 else 'are'} visible; not running (--dist-backend gloo rehearses the "
+            f"multi-rank path on fewer GPUs)")
+        return 2
+    return launch_ranks([sys.executable, os.path.abspath(__file__), *argv], n)
+
+
 def algorithmic_bytes(kernel: str, nR: int, nS: int, passes: int = 2, pass2_bits: int = 8, elem: int = 8) -> int:
     """Bytes a kernel must move per launch (DESIGN.md 'Kernels and their rooflines').
 
@@ -217,6 +302,10 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="time budget per CPU baseline leg")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        rc = spawn_ranks(args, sys.argv[1:])
+        sys.exit(rc if 0 <= rc < 256 else 1)
+
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -230,7 +319,9 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+        # never print a line whose n_gpus differs from the --gpus asked for
+        log(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}: refusing to measure")
+        sys.exit(2)
     if args.dist_backend == "gloo":  # rehearsal: ranks may share a device
         local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
@@ -337,6 +428,25 @@ def main():
             raise SystemExit(f"{workload}: wrong match count {[r.matches for r in results]} != {N_glob}")
         return results, per_kernel, elapsed
 
+    def gather_multi(res) -> dict | None:
+        """N > 1: every rank's exchange record (mi355_multi_stats of the C++ RCCL path, or
+        the torch.distributed path's equivalent) gathered to every rank (collective)."""
+        if world == 1:
+            return None
+        mine = dict(res.multi)
+        mine.update(rank=rank, recv_r=res.recv_r, recv_s=res.recv_s, local_matches=res.local_matches)
+        allm = [None] * world
+        dist.all_gather_object(allm, mine)
+        phases = ("ms_exchange_post", "ms_local", "ms_allreduce")
+        m0 = allm[0]
+        return {"world": m0.get("world"), "transport": m0.get("transport"), "pieces": m0.get("pieces"),
+                "elem_bytes": m0.get("elem_bytes"), "sent_bytes_total": sum(int(m.get("sent_bytes", 0)) for m in allm),
+                **{k + "_max": round(max(float(m.get(k, 0.0)) for m in allm), 4) for k in phases},
+                "per_rank": [{"rank": m["rank"], "recv_r": m["recv_r"], "recv_s": m["recv_s"],
+                              "sent_bytes": int(m.get("sent_bytes", 0)), "local_matches": m["local_matches"],
+                              **{k: round(float(m.get(k, 0.0)), 4) for k in phases}} for m in allm],
+                "mi355_multi_stats_rank0": {k: v for k, v in m0.items() if k not in ("per_rank",)}}
+
     def load_report(res, nS: int) -> dict:
         """Per-GPU received S tuples and per-partition S sizes (SURVEY.md 8(e) skew report)."""
         ls = res.local_stats
@@ -415,6 +525,7 @@ def main():
     }
     if args.workload == "c5":
         rho_info["load_report"] = load_report(results[-1], nS)
+    multi_info = gather_multi(results[-1])
 
     # the same join moving whole 8-byte tuples (the reference's data movement), measured
     # beside the headline: the probe phase's HBM fraction on the tuple layout
@@ -449,7 +560,10 @@ def main():
     # BASELINE configs 4 and 5 in the same run (strong totals over the N GPUs), each
     # with its load report; the headline value stays config 2
     configs_info = {}
-    if args.workload == "c2" and not args.no_configs:
+    if args.workload == "c2" and not args.no_configs and args.dist_backend == "gloo" and world > 1:
+        configs_info["skipped"] = ("configs 4 / 5 are not run in the gloo rehearsal (tuples staged through host "
+                                   "memory; not a scaling number)")
+    elif args.workload == "c2" and not args.no_configs:
         for wl in ("c4", "c5"):
             Rw, Sw, gRw, gSw, desc_w, gen_w = make_relations(wl)
             res_w, pk_w, el_w = measure_rho(wl, Rw, Sw, gRw, gSw)
@@ -471,6 +585,8 @@ def main():
                                       for k, v in res_w[-1].ms.items()},
                 "load_report": load_report(res_w[-1], nSw),
             }
+            if world > 1:
+                configs_info[wl]["multi"] = gather_multi(res_w[-1])
             del Rw, Sw
             torch.cuda.empty_cache()
         # config 2 on the reference's own relations (native.cpp:62-101: glibc rand() Knuth
@@ -543,9 +659,10 @@ def main():
         ev1.record()
         ev1.synchronize()
         best = min(best, ev0.elapsed_time(ev1))
-    roofline["measured_copy_ceiling"] = {"GB_per_s": round(2 * src.numel() * 8 / (best * 1e-3) / 1e9, 1),
-                                         "how": "torch copy_ of 2 GiB device to device, read + write bytes, "
-                                                "best of 5 (HIP events)"}
+    # scalars: the driver's parser keeps the roofline's scalar fields only
+    roofline["measured_copy_ceiling_GB_per_s"] = round(2 * src.numel() * 8 / (best * 1e-3) / 1e9, 1)
+    roofline["measured_copy_ceiling_how"] = ("torch copy_ of 2 GiB device to device, read + write bytes, best of 5 "
+                                             "(HIP events)")
     del src, dst
     torch.cuda.empty_cache()
 
@@ -633,14 +750,35 @@ def main():
         for _ in range(max(1, args.warmup)):
             assert sgxamd.rho_join(Rp, nRp, Sp, nSp, stream=stream).matches == nSp
         barrier()
+        # every call is synchronous (it returns the count): per-call wall times, their
+        # median (the reference reports the median of its runs) beside the mean, and
+        # the per-kernel event times and plan of the same calls
+        call_ms, kt_p = [], {}
         t1 = time.perf_counter()
         for _ in range(args.steps):
-            assert sgxamd.rho_join(Rp, nRp, Sp, nSp, stream=stream).matches == nSp
+            tc = time.perf_counter()
+            rp = sgxamd.rho_join(Rp, nRp, Sp, nSp, stream=stream)
+            call_ms.append((time.perf_counter() - tc) * 1e3)
+            assert rp.matches == nSp
+            for name, ms in sgxamd.timings():
+                kt_p.setdefault(name, []).append(ms)
         barrier()
         el = (time.perf_counter() - t1) / args.steps
-        rho_p = round((nRp + nSp) / el / 1e6, 1)
+        med = statistics.median(call_ms) * 1e-3
+        rho_p = round((nRp + nSp) / med / 1e6, 1)
+        stp = rp.stats
         paper_info = {"rho": {"shape": "|R|=13,107,200 |S|=52,428,800 (100/400 MiB), pk/fk, count only",
-                              "M_rec_per_s": rho_p, "ms": round(el * 1e3, 4),
+                              "M_rec_per_s": rho_p, "ms": round(med * 1e3, 4), "ms_median": round(med * 1e3, 4),
+                              "ms_mean": round(el * 1e3, 4), "ms_min": round(min(call_ms), 4),
+                              "ms_max": round(max(call_ms), 4), "calls": len(call_ms),
+                              "device_ms_total_median": round(statistics.median(
+                                  sum(v[i] for v in kt_p.values()) for i in range(len(call_ms))), 4)
+                              if kt_p and all(len(v) == len(call_ms) for v in kt_p.values()) else None,
+                              "plan": {k: stp.get(k) for k in ("radix_bits", "passes", "pass1_bits", "pass2_bits",
+                                                               "num_partitions", "num_tasks", "max_part_r",
+                                                               "max_part_s", "layout", "elem_bytes")},
+                              "kernel_ms_avg": {k: round(statistics.mean(v), 4) for k, v in sorted(kt_p.items())},
+                              "kernel_ms_max": {k: round(max(v), 4) for k, v in sorted(kt_p.items())},
                               "reference_M_rec_per_s": 1493.97,
                               "reference": "Xeon Gold 6326, 16 threads, native, UNROLL+FORCE_2_PHASES "
                                            "(scaling-perf.csv median)",
@@ -837,6 +975,8 @@ def main():
             "roofline": roofline, "cpu_baseline": cpu, "rho": rho_info, "scan": scan_info, "tpch": tpch_info,
             "reference_shapes": paper_info, "configs": configs_info,
         }
+        if multi_info is not None:
+            line["multi"] = multi_info
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

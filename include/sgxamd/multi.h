@@ -107,9 +107,22 @@ void mi355_multi_set_pieces(int pieces);
 int mi355_multi_release(void);
 
 /* Test hook: rank `rank` fails at `step` of every later multi-GPU join (1: exchange
- * buffer allocation, 2: a shard pass of S, 3: the local join) as an allocation or
- * kernel error would; step 0 clears it. */
+ * buffer allocation, 2: a shard pass of S, 3: the local join, 4: no device context,
+ * 5: the stream synchronisation after the local join, as an asynchronous kernel fault
+ * would) as an allocation or kernel error would; step 0 clears it. */
 void mi355_multi_inject_failure(int rank, int step);
+
+/* Test hook: the RCCL library later multi-GPU calls load instead of librccl.so.1 (NULL:
+ * back to librccl.so.1).  It must export the RCCL entry points the transport uses
+ * (ncclGetUniqueId, ncclCommInitRank/InitAll/Split/Destroy/Abort, ncclGroupStart/End,
+ * ncclSend/Recv, ncclAllGather/AllReduce, ncclGetErrorString).  A library named here is
+ * taken to be a test double that may hold several ranks on one GPU (tests/rccl_double:
+ * ranks are threads of one process, data moves by device copies): the single-process
+ * RCCL mode then runs every rank on the current GPU with a context of its own, so the
+ * RCCL transport itself runs at G > 1 on one MI355X.  Refused (MI355_ERR_INVALID) while
+ * communicators of mi355_multi_comm_init exist; the single-process communicators of the
+ * previous library are aborted. */
+int mi355_multi_set_rccl_library(const char *path);
 
 #ifdef __cplusplus
 } /* extern "C" */

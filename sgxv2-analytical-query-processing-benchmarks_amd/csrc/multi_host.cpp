@@ -53,6 +53,17 @@ double ms_since(Clock::time_point t) { return std::chrono::duration<double, std:
         }                                                                                  \
     } while (0)
 
+// A HIP call inside a transport: the transport is broken, not just this rank's compute
+// (the rank leaves the collective sequence; its peers are released by abort()).
+#define MH_HIPC(call)                                                                      \
+    do {                                                                                   \
+        hipError_t _e = (call);                                                            \
+        if (_e != hipSuccess) {                                                            \
+            set_last_error(std::string(#call) + ": " + hipGetErrorString(_e));             \
+            return MI355_ERR_COMM;                                                         \
+        }                                                                                  \
+    } while (0)
+
 #define MH_RC(call)                  \
     do {                             \
         const int _rc = (call);      \
@@ -62,6 +73,9 @@ double ms_since(Clock::time_point t) { return std::chrono::duration<double, std:
 // ---------------------------------------------------------------- RCCL, loaded on first use
 // libsgxamd.so keeps no link-time dependency on RCCL: the single-GPU library loads on
 // hosts without it, and a process that already holds librccl.so.1 (PyTorch's) shares it.
+// mi355_multi_set_rccl_library names another library with the same entry points (the
+// in-tree test double of tests/rccl_double, which moves data between ranks of one
+// process with device copies, so that RcclTransport runs at G > 1 on one GPU).
 struct Rccl {
     decltype(&ncclGetUniqueId) GetUniqueId = nullptr;
     decltype(&ncclCommInitRank) CommInitRank = nullptr;
@@ -77,38 +91,66 @@ struct Rccl {
     decltype(&ncclAllReduce) AllReduce = nullptr;
     decltype(&ncclGetErrorString) ErrorString = nullptr;
     std::string error;
+    std::string name;      // the library loaded
+    bool double_ = false;  // a test double (mi355_multi_set_rccl_library): ranks may share a GPU
+    // ncclCommAbort where the library has it, else ncclCommDestroy
+    void abort_comm(ncclComm_t c) const {
+        if (!c) return;
+        if (CommAbort) (void)CommAbort(c);
+        else if (CommDestroy) (void)CommDestroy(c);
+    }
 };
 
-const Rccl &rccl() {
-    static const Rccl lib = [] {
-        Rccl r;
-        void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
-        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
-        if (!h) {
-            const char *e = dlerror();
-            r.error = std::string("cannot load librccl.so.1: ") + (e ? e : "?");
-            return r;
-        }
-        auto sym = [&](auto &fn, const char *name) {
-            fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
-            if (!fn && r.error.empty()) r.error = std::string("librccl.so.1 lacks ") + name;
-        };
-        sym(r.GetUniqueId, "ncclGetUniqueId");
-        sym(r.CommInitRank, "ncclCommInitRank");
-        sym(r.CommInitAll, "ncclCommInitAll");
-        sym(r.CommDestroy, "ncclCommDestroy");
-        sym(r.CommAbort, "ncclCommAbort");
-        sym(r.CommSplit, "ncclCommSplit");
-        sym(r.GroupStart, "ncclGroupStart");
-        sym(r.GroupEnd, "ncclGroupEnd");
-        sym(r.Send, "ncclSend");
-        sym(r.Recv, "ncclRecv");
-        sym(r.AllGather, "ncclAllGather");
-        sym(r.AllReduce, "ncclAllReduce");
-        sym(r.ErrorString, "ncclGetErrorString");
+Rccl load_rccl(const std::string &path) {
+    Rccl r;
+    r.name = path.empty() ? "librccl.so.1" : path;
+    r.double_ = !path.empty();
+    void *h = dlopen(r.name.c_str(), RTLD_NOW | RTLD_LOCAL);
+    if (!h && path.empty()) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) {
+        const char *e = dlerror();
+        r.error = "cannot load " + r.name + ": " + (e ? e : "?");
         return r;
-    }();
-    return lib;
+    }
+    auto sym = [&](auto &fn, const char *name, bool required) {
+        fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
+        if (!fn && required && r.error.empty()) r.error = r.name + " lacks " + name;
+    };
+    sym(r.GetUniqueId, "ncclGetUniqueId", true);
+    sym(r.CommInitRank, "ncclCommInitRank", true);
+    sym(r.CommInitAll, "ncclCommInitAll", true);
+    sym(r.CommDestroy, "ncclCommDestroy", true);
+    // optional: ncclCommSplit is needed only by the one-process-per-GPU communicator
+    // (mi355_multi_comm_init checks it); without ncclCommAbort a broken communicator is
+    // destroyed instead
+    sym(r.CommAbort, "ncclCommAbort", false);
+    sym(r.CommSplit, "ncclCommSplit", false);
+    sym(r.GroupStart, "ncclGroupStart", true);
+    sym(r.GroupEnd, "ncclGroupEnd", true);
+    sym(r.Send, "ncclSend", true);
+    sym(r.Recv, "ncclRecv", true);
+    sym(r.AllGather, "ncclAllGather", true);
+    sym(r.AllReduce, "ncclAllReduce", true);
+    sym(r.ErrorString, "ncclGetErrorString", true);
+    return r;
+}
+
+// The current function table.  Tables are never freed (a library is never unloaded), so
+// a reference stays valid after mi355_multi_set_rccl_library switched libraries; the
+// switch is refused while communicators exist.
+std::mutex g_rccl_mu;
+std::string g_rccl_path;                    // "" = the system librccl.so.1
+const Rccl *g_rccl = nullptr;
+std::vector<std::unique_ptr<Rccl>> g_rccl_tables;
+std::atomic<int> g_live_handles{0};         // communicators of mi355_multi_comm_init alive
+
+const Rccl &rccl() {
+    std::lock_guard<std::mutex> lk(g_rccl_mu);
+    if (!g_rccl) {
+        g_rccl_tables.push_back(std::make_unique<Rccl>(load_rccl(g_rccl_path)));
+        g_rccl = g_rccl_tables.back().get();
+    }
+    return *g_rccl;
 }
 
 #define MH_NCCL(call)                                                                              \
@@ -152,6 +194,10 @@ class Barrier {
         aborted_ = true;
         cv_.notify_all();
     }
+    bool aborted() {
+        std::lock_guard<std::mutex> lk(m_);
+        return aborted_;
+    }
 
    private:
     std::mutex m_;
@@ -187,9 +233,12 @@ class Transport {
                               const uint64_t *send_counts, void *recv, const uint64_t *recv_counts, size_t elem) = 0;
     // collective: v[0..n) = element-wise sum / max over the ranks (n <= kMaxReduce)
     virtual int allreduce(int rank, hipStream_t s, uint64_t *v, int n, ReduceOp op) = 0;
-    // a rank's transport call failed (the transport itself is broken): release the
-    // host-side waiters; communicators are torn down by the owner afterwards
+    // a rank left the collective sequence (a transport call or a HIP call around one
+    // failed): release the host-side waiters; communicators are torn down by the owner
+    // afterwards
     virtual void abort() {}
+    // abort() was called: a collective that failed now failed because of another rank
+    virtual bool aborted() { return false; }
 };
 
 std::vector<uint64_t> prefix(const uint64_t *c, int n) {
@@ -208,35 +257,36 @@ class HostCollectives {
     int world() const { return world_; }
     bool wait() { return bar_.wait(); }
     void abort() { bar_.abort(); }
+    bool aborted() { return bar_.aborted(); }
 
     int exchange_counts(int rank, const uint64_t *send, bool fail, uint64_t *recv, bool *any_fail) {
         std::copy(send, send + world_, counts_[rank].begin());
         counts_[rank][world_] = fail ? 1 : 0;
-        if (!bar_.wait()) return aborted();
+        if (!bar_.wait()) return aborted_rc();
         bool f = false;
         for (int q = 0; q < world_; ++q) {
             recv[q] = counts_[q][rank];
             f = f || counts_[q][world_];
         }
         *any_fail = f;
-        if (!bar_.wait()) return aborted();  // the table is reused by the next piece
+        if (!bar_.wait()) return aborted_rc();  // the table is reused by the next piece
         return MI355_OK;
     }
 
     int allreduce(int rank, uint64_t *v, int n, ReduceOp op) {
         std::copy(v, v + n, red_[rank].begin());
-        if (!bar_.wait()) return aborted();
+        if (!bar_.wait()) return aborted_rc();
         for (int j = 0; j < n; ++j) {
             uint64_t r = op == kSum ? 0 : red_[0][j];
             for (int q = 0; q < world_; ++q) r = op == kSum ? r + red_[q][j] : std::max(r, red_[q][j]);
             v[j] = r;
         }
-        if (!bar_.wait()) return aborted();
+        if (!bar_.wait()) return aborted_rc();
         return MI355_OK;
     }
 
    private:
-    int aborted() {
+    int aborted_rc() {
         set_last_error("another rank's transport failed");
         return MI355_ERR_COMM;
     }
@@ -277,10 +327,10 @@ class RcclTransport final : public Transport {
         MH_RC(scratch(i, &d, &h));
         std::memcpy(h, send, sizeof(uint64_t) * world_);
         h[world_] = fail ? 1 : 0;
-        MH_HIP(hipMemcpyAsync(d, h, sizeof(uint64_t) * w1, hipMemcpyHostToDevice, s));
+        MH_HIPC(hipMemcpyAsync(d, h, sizeof(uint64_t) * w1, hipMemcpyHostToDevice, s));
         MH_NCCL(rccl().AllGather(d, d + w1, w1, ncclUint64, ccomms_[i], s));
-        MH_HIP(hipMemcpyAsync(h + w1, d + w1, sizeof(uint64_t) * w1 * world_, hipMemcpyDeviceToHost, s));
-        MH_HIP(hipStreamSynchronize(s));
+        MH_HIPC(hipMemcpyAsync(h + w1, d + w1, sizeof(uint64_t) * w1 * world_, hipMemcpyDeviceToHost, s));
+        MH_HIPC(hipStreamSynchronize(s));
         bool f = false;
         for (int q = 0; q < world_; ++q) {
             recv[q] = h[w1 + q * w1 + rank];
@@ -297,17 +347,33 @@ class RcclTransport final : public Transport {
         const char *send = static_cast<const char *>(send_v);
         char *recv = static_cast<char *>(recv_v);
         const ncclDataType_t type = elem == 8 ? ncclUint64 : ncclUint32;
-        MH_HIP(hipStreamWaitEvent(c, ready, 0));
+        MH_HIPC(hipStreamWaitEvent(c, ready, 0));
         if (send_counts[rank])  // this rank's own run: a local copy
-            MH_HIP(hipMemcpyAsync(recv + ro[rank] * elem, send + so[rank] * elem, send_counts[rank] * elem,
+            MH_HIPC(hipMemcpyAsync(recv + ro[rank] * elem, send + so[rank] * elem, send_counts[rank] * elem,
                                   hipMemcpyDeviceToDevice, c));
-        MH_NCCL(rccl().GroupStart());
-        for (int p = 0; p < world_; ++p) {
+        const Rccl &L = rccl();
+        MH_NCCL(L.GroupStart());
+        ncclResult_t r = ncclSuccess;
+        const char *what = "";
+        for (int p = 0; p < world_ && r == ncclSuccess; ++p) {
             if (p == rank) continue;
-            if (send_counts[p]) MH_NCCL(rccl().Send(send + so[p] * elem, send_counts[p], type, p, comms_[i], c));
-            if (recv_counts[p]) MH_NCCL(rccl().Recv(recv + ro[p] * elem, recv_counts[p], type, p, comms_[i], c));
+            if (send_counts[p] && (r = L.Send(send + so[p] * elem, send_counts[p], type, p, comms_[i], c)) != ncclSuccess)
+                what = "ncclSend";
+            else if (recv_counts[p] &&
+                     (r = L.Recv(recv + ro[p] * elem, recv_counts[p], type, p, comms_[i], c)) != ncclSuccess)
+                what = "ncclRecv";
         }
-        MH_NCCL(rccl().GroupEnd());
+        // the group is closed even after a failed call (the thread's group state stays
+        // balanced); the communicators are aborted by the caller then
+        const ncclResult_t re = L.GroupEnd();
+        if (r == ncclSuccess && re != ncclSuccess) {
+            r = re;
+            what = "ncclGroupEnd";
+        }
+        if (r != ncclSuccess) {
+            set_last_error(std::string(what) + " (piece exchange): " + L.ErrorString(r));
+            return MI355_ERR_COMM;
+        }
         return MI355_OK;
     }
 
@@ -317,29 +383,32 @@ class RcclTransport final : public Transport {
         uint64_t *d = nullptr, *h = nullptr;
         MH_RC(scratch(i, &d, &h));
         std::memcpy(h, v, sizeof(uint64_t) * n);
-        MH_HIP(hipMemcpyAsync(d, h, sizeof(uint64_t) * n, hipMemcpyHostToDevice, s));
+        MH_HIPC(hipMemcpyAsync(d, h, sizeof(uint64_t) * n, hipMemcpyHostToDevice, s));
         MH_NCCL(rccl().AllReduce(d, d, n, ncclUint64, op == kSum ? ncclSum : ncclMax, ccomms_[i], s));
-        MH_HIP(hipMemcpyAsync(h, d, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, s));
-        MH_HIP(hipStreamSynchronize(s));
+        MH_HIPC(hipMemcpyAsync(h, d, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, s));
+        MH_HIPC(hipStreamSynchronize(s));
         std::memcpy(v, h, sizeof(uint64_t) * n);
         return MI355_OK;
     }
 
     void abort() override {
+        aborted_ = true;
         if (host_) host_->abort();
     }
+    bool aborted() override { return aborted_ || (host_ && host_->aborted()); }
 
    private:
     // per local rank: device [(G+1) + G(G+1)] u64 and its pinned host mirror
     int scratch(int i, uint64_t **d, uint64_t **h) {
         const size_t bytes = sizeof(uint64_t) * std::max<size_t>((world_ + 1) * (size_t)(world_ + 1), kMaxReduce);
-        MH_HIP(buf_[i].ensure(bytes));
-        if (!pinned_[i]) MH_HIP(hipHostMalloc(reinterpret_cast<void **>(&pinned_[i]), bytes));
+        MH_HIPC(buf_[i].ensure(bytes));
+        if (!pinned_[i]) MH_HIPC(hipHostMalloc(reinterpret_cast<void **>(&pinned_[i]), bytes));
         *d = buf_[i].as<uint64_t>();
         *h = pinned_[i];
         return MI355_OK;
     }
     int world_, first_;
+    std::atomic<bool> aborted_{false};
     std::vector<ncclComm_t> comms_, ccomms_;
     std::shared_ptr<HostCollectives> host_;
     std::vector<DeviceBuffer> buf_;
@@ -366,7 +435,7 @@ class RehearsalTransport final : public Transport {
         const int G = host_.world();
         char *recv = static_cast<char *>(recv_v);
         posts_[rank] = Post{static_cast<const char *>(send), prefix(send_counts, G), ready};
-        if (!host_.wait()) return aborted();
+        if (!host_.wait()) return aborted_rc();
         uint64_t off = 0;
         int rc = MI355_OK;
         for (int q = 0; q < G && rc == MI355_OK; ++q) {
@@ -376,11 +445,11 @@ class RehearsalTransport final : public Transport {
                 hipMemcpyAsync(recv + off * elem, p.send + p.off[rank] * elem, recv_counts[q] * elem,
                                hipMemcpyDeviceToDevice, c) != hipSuccess) {
                 set_last_error("rehearsal exchange copy failed");
-                rc = MI355_ERR_HIP;
+                rc = MI355_ERR_COMM;
             }
             off += recv_counts[q];
         }
-        if (!host_.wait()) return aborted();  // the posts table is reused by the next piece
+        if (!host_.wait()) return aborted_rc();  // the posts table is reused by the next piece
         return rc;
     }
 
@@ -389,9 +458,10 @@ class RehearsalTransport final : public Transport {
     }
 
     void abort() override { host_.abort(); }
+    bool aborted() override { return host_.aborted(); }
 
    private:
-    int aborted() {
+    int aborted_rc() {
         set_last_error("another rank's transport failed");
         return MI355_ERR_COMM;
     }
@@ -432,6 +502,8 @@ struct RankOut {
     uint64_t global = 0, local = 0, recv_r = 0, recv_s = 0, sent = 0;
     bool keys = false;       // the exchange moved keys only
     bool peer_fail = false;  // the call failed because another rank did
+    bool together = false;   // the call failed at a collective every rank left at (the
+                             // sequence is intact; nothing to abort)
     double ms_post = 0, ms_local = 0, ms_allreduce = 0, ms_total = 0;
     mi355_rho_stats st{};
 };
@@ -445,7 +517,7 @@ uint32_t log2_exact(int g) {
 // Test hook (mi355_multi_inject_failure): rank `g_fail_rank` fails at step
 // `g_fail_step` of its next multi-GPU join, as an allocation or kernel error would.
 std::atomic<int> g_fail_rank{-1}, g_fail_step{0};
-enum FailStep { kFailBuffers = 1, kFailPiece = 2, kFailLocal = 3 };
+enum FailStep { kFailBuffers = 1, kFailPiece = 2, kFailLocal = 3, kFailContext = 4, kFailLocalSync = 5 };
 bool injected(int rank, int step) {
     if (g_fail_rank.load() != rank || g_fail_step.load() != step) return false;
     set_last_error("injected failure (mi355_multi_inject_failure)");
@@ -499,7 +571,22 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
             fail_msg = last_error();
         }
     };
+    // a HIP call of this rank's own compute or ordering: a failure is flagged at the next
+    // collective like any other local failure (the rank stays in the sequence)
+    auto hip_ok = [&](hipError_t e, const char *what) {
+        if (e == hipSuccess) return true;
+        set_last_error(std::string(what) + ": " + hipGetErrorString(e));
+        fail(e == hipErrorOutOfMemory ? MI355_ERR_OOM : MI355_ERR_HIP);
+        return false;
+    };
+    // a transport call failed: when the transport was aborted by another rank that left
+    // the sequence, this rank failed because of it
+    auto transport_rc = [&](int rc) {
+        if (rc != MI355_OK && T.aborted()) o.peer_fail = true;
+        return rc;
+    };
     auto peer_failed = [&]() {
+        o.together = true;
         if (fail_rc != MI355_OK) {
             set_last_error(fail_msg);
             return fail_rc;
@@ -512,15 +599,15 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
     // global sizes: the mean local sizes plan the local join, the largest slices size
     // the receive buffers for the worst case (every rank's piece i comes to this rank)
     uint64_t sum[2] = {nR, nS}, mx[2] = {nR, nS};
-    MH_RC(T.allreduce(rank, s, sum, 2, kSum));
-    MH_RC(T.allreduce(rank, s, mx, 2, kMax));
+    MH_RC(transport_rc(T.allreduce(rank, s, sum, 2, kSum)));
+    MH_RC(transport_rc(T.allreduce(rank, s, mx, 2, kMax)));
     const uint64_t cR = (uint64_t)G * K * ((mx[0] + K - 1) / K), cS = (uint64_t)G * K * ((mx[1] + K - 1) / K);
     // the element format must be the same on every rank (the SGXAMD_KEYS switch and the
     // calling thread's key layout are per process / per thread): keys only when every
     // rank's plan, from the same global sizes, takes the pooled keys layout
     mi355_rho_opts kl = lo;
     uint64_t notkeys = rho::keys_exchange_plan(sum[0] / G, sum[1] / G, cR, cS, &kl) ? 0 : 1;
-    MH_RC(T.allreduce(rank, s, &notkeys, 1, kMax));
+    MH_RC(transport_rc(T.allreduce(rank, s, &notkeys, 1, kMax)));
     o.keys = notkeys == 0;
     if (o.keys) lo = kl;  // the local policy fixed from the global sizes
     const size_t elem = o.keys ? sizeof(uint32_t) : sizeof(row_t);
@@ -543,8 +630,10 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
     for (int rel = 0; rel < 2 && !any_fail; ++rel) {
         const row_t *in = rel ? S : R;
         const uint64_t n = rel ? nS : nR;
-        char *snd = (rel ? ctx->xsendS : ctx->xsendR).as<char>();
-        char *rcv = (rel ? ctx->xrecvS : ctx->xrecvR).as<char>();
+        // without a context (pre_fail) the rank only takes part in the count exchange,
+        // flagged as failed, and posts nothing
+        char *snd = ctx ? (rel ? ctx->xsendS : ctx->xsendR).as<char>() : nullptr;
+        char *rcv = ctx ? (rel ? ctx->xrecvS : ctx->xrecvR).as<char>() : nullptr;
         const uint64_t per = (n + K - 1) / K;
         for (int i = 0; i < K; ++i) {
             const uint64_t a = std::min(n, i * per), b = std::min(n, (i + 1) * per);
@@ -555,21 +644,23 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
                 if (rel == 1 && i == K / 2 && injected(rank, kFailPiece)) fail(MI355_ERR_HIP);
             }
             if (fail_rc != MI355_OK) std::fill(sc.begin(), sc.end(), 0);
-            MH_RC(T.exchange_counts(rank, s, sc.data(), fail_rc != MI355_OK, rc.data(), &any_fail));
+            MH_RC(transport_rc(T.exchange_counts(rank, s, sc.data(), fail_rc != MI355_OK, rc.data(), &any_fail)));
             if (any_fail) break;  // every rank sees the same flags: none posts this piece
+            // the counts went out unflagged, so the piece is posted whatever happens now;
+            // a failure here is flagged at the next collective
             hipEvent_t ready = rs->ev[rel * K + i];
-            MH_HIP(hipEventRecord(ready, s));
-            MH_RC(T.post_exchange(rank, rs->comm, ready, snd + a * elem, sc.data(), rcv + total[rel] * elem,
-                                  rc.data(), elem));
+            hip_ok(hipEventRecord(ready, s), "hipEventRecord (piece ready)");
+            MH_RC(transport_rc(T.post_exchange(rank, rs->comm, ready, snd + a * elem, sc.data(),
+                                               rcv + total[rel] * elem, rc.data(), elem)));
             for (int q = 0; q < G; ++q) {
                 total[rel] += rc[q];
                 if (q != rank) o.sent += sc[q] * elem;
             }
         }
-        if (!any_fail) MH_HIP(hipEventRecord(rs->ev[2 * K + rel], rs->comm));
+        if (!any_fail) hip_ok(hipEventRecord(rs->ev[2 * K + rel], rs->comm), "hipEventRecord (relation landed)");
     }
     if (any_fail) {  // the pieces posted so far were posted by every rank: let them land
-        if (rs) MH_HIP(hipStreamSynchronize(rs->comm));
+        if (rs) (void)hipStreamSynchronize(rs->comm);
         return peer_failed();
     }
     o.recv_r = total[0];
@@ -577,25 +668,31 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
     const auto t1 = Clock::now();
     o.ms_post = std::chrono::duration<double, std::milli>(t1 - t0).count();
 
-    // local join: R's passes once R has landed, S's passes and build/probe once S has
-    MH_HIP(hipStreamWaitEvent(s, rs->ev[2 * K], 0));
-    if (total[0] && total[1]) {
-        int lrc = injected(rank, kFailLocal) ? MI355_ERR_OOM
-                                             : rho::join_pipelined_begin(ctx, s, ctx->xrecvR.ptr, total[0], total[1],
-                                                                         &lo, (uint32_t)elem);
-        MH_HIP(hipStreamWaitEvent(s, rs->ev[2 * K + 1], 0));
-        if (lrc == MI355_OK) lrc = rho::join_pipelined_finish(ctx, ctx->xrecvS.ptr, total[1], &o.st);
-        fail(lrc);
-        o.local = lrc == MI355_OK ? o.st.matches : 0;
-    } else {
-        MH_HIP(hipStreamWaitEvent(s, rs->ev[2 * K + 1], 0));
+    // local join: R's passes once R has landed, S's passes and build/probe once S has.
+    // Every failure from here on is this rank's own and is flagged in the final all-reduce.
+    if (fail_rc == MI355_OK) {
+        const bool waited = hip_ok(hipStreamWaitEvent(s, rs->ev[2 * K], 0), "hipStreamWaitEvent (R landed)");
+        if (waited && total[0] && total[1]) {
+            int lrc = injected(rank, kFailLocal) ? MI355_ERR_OOM
+                                                 : rho::join_pipelined_begin(ctx, s, ctx->xrecvR.ptr, total[0],
+                                                                             total[1], &lo, (uint32_t)elem);
+            if (lrc == MI355_OK && hip_ok(hipStreamWaitEvent(s, rs->ev[2 * K + 1], 0), "hipStreamWaitEvent (S landed)"))
+                lrc = rho::join_pipelined_finish(ctx, ctx->xrecvS.ptr, total[1], &o.st);
+            fail(lrc);
+            o.local = lrc == MI355_OK ? o.st.matches : 0;
+        } else if (waited) {
+            hip_ok(hipStreamWaitEvent(s, rs->ev[2 * K + 1], 0), "hipStreamWaitEvent (S landed)");
+        }
     }
-    MH_HIP(hipStreamSynchronize(s));
-    MH_HIP(hipStreamSynchronize(rs->comm));
+    // an asynchronous error of the local join's kernels surfaces here
+    hipError_t se = hipStreamSynchronize(s);
+    if (injected(rank, kFailLocalSync)) se = hipErrorLaunchFailure;
+    hip_ok(se, "hipStreamSynchronize (local join)");
+    hip_ok(hipStreamSynchronize(rs->comm), "hipStreamSynchronize (exchange)");
     const auto t2 = Clock::now();
     o.ms_local = std::chrono::duration<double, std::milli>(t2 - t1).count();
-    uint64_t m[2] = {o.local, fail_rc != MI355_OK ? 1u : 0u};
-    MH_RC(T.allreduce(rank, s, m, 2, kSum));
+    uint64_t m[2] = {fail_rc == MI355_OK ? o.local : 0, fail_rc != MI355_OK ? 1u : 0u};
+    MH_RC(transport_rc(T.allreduce(rank, s, m, 2, kSum)));
     if (m[1]) return peer_failed();
     o.global = m[0];
     o.ms_allreduce = ms_since(t2);
@@ -630,14 +727,15 @@ Context *rehearsal_context(int device, int rank, int *status) {
 std::mutex g_all_mu;
 std::unordered_map<int, std::vector<ncclComm_t>> g_all;
 
-int comms_all(int G, std::vector<ncclComm_t> *out) {
+// same_dev >= 0: every rank on that device (an RCCL test double only).
+int comms_all(int G, int same_dev, std::vector<ncclComm_t> *out) {
     MH_RC(require_rccl());
     std::lock_guard<std::mutex> lk(g_all_mu);
     auto it = g_all.find(G);
     if (it == g_all.end()) {
         std::vector<ncclComm_t> comms(G);
         std::vector<int> devs(G);
-        for (int g = 0; g < G; ++g) devs[g] = g;
+        for (int g = 0; g < G; ++g) devs[g] = same_dev >= 0 ? same_dev : g;
         MH_NCCL(rccl().CommInitAll(comms.data(), G, devs.data()));
         it = g_all.emplace(G, std::move(comms)).first;
     }
@@ -652,8 +750,7 @@ void drop_comms_all(int G) {
     std::lock_guard<std::mutex> lk(g_all_mu);
     auto it = g_all.find(G);
     if (it == g_all.end()) return;
-    for (ncclComm_t c : it->second)
-        if (c && rccl().CommAbort) (void)rccl().CommAbort(c);
+    for (ncclComm_t c : it->second) rccl().abort_comm(c);
     g_all.erase(it);
 }
 
@@ -706,14 +803,17 @@ int join_multi(const row_t *R, uint64_t nR, const row_t *S, uint64_t nS, int G, 
     int cur = 0;
     MH_HIP(hipGetDevice(&cur));
     const int kind = resolve_transport(transport, G);
-    if (kind == MI355_TRANSPORT_RCCL && ndev < G) {
+    // a test double of RCCL (mi355_multi_set_rccl_library) runs every rank on the
+    // current GPU, each with a context of its own, like the rehearsal
+    const bool one_gpu = kind == MI355_TRANSPORT_RCCL && rccl().double_;
+    if (kind == MI355_TRANSPORT_RCCL && ndev < G && !one_gpu) {
         set_last_error("RCCL transport needs " + std::to_string(G) + " visible GPUs");
         return MI355_ERR_INVALID;
     }
     std::unique_ptr<Transport> T;
     if (kind == MI355_TRANSPORT_RCCL) {
         std::vector<ncclComm_t> comms;
-        MH_RC(comms_all(G, &comms));
+        MH_RC(comms_all(G, one_gpu ? cur : -1, &comms));
         T = std::make_unique<RcclTransport>(G, 0, comms, std::vector<ncclComm_t>{},
                                             std::make_shared<HostCollectives>(G));
     } else {
@@ -728,14 +828,17 @@ int join_multi(const row_t *R, uint64_t nR, const row_t *S, uint64_t nS, int G, 
     auto body = [&](int g) -> int {
         mi355_set_key_layout(keys ? 1 : 0);
         mi355_timing_enable(timing ? 1 : 0);
-        const int dev = kind == MI355_TRANSPORT_RCCL ? g : cur;
+        const int dev = kind == MI355_TRANSPORT_RCCL && !one_gpu ? g : cur;
         int status = MI355_OK;
         Context *ctx = nullptr;
         if (hipSetDevice(dev) != hipSuccess) {
             set_last_error("hipSetDevice(" + std::to_string(dev) + ") failed");
             status = MI355_ERR_HIP;
+        } else if (injected(g, kFailContext)) {
+            status = MI355_ERR_HIP;
         } else {
-            ctx = kind == MI355_TRANSPORT_RCCL ? current_context(&status) : rehearsal_context(dev, g, &status);
+            ctx = kind == MI355_TRANSPORT_RCCL && !one_gpu ? current_context(&status)
+                                                           : rehearsal_context(dev, g, &status);
         }
         // this rank's slices (radix_join.cpp:1488-1499: floor(n/T) each, the last the rest)
         const uint64_t pr = nR / G, ps = nS / G;
@@ -773,15 +876,16 @@ int join_multi(const row_t *R, uint64_t nR, const row_t *S, uint64_t nS, int G, 
             rcs[g] = body(g);
             if (rcs[g] != MI355_OK) {
                 errs[g] = last_error();
-                // a failed transport call leaves the sequence of collectives: release the
-                // other ranks' host waits (flagged failures keep it and need nothing)
-                if (rcs[g] == MI355_ERR_COMM && !outs[g].peer_fail) T->abort();
+                // a rank that left the sequence of collectives alone (a transport call
+                // failed) releases the other ranks' host waits; flagged failures end
+                // every rank at the same collective and need nothing
+                if (!outs[g].together) T->abort();
             }
         });
     for (auto &t : th) t.join();
     (void)hipSetDevice(cur);
     bool comm_broken = false;
-    for (int g = 0; g < G; ++g) comm_broken = comm_broken || (rcs[g] == MI355_ERR_COMM && !outs[g].peer_fail);
+    for (int g = 0; g < G; ++g) comm_broken = comm_broken || (rcs[g] != MI355_OK && !outs[g].together);
     if (comm_broken && kind == MI355_TRANSPORT_RCCL) {
         T.reset();
         drop_comms_all(G);
@@ -803,21 +907,50 @@ thread_local mi355_multi_stats t_last_multi{};
 // ---------------------------------------------------------------- one process per GPU
 // comm carries the tuples, ccomm (ncclCommSplit of comm, same ranks) the counts, flags
 // and reductions.  broken: a transport call failed; both were aborted.
+// ctx: the device's shared context, or -- when another rank of this process already
+// holds a communicator on the same device (only an RCCL test double allows that) -- a
+// context of its own, so that the ranks' joins do not serialise on one context's lock.
 struct CommHandle {
     int world = 0, rank = 0, device = 0;
     ncclComm_t comm = nullptr, ccomm = nullptr;
     bool broken = false;
     std::unique_ptr<RcclTransport> T;
+    Context *ctx = nullptr;
+    std::unique_ptr<Context> own;
     void abort_comms() {
         T.reset();
-        for (ncclComm_t *c : {&comm, &ccomm})
-            if (*c && rccl().CommAbort) {
-                (void)rccl().CommAbort(*c);
-                *c = nullptr;
-            }
+        for (ncclComm_t *c : {&comm, &ccomm}) {
+            rccl().abort_comm(*c);
+            *c = nullptr;
+        }
         broken = true;
     }
 };
+
+std::mutex g_dev_handles_mu;
+std::unordered_map<int, int> g_dev_handles;  // live communicators per device
+
+// Frees a context of its own (its stream, pinned block and workspace) once idle.
+void destroy_own_context(std::unique_ptr<Context> &c) {
+    if (!c) return;
+    {
+        std::lock_guard<std::mutex> lk(c->mu);
+        (void)hipStreamSynchronize(c->stream);
+        release_workspace(c.get());
+    }
+    {
+        std::lock_guard<std::mutex> lk(g_streams_mu);
+        auto it = g_streams.find(c.get());
+        if (it != g_streams.end()) {
+            if (it->second.comm) (void)hipStreamSynchronize(it->second.comm), (void)hipStreamDestroy(it->second.comm);
+            for (hipEvent_t e : it->second.ev) (void)hipEventDestroy(e);
+            g_streams.erase(it);
+        }
+    }
+    (void)hipStreamDestroy(c->stream);
+    if (c->host_result) (void)hipHostFree(c->host_result);
+    c.reset();
+}
 
 }  // namespace multi
 }  // namespace sgxamd
@@ -916,21 +1049,41 @@ int mi355_multi_comm_init(const void *id128, int nranks, int rank, void **comm) 
         return MI355_ERR_INVALID;
     }
     MH_RC(multi::require_rccl());
+    const multi::Rccl &lib = multi::rccl();
+    if (!lib.CommSplit) {
+        set_last_error(lib.name + " lacks ncclCommSplit (the count communicator of mi355_multi_comm_init)");
+        return MI355_ERR_COMM;
+    }
     auto h = std::make_unique<multi::CommHandle>();
     h->world = nranks;
     h->rank = rank;
     MH_HIP(hipGetDevice(&h->device));
     ncclUniqueId id;
     std::memcpy(&id, id128, sizeof(id));
-    MH_NCCL(multi::rccl().CommInitRank(&h->comm, nranks, id, rank));
-    const ncclResult_t sr = multi::rccl().CommSplit(h->comm, 0, rank, &h->ccomm, nullptr);
+    MH_NCCL(lib.CommInitRank(&h->comm, nranks, id, rank));
+    const ncclResult_t sr = lib.CommSplit(h->comm, 0, rank, &h->ccomm, nullptr);
     if (sr != ncclSuccess) {
-        set_last_error(std::string("ncclCommSplit (count communicator): ") + multi::rccl().ErrorString(sr));
+        set_last_error(std::string("ncclCommSplit (count communicator): ") + lib.ErrorString(sr));
         h->abort_comms();
         return MI355_ERR_COMM;
     }
     h->T = std::make_unique<multi::RcclTransport>(nranks, rank, std::vector<ncclComm_t>{h->comm},
                                                   std::vector<ncclComm_t>{h->ccomm}, nullptr);
+    bool shared_dev;
+    {
+        std::lock_guard<std::mutex> lk(multi::g_dev_handles_mu);
+        shared_dev = multi::g_dev_handles[h->device]++ > 0;
+    }
+    int status = MI355_OK;
+    if (shared_dev) {
+        h->own = make_context(h->device, &status);
+        h->ctx = h->own.get();
+    } else {
+        h->ctx = current_context(&status);
+    }
+    // without a context the rank still takes part in the joins' collectives, flagged as
+    // failed (mi355_rho_join_sharded), so the communicator is kept
+    ++multi::g_live_handles;
     *comm = h.release();
     return MI355_OK;
 }
@@ -941,7 +1094,35 @@ int mi355_multi_comm_destroy(void *comm) {
     h->T.reset();
     for (ncclComm_t c : {h->ccomm, h->comm})
         if (c && multi::rccl().CommDestroy) (void)multi::rccl().CommDestroy(c);
+    multi::destroy_own_context(h->own);
+    {
+        std::lock_guard<std::mutex> lk(multi::g_dev_handles_mu);
+        --multi::g_dev_handles[h->device];
+    }
+    --multi::g_live_handles;
     delete h;
+    return MI355_OK;
+}
+
+int mi355_multi_set_rccl_library(const char *path) {
+    std::string p = path ? path : "";
+    {
+        std::lock_guard<std::mutex> lk(multi::g_all_mu);
+        if (multi::g_live_handles.load() > 0) {
+            set_last_error("mi355_multi_set_rccl_library: communicators of mi355_multi_comm_init are alive");
+            return MI355_ERR_INVALID;
+        }
+    }
+    // the single-process communicators of the old library go first
+    std::vector<int> sizes;
+    {
+        std::lock_guard<std::mutex> lk(multi::g_all_mu);
+        for (auto &kv : multi::g_all) sizes.push_back(kv.first);
+    }
+    for (int G : sizes) multi::drop_comms_all(G);
+    std::lock_guard<std::mutex> lk(multi::g_rccl_mu);
+    multi::g_rccl_path = p;
+    multi::g_rccl = nullptr;  // loaded on next use
     return MI355_OK;
 }
 
@@ -966,10 +1147,15 @@ int mi355_rho_join_sharded(void *comm, const row_t *R, uint64_t nR, const row_t 
     }
     MH_HIP(hipSetDevice(h->device));
     int status = MI355_OK;
-    Context *ctx = current_context(&status);
+    Context *ctx = h->ctx ? h->ctx : current_context(&status);
+    if (ctx && multi::injected(h->rank, multi::kFailContext)) {
+        ctx = nullptr;
+        status = MI355_ERR_HIP;
+    }
     std::vector<multi::RankOut> outs(1);
     int rc;
     if (!ctx) {  // take part in the collectives, flagged as failed
+        if (status == MI355_OK) status = MI355_ERR_HIP;
         rc = multi::rank_join(*h->T, h->rank, nullptr, nullptr, nullptr, 0, nullptr, 0, opts, outs[0], status);
     } else {
         std::lock_guard<std::mutex> lk(ctx->mu);
@@ -978,9 +1164,10 @@ int mi355_rho_join_sharded(void *comm, const row_t *R, uint64_t nR, const row_t 
         rc = multi::rank_join(*h->T, h->rank, ctx, s, R, nR, S, nS, opts, outs[0]);
     }
     if (rc != MI355_OK) {
-        // a failed RCCL call leaves unmatched operations behind: abort this rank's
+        // a rank that left the sequence of collectives (a failed RCCL call, or a HIP call
+        // inside the transport) leaves unmatched operations behind: abort this rank's
         // communicators (the peers' calls fail or are torn down with the job)
-        if (rc == MI355_ERR_COMM && !outs[0].peer_fail) {
+        if (!outs[0].together) {
             const std::string e = last_error();
             h->abort_comms();
             set_last_error(e);

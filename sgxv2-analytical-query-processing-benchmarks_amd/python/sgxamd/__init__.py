@@ -227,6 +227,7 @@ SIGNATURES = {
     "mi355_last_multi_stats": (C.c_int, [C.POINTER(multi_stats)]),
     "mi355_multi_set_pieces": (None, [C.c_int]),
     "mi355_multi_inject_failure": (None, [C.c_int, C.c_int]),
+    "mi355_multi_set_rccl_library": (C.c_int, [C.c_char_p]),
     "mi355_multi_release": (C.c_int, []),
     "mi355_release_workspace": (C.c_int, []),
     # scan.h
@@ -467,9 +468,16 @@ def multi_release() -> None:
 
 
 def multi_inject_failure(rank: int, step: int) -> None:
-    """Test hook: `rank` fails at `step` (1 buffers, 2 a shard pass, 3 the local join) of
-    every later multi-GPU join; step 0 clears it."""
+    """Test hook: `rank` fails at `step` (1 buffers, 2 a shard pass, 3 the local join, 4 no
+    device context, 5 the local join's stream synchronisation) of every later
+    multi-GPU join; step 0 clears it."""
     lib.mi355_multi_inject_failure(rank, step)
+
+
+def multi_set_rccl_library(path: str | None) -> None:
+    """Test hook (mi355_multi_set_rccl_library): load `path` instead of librccl.so.1 for
+    later multi-GPU calls (None: librccl.so.1 again)."""
+    _check(lib.mi355_multi_set_rccl_library(path.encode() if path else None))
 
 
 def rho_join_tables(R, nR: int, S, nS: int, nthreads: int = 1, materialize: bool = False,

@@ -57,6 +57,8 @@ import torch.distributed as dist
 from . import (Mi355Error, multi_comm_init, multi_unique_id, rho_join, rho_join_begin, rho_join_finish,
                rho_join_sharded, shard_partition)
 
+MI355_ERR_COMM = -6  # sgxamd/multi.h
+
 
 def _log2_exact(g: int) -> int:
     b = g.bit_length() - 1
@@ -73,6 +75,9 @@ class ShardedJoinResult:
     recv_s: int
     ms: dict = field(default_factory=dict)
     local_stats: dict = field(default_factory=dict)
+    # this rank's exchange record: world, transport, sent_bytes, elem_bytes and the
+    # ms_exchange_post / ms_local / ms_allreduce phases (mi355_multi_stats in C++)
+    multi: dict = field(default_factory=dict)
 
 
 class _Done:
@@ -187,6 +192,8 @@ class _Exchange:
         cap = world * chunks * -(-int(nmax.item()) // chunks)
         self.out = torch.empty(max(cap, 1), dtype=torch.int64, device=t.device)
         self.world = world
+        self.rank = dist.get_rank(group)
+        self.sent = 0  # elements sent to other ranks
         self.total = 0
         self.works = []
         self.keep = []  # send buffers stay alive until their exchange completed
@@ -200,6 +207,7 @@ class _Exchange:
         else:
             p, c = self.t[:0], [0] * self.world
         rc = _exchange_counts(c, self.cgroup)
+        self.sent += sum(c) - c[self.rank]
         got = sum(rc)
         dst = self.out[self.total:self.total + got]
         self.total += got
@@ -254,14 +262,15 @@ def _cxx_comm(group) -> int:
         dist.broadcast_object_list(obj, src=src, group=group)
         status, payload = obj[0]
         if status != "ok":
-            raise Mi355Error(f"sgxamd.dist: rank 0 could not create the RCCL unique id: {payload}")
+            raise Mi355Error(MI355_ERR_COMM, f"sgxamd.dist: rank 0 could not create the RCCL unique id: {payload}")
         handle, err = None, None
         try:
             handle = multi_comm_init(payload, dist.get_world_size(group), rank)
         except Mi355Error as e:
             err = e
         if not _agree_ok(err is None, group):
-            raise Mi355Error(f"sgxamd.dist: RCCL communicator init failed on some rank"
+            raise Mi355Error(err.code if err else MI355_ERR_COMM,
+                             "sgxamd.dist: RCCL communicator init failed on some rank"
                              + (f" (this rank: {err})" if err else ""))
         _comms[key] = handle
     return _comms[key]
@@ -286,8 +295,9 @@ def _sharded_cxx(R: torch.Tensor, S: torch.Tensor, group, algorithm: str, chunks
                   + ("keys only: 4 B per tuple on xGMI (counting join)" if st.get("elem_bytes") == 4
                      else "8-byte tuples on xGMI"),
           "sent_bytes": st["sent_bytes"]}
+    multi = {k: v for k, v in st.items() if k != "local"}
     return ShardedJoinResult(res.matches, int(st["local_matches"]), int(st["recv_r_max"]), int(st["recv_s_max"]), ms,
-                             st["local"])
+                             st["local"], multi)
 
 
 def sharded_rho_join(R: torch.Tensor, S: torch.Tensor, *, group=None, partition_fn=None,
@@ -346,6 +356,11 @@ def sharded_rho_join(R: torch.Tensor, S: torch.Tensor, *, group=None, partition_
     tot = torch.tensor([int(m)], dtype=torch.int64)
     dist.all_reduce(tot, op=dist.ReduceOp.SUM, group=cgroup)
     ms["all_reduce"] = (time.perf_counter() - t2) * 1e3
+    multi = {"world": world, "transport": f"torch.distributed {dist.get_backend(group)} (sgxamd.dist python)",
+             "rank": dist.get_rank(group), "pieces": len(xR.bounds), "elem_bytes": 8,
+             "sent_bytes": 8 * (xR.sent + xS.sent), "recv_r": nR, "recv_s": nS,
+             "ms_exchange_post": ms["shard_partition_and_post_exchange"],
+             "ms_local": ms["exchange_wait_and_local_join"], "ms_allreduce": ms["all_reduce"]}
     # keep the send buffers alive until both exchanges completed
     del xR, xS
-    return ShardedJoinResult(int(tot.item()), int(m), nR, nS, ms, st)
+    return ShardedJoinResult(int(tot.item()), int(m), nR, nS, ms, st, multi)

@@ -1,0 +1,450 @@
+// Test double of RCCL for the multi-GPU join's RcclTransport (csrc/multi_host.cpp).
+//
+// RCCL refuses two ranks on one GPU, so on a one-GPU box the transport's grouped
+// Send/Recv, its count all-gather on the split communicator and its all-reduces could
+// otherwise first run at G > 1 on the driver's 8-GPU node.  This library exports the
+// RCCL entry points the transport binds (loaded through mi355_multi_set_rccl_library)
+// and implements them for ranks that are threads of ONE process, each with its own
+// stream, all on one GPU:
+//   - communicators: ncclCommInitRank (a registry keyed by the unique id; blocks until
+//     every rank joined, like RCCL), ncclCommInitAll, ncclCommSplit (a collective over
+//     the parent), ncclCommDestroy, ncclCommAbort (releases every waiter of the world
+//     with an error);
+//   - ncclSend/ncclRecv inside ncclGroupStart/End: at GroupEnd a rank publishes its
+//     sends (source, size, an event recorded on its stream), then for every receive
+//     takes the peer's next send on that channel, makes its stream wait for the
+//     sender's event and copies device to device on its own stream; the sender's stream
+//     then waits for the receiver's copy (the sender must not overwrite its buffer
+//     before the copy ran: RCCL's stream semantics).  Sizes must match (else
+//     ncclInvalidUsage), as RCCL's would;
+//   - ncclAllGather: every rank copies every rank's block into its receive buffer on its
+//     own stream after the owner's ready event; every stream then waits for every copy;
+//   - ncclAllReduce: staged through the host (sum / max / min of integer and double
+//     types), synchronous with respect to the caller's stream.
+// Fault injection for the failure protocol tests: rccl_double_fail(rank, n) makes rank's
+// n-th later call (counting Send, Recv, AllGather, AllReduce and CommSplit) return
+// ncclSystemError.  Unlike RCCL, GroupEnd and the collectives block the calling host
+// thread until the peers' matching calls arrived; every such wait is bounded
+// (rccl_double_set_timeout_ms, default 20 s) and then fails with ncclSystemError, so a
+// rank that never posts its part cannot hang a test.  ncclCommAbort releases every
+// waiter of the communicator's world at once.
+//
+// Test infrastructure only: the product loads librccl.so.1; nothing here is on the path.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdint>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+namespace {
+
+struct SendPost {
+    const void *src = nullptr;
+    size_t bytes = 0;
+    hipEvent_t ready = nullptr;  // on the sender's stream, after everything before the send
+    hipEvent_t done = nullptr;   // on the receiver's stream, after the copy (set by the receiver)
+    bool failed = false;         // the receiver rejected it (size mismatch)
+};
+
+struct Slot {  // one rank's part of a collective
+    const void *ptr = nullptr;
+    hipEvent_t ev = nullptr;
+    std::vector<uint64_t> host;  // all-reduce operands (as raw 8-byte words)
+    int color = 0, key = 0;
+};
+
+struct World {
+    explicit World(int n) : n(n), slots(n), done(n) {}
+    const int n;
+    std::mutex mu;
+    std::condition_variable cv;
+    bool aborted = false;
+    uint64_t gen = 0;
+    int waiting = 0;
+    std::map<std::pair<int, int>, std::deque<std::shared_ptr<SendPost>>> chan;  // (src, dst)
+    std::vector<Slot> slots;
+    std::vector<hipEvent_t> done;
+    std::map<int, std::shared_ptr<World>> split;  // color -> new world (one split at a time)
+
+    // all n ranks meet; false when the world was aborted or the wait timed out (lk held)
+    bool barrier(std::unique_lock<std::mutex> &lk);
+    template <typename Pred>
+    bool wait(std::unique_lock<std::mutex> &lk, Pred p);
+};
+
+std::atomic<int> g_timeout_ms{20000};
+
+template <typename Pred>
+bool World::wait(std::unique_lock<std::mutex> &lk, Pred p) {
+    const bool ok = cv.wait_for(lk, std::chrono::milliseconds(g_timeout_ms.load()), [&] { return p() || aborted; });
+    if (!ok) {  // a peer never came: the world is unusable for every rank
+        aborted = true;
+        cv.notify_all();
+    }
+    return ok && !aborted;
+}
+
+bool World::barrier(std::unique_lock<std::mutex> &lk) {
+    if (aborted) return false;
+    const uint64_t g = gen;
+    if (++waiting == n) {
+        waiting = 0;
+        ++gen;
+        cv.notify_all();
+        return true;
+    }
+    if (wait(lk, [&] { return gen != g; })) return true;
+    if (gen == g) --waiting;  // timed out or aborted: leave the barrier
+    return gen != g;
+}
+
+}  // namespace
+
+struct ncclComm {
+    std::shared_ptr<World> w;
+    int rank = 0, dev = 0;
+};
+
+namespace {
+
+std::mutex g_reg_mu;
+std::condition_variable g_reg_cv;
+struct Pending {
+    std::shared_ptr<World> w;
+    int joined = 0;
+};
+std::map<std::string, Pending> g_reg;  // unique id -> world being formed
+
+// fault injection: per rank, calls left before the failing one (0 = none)
+std::mutex g_fail_mu;
+std::map<int, int> g_fail;
+
+bool fail_now(int rank) {
+    std::lock_guard<std::mutex> lk(g_fail_mu);
+    auto it = g_fail.find(rank);
+    if (it == g_fail.end()) return false;
+    if (--it->second > 0) return false;
+    g_fail.erase(it);
+    return true;
+}
+
+thread_local int t_group = 0;
+struct Op {
+    bool send;
+    ncclComm_t comm;
+    int peer;
+    void *buf;
+    size_t bytes;
+    hipStream_t stream;
+};
+thread_local std::vector<Op> t_ops;
+
+size_t type_size(ncclDataType_t t) {
+    switch (t) {
+        case ncclInt8: case ncclUint8: return 1;
+        case ncclFloat16: case ncclBfloat16: return 2;
+        case ncclInt32: case ncclUint32: case ncclFloat32: return 4;
+        case ncclInt64: case ncclUint64: case ncclFloat64: return 8;
+        default: return 0;
+    }
+}
+
+ncclResult_t run_group(std::vector<Op> &ops) {
+    // phase 1: publish every send
+    std::vector<std::shared_ptr<SendPost>> mine;
+    for (const Op &o : ops) {
+        if (!o.send) continue;
+        auto p = std::make_shared<SendPost>();
+        p->src = o.buf;
+        p->bytes = o.bytes;
+        if (hipEventCreateWithFlags(&p->ready, hipEventDisableTiming) != hipSuccess ||
+            hipEventRecord(p->ready, o.stream) != hipSuccess)
+            return ncclUnhandledCudaError;
+        World &w = *o.comm->w;
+        std::lock_guard<std::mutex> lk(w.mu);
+        w.chan[{o.comm->rank, o.peer}].push_back(p);
+        w.cv.notify_all();
+        mine.push_back(p);
+    }
+    // phase 2: every receive takes the peer's next send on the channel
+    ncclResult_t rc = ncclSuccess;
+    for (const Op &o : ops) {
+        if (o.send) continue;
+        World &w = *o.comm->w;
+        std::shared_ptr<SendPost> p;
+        {
+            std::unique_lock<std::mutex> lk(w.mu);
+            auto &q = w.chan[{o.peer, o.comm->rank}];
+            if (!w.wait(lk, [&] { return !q.empty(); })) return ncclSystemError;
+            p = q.front();
+            q.pop_front();
+        }
+        hipEvent_t done = nullptr;
+        bool ok = p->bytes == o.bytes;
+        if (!ok) rc = ncclInvalidUsage;
+        if (ok && (hipStreamWaitEvent(o.stream, p->ready, 0) != hipSuccess ||
+                   hipMemcpyAsync(o.buf, p->src, o.bytes, hipMemcpyDeviceToDevice, o.stream) != hipSuccess))
+            return ncclUnhandledCudaError;
+        if (hipEventCreateWithFlags(&done, hipEventDisableTiming) != hipSuccess ||
+            hipEventRecord(done, o.stream) != hipSuccess)
+            return ncclUnhandledCudaError;
+        std::lock_guard<std::mutex> lk(w.mu);
+        p->failed = !ok;
+        p->done = done;
+        w.cv.notify_all();
+    }
+    // phase 3: the sender's stream waits for the receiver's copy
+    size_t k = 0;
+    for (const Op &o : ops) {
+        if (!o.send) continue;
+        auto &p = mine[k++];
+        World &w = *o.comm->w;
+        {
+            std::unique_lock<std::mutex> lk(w.mu);
+            if (!w.wait(lk, [&] { return p->done != nullptr; })) return ncclSystemError;
+        }
+        if (p->failed) rc = ncclInvalidUsage;
+        if (hipStreamWaitEvent(o.stream, p->done, 0) != hipSuccess) return ncclUnhandledCudaError;
+        (void)hipEventDestroy(p->ready);
+        (void)hipEventDestroy(p->done);
+    }
+    return rc;
+}
+
+ncclResult_t enqueue(bool send, void *buf, size_t count, ncclDataType_t t, int peer, ncclComm_t comm,
+                     hipStream_t s) {
+    if (!comm || peer < 0 || peer >= comm->w->n || !type_size(t)) return ncclInvalidArgument;
+    if (fail_now(comm->rank)) return ncclSystemError;
+    t_ops.push_back(Op{send, comm, peer, buf, count * type_size(t), s});
+    if (t_group > 0) return ncclSuccess;
+    std::vector<Op> ops;
+    ops.swap(t_ops);
+    return run_group(ops);
+}
+
+template <typename T>
+void reduce_into(std::vector<uint64_t> &acc, const std::vector<uint64_t> &x, size_t count, ncclRedOp_t op) {
+    T *a = reinterpret_cast<T *>(acc.data());
+    const T *b = reinterpret_cast<const T *>(x.data());
+    for (size_t i = 0; i < count; ++i) {
+        if (op == ncclSum) a[i] = a[i] + b[i];
+        else if (op == ncclMax) a[i] = std::max(a[i], b[i]);
+        else a[i] = std::min(a[i], b[i]);
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+void rccl_double_set_timeout_ms(int ms) { g_timeout_ms = ms > 0 ? ms : 20000; }
+
+void rccl_double_fail(int rank, int nth_call) {
+    std::lock_guard<std::mutex> lk(g_fail_mu);
+    if (nth_call > 0) g_fail[rank] = nth_call;
+    else g_fail.erase(rank);
+}
+
+const char *ncclGetErrorString(ncclResult_t r) {
+    switch (r) {
+        case ncclSuccess: return "no error (rccl double)";
+        case ncclUnhandledCudaError: return "unhandled HIP error (rccl double)";
+        case ncclSystemError: return "system error: injected, or the communicator was aborted (rccl double)";
+        case ncclInvalidArgument: return "invalid argument (rccl double)";
+        case ncclInvalidUsage: return "invalid usage: send/recv sizes differ (rccl double)";
+        default: return "error (rccl double)";
+    }
+}
+
+ncclResult_t ncclGetUniqueId(ncclUniqueId *id) {
+    static std::atomic<uint64_t> seq{1};
+    std::memset(id, 0, sizeof(*id));
+    const uint64_t v[3] = {0x52434344424cULL, (uint64_t)getpid(),
+                           seq++ ^ (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count()};
+    std::memcpy(id->internal, v, sizeof(v));
+    return ncclSuccess;
+}
+
+ncclResult_t ncclCommInitRank(ncclComm_t *comm, int nranks, ncclUniqueId id, int rank) {
+    if (!comm || nranks < 1 || rank < 0 || rank >= nranks) return ncclInvalidArgument;
+    const std::string key(id.internal, sizeof(id.internal));
+    std::shared_ptr<World> w;
+    {
+        std::unique_lock<std::mutex> lk(g_reg_mu);
+        Pending &p = g_reg[key];
+        if (!p.w) p.w = std::make_shared<World>(nranks);
+        if (p.w->n != nranks) return ncclInvalidArgument;
+        w = p.w;
+        if (++p.joined == nranks) {
+            g_reg.erase(key);
+            g_reg_cv.notify_all();
+        } else if (!g_reg_cv.wait_for(lk, std::chrono::milliseconds(g_timeout_ms.load()),
+                                      [&] { return !g_reg.count(key) || g_reg[key].w != w; })) {
+            g_reg.erase(key);  // not every rank came
+            return ncclSystemError;
+        }
+    }
+    auto *c = new ncclComm;
+    c->w = w;
+    c->rank = rank;
+    (void)hipGetDevice(&c->dev);
+    *comm = c;
+    return ncclSuccess;
+}
+
+ncclResult_t ncclCommInitAll(ncclComm_t *comms, int ndev, const int *devlist) {
+    if (!comms || ndev < 1) return ncclInvalidArgument;
+    auto w = std::make_shared<World>(ndev);
+    for (int i = 0; i < ndev; ++i) {
+        comms[i] = new ncclComm;
+        comms[i]->w = w;
+        comms[i]->rank = i;
+        comms[i]->dev = devlist ? devlist[i] : i;
+    }
+    return ncclSuccess;
+}
+
+ncclResult_t ncclCommSplit(ncclComm_t comm, int color, int key, ncclComm_t *newcomm, ncclConfig_t *) {
+    if (!comm || !newcomm) return ncclInvalidArgument;
+    if (fail_now(comm->rank)) return ncclSystemError;
+    World &w = *comm->w;
+    std::unique_lock<std::mutex> lk(w.mu);
+    w.slots[comm->rank].color = color;
+    w.slots[comm->rank].key = key;
+    if (!w.barrier(lk)) return ncclSystemError;
+    // members of this color, ordered by (key, parent rank)
+    std::vector<std::pair<int, int>> members;
+    for (int r = 0; r < w.n; ++r)
+        if (w.slots[r].color == color) members.push_back({w.slots[r].key, r});
+    std::sort(members.begin(), members.end());
+    int newrank = 0;
+    while (members[newrank].second != comm->rank) ++newrank;
+    if (color != NCCL_SPLIT_NOCOLOR && !w.split.count(color)) w.split[color] = std::make_shared<World>((int)members.size());
+    if (!w.barrier(lk)) return ncclSystemError;
+    if (color == NCCL_SPLIT_NOCOLOR) {
+        *newcomm = nullptr;
+    } else {
+        auto *c = new ncclComm;
+        c->w = w.split[color];
+        c->rank = newrank;
+        c->dev = comm->dev;
+        *newcomm = c;
+    }
+    if (!w.barrier(lk)) return ncclSystemError;
+    if (comm->rank == 0) w.split.clear();
+    return w.barrier(lk) ? ncclSuccess : ncclSystemError;
+}
+
+ncclResult_t ncclCommDestroy(ncclComm_t comm) {
+    delete comm;
+    return ncclSuccess;
+}
+
+// The comm object is not freed: another thread may still be inside a call on it (the
+// waiters this abort releases); a few bytes per aborted communicator are leaked.
+ncclResult_t ncclCommAbort(ncclComm_t comm) {
+    if (!comm) return ncclSuccess;
+    std::lock_guard<std::mutex> lk(comm->w->mu);
+    comm->w->aborted = true;
+    comm->w->cv.notify_all();
+    return ncclSuccess;
+}
+
+ncclResult_t ncclGroupStart() {
+    ++t_group;
+    return ncclSuccess;
+}
+
+ncclResult_t ncclGroupEnd() {
+    if (t_group <= 0) return ncclInvalidUsage;
+    if (--t_group > 0) return ncclSuccess;
+    std::vector<Op> ops;
+    ops.swap(t_ops);
+    return run_group(ops);
+}
+
+ncclResult_t ncclSend(const void *buf, size_t count, ncclDataType_t t, int peer, ncclComm_t comm, hipStream_t s) {
+    return enqueue(true, const_cast<void *>(buf), count, t, peer, comm, s);
+}
+
+ncclResult_t ncclRecv(void *buf, size_t count, ncclDataType_t t, int peer, ncclComm_t comm, hipStream_t s) {
+    return enqueue(false, buf, count, t, peer, comm, s);
+}
+
+ncclResult_t ncclAllGather(const void *send, void *recv, size_t count, ncclDataType_t t, ncclComm_t comm,
+                           hipStream_t s) {
+    const size_t bytes = count * type_size(t);
+    if (!comm || !bytes) return ncclInvalidArgument;
+    if (fail_now(comm->rank)) return ncclSystemError;
+    World &w = *comm->w;
+    const int r = comm->rank;
+    hipEvent_t ready = nullptr, done = nullptr;
+    if (hipEventCreateWithFlags(&ready, hipEventDisableTiming) != hipSuccess || hipEventRecord(ready, s) != hipSuccess)
+        return ncclUnhandledCudaError;
+    std::unique_lock<std::mutex> lk(w.mu);
+    w.slots[r].ptr = send;
+    w.slots[r].ev = ready;
+    if (!w.barrier(lk)) return ncclSystemError;
+    for (int q = 0; q < w.n; ++q)
+        if (hipStreamWaitEvent(s, w.slots[q].ev, 0) != hipSuccess ||
+            hipMemcpyAsync(static_cast<char *>(recv) + q * bytes, w.slots[q].ptr, bytes, hipMemcpyDeviceToDevice,
+                           s) != hipSuccess)
+            return ncclUnhandledCudaError;
+    if (hipEventCreateWithFlags(&done, hipEventDisableTiming) != hipSuccess || hipEventRecord(done, s) != hipSuccess)
+        return ncclUnhandledCudaError;
+    w.done[r] = done;
+    if (!w.barrier(lk)) return ncclSystemError;
+    for (int q = 0; q < w.n; ++q)  // no rank reuses its send buffer before every copy of it ran
+        if (hipStreamWaitEvent(s, w.done[q], 0) != hipSuccess) return ncclUnhandledCudaError;
+    if (!w.barrier(lk)) return ncclSystemError;
+    (void)hipEventDestroy(ready);
+    (void)hipEventDestroy(done);
+    return ncclSuccess;
+}
+
+ncclResult_t ncclAllReduce(const void *send, void *recv, size_t count, ncclDataType_t t, ncclRedOp_t op,
+                           ncclComm_t comm, hipStream_t s) {
+    const size_t es = type_size(t);
+    if (!comm || !count || (es != 4 && es != 8) || t == ncclFloat32 ||
+        (op != ncclSum && op != ncclMax && op != ncclMin))
+        return ncclInvalidArgument;
+    if (fail_now(comm->rank)) return ncclSystemError;
+    World &w = *comm->w;
+    const int r = comm->rank;
+    std::vector<uint64_t> mine((count * es + 7) / 8);
+    if (hipMemcpyAsync(mine.data(), send, count * es, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return ncclUnhandledCudaError;
+    std::unique_lock<std::mutex> lk(w.mu);
+    w.slots[r].host = mine;
+    if (!w.barrier(lk)) return ncclSystemError;
+    std::vector<uint64_t> acc = w.slots[0].host;
+    for (int q = 1; q < w.n; ++q) {
+        switch (t) {
+            case ncclInt32: reduce_into<int32_t>(acc, w.slots[q].host, count, op); break;
+            case ncclUint32: reduce_into<uint32_t>(acc, w.slots[q].host, count, op); break;
+            case ncclInt64: reduce_into<int64_t>(acc, w.slots[q].host, count, op); break;
+            case ncclUint64: reduce_into<uint64_t>(acc, w.slots[q].host, count, op); break;
+            default: reduce_into<double>(acc, w.slots[q].host, count, op); break;
+        }
+    }
+    if (!w.barrier(lk)) return ncclSystemError;
+    lk.unlock();
+    if (hipMemcpyAsync(recv, acc.data(), count * es, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return ncclUnhandledCudaError;
+    return ncclSuccess;
+}
+
+}  // extern "C"

@@ -101,6 +101,67 @@ def test_sharded_join_gloo(world, nR, nS, kind, chunks):
         assert tot == [nR, nS]  # every tuple was delivered exactly once
 
 
+def _comm_init_worker(rank, world, port, fail, q):
+    """_cxx_comm (the RCCL communicator set-up of sgxamd.dist) with the library calls
+    replaced: rank 0's unique id fails ("uid"), or rank 1's communicator init ("init").
+    Every rank must raise Mi355Error with a code (no TypeError, no rank left waiting)."""
+    import sys
+
+    from conftest import PKG
+
+    sys.path.insert(0, os.path.join(PKG, "python"))
+    import sgxamd
+    import sgxamd.dist as D
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def uid():
+        if fail == "uid":
+            raise sgxamd.Mi355Error(-6, "cannot load librccl.so.1 (test)")
+        return bytes(128)
+
+    def init(u, n, r):
+        if fail == "init" and r == 1:
+            raise sgxamd.Mi355Error(-6, "ncclCommInitRank: unhandled system error (test)")
+        return 1000 + r
+
+    D.multi_unique_id, D.multi_comm_init = uid, init
+    try:
+        h = D._cxx_comm(None)
+        out = ("ok", h)
+    except sgxamd.Mi355Error as e:
+        out = ("Mi355Error", e.code, str(e))
+    except Exception as e:  # noqa: BLE001 - the test checks the type
+        out = (type(e).__name__, str(e))
+    q.put((rank, out))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fail", ["uid", "init", "none"])
+def test_cxx_comm_init_failures_gloo(fail):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_comm_init_worker, args=(r, 2, port, fail, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=240) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    if fail == "none":
+        assert out == {0: ("ok", 1000), 1: ("ok", 1001)}
+        return
+    for r in (0, 1):
+        assert out[r][0] == "Mi355Error" and out[r][1] == -6, out
+    if fail == "uid":
+        assert all("unique id" in out[r][2] for r in (0, 1))
+    else:
+        assert "this rank" in out[1][2] and "some rank" in out[0][2]
+
+
 def test_non_power_of_two_world_rejected():
     from sgxamd.dist import _log2_exact
 

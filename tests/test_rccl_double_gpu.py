@@ -1,0 +1,333 @@
+"""RcclTransport (csrc/multi_host.cpp) at G = 2 / 4 / 8 on ONE MI355X, through the RCCL
+test double of tests/rccl_double (loaded with mi355_multi_set_rccl_library).
+
+RCCL refuses two ranks on one GPU, so without the double the transport's grouped
+Send/Recv offsets, its ncclUint32 key typing, the count all-gather on the split
+communicator (recv[q] = h[w1 + q*w1 + rank]) and its all-reduces would first run at
+G > 1 on the driver's 8-GPU node.  Here they run with the product's own code:
+  - single process (mi355_rho_join_multi_ex, transport "rccl"): ncclCommInitAll
+    communicators, the tuples through ncclSend/ncclRecv, counts through the host table;
+  - one process per GPU (mi355_multi_comm_init + mi355_rho_join_sharded): G Python
+    threads stand in for the G processes, each with its own communicator pair
+    (ncclCommInitRank + ncclCommSplit), the count all-gathers and all-reduces through
+    RCCL calls.
+Counts are compared bit-exactly with the oracle's restated RHO (radix_join.cpp) and the
+sort counter; the reference's cross-thread prefix (radix_join.cpp:897-915) is what the
+exchange replaces."""
+import ctypes as C
+import os
+import threading
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+DOUBLE = os.path.join(ROOT, "tests", "rccl_double", "librccl_double.so")
+DT = np.dtype([("key", "<u4"), ("payload", "<u4")])
+
+
+def rel(keys):
+    x = np.empty(len(keys), dtype=DT)
+    x["key"] = keys
+    x["payload"] = np.arange(len(keys), dtype=np.uint32)
+    return x
+
+
+@pytest.fixture
+def dbl(sgx, gpu):
+    assert os.path.exists(DOUBLE), "build tests/rccl_double (make -C tests/rccl_double or __graft_entry__.build())"
+    sgx.multi_set_rccl_library(DOUBLE)
+    lib = C.CDLL(DOUBLE)  # the same instance libsgxamd.so loaded (fault injection, timeout)
+    lib.rccl_double_set_timeout_ms(20000)
+    try:
+        yield lib
+    finally:
+        lib.rccl_double_fail(-1, 0)
+        for r in range(8):
+            lib.rccl_double_fail(r, 0)
+        sgx.multi_inject_failure(-1, 0)
+        sgx.multi_set_rccl_library(None)
+        sgx.multi_release()
+
+
+def multi(sgx, R, S, g, **kw):
+    return sgx.rho_join_multi(R, len(R), S, len(S), g, transport="rccl", **kw)
+
+
+# ---------------------------------------------------------------- single process
+@pytest.mark.parametrize("g", [2, 4, 8])
+def test_inprocess_reference_pk_fk(sgx, orc, dbl, g):
+    n = 1 << 18
+    R, S = sgx.reference_relations(n, n)
+    res = multi(sgx, R, S, g)
+    assert res.matches == orc.rho_join(R, S, 4)[0] == n
+    st = res.stats
+    assert st["world"] == g and st["transport"] == "rccl"
+    assert st["recv_r_min"] == st["recv_r_max"] == n // g
+
+
+@pytest.mark.parametrize("seed,nR,nS,kmax,g", [(1, 5000, 7001, 300, 4), (2, 100_003, 77_777, 2**32 - 1, 8),
+                                               (3, 3, 5, 2, 4), (5, 1 << 20, 1 << 20, 1 << 19, 8)])
+def test_inprocess_random_with_duplicates(sgx, orc, dbl, seed, nR, nS, kmax, g):
+    """Duplicates over the full u32 range, tiny slices (empty pieces skipped on both sides
+    of the send/recv pairs), tuples (one-pass plans) and keys (two-pass plans) on the wire."""
+    rng = np.random.default_rng(seed)
+    R = rel(rng.integers(0, kmax + 1, nR, dtype=np.uint64).astype(np.uint32))
+    S = rel(rng.integers(0, kmax + 1, nS, dtype=np.uint64).astype(np.uint32))
+    exp = orc.count_join_sort(R, S)
+    assert multi(sgx, R, S, g).matches == exp
+    assert multi(sgx, R, S, g, algorithm="RHT").matches == exp
+    keys = multi(sgx, R, S, g, radix_bits=14, passes=2)
+    assert keys.matches == exp
+
+
+@pytest.mark.parametrize("step", [1, 2, 3, 4, 5])
+def test_inprocess_failure_on_one_rank(sgx, orc, dbl, step):
+    """A rank that fails (buffers, a shard pass, the local join, no context, the local
+    join's stream sync) flags it at the next collective; every rank leaves together and
+    the communicators stay usable: the next join is exact."""
+    R, S = sgx.reference_relations(1 << 17, (1 << 17) + 5)
+    exp = orc.rho_join(R, S, 4)[0]
+    sgx.multi_inject_failure(2, step)
+    want = "hipStreamSynchronize \\(local join\\)" if step == 5 else "injected failure"
+    try:
+        with pytest.raises(sgx.Mi355Error, match="rank 2: " + want):
+            multi(sgx, R, S, 4)
+    finally:
+        sgx.multi_inject_failure(-1, 0)
+    assert multi(sgx, R, S, 4).matches == exp
+
+
+def test_inprocess_transport_failure(sgx, orc, dbl):
+    """An RCCL call fails on one rank: it leaves the collective sequence, the other rank
+    threads are released (host waits aborted; the double's waits time out), the call
+    returns MI355_ERR_COMM naming that rank, and the next call builds new communicators."""
+    R, S = sgx.reference_relations(1 << 16, 1 << 16)
+    exp = orc.rho_join(R, S, 4)[0]
+    dbl.rccl_double_set_timeout_ms(3000)
+    dbl.rccl_double_fail(1, 3)  # rank 1's third Send/Recv
+    with pytest.raises(sgx.Mi355Error) as ei:
+        multi(sgx, R, S, 4)
+    assert ei.value.code == -6 and "rank 1:" in str(ei.value)
+    dbl.rccl_double_set_timeout_ms(20000)
+    assert multi(sgx, R, S, 4).matches == exp
+
+
+def test_inprocess_config4_full_size(sgx, dbl, gpu):
+    """BASELINE config 4 at its size over 8 RCCL ranks (the double on one GPU): pk(2^27)
+    join fk(2^30): matches == 2^30, 4-byte keys as ncclUint32 on the wire, exactly 2^24 R
+    and 2^27 S keys received per rank, and the sent bytes of every key whose low 3 bits
+    name another rank (counted on the device)."""
+    import torch
+
+    from test_multi_gpu import _slices_sent
+
+    nR, nS, g = 1 << 27, 1 << 30, 8
+    R = torch.empty(nR, dtype=torch.int64, device=gpu)
+    S = torch.empty(nS, dtype=torch.int64, device=gpu)
+    sgx.gen_pk_dev(R, nR, 0, nR, 11111)
+    sgx.gen_fk_dev(S, nS, 0, nR, 22222)
+    torch.cuda.synchronize()
+    try:
+        res = sgx.rho_join_multi(R, nR, S, nS, g, transport="rccl")
+        st = res.stats
+        assert res.matches == nS
+        assert st["transport"] == "rccl" and st["world"] == g and st["elem_bytes"] == 4
+        assert st["recv_r_max"] == st["recv_r_min"] == nR // g
+        assert st["recv_s_max"] == st["recv_s_min"] == nS // g
+        assert st["sent_bytes"] == _slices_sent(R & 0xFFFFFFFF, g, 4) + _slices_sent(S & 0xFFFFFFFF, g, 4)
+        print(f"c4 rccl-double G=8: {st['ms_total']:.2f} ms, sent {st['sent_bytes'] / 1e9:.3f} GB")
+    finally:
+        del R, S
+        sgx.multi_release()
+        torch.cuda.empty_cache()
+
+
+# ---------------------------------------------------------------- one "process" per GPU
+def sharded(sgx, R, S, g, *, handles=None, algorithm="RHO", timeout=120):
+    """Rank r's slice of the device tensors R and S (radix_join.cpp:1488-1499 slicing)
+    joined by G threads, each standing for one process with its own communicator
+    (created here unless `handles` are given).  Returns (results, errors, handles)."""
+    import torch
+
+    torch.cuda.synchronize()
+    own = handles is None
+    if own:
+        uid = sgx.multi_unique_id()
+        handles = [None] * g
+    res, errs = [None] * g, [None] * g
+    nR, nS = R.numel(), S.numel()
+
+    def body(r):
+        try:
+            if own:
+                handles[r] = sgx.multi_comm_init(uid, g, r)
+            ra, rb = r * (nR // g), (nR if r == g - 1 else (r + 1) * (nR // g))
+            sa, sb = r * (nS // g), (nS if r == g - 1 else (r + 1) * (nS // g))
+            res[r] = sgx.rho_join_sharded(handles[r], R[ra:rb], rb - ra, S[sa:sb], sb - sa, algorithm=algorithm)
+        except Exception as e:  # noqa: BLE001 - every rank's outcome is checked by the caller
+            errs[r] = e
+
+    th = [threading.Thread(target=body, args=(r,)) for r in range(g)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout)
+        assert not t.is_alive(), "a rank thread hung"
+    return res, errs, handles
+
+
+def destroy(sgx, handles):
+    for h in handles:
+        if h:
+            sgx.multi_comm_destroy(h)
+
+
+@pytest.mark.parametrize("g", [2, 4, 8])
+def test_sharded_reference_pk_fk(sgx, orc, dbl, gpu, g):
+    import torch
+
+    n = 1 << 18
+    Rh, Sh = sgx.reference_relations(n, n)
+    R = torch.from_numpy(Rh.view(np.int64)).to(gpu)
+    S = torch.from_numpy(Sh.view(np.int64)).to(gpu)
+    res, errs, hs = sharded(sgx, R, S, g)
+    try:
+        assert errs == [None] * g, errs
+        exp = orc.rho_join(Rh, Sh, 4)[0]
+        assert [r.matches for r in res] == [exp] * g
+        for r, x in enumerate(res):
+            st = x.stats
+            assert st["transport"] == "rccl" and st["world"] == g and st["rank"] == r
+            assert st["recv_r_max"] == n // g  # every rank's own receive: 1/g of 1..n
+        assert sum(x.stats["local_matches"] for x in res) == exp
+    finally:
+        destroy(sgx, hs)
+
+
+@pytest.mark.parametrize("g,kmax", [(4, 1000), (8, 2**32 - 1)])
+def test_sharded_random_with_duplicates_and_rht(sgx, orc, dbl, gpu, g, kmax):
+    import torch
+
+    rng = np.random.default_rng(g)
+    Rh = rel(rng.integers(0, kmax + 1, 300_001, dtype=np.uint64).astype(np.uint32))
+    Sh = rel(rng.integers(0, kmax + 1, 200_003, dtype=np.uint64).astype(np.uint32))
+    R = torch.from_numpy(Rh.view(np.int64)).to(gpu)
+    S = torch.from_numpy(Sh.view(np.int64)).to(gpu)
+    exp = orc.count_join_sort(Rh, Sh)
+    res, errs, hs = sharded(sgx, R, S, g)
+    try:
+        assert errs == [None] * g, errs
+        assert {r.matches for r in res} == {exp}
+        res2, errs2, _ = sharded(sgx, R, S, g, handles=hs, algorithm="RHT")  # communicators reused
+        assert errs2 == [None] * g, errs2
+        assert {r.matches for r in res2} == {exp}
+    finally:
+        destroy(sgx, hs)
+
+
+def test_sharded_keys_exchange_exact_bytes(sgx, dbl, gpu):
+    """pk(2^24) join fk(2^25) over 8 ranks: the keys-only plan (elem_bytes 4) and every
+    rank's sent bytes = 4 x its keys whose low 3 bits name another rank."""
+    import torch
+
+    g, nR, nS = 8, 1 << 24, 1 << 25
+    R = torch.empty(nR, dtype=torch.int64, device=gpu)
+    S = torch.empty(nS, dtype=torch.int64, device=gpu)
+    sgx.gen_pk_dev(R, nR, 0, nR, 11111)
+    sgx.gen_fk_dev(S, nS, 0, nR, 22222)
+    res, errs, hs = sharded(sgx, R, S, g)
+    try:
+        assert errs == [None] * g, errs
+        assert {r.matches for r in res} == {nS}
+        for r, x in enumerate(res):
+            st = x.stats
+            assert st["elem_bytes"] == 4
+            kept = 0
+            for X in (R, S):
+                n = X.numel()
+                a, b = r * (n // g), (n if r == g - 1 else (r + 1) * (n // g))
+                k = X[a:b] & 0xFFFFFFFF
+                kept += int(((k & (g - 1)) != r).sum().item())
+            assert st["sent_bytes"] == 4 * kept
+            assert st["recv_r_max"] == nR // g and st["recv_s_max"] == nS // g
+    finally:
+        destroy(sgx, hs)
+        del R, S
+        torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("step", [1, 2, 3, 4, 5])
+def test_sharded_failure_on_one_rank(sgx, orc, dbl, gpu, step):
+    """One process per GPU: rank 2 fails at `step`; every rank raises at the same
+    collective (rank 2 its own error, the others MI355_ERR_COMM 'another rank failed'),
+    no rank hangs, the communicators are not aborted, and the next join is exact."""
+    import torch
+
+    Rh, Sh = sgx.reference_relations(1 << 17, (1 << 17) + 5)
+    R = torch.from_numpy(Rh.view(np.int64)).to(gpu)
+    S = torch.from_numpy(Sh.view(np.int64)).to(gpu)
+    exp = orc.rho_join(Rh, Sh, 4)[0]
+    uid = sgx.multi_unique_id()
+    hs = [None] * 4
+
+    def init(r):
+        hs[r] = sgx.multi_comm_init(uid, 4, r)
+
+    th = [threading.Thread(target=init, args=(r,)) for r in range(4)]
+    [t.start() for t in th]
+    [t.join(60) for t in th]
+    try:
+        sgx.multi_inject_failure(2, step)
+        try:
+            res, errs, _ = sharded(sgx, R, S, 4, handles=hs)
+        finally:
+            sgx.multi_inject_failure(-1, 0)
+        assert all(isinstance(e, sgx.Mi355Error) for e in errs), errs
+        want = "hipStreamSynchronize (local join)" if step == 5 else "injected failure"
+        assert want in str(errs[2])
+        for r in (0, 1, 3):
+            assert errs[r].code == -6 and "another rank failed" in str(errs[r])
+        res, errs, _ = sharded(sgx, R, S, 4, handles=hs)
+        assert errs == [None] * 4 and {x.matches for x in res} == {exp}
+    finally:
+        destroy(sgx, hs)
+
+
+@pytest.mark.parametrize("nth", [1, 4])
+def test_sharded_transport_failure(sgx, orc, dbl, gpu, nth):
+    """An RCCL call fails on rank 1 (its 1st: the sizes all-reduce; its 4th: a count
+    all-gather): rank 1 leaves the sequence and aborts its communicators, the peers'
+    waits in RCCL are released with an error, every rank raises MI355_ERR_COMM, the
+    handles refuse further joins, and new communicators join exactly."""
+    import torch
+
+    Rh, Sh = sgx.reference_relations(1 << 16, 1 << 16)
+    R = torch.from_numpy(Rh.view(np.int64)).to(gpu)
+    S = torch.from_numpy(Sh.view(np.int64)).to(gpu)
+    exp = orc.rho_join(Rh, Sh, 4)[0]
+    uid = sgx.multi_unique_id()
+    hs = [None] * 4
+    th = [threading.Thread(target=lambda r: hs.__setitem__(r, sgx.multi_comm_init(uid, 4, r)), args=(r,))
+          for r in range(4)]
+    [t.start() for t in th]
+    [t.join(60) for t in th]
+    try:
+        dbl.rccl_double_set_timeout_ms(5000)
+        dbl.rccl_double_fail(1, nth)
+        res, errs, _ = sharded(sgx, R, S, 4, handles=hs)
+        assert all(isinstance(e, sgx.Mi355Error) and e.code == -6 for e in errs), errs
+        assert "injected" in str(errs[1]) or "system error" in str(errs[1])
+        res, errs, _ = sharded(sgx, R, S, 4, handles=hs)
+        assert all("communicator was aborted" in str(e) for e in errs), errs
+    finally:
+        dbl.rccl_double_set_timeout_ms(20000)
+        destroy(sgx, hs)
+    res, errs, hs = sharded(sgx, R, S, 4)
+    try:
+        assert errs == [None] * 4 and {x.matches for x in res} == {exp}
+    finally:
+        destroy(sgx, hs)
