@@ -159,6 +159,8 @@ LAYOUTS = {
     1: "8-byte tuples, pooled pass 1 (per-workgroup block chains, no pass-1 histogram)",
     2: "pooled pass 1; a counting join moves 4-byte keys after reading the 8-byte input tuples "
        "(the payloads are never read by the count; SGXAMD_KEYS=0 moves whole tuples)",
+    3: "pooled pass 1 of 4-byte keys with per-chain pass-2 digit histograms counted in LDS (no digit side "
+       "stream; chain-aligned pass-2 segments; SGXAMD_CHAIN_HIST=0 keeps the side stream)",
 }
 
 
@@ -247,7 +249,8 @@ def spawn_ranks(args, argv: list[str]) -> int:
     return launch_ranks([sys.executable, os.path.abspath(__file__), *argv], n)
 
 
-def algorithmic_bytes(kernel: str, nR: int, nS: int, passes: int = 2, pass2_bits: int = 8, elem: int = 8) -> int:
+def algorithmic_bytes(kernel: str, nR: int, nS: int, passes: int = 2, pass2_bits: int = 8, elem: int = 8,
+                      layout: int = 2) -> int:
     """Bytes a kernel must move per launch (DESIGN.md 'Kernels and their rooflines').
 
     Two-pass plans: the pass-1 scatter also writes one pass-2 digit byte per tuple (the
@@ -256,7 +259,8 @@ def algorithmic_bytes(kernel: str, nR: int, nS: int, passes: int = 2, pass2_bits
     (counting joins move keys only: the pass-1 scatter reads 8-byte tuples and
     writes 4-byte keys, pass 2 and the build/probe read and write keys)."""
     n = nR if kernel.startswith("R_") else nS
-    side = passes == 2 and pass2_bits <= 8 and os.environ.get("SGXAMD_DIGIT_SIDE", "1") != "0"  # uses_digit_side()
+    # uses_digit_side(); layout 3 (chain histograms) writes and reads no side stream
+    side = (passes == 2 and pass2_bits <= 8 and os.environ.get("SGXAMD_DIGIT_SIDE", "1") != "0" and layout != 3)
     if kernel.endswith("pass2_hist") and side:
         return n              # one digit byte per tuple
     if kernel.endswith("_hist"):
@@ -437,7 +441,7 @@ def main():
         mine.update(rank=rank, recv_r=res.recv_r, recv_s=res.recv_s, local_matches=res.local_matches)
         allm = [None] * world
         dist.all_gather_object(allm, mine)
-        phases = ("ms_exchange_post", "ms_local", "ms_allreduce")
+        phases = ("ms_exchange_post", "ms_local", "ms_allreduce", "ms_tail")
         m0 = allm[0]
         return {"world": m0.get("world"), "transport": m0.get("transport"), "pieces": m0.get("pieces"),
                 "elem_bytes": m0.get("elem_bytes"), "sent_bytes_total": sum(int(m.get("sent_bytes", 0)) for m in allm),
@@ -492,7 +496,7 @@ def main():
     nS = results[-1].recv_s
     avg = {k: statistics.mean(v) for k, v in per_kernel.items()}
     plan = (results[-1].local_stats.get("passes") or 2, results[-1].local_stats.get("pass2_bits") or 0,
-            results[-1].local_stats.get("elem_bytes") or 8)
+            results[-1].local_stats.get("elem_bytes") or 8, results[-1].local_stats.get("layout") or 0)
     byte_kernels = {k: v for k, v in avg.items() if algorithmic_bytes(k, nR, nS, *plan) > 0}
     dom = max(byte_kernels, key=byte_kernels.get)
     achieved = algorithmic_bytes(dom, nR, nS, *plan) / (avg[dom] * 1e-3) / 1e9
@@ -538,7 +542,8 @@ def main():
             sgxamd.set_key_layout(True)
         avg_t = {k: statistics.mean(v) for k, v in pk_t.items()}
         ls_t = res_t[-1].local_stats
-        plan_t = (ls_t.get("passes") or 2, ls_t.get("pass2_bits") or 0, ls_t.get("elem_bytes") or 8)
+        plan_t = (ls_t.get("passes") or 2, ls_t.get("pass2_bits") or 0, ls_t.get("elem_bytes") or 8,
+                  ls_t.get("layout") or 0)
         pb_t = algorithmic_bytes("join_build_probe", nR, nS, *plan_t) / (avg_t["join_build_probe"] * 1e-3) / 1e9
         rho_info["tuple_layout"] = {
             "partition_layout": LAYOUTS.get(ls_t.get("layout"), "unknown"), "timed": "untimed for value; own K steps",
@@ -570,7 +575,8 @@ def main():
             avg_w = {k: statistics.mean(v) for k, v in pk_w.items()}
             nRw, nSw = res_w[-1].recv_r, res_w[-1].recv_s
             ls_w = res_w[-1].local_stats
-            plan_w = (ls_w.get("passes") or 2, ls_w.get("pass2_bits") or 0, ls_w.get("elem_bytes") or 8)
+            plan_w = (ls_w.get("passes") or 2, ls_w.get("pass2_bits") or 0, ls_w.get("elem_bytes") or 8,
+                      ls_w.get("layout") or 0)
             pb = algorithmic_bytes("join_build_probe", nRw, nSw, *plan_w) / (avg_w["join_build_probe"] * 1e-3) / 1e9
             configs_info[wl] = {
                 "workload": desc_w, "generator": gen_w, "scaling": "strong", "global_R": gRw, "global_S": gSw,

@@ -67,6 +67,9 @@ typedef struct mi355_multi_stats {
     mi355_rho_stats local;     /* the local join of rank 0 (or of the calling rank) */
     uint32_t elem_bytes;       /* bytes per exchanged element: 8 (tuples) or 4 (keys only: a
                                   counting join whose local join reads keys) */
+    double ms_tail;            /* device time from S's last piece landing to the local join's
+                                  end (max over the ranks seen; the part of the join that no
+                                  exchange hides) */
 } mi355_multi_stats;
 
 /* Single process, `ngpus` ranks driven by one host thread each.  R and S are host or

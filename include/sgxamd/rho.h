@@ -79,7 +79,8 @@ typedef struct mi355_rho_stats {
     double ms_build;          /* "Build": ms_join split by the build/probe wall-clock ticks the */
     double ms_probe;          /* "Join":   fused build+probe kernel measures per workgroup */
     /* partition layout: 0 = tuples, pass-1 histogram + cursors; 1 = pooled pass 1 (no
-     * pass-1 histogram), tuples; 2 = pooled pass 1, 4-byte keys (counting joins, RHO and RHT) */
+     * pass-1 histogram), tuples; 2 = pooled pass 1, 4-byte keys (counting joins, RHO and RHT);
+     * 3 = as 2, with the pass-2 digits counted per chain in pass 1 (no digit side stream) */
     uint32_t layout;
     uint32_t elem_bytes;      /* bytes per partitioned element after the input read (8 or 4) */
 } mi355_rho_stats;

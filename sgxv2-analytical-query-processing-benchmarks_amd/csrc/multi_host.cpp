@@ -220,10 +220,10 @@ class Transport {
     virtual ~Transport() = default;
     virtual int world() const = 0;
     virtual int kind() const = 0;
-    // collective: send[d] = tuples this rank sends to rank d in this piece, fail = this
-    // rank has failed; recv[q] = tuples rank q sends to this rank, *any_fail = some rank
-    // has failed (then nothing of this piece is posted, by any rank)
-    virtual int exchange_counts(int rank, hipStream_t s, const uint64_t *send, bool fail, uint64_t *recv,
+    // collective: send[j * G + d] = tuples this rank sends to rank d in piece j (j < m),
+    // fail = this rank has failed; recv[j * G + q] = tuples rank q sends to this rank in
+    // piece j, *any_fail = some rank has failed (then nothing is posted, by any rank)
+    virtual int exchange_counts(int rank, hipStream_t s, const uint64_t *send, int m, bool fail, uint64_t *recv,
                                 bool *any_fail) = 0;
     // collective: after `ready` (the piece's partition on the compute stream), move the
     // piece: the run for destination d starts at send + sum_{d'<d} send_counts[d'];
@@ -259,14 +259,17 @@ class HostCollectives {
     void abort() { bar_.abort(); }
     bool aborted() { return bar_.aborted(); }
 
-    int exchange_counts(int rank, const uint64_t *send, bool fail, uint64_t *recv, bool *any_fail) {
-        std::copy(send, send + world_, counts_[rank].begin());
-        counts_[rank][world_] = fail ? 1 : 0;
+    int exchange_counts(int rank, const uint64_t *send, int m, bool fail, uint64_t *recv, bool *any_fail) {
+        const size_t w = (size_t)m * world_;  // the fail flag follows the m rows
+        std::vector<uint64_t> &mine = counts_[rank];
+        if (mine.size() < w + 1) mine.resize(w + 1);
+        std::copy(send, send + w, mine.begin());
+        mine[w] = fail ? 1 : 0;
         if (!bar_.wait()) return aborted_rc();
         bool f = false;
         for (int q = 0; q < world_; ++q) {
-            recv[q] = counts_[q][rank];
-            f = f || counts_[q][world_];
+            for (int j = 0; j < m; ++j) recv[(size_t)j * world_ + q] = counts_[q][(size_t)j * world_ + rank];
+            f = f || counts_[q][w];
         }
         *any_fail = f;
         if (!bar_.wait()) return aborted_rc();  // the table is reused by the next piece
@@ -292,7 +295,7 @@ class HostCollectives {
     }
     int world_;
     Barrier bar_;
-    std::vector<std::vector<uint64_t>> counts_;  // [rank][G counts + fail flag]
+    std::vector<std::vector<uint64_t>> counts_;  // [rank][m rows of G counts + fail flag]
     std::vector<std::array<uint64_t, kMaxReduce>> red_;
 };
 
@@ -309,7 +312,8 @@ class RcclTransport final : public Transport {
     RcclTransport(int world, int first_rank, std::vector<ncclComm_t> comms, std::vector<ncclComm_t> ccomms,
                   std::shared_ptr<HostCollectives> host)
         : world_(world), first_(first_rank), comms_(std::move(comms)), ccomms_(std::move(ccomms)),
-          host_(std::move(host)), buf_(comms_.size()), pinned_(comms_.size(), nullptr) {}
+          host_(std::move(host)), buf_(comms_.size()), pinned_(comms_.size(), nullptr),
+          pinned_bytes_(comms_.size(), 0) {}
     ~RcclTransport() override {
         for (auto &b : buf_) b.release();
         for (auto *h : pinned_)
@@ -318,23 +322,24 @@ class RcclTransport final : public Transport {
     int world() const override { return world_; }
     int kind() const override { return MI355_TRANSPORT_RCCL; }
 
-    int exchange_counts(int rank, hipStream_t s, const uint64_t *send, bool fail, uint64_t *recv,
+    int exchange_counts(int rank, hipStream_t s, const uint64_t *send, int m, bool fail, uint64_t *recv,
                         bool *any_fail) override {
-        if (host_) return host_->exchange_counts(rank, send, fail, recv, any_fail);
+        if (host_) return host_->exchange_counts(rank, send, m, fail, recv, any_fail);
         const int i = rank - first_;
-        const size_t w1 = world_ + 1;  // G counts + the fail flag
+        const size_t w = (size_t)m * world_, w1 = w + 1;  // m rows of G counts + the fail flag
         uint64_t *d = nullptr, *h = nullptr;
-        MH_RC(scratch(i, &d, &h));
-        std::memcpy(h, send, sizeof(uint64_t) * world_);
-        h[world_] = fail ? 1 : 0;
+        MH_RC(scratch(i, w1 * (world_ + 1), &d, &h));
+        std::memcpy(h, send, sizeof(uint64_t) * w);
+        h[w] = fail ? 1 : 0;
         MH_HIPC(hipMemcpyAsync(d, h, sizeof(uint64_t) * w1, hipMemcpyHostToDevice, s));
         MH_NCCL(rccl().AllGather(d, d + w1, w1, ncclUint64, ccomms_[i], s));
         MH_HIPC(hipMemcpyAsync(h + w1, d + w1, sizeof(uint64_t) * w1 * world_, hipMemcpyDeviceToHost, s));
         MH_HIPC(hipStreamSynchronize(s));
         bool f = false;
         for (int q = 0; q < world_; ++q) {
-            recv[q] = h[w1 + q * w1 + rank];
-            f = f || h[w1 + q * w1 + world_];
+            const uint64_t *row = h + w1 + (size_t)q * w1;
+            for (int j = 0; j < m; ++j) recv[(size_t)j * world_ + q] = row[(size_t)j * world_ + rank];
+            f = f || row[w];
         }
         *any_fail = f;
         return MI355_OK;
@@ -381,7 +386,7 @@ class RcclTransport final : public Transport {
         if (host_) return host_->allreduce(rank, v, n, op);
         const int i = rank - first_;
         uint64_t *d = nullptr, *h = nullptr;
-        MH_RC(scratch(i, &d, &h));
+        MH_RC(scratch(i, kMaxReduce, &d, &h));
         std::memcpy(h, v, sizeof(uint64_t) * n);
         MH_HIPC(hipMemcpyAsync(d, h, sizeof(uint64_t) * n, hipMemcpyHostToDevice, s));
         MH_NCCL(rccl().AllReduce(d, d, n, ncclUint64, op == kSum ? ncclSum : ncclMax, ccomms_[i], s));
@@ -398,11 +403,18 @@ class RcclTransport final : public Transport {
     bool aborted() override { return aborted_ || (host_ && host_->aborted()); }
 
    private:
-    // per local rank: device [(G+1) + G(G+1)] u64 and its pinned host mirror
-    int scratch(int i, uint64_t **d, uint64_t **h) {
-        const size_t bytes = sizeof(uint64_t) * std::max<size_t>((world_ + 1) * (size_t)(world_ + 1), kMaxReduce);
+    // per local rank: at least `words` u64 of device memory and a pinned host mirror
+    // (a count exchange: (G + 1) rows of m * G + 1 words)
+    int scratch(int i, size_t words, uint64_t **d, uint64_t **h) {
+        const size_t bytes = sizeof(uint64_t) * std::max<size_t>(words, kMaxReduce);
         MH_HIPC(buf_[i].ensure(bytes));
-        if (!pinned_[i]) MH_HIPC(hipHostMalloc(reinterpret_cast<void **>(&pinned_[i]), bytes));
+        if (pinned_bytes_[i] < bytes) {
+            if (pinned_[i]) (void)hipHostFree(pinned_[i]);
+            pinned_[i] = nullptr;
+            pinned_bytes_[i] = 0;
+            MH_HIPC(hipHostMalloc(reinterpret_cast<void **>(&pinned_[i]), bytes));
+            pinned_bytes_[i] = bytes;
+        }
         *d = buf_[i].as<uint64_t>();
         *h = pinned_[i];
         return MI355_OK;
@@ -413,6 +425,7 @@ class RcclTransport final : public Transport {
     std::shared_ptr<HostCollectives> host_;
     std::vector<DeviceBuffer> buf_;
     std::vector<uint64_t *> pinned_;
+    std::vector<size_t> pinned_bytes_;
 };
 
 // G logical ranks on one GPU, one host thread each: counts and reductions through the
@@ -425,9 +438,9 @@ class RehearsalTransport final : public Transport {
     int world() const override { return host_.world(); }
     int kind() const override { return MI355_TRANSPORT_REHEARSAL; }
 
-    int exchange_counts(int rank, hipStream_t, const uint64_t *send, bool fail, uint64_t *recv,
+    int exchange_counts(int rank, hipStream_t, const uint64_t *send, int m, bool fail, uint64_t *recv,
                         bool *any_fail) override {
-        return host_.exchange_counts(rank, send, fail, recv, any_fail);
+        return host_.exchange_counts(rank, send, m, fail, recv, any_fail);
     }
 
     int post_exchange(int rank, hipStream_t c, hipEvent_t ready, const void *send, const uint64_t *send_counts,
@@ -481,6 +494,7 @@ std::atomic<int> g_pieces{4};
 struct RankStreams {
     hipStream_t comm = nullptr;
     std::vector<hipEvent_t> ev;
+    hipEvent_t t_land = nullptr, t_done = nullptr;  // timed: S landed, local join done
 };
 std::mutex g_streams_mu;
 std::unordered_map<const Context *, RankStreams> g_streams;
@@ -489,6 +503,8 @@ int rank_streams(Context *ctx, int nev, RankStreams **out) {
     std::lock_guard<std::mutex> lk(g_streams_mu);
     RankStreams &rs = g_streams[ctx];
     if (!rs.comm) MH_HIP(hipStreamCreateWithFlags(&rs.comm, hipStreamNonBlocking));
+    if (!rs.t_land) MH_HIP(hipEventCreate(&rs.t_land));
+    if (!rs.t_done) MH_HIP(hipEventCreate(&rs.t_done));
     while ((int)rs.ev.size() < nev) {
         hipEvent_t e = nullptr;
         MH_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -505,6 +521,7 @@ struct RankOut {
     bool together = false;   // the call failed at a collective every rank left at (the
                              // sequence is intact; nothing to abort)
     double ms_post = 0, ms_local = 0, ms_allreduce = 0, ms_total = 0;
+    double ms_tail = -1;  // device time from S's last piece landing to the local join's end
     mi355_rho_stats st{};
 };
 
@@ -624,45 +641,51 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
         if (injected(rank, kFailBuffers)) fail(MI355_ERR_OOM);
     }
 
-    std::vector<uint64_t> sc(G), rc(G);
-    uint64_t total[2] = {0, 0};
-    bool any_fail = false;
-    for (int rel = 0; rel < 2 && !any_fail; ++rel) {
-        const row_t *in = rel ? S : R;
-        const uint64_t n = rel ? nS : nR;
-        // without a context (pre_fail) the rank only takes part in the count exchange,
-        // flagged as failed, and posts nothing
-        char *snd = ctx ? (rel ? ctx->xsendS : ctx->xsendR).as<char>() : nullptr;
-        char *rcv = ctx ? (rel ? ctx->xrecvS : ctx->xrecvR).as<char>() : nullptr;
-        const uint64_t per = (n + K - 1) / K;
+    // every piece's destination counts first (both relations), then ONE count exchange,
+    // then every piece's scatter and post enqueued without a host wait: piece i+1's
+    // scatter runs while piece i moves on the communication stream
+    const int M = 2 * K;
+    std::vector<uint64_t> sc((size_t)M * G, 0), rc((size_t)M * G, 0);
+    std::array<uint64_t, 2> nrel{nR, nS};
+    std::vector<uint64_t> pa(M), pn(M);  // piece j = rel * K + i: first tuple, tuples
+    std::vector<const row_t *> pin(M);
+    for (int rel = 0; rel < 2; ++rel) {
+        const uint64_t n = nrel[rel], per = (n + K - 1) / K;
         for (int i = 0; i < K; ++i) {
-            const uint64_t a = std::min(n, i * per), b = std::min(n, (i + 1) * per);
-            std::fill(sc.begin(), sc.end(), 0);
-            if (fail_rc == MI355_OK && b > a) {
-                fail(rho::shard_partition_device(ctx, s, in + a, b - a, 0, dest_bits, snd + a * elem, sc.data(),
-                                                 (uint32_t)elem));
-                if (rel == 1 && i == K / 2 && injected(rank, kFailPiece)) fail(MI355_ERR_HIP);
-            }
-            if (fail_rc != MI355_OK) std::fill(sc.begin(), sc.end(), 0);
-            MH_RC(transport_rc(T.exchange_counts(rank, s, sc.data(), fail_rc != MI355_OK, rc.data(), &any_fail)));
-            if (any_fail) break;  // every rank sees the same flags: none posts this piece
-            // the counts went out unflagged, so the piece is posted whatever happens now;
-            // a failure here is flagged at the next collective
-            hipEvent_t ready = rs->ev[rel * K + i];
-            hip_ok(hipEventRecord(ready, s), "hipEventRecord (piece ready)");
-            MH_RC(transport_rc(T.post_exchange(rank, rs->comm, ready, snd + a * elem, sc.data(),
-                                               rcv + total[rel] * elem, rc.data(), elem)));
-            for (int q = 0; q < G; ++q) {
-                total[rel] += rc[q];
-                if (q != rank) o.sent += sc[q] * elem;
-            }
+            const int j = rel * K + i;
+            pa[j] = std::min(n, i * per);
+            pn[j] = std::min(n, (i + 1) * per) - pa[j];
+            pin[j] = (rel ? S : R) + pa[j];
         }
-        if (!any_fail) hip_ok(hipEventRecord(rs->ev[2 * K + rel], rs->comm), "hipEventRecord (relation landed)");
     }
-    if (any_fail) {  // the pieces posted so far were posted by every rank: let them land
-        if (rs) (void)hipStreamSynchronize(rs->comm);
-        return peer_failed();
+    if (fail_rc == MI355_OK) {
+        fail(rho::shard_count_pieces(ctx, s, pin.data(), pn.data(), M, 0, dest_bits, (uint32_t)elem, sc.data()));
+        if (injected(rank, kFailPiece)) fail(MI355_ERR_HIP);
     }
+    if (fail_rc != MI355_OK) std::fill(sc.begin(), sc.end(), 0);
+    bool any_fail = false;
+    MH_RC(transport_rc(T.exchange_counts(rank, s, sc.data(), M, fail_rc != MI355_OK, rc.data(), &any_fail)));
+    if (any_fail) return peer_failed();  // every rank sees the same flags: none posts anything
+    // the counts went out unflagged, so every piece is posted whatever happens now; a
+    // failure from here on is flagged at the final all-reduce
+    uint64_t total[2] = {0, 0};
+    for (int j = 0; j < M; ++j) {
+        const int rel = j / K;
+        char *snd = (rel ? ctx->xsendS : ctx->xsendR).as<char>() + pa[j] * elem;
+        char *rcv = (rel ? ctx->xrecvS : ctx->xrecvR).as<char>() + total[rel] * elem;
+        if (fail_rc == MI355_OK) fail(rho::shard_scatter_piece(ctx, s, j, snd));
+        hipEvent_t ready = rs->ev[j];
+        hip_ok(hipEventRecord(ready, s), "hipEventRecord (piece ready)");
+        const uint64_t *scj = sc.data() + (size_t)j * G, *rcj = rc.data() + (size_t)j * G;
+        MH_RC(transport_rc(T.post_exchange(rank, rs->comm, ready, snd, scj, rcv, rcj, elem)));
+        for (int q = 0; q < G; ++q) {
+            total[rel] += rcj[q];
+            if (q != rank) o.sent += scj[q] * elem;
+        }
+        if ((j + 1) % K == 0)
+            hip_ok(hipEventRecord(rs->ev[2 * K + rel], rs->comm), "hipEventRecord (relation landed)");
+    }
+    const bool timed = hipEventRecord(rs->t_land, rs->comm) == hipSuccess;
     o.recv_r = total[0];
     o.recv_s = total[1];
     const auto t1 = Clock::now();
@@ -684,6 +707,7 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
             hip_ok(hipStreamWaitEvent(s, rs->ev[2 * K + 1], 0), "hipStreamWaitEvent (S landed)");
         }
     }
+    const bool timed_end = timed && fail_rc == MI355_OK && hipEventRecord(rs->t_done, s) == hipSuccess;
     // an asynchronous error of the local join's kernels surfaces here
     hipError_t se = hipStreamSynchronize(s);
     if (injected(rank, kFailLocalSync)) se = hipErrorLaunchFailure;
@@ -691,6 +715,9 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
     hip_ok(hipStreamSynchronize(rs->comm), "hipStreamSynchronize (exchange)");
     const auto t2 = Clock::now();
     o.ms_local = std::chrono::duration<double, std::milli>(t2 - t1).count();
+    float tail = -1.f;
+    if (timed_end && fail_rc == MI355_OK && hipEventElapsedTime(&tail, rs->t_land, rs->t_done) == hipSuccess)
+        o.ms_tail = tail;
     uint64_t m[2] = {fail_rc == MI355_OK ? o.local : 0, fail_rc != MI355_OK ? 1u : 0u};
     MH_RC(transport_rc(T.allreduce(rank, s, m, 2, kSum)));
     if (m[1]) return peer_failed();
@@ -774,6 +801,7 @@ void fill_stats(mi355_multi_stats *st, const std::vector<RankOut> &outs, int G, 
         st->ms_exchange_post = std::max(st->ms_exchange_post, o.ms_post);
         st->ms_local = std::max(st->ms_local, o.ms_local);
         st->ms_allreduce = std::max(st->ms_allreduce, o.ms_allreduce);
+        st->ms_tail = std::max(st->ms_tail, o.ms_tail);
     }
     if (!outs.empty()) {
         st->local_matches = outs[0].local;

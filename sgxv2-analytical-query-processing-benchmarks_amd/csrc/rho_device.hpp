@@ -22,6 +22,15 @@ int join_device(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const
 // out_elem 8: out holds the tuples; 4: only their key words (a keys-only exchange).
 int shard_partition_device(Context *ctx, hipStream_t s, const row_t *in, uint64_t n, uint32_t key_shift,
                            uint32_t dest_bits, void *out, uint64_t *dest_counts, uint32_t out_elem = 8);
+// The same partition in two phases over several pieces, so that one count exchange
+// serves a whole join: shard_count_pieces plans pieces (in[j], n[j]), j < npieces, runs
+// their histograms and returns every piece's destination counts in counts[j * G + d]
+// (G = 2^dest_bits; one synchronisation of s); shard_scatter_piece then enqueues piece
+// j's scatter into out (no wait).  The plans stay valid until the next shard or join
+// call on ctx, which reuses the scratch in stream order.
+int shard_count_pieces(Context *ctx, hipStream_t s, const row_t *const *in, const uint64_t *n, int npieces,
+                       uint32_t key_shift, uint32_t dest_bits, uint32_t out_elem, uint64_t *counts);
+int shard_scatter_piece(Context *ctx, hipStream_t s, int j, void *out);
 // in_elem 8: dR / dS are row_t relations; 4: packed keys (needs keys_exchange_plan's plan).
 int join_pipelined_begin(Context *ctx, hipStream_t s, const void *dR, uint64_t nR, uint64_t nS,
                          const mi355_rho_opts *opts, uint32_t in_elem = 8);

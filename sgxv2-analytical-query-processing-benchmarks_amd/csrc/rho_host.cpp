@@ -13,6 +13,8 @@
 #include <cstring>
 #include <string>
 #include <unordered_map>
+#include <vector>
+#include <cstdio>
 
 #include "common.hpp"
 #include "rho_device.hpp"
@@ -149,6 +151,18 @@ inline bool keys_enabled() {
     }();
     return on && thread_key_layout();
 }
+// Pooled key plans with a 7-bit pass 1 and a 6- or 7-bit pass 2 count every chain's
+// pass-2 digits in the pass-1 scatter (chain histograms, rho_internal.hpp
+// launch_scatter_pool): no digit side stream is written or read, and the pass-2
+// histogram pass becomes one scan over the chain histograms (launch_chain_scan).
+// SGXAMD_CHAIN_HIST=0 keeps the side stream (development A/B switch; results identical).
+inline bool chain_enabled() {
+    static const bool on = [] {
+        const char *e = std::getenv("SGXAMD_CHAIN_HIST");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return on;
+}
 constexpr uint32_t kPoolSegs = 512;  // two 512-thread workgroups per CU: one wave of workgroups
 inline uint32_t pool_segs() {
     static const uint32_t v = [] {
@@ -174,12 +188,14 @@ struct RelPlan {
     uint32_t grid2;
     bool pooled;           // pooled pass 1 + block-list pass 2
     bool keys;             // the partitions hold 4-byte keys (counting joins; pooled, or a shard pass)
+    bool chain;            // chain histograms instead of the digit side stream (pooled keys)
     uint32_t in_size;      // bytes per input element: 8 (row_t) or 4 (keys, a keys-only exchange)
     uint32_t pool_blocks;  // blocks per pass-1 segment pool
     uint64_t t1_tuples;    // capacity of the pass-1 output (and side stream) in tuples
     // scratch offsets (pooled: hist1 holds the chain records, tot1 their column totals)
     size_t hist1, tot1, start1, cnt1, segbase2, hist2, pstart, pcnt;
     size_t binfo, used, lbase, lcount, list;
+    size_t chist, seglb, segle, segc0;  // chain histograms [F1][nseg1][F2], pass-2 segment ranges
 };
 
 #define RHO_HIP(call)                                                                      \
@@ -207,13 +223,13 @@ int partition_relation_pooled(Context *ctx, hipStream_t s, Timer &tm, const std:
         const SegMap m1{nullptr, nullptr, nullptr, 1, rp.seg1, rp.n};
         const PoolOut po{A.at<uint32_t>(rp.binfo), A.at<uint64_t>(rp.hist1), A.at<uint32_t>(rp.used), rp.pool_blocks,
                          rp.nseg1};
-        const DigitSide ds{side, key_shift + pol.b1, pol.b2};
+        const DigitSide ds{rp.chain ? nullptr : side, key_shift + pol.b1, pol.b2};
         tm.mark((t + "pass1_scatter").c_str());
         RHO_HIP(launch_scatter_pool(in, rp.in_size, t1, rp.keys ? 4u : 8u, m1, rp.nseg1, key_shift, pol.b1, po, ds,
-                                    s));
+                                    s, rp.chain ? A.at<uint32_t>(rp.chist) : nullptr));
         tm.mark((t + "pass1_scan").c_str());
         RHO_HIP(launch_pool_layout(po.cnt, rp.nseg1, pol.b1, A.at<uint64_t>(rp.tot1), start1, cnt1, lbase, lcount,
-                                   segbase2, s));
+                                   segbase2, s, rp.chain));
         RHO_HIP(launch_block_list(po, lbase, list, s));
         *final_rel = t1;
         *pstart = start1;
@@ -224,6 +240,27 @@ int partition_relation_pooled(Context *ctx, hipStream_t s, Timer &tm, const std:
     uint64_t *ps = A.at<uint64_t>(rp.pstart);
     uint64_t *pc = A.at<uint64_t>(rp.pcnt);
     const SegMap m2{lbase, lcount, segbase2, F1, kPass2Ents, rp.n};
+    if (rp.chain) {
+        // the chain histograms (recounted where a count may have wrapped) give the
+        // chain-aligned pass-2 segments, their cursors and the partition table
+        uint32_t *seglb = A.at<uint32_t>(rp.seglb), *segle = A.at<uint32_t>(rp.segle);
+        tm.mark((t + "pass2_chain").c_str());
+        RHO_HIP(launch_chain_fix(A.at<uint64_t>(rp.hist1), A.at<uint64_t>(rp.tot1), rp.nseg1, pol.b1, pol.b2, lbase,
+                                 list, reinterpret_cast<const uint32_t *>(t1), key_shift + pol.b1,
+                                 A.at<uint32_t>(rp.chist), s));
+        RHO_HIP(launch_chain_scan(A.at<uint64_t>(rp.hist1), rp.nseg1, A.at<uint32_t>(rp.chist), pol.b1, pol.b2,
+                                  start1, lbase, lcount, segbase2, hist2, seglb, segle, A.at<uint32_t>(rp.segc0), ps,
+                                  pc, s));
+        SegMap mc = m2;
+        mc.seg_lb = seglb;
+        mc.seg_le = segle;
+        tm.mark((t + "pass2_scatter").c_str());
+        RHO_HIP(launch_scatter_blk(t1, list, t2, 4u, mc, rp.grid2, key_shift + pol.b1, pol.b2, hist2, s));
+        *final_rel = t2;
+        *pstart = ps;
+        *pcnt = pc;
+        return MI355_OK;
+    }
     tm.mark((t + "pass2_hist").c_str());
     RHO_HIP(launch_hist_side_blk(side, list, m2, rp.grid2, pol.b2, hist2, s));
     tm.mark((t + "pass2_scan").c_str());
@@ -236,6 +273,39 @@ int partition_relation_pooled(Context *ctx, hipStream_t s, Timer &tm, const std:
     return MI355_OK;
 }
 
+// Pass 1 of an unpooled plan in its two halves: the histogram and its scan (digit
+// starts / counts in start1 / cnt1), then the scatter (side: the pass-2 digit stream, or
+// null).  The shard exchange runs every piece's first half before any second half.
+int pass1_counts(Context *ctx, hipStream_t s, Timer &tm, const std::string &t, const row_t *in, const RelPlan &rp,
+                 const Policy &pol, uint32_t key_shift) {
+    Arena &A = ctx->scratch;
+    const SegMap m1{nullptr, nullptr, nullptr, 1, rp.seg1, rp.n};
+    uint64_t *hist1 = A.at<uint64_t>(rp.hist1);
+    tm.mark((t + "pass1_hist").c_str());
+    RHO_HIP(launch_hist(in, m1, rp.nseg1, key_shift, pol.b1, hist1, kDigitMajor, rp.nseg1, s));
+    tm.mark((t + "pass1_scan").c_str());
+    RHO_HIP(launch_scan_single(hist1, rp.nseg1, pol.b1, A.at<uint64_t>(rp.tot1), A.at<uint64_t>(rp.start1),
+                               A.at<uint64_t>(rp.cnt1), 0, pol.passes == 2 ? A.at<uint32_t>(rp.segbase2) : nullptr,
+                               rp.seg2, s));
+    return MI355_OK;
+}
+
+int pass1_scatter(Context *ctx, hipStream_t s, Timer &tm, const std::string &t, const row_t *in, row_t *t1,
+                  uint8_t *side, const RelPlan &rp, const Policy &pol, uint32_t key_shift) {
+    Arena &A = ctx->scratch;
+    const SegMap m1{nullptr, nullptr, nullptr, 1, rp.seg1, rp.n};
+    uint64_t *hist1 = A.at<uint64_t>(rp.hist1), *start1 = A.at<uint64_t>(rp.start1);
+    tm.mark((t + "pass1_scatter").c_str());
+    const DigitSide ds{side, key_shift + pol.b1, pol.b2};
+    if (rp.keys)  // one pass writing key words (the keys-only shard partition)
+        RHO_HIP(launch_scatter_keys(in, reinterpret_cast<uint32_t *>(t1), m1, rp.nseg1, key_shift, pol.b1, hist1,
+                                    kDigitMajor, rp.nseg1, start1, s));
+    else
+        RHO_HIP(launch_scatter(in, t1, m1, rp.nseg1, key_shift, pol.b1, hist1, kDigitMajor, rp.nseg1, start1,
+                               side ? &ds : nullptr, s));
+    return MI355_OK;
+}
+
 // One relation through pass 1 (and pass 2).  Returns the final buffer and
 // partition table pointers through *final / *pstart / *pcnt.  side (n bytes, two-pass
 // plans whose pass-2 digit fits a byte): the pass-1 scatter writes every tuple's pass-2
@@ -244,8 +314,6 @@ int partition_relation(Context *ctx, hipStream_t s, Timer &tm, const char *tag, 
                        row_t *t2, uint8_t *side, RelPlan &rp, const Policy &pol, uint32_t key_shift,
                        const row_t **final_rel, const uint64_t **pstart, const uint64_t **pcnt, bool pass2_now) {
     Arena &A = ctx->scratch;
-    uint64_t *hist1 = A.at<uint64_t>(rp.hist1);
-    uint64_t *tot1 = A.at<uint64_t>(rp.tot1);
     uint64_t *start1 = A.at<uint64_t>(rp.start1);
     uint64_t *cnt1 = A.at<uint64_t>(rp.cnt1);
     uint32_t *segbase2 = A.at<uint32_t>(rp.segbase2);
@@ -254,20 +322,9 @@ int partition_relation(Context *ctx, hipStream_t s, Timer &tm, const char *tag, 
     if (rp.pooled) return partition_relation_pooled(ctx, s, tm, t, in, t1, t2, side, rp, pol, key_shift, final_rel,
                                                     pstart, pcnt, pass2_now);
     if (!pass2_now) {
-        SegMap m1{nullptr, nullptr, nullptr, 1, rp.seg1, rp.n};
-        tm.mark((t + "pass1_hist").c_str());
-        RHO_HIP(launch_hist(in, m1, rp.nseg1, key_shift, pol.b1, hist1, kDigitMajor, rp.nseg1, s));
-        tm.mark((t + "pass1_scan").c_str());
-        RHO_HIP(launch_scan_single(hist1, rp.nseg1, pol.b1, tot1, start1, cnt1, 0,
-                                   pol.passes == 2 ? segbase2 : nullptr, rp.seg2, s));
-        tm.mark((t + "pass1_scatter").c_str());
-        const DigitSide ds{side, key_shift + pol.b1, pol.b2};
-        if (rp.keys)  // one pass writing key words (the keys-only shard partition)
-            RHO_HIP(launch_scatter_keys(in, reinterpret_cast<uint32_t *>(t1), m1, rp.nseg1, key_shift, pol.b1, hist1,
-                                        kDigitMajor, rp.nseg1, start1, s));
-        else
-            RHO_HIP(launch_scatter(in, t1, m1, rp.nseg1, key_shift, pol.b1, hist1, kDigitMajor, rp.nseg1, start1,
-                                   use_side ? &ds : nullptr, s));
+        int rc = pass1_counts(ctx, s, tm, t, in, rp, pol, key_shift);
+        if (!rc) rc = pass1_scatter(ctx, s, tm, t, in, t1, use_side ? side : nullptr, rp, pol, key_shift);
+        if (rc) return rc;
         *final_rel = t1;
         *pstart = start1;
         *pcnt = cnt1;
@@ -319,6 +376,7 @@ void plan_relation(Arena &A, RelPlan &rp, uint64_t n, const Policy &pol, int poo
     rp.t1_tuples = n;
     rp.pooled = false;
     rp.keys = false;
+    rp.chain = false;
     rp.in_size = sizeof(row_t);
     if (pool != kNoPool) {
         // pass-1 segments of whole tiles, about pool_segs() of them; every digit of a
@@ -330,11 +388,16 @@ void plan_relation(Arena &A, RelPlan &rp, uint64_t n, const Policy &pol, int poo
         const uint64_t max_blocks = n / kBlk + (uint64_t)nseg * F1;
         rp.pooled = true;
         rp.keys = pool == kPoolKeys;
+        // chain histograms: 32-bit list positions and a u32 segment slot table
+        rp.chain = rp.keys && chain_enabled() && sort2_enabled() && chain_hist_supported(pol.b1, pol.b2) &&
+                   max_blocks < (1ull << 31);
         rp.seg1 = seg;
         rp.nseg1 = nseg;
         rp.pool_blocks = (uint32_t)pb;
         rp.t1_tuples = (uint64_t)nseg * pb * kBlk;
-        rp.grid2 = (uint32_t)(max_blocks / kPass2Ents) + F1 + 1;
+        // pass-2 segments: kPass2Ents blocks, or chain-aligned slots of at least kPass2Ents / 2
+        // blocks (chain_slot_target), at most one partial slot per region either way
+        rp.grid2 = (uint32_t)(max_blocks / (rp.chain ? kPass2Ents / 2 : kPass2Ents)) + F1 + 1;
     }
     rp.hist1 = A.reserve(sizeof(uint64_t) * (size_t)F1 * std::max<uint32_t>(rp.nseg1, 1));
     rp.tot1 = A.reserve(sizeof(uint64_t) * F1);
@@ -352,6 +415,12 @@ void plan_relation(Arena &A, RelPlan &rp, uint64_t n, const Policy &pol, int poo
         rp.lbase = A.reserve(sizeof(uint64_t) * F1);
         rp.lcount = A.reserve(sizeof(uint64_t) * F1);
         rp.list = A.reserve(sizeof(uint64_t) * (size_t)(rp.n / kBlk + (uint64_t)rp.nseg1 * F1));
+    }
+    if (rp.chain) {
+        rp.chist = A.reserve(sizeof(uint32_t) * (size_t)F1 * rp.nseg1 * F2);
+        rp.seglb = A.reserve(sizeof(uint32_t) * (size_t)rp.grid2);
+        rp.segle = A.reserve(sizeof(uint32_t) * (size_t)rp.grid2);
+        rp.segc0 = A.reserve(sizeof(uint32_t) * (size_t)rp.grid2);
     }
 }
 
@@ -422,7 +491,7 @@ int plan_join(Context *ctx, hipStream_t s, uint64_t nR, uint64_t nS, const mi355
         RHO_HIP(ctx->t2R.ensure(std::max<uint64_t>(nR, 1) * sizeof(row_t)));
         RHO_HIP(ctx->t2S.ensure(std::max<uint64_t>(nS, 1) * sizeof(row_t)));
     }
-    if (uses_digit_side(pol)) {
+    if (uses_digit_side(pol) && !(pj.pr.chain && pj.ps.chain)) {  // chain histograms need no side stream
         RHO_HIP(ctx->sideR.ensure(std::max<uint64_t>(c1R, 16)));
         RHO_HIP(ctx->sideS.ensure(std::max<uint64_t>(c1S, 16)));
     }
@@ -449,8 +518,9 @@ int plan_join(Context *ctx, hipStream_t s, uint64_t nR, uint64_t nS, const mi355
     pj.off_counts = A.reserve(sizeof(uint64_t) * (pj.materialize ? P + pj.over_cap : pj.join_grid));
     pj.off_toff = A.reserve(sizeof(uint64_t) * (pj.materialize ? P + pj.over_cap : 1));
     // result[0] = matches, [1] / [2] = largest R / S partition, [3] = extra S-chunk tasks
-    // (u32), [4] / [5] = build / probe ticks: one read-back for all six
-    pj.off_result = A.reserve(sizeof(uint64_t) * 6);
+    // (u32), [4] / [5] = build / probe ticks: one read-back for all six; [6] = the
+    // build/probe's task tickets (zeroed by launch_make_tasks with [1..5])
+    pj.off_result = A.reserve(sizeof(uint64_t) * 7);
     pj.off_cyc = A.reserve(sizeof(uint64_t) * 2 * pj.join_grid);
     RHO_HIP(A.buf.ensure(A.used));
     return MI355_OK;
@@ -507,7 +577,7 @@ void fill_join_stats(const Context *ctx, const PendingJoin &pj, const Timer &tm,
         st->passes = pol.passes;
         st->pass1_bits = pol.b1;
         st->pass2_bits = pol.b2;
-        st->layout = pj.pr.keys ? 2u : (pj.pr.pooled ? 1u : 0u);
+        st->layout = pj.pr.chain ? 3u : (pj.pr.keys ? 2u : (pj.pr.pooled ? 1u : 0u));
         st->elem_bytes = pj.pr.keys ? 4u : 8u;
         st->num_partitions = P;
         st->num_tasks = P + (uint32_t)ctx->host_result[3];
@@ -597,8 +667,8 @@ int join_finish(Context *ctx, PendingJoin &pj, const row_t *dS, uint64_t nS, mi3
     if (!pj.materialize) {
         tm.mark("join_build_probe");
         RHO_HIP(launch_join(fR, fS, psR, pcR, psS, pcS, P, over, n_over, hash_shift, pol.rcap, pj.s_chunk, join_grid,
-                            kJoinCount, algo, counts, nullptr, nullptr, cyc, s, nullptr,
-                            pj.pr.keys ? 1 : 2));
+                            kJoinCount, algo, counts, nullptr, nullptr, cyc, s, nullptr, pj.pr.keys ? 1 : 2,
+                            reinterpret_cast<uint32_t *>(result + 6)));
         tm.mark("join_reduce");
         RHO_HIP(launch_reduce(counts, join_grid, result, cyc, join_grid, s));
     } else {
@@ -632,6 +702,28 @@ int join_finish(Context *ctx, PendingJoin &pj, const row_t *dS, uint64_t nS, mi3
     if (s2) RHO_HIP(hipEventRecord(ctx->ev_t1, s));
     RHO_HIP(hipMemcpyAsync(ctx->host_result, result, 6 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     RHO_HIP(hipStreamSynchronize(s));
+    if (std::getenv("SGXAMD_DEBUG_WG_TICKS") && !pj.materialize) {
+        // development: the build/probe workgroups' wall-clock ticks (load balance)
+        const uint32_t ng = std::min<uint32_t>(join_grid, 4096);
+        std::vector<uint64_t> c(2 * (size_t)ng);
+        if (hipMemcpy(c.data(), cyc, c.size() * sizeof(uint64_t), hipMemcpyDeviceToHost) == hipSuccess) {
+            uint64_t mx = 0, sum = 0, n = 0, mb = 0, mp = 0;
+            for (uint32_t i = 0; i < ng; ++i) {
+                const uint64_t t = c[2 * i] + c[2 * i + 1];
+                if (!t) continue;
+                ++n;
+                sum += t;
+                if (t > mx) {
+                    mx = t;
+                    mb = c[2 * i];
+                    mp = c[2 * i + 1];
+                }
+            }
+            std::fprintf(stderr, "[wg ticks] wgs %llu mean %.0f max %llu (build %llu probe %llu) max/mean %.3f\n",
+                         (unsigned long long)n, n ? (double)sum / n : 0.0, (unsigned long long)mx,
+                         (unsigned long long)mb, (unsigned long long)mp, n && sum ? (double)mx * n / sum : 0.0);
+        }
+    }
     tm.collect();
     float wall = -1.f;
     if (s2) {
@@ -852,6 +944,84 @@ int shard_partition_device(Context *ctx, hipStream_t s, const row_t *in, uint64_
     RHO_HIP(hipStreamSynchronize(s));
     tm.collect();
     return MI355_OK;
+}
+
+// The pieces of a two-phase shard partition (shard_count_pieces / shard_scatter_piece).
+struct ShardPieces {
+    Policy pol{};
+    uint32_t key_shift = 0;
+    std::vector<RelPlan> rp;
+    std::vector<const row_t *> in;
+    uint64_t *host = nullptr;  // pinned: every piece's destination counts
+    size_t host_words = 0;
+};
+namespace {
+std::mutex g_shard_mu;
+std::unordered_map<const Context *, ShardPieces> g_shard;
+ShardPieces &shard_of(const Context *ctx) {
+    std::lock_guard<std::mutex> lk(g_shard_mu);
+    return g_shard[ctx];
+}
+}  // namespace
+
+int shard_count_pieces(Context *ctx, hipStream_t s, const row_t *const *in, const uint64_t *n, int npieces,
+                       uint32_t key_shift, uint32_t dest_bits, uint32_t out_elem, uint64_t *counts) {
+    if (pending_of(ctx).active) {
+        set_last_error("shard_count_pieces while a pipelined join is pending on this device");
+        return MI355_ERR_INVALID;
+    }
+    ShardPieces &sp = shard_of(ctx);
+    sp.pol = Policy{};
+    sp.pol.bits = sp.pol.b1 = dest_bits;
+    sp.pol.passes = 1;
+    sp.key_shift = key_shift;
+    Arena &A = ctx->scratch;
+    A.reset();
+    sp.rp.assign(npieces, RelPlan{});
+    sp.in.assign(in, in + npieces);
+    for (int j = 0; j < npieces; ++j) {
+        plan_relation(A, sp.rp[j], n[j], sp.pol);
+        sp.rp[j].keys = out_elem == 4;
+    }
+    RHO_HIP(A.buf.ensure(A.used));
+    const size_t F = 1u << dest_bits, words = F * (size_t)npieces;
+    if (sp.host_words < words) {
+        if (sp.host) (void)hipHostFree(sp.host);
+        sp.host = nullptr;
+        sp.host_words = 0;
+        RHO_HIP(hipHostMalloc(reinterpret_cast<void **>(&sp.host), words * sizeof(uint64_t)));
+        sp.host_words = words;
+    }
+    Timer &tm = thread_timer();
+    tm.begin_call(s, thread_timing_enabled());
+    for (int j = 0; j < npieces; ++j) {
+        if (!n[j]) continue;
+        const int rc = pass1_counts(ctx, s, tm, "shard_", in[j], sp.rp[j], sp.pol, key_shift);
+        if (rc) return rc;
+        RHO_HIP(hipMemcpyAsync(sp.host + (size_t)j * F, A.at<uint64_t>(sp.rp[j].cnt1), F * sizeof(uint64_t),
+                               hipMemcpyDeviceToHost, s));
+    }
+    tm.end_call();
+    RHO_HIP(hipStreamSynchronize(s));
+    tm.collect();
+    for (int j = 0; j < npieces; ++j)
+        for (size_t d = 0; d < F; ++d) counts[(size_t)j * F + d] = n[j] ? sp.host[(size_t)j * F + d] : 0;
+    return MI355_OK;
+}
+
+int shard_scatter_piece(Context *ctx, hipStream_t s, int j, void *out) {
+    ShardPieces &sp = shard_of(ctx);
+    if (j < 0 || j >= (int)sp.rp.size()) {
+        set_last_error("shard_scatter_piece: no such piece");
+        return MI355_ERR_INVALID;
+    }
+    if (!sp.rp[j].n) return MI355_OK;
+    Timer &tm = thread_timer();
+    tm.begin_call(s, false);
+    const int rc = pass1_scatter(ctx, s, tm, "shard_", sp.in[j], static_cast<row_t *>(out), nullptr, sp.rp[j], sp.pol,
+                                 sp.key_shift);
+    tm.end_call();
+    return rc;
 }
 
 }  // namespace rho

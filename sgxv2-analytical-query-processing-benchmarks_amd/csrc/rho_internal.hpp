@@ -20,6 +20,8 @@ constexpr int kTile = kScatterThreads * kScatterItems;  // tuples per scatter ti
 // Which contiguous slice of the input a partition workgroup owns.  Regions are
 // the bins of the previous pass (or the whole relation); each region is cut into
 // segments of seg_size tuples, one workgroup per segment.
+// seg_lb / seg_le (chain-aligned block-list segments, launch_chain_scan): segment g is
+// [seg_lb[g], seg_le[g]) of the list, for g < seg_base[nreg]; empty segments are holes.
 struct SegMap {
     const uint64_t *reg_start;  // nullptr => one region [0, single_n)
     const uint64_t *reg_count;
@@ -27,6 +29,8 @@ struct SegMap {
     uint32_t nreg;
     uint64_t seg_size;
     uint64_t single_n;
+    const uint32_t *seg_lb = nullptr;
+    const uint32_t *seg_le = nullptr;
 };
 
 // Histogram layout selector: digit-major [d][g] (single region: column scans)
@@ -110,17 +114,45 @@ struct PoolOut {
     uint32_t nseg;
 };
 // Pass 1 of a pooled plan: contiguous input segments (m), pooled output in out, digit
-// side stream ds (required) beside every stored element.  Elements: in_size-byte input
+// side stream ds beside every stored element.  Elements: in_size-byte input
 // (8: row_t, 4: keys), out_size-byte output (8: row_t; 4: the key words only — counting
 // joins, whose build/probe reads nothing but keys).
+// chain (chain histograms, keys only, chain_hist_supported): instead of the side stream,
+// every chain's (segment g, pass-1 digit d) histogram of pass-2 digits (ds.shift2,
+// ds.bits2), counted in LDS while the tile is in registers, u32 [d][g][F2] in chain.
 hipError_t launch_scatter_pool(const void *in, uint32_t in_size, void *out, uint32_t out_size, const SegMap &m,
                                uint32_t grid, uint32_t shift, uint32_t bits, const PoolOut &po, const DigitSide &ds,
-                               hipStream_t s);
+                               hipStream_t s, uint32_t *chain = nullptr);
+// Digit widths (pass 1, pass 2) with a chain-histogram pass 1.
+bool chain_hist_supported(uint32_t bits1, uint32_t bits2);
+// Whether pass 2 of key partitions is the LDS sort k_sort_blk (SGXAMD_SORT2).
+bool sort2_enabled();
+// Recount the chain histograms of chains with more than 65,535 elements (their u16 counts
+// may have wrapped) from their blocks: cnt / tot the column-scanned chain records and
+// their totals, keys the pass-1 output, shift2 the pass-2 digit's shift.
+hipError_t launch_chain_fix(const uint64_t *cnt, const uint64_t *tot, uint32_t nseg, uint32_t bits1, uint32_t bits2,
+                            const uint64_t *lbase, const uint64_t *list, const uint32_t *keys, uint32_t shift2,
+                            uint32_t *chain, hipStream_t s);
+// Chain-histogram plans: one workgroup per region from the column-scanned chain records
+// (po.cnt) and the chain histograms: the pass-2 segments, cut at chain boundaries (slot k
+// of region d holds the chains whose first block lies in [T*k, T*(k+1)) of d's list, T a
+// little below kPass2Ents (rho_kernels.hip chain_slot_target), so a segment is T blocks
+// + the rest of one chain; empty slots are holes), as list
+// ranges seg_lb / seg_le; the pass-2 cursors [slot][F2] (the histogram + scan of
+// launch_hist_side_blk + launch_scan_regions, without reading the elements) and the
+// partition table part_start / part_count [d][F2].  seg_c0: scratch, one u32 per slot.
+hipError_t launch_chain_scan(const uint64_t *cnt, uint32_t nseg, const uint32_t *chain, uint32_t bits1,
+                             uint32_t bits2, const uint64_t *region_start, const uint64_t *lbase,
+                             const uint64_t *lcount, const uint32_t *seg_base, uint64_t *cursors, uint32_t *seg_lb,
+                             uint32_t *seg_le, uint32_t *seg_c0, uint64_t *part_start, uint64_t *part_count,
+                             hipStream_t s);
 // After launch_scan_single-style column scans of po.cnt (k_scan_cols, in place): region
 // tuple starts / counts (the pass-2 output layout), region block-list bases / lengths
 // and the pass-2 segment table (kPass2Ents blocks per segment).
+// chain_slots: the slots of chain-aligned segments (launch_chain_scan) instead.
 hipError_t launch_pool_layout(uint64_t *cnt, uint32_t nseg, uint32_t bits, uint64_t *totals, uint64_t *start,
-                              uint64_t *count, uint64_t *lbase, uint64_t *lcount, uint32_t *seg_base, hipStream_t s);
+                              uint64_t *count, uint64_t *lbase, uint64_t *lcount, uint32_t *seg_base, hipStream_t s,
+                              bool chain_slots = false);
 // The block list: region d's blocks at [lbase[d], lbase[d] + lcount[d]) as
 // physical block | fill << 32.
 hipError_t launch_block_list(const PoolOut &po, const uint64_t *lbase, uint64_t *list, hipStream_t s);
@@ -167,7 +199,8 @@ enum JoinMode : int { kJoinCount = 0, kJoinTaskCount = 1, kJoinWrite = 2 };
 // Build/probe algorithm of one task: RHO's bucket chaining or RHT's histogram join.
 enum JoinAlgo : int { kAlgoChaining = 0, kAlgoHistogram = 1 };
 // meta (zeroed here): [0] = largest R partition, [1] = largest S partition,
-// [2] = the number of extra tasks (u32 n_over, read by launch_join / launch_excl_scan).
+// [2] = the number of extra tasks (u32 n_over, read by launch_join / launch_excl_scan),
+// [3..5] zero as well ([5]: launch_join's task tickets).
 hipError_t launch_make_tasks(const uint64_t *r_count, const uint64_t *s_count, uint64_t P, uint64_t *over,
                              uint32_t over_cap, uint64_t *meta, uint64_t s_chunk, hipStream_t s);
 // reduce (mode 0, nullable): the last workgroup to finish sums the partial counts and
@@ -180,9 +213,13 @@ hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, 
                        const uint64_t *s_start, const uint64_t *s_count, uint64_t P, const uint64_t *over,
                        const uint32_t *n_over, uint32_t hash_shift, uint32_t rcap, uint64_t s_chunk, uint32_t grid,
                        int mode, int algo, uint64_t *counts, const uint64_t *task_off, output_triple_t *out,
-                       uint64_t *cyc, hipStream_t s, const JoinReduce *reduce = nullptr, int key_stride = 2);
+                       uint64_t *cyc, hipStream_t s, const JoinReduce *reduce = nullptr, int key_stride = 2,
+                       uint32_t *tickets = nullptr);
 // key_stride 2: R / S are row_t partitions; 1: packed u32 keys (counting RHO only —
 // the partitions of a counting join carry keys only after the input read).
+// tickets (nullable; a u32 that is zero at the launch, e.g. meta[5] of launch_make_tasks):
+// the 16,384-key counting table takes its tasks by ticket (k_join_x, SGXAMD_JOIN_TICKETS
+// builds) instead of by grid stride.
 // One-block exclusive scan of n_base + *n_extra values; *total = their sum.
 hipError_t launch_excl_scan(const uint64_t *in, const uint32_t *n_extra, uint64_t n_base, uint64_t *out,
                             uint64_t *total, hipStream_t s);

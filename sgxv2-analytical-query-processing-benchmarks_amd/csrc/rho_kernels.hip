@@ -24,6 +24,13 @@ constexpr int kWaves = kBlock / kWave;
 // __syncthreads() (every thread of the block must call it).
 __device__ __forceinline__ bool seg_lookup(const SegMap &m, uint32_t g, uint32_t *lds_base, uint32_t &r,
                                            uint64_t &b, uint64_t &e) {
+    if (m.seg_lb != nullptr) {  // chain-aligned segments (launch_chain_scan): explicit ranges, holes empty
+        r = 0;
+        if (g >= m.seg_base[m.nreg]) return false;
+        b = m.seg_lb[g];
+        e = m.seg_le[g];
+        return b < e;
+    }
     if (m.reg_start == nullptr) {
         r = 0;
         b = (uint64_t)g * m.seg_size;
@@ -395,6 +402,186 @@ hipError_t launch_scan_regions(uint64_t *hist, const uint32_t *seg_base, const u
     return hipGetLastError();
 }
 
+// Chain-aligned pass-2 segments (chain histograms): slot k of a region holds the chains
+// whose first block lies in [T*k, T*(k+1)) of its list, so a segment is T blocks plus the
+// part of its last chain past the boundary.  T = kPass2Ents less two mean chains of the
+// region (at least half of kPass2Ents): k_sort_blk's 64-block tiles then stay at four
+// per segment, where T = kPass2Ents made 4.25 (a fifth, nearly empty tile: pass 2 5 %
+// slower, r04f).
+__host__ __device__ __forceinline__ uint32_t chain_slot_target(uint64_t blocks, uint32_t nseg) {
+#ifdef SGXAMD_CHAIN_T_FIXED
+    (void)blocks, (void)nseg;
+    return kPass2Ents;
+#else
+    const uint64_t mean = nseg ? (blocks + nseg - 1) / nseg : 0;
+    return kPass2Ents - (uint32_t)min<uint64_t>(kPass2Ents / 2, 2 * mean);
+#endif
+}
+
+// Chain-histogram plans (launch_chain_scan): one workgroup of 1,024 threads per region r
+// (pass-1 digit).  cnt: the chain records [r][g] after the column scan (exclusive
+// prefixes blocks << 40 | elements of the chains before g); chain: u32 [r][g][F2].
+constexpr uint32_t kChainLds = 4096;  // chain starts / slot chains staged in LDS (more: read in place)
+__global__ __launch_bounds__(1024) void k_chain_scan(const uint64_t *__restrict__ cnt, uint32_t nseg,
+                                                     const uint32_t *__restrict__ chain, uint32_t F2,
+                                                     const uint64_t *__restrict__ region_start,
+                                                     const uint64_t *__restrict__ lbase,
+                                                     const uint64_t *__restrict__ lcount,
+                                                     const uint32_t *__restrict__ seg_base,
+                                                     uint64_t *__restrict__ cursors, uint32_t *__restrict__ seg_lb,
+                                                     uint32_t *__restrict__ seg_le, uint32_t *__restrict__ seg_c0,
+                                                     uint64_t *__restrict__ part_start,
+                                                     uint64_t *__restrict__ part_count) {
+    __shared__ uint64_t scratch[1024 / kWave + 1];
+    __shared__ uint64_t part[1024];  // [j][d]: group j's column sums, then their exclusive prefix inside d
+    __shared__ uint64_t pst[1024];   // partition starts of the region (d < F2)
+    __shared__ uint32_t cst[kChainLds];  // chain g's first block inside the region's list
+    __shared__ uint32_t sc0[kChainLds];  // slot k's first chain
+    const uint32_t r = blockIdx.x, tid = threadIdx.x;
+    const uint64_t *rec = cnt + (uint64_t)r * nseg;
+    const uint32_t *ch = chain + (uint64_t)r * nseg * F2;
+    const uint32_t s0 = seg_base[r], ns = seg_base[r + 1] - s0;
+    const uint64_t B = lcount[r], lb0 = lbase[r];
+    const uint32_t T = chain_slot_target(B, nseg);
+    const bool lds_c = nseg <= kChainLds, lds_s = ns <= kChainLds;  // workgroup-uniform
+    if (lds_c)
+        for (uint32_t g = tid; g < nseg; g += 1024) cst[g] = (uint32_t)(rec[g] >> 40);
+    __syncthreads();
+    const auto start_of = [&](uint32_t g) -> uint32_t { return lds_c ? cst[g] : (uint32_t)(rec[g] >> 40); };
+    const auto first_at = [&](uint64_t x) -> uint32_t {  // first chain whose blocks start at or after x
+        uint32_t lo = 0, hi = nseg;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (start_of(mid) < x) lo = mid + 1; else hi = mid;
+        }
+        return lo;
+    };
+    for (uint32_t k = tid; k < ns; k += 1024) {
+        const uint32_t c0 = first_at((uint64_t)T * k), c1 = first_at((uint64_t)T * (k + 1));
+        seg_lb[s0 + k] = (uint32_t)(lb0 + (c0 < nseg ? start_of(c0) : B));
+        seg_le[s0 + k] = (uint32_t)(lb0 + (c1 < nseg ? start_of(c1) : B));
+        if (lds_s) sc0[k] = c0; else seg_c0[s0 + k] = c0;
+    }
+    // column sums of the chain histograms, nseg split among S = 1024 / F2 threads per digit
+    const uint32_t S = 1024 / F2, d = tid % F2, j = tid / F2;
+    const uint32_t per = (nseg + S - 1) / S, ga = min(nseg, j * per), gb = min(nseg, ga + per);
+    uint64_t sum = 0;
+#pragma unroll 8
+    for (uint32_t g = ga; g < gb; ++g) sum += ch[(uint64_t)g * F2 + d];
+    part[tid] = sum;
+    __syncthreads();
+    uint64_t total = 0;
+    if (j == 0)
+        for (uint32_t jj = 0; jj < S; ++jj) {
+            const uint64_t t = part[jj * F2 + d];
+            part[jj * F2 + d] = total;
+            total += t;
+        }
+    uint64_t tot;
+    const uint64_t ex = block_excl_scan_u64(j == 0 ? total : 0, scratch, &tot);  // digits are tids 0..F2-1
+    if (j == 0) {
+        const uint64_t st = region_start[r] + ex;
+        pst[d] = st;
+        part_start[(uint64_t)r * F2 + d] = st;
+        part_count[(uint64_t)r * F2 + d] = total;
+    }
+    __syncthreads();  // pst, part and the slot chains
+    // cursors: slot k starts at chain c0(k), so its cursor of digit d is the partition's
+    // start plus the counts of d in every chain before c0(k)
+    const auto c0_of = [&](uint32_t k) -> uint32_t { return lds_s ? sc0[k] : seg_c0[s0 + k]; };
+    uint64_t run = pst[d] + part[tid];
+    uint32_t lo = 0, hi = ns;  // first slot with c0 >= ga
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (c0_of(mid) < ga) lo = mid + 1; else hi = mid;
+    }
+    uint32_t k = lo;
+    for (uint32_t g = ga; g < gb; ++g) {
+        for (; k < ns && c0_of(k) == g; ++k) cursors[(uint64_t)(s0 + k) * F2 + d] = run;
+        run += ch[(uint64_t)g * F2 + d];
+    }
+}
+
+hipError_t launch_chain_scan(const uint64_t *cnt, uint32_t nseg, const uint32_t *chain, uint32_t bits1,
+                             uint32_t bits2, const uint64_t *region_start, const uint64_t *lbase,
+                             const uint64_t *lcount, const uint32_t *seg_base, uint64_t *cursors, uint32_t *seg_lb,
+                             uint32_t *seg_le, uint32_t *seg_c0, uint64_t *part_start, uint64_t *part_count,
+                             hipStream_t s) {
+    const uint32_t F2 = 1u << bits2;
+    if (F2 < 2 || F2 > 1024 || 1024 % F2) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_chain_scan, dim3(1u << bits1), dim3(1024), 0, s, cnt, nseg, chain, F2, region_start, lbase,
+                       lcount, seg_base, cursors, seg_lb, seg_le, seg_c0, part_start, part_count);
+    return hipGetLastError();
+}
+
+// Chains whose u16 chain-histogram counts may have wrapped (more than 65,535 elements;
+// the chain records say so): recounted from their blocks.  One workgroup per pass-1
+// segment g, its chains in turn (a uniform test per chain; nothing to do for any chain
+// of fewer elements, i.e. every chain of unskewed data).  Four waves, four blocks per
+// wave and step, a 16-byte piece of a block per lane.
+__global__ __launch_bounds__(256) void k_chain_fix(const uint64_t *__restrict__ cnt, const uint64_t *__restrict__ tot,
+                                                   uint32_t nseg, uint32_t F1, uint32_t F2,
+                                                   const uint64_t *__restrict__ lbase,
+                                                   const uint64_t *__restrict__ list, const uint32_t *__restrict__ keys,
+                                                   uint32_t shift2, uint32_t *__restrict__ chain) {
+    __shared__ uint32_t h[kMaxF];
+    __shared__ uint64_t rng[kMaxF][2];  // chain d's records: its own and the next (its end)
+    __shared__ uint32_t big[kMaxF / 32];
+    constexpr uint64_t M40 = (1ull << 40) - 1;
+    constexpr int U = 4;
+    const uint32_t g = blockIdx.x, tid = threadIdx.x, lane = __lane_id(), wave = tid / kWave;
+    // which chains of segment g need a recount: every record read at once
+    for (uint32_t d = tid; d < kMaxF / 32; d += 256) big[d] = 0;
+    __syncthreads();
+    for (uint32_t d = tid; d < F1; d += 256) {
+        const uint64_t e0 = cnt[(uint64_t)d * nseg + g];
+        const uint64_t e1 = g + 1 < nseg ? cnt[(uint64_t)d * nseg + g + 1] : tot[d];
+        rng[d][0] = e0;
+        rng[d][1] = e1;
+        if ((e1 & M40) - (e0 & M40) > 65535) atomicOr(&big[d / 32], 1u << (d % 32));
+    }
+    __syncthreads();
+    for (uint32_t d = 0; d < F1; ++d) {
+        if (!((big[d / 32] >> (d % 32)) & 1u)) continue;  // workgroup-uniform
+        const uint64_t e0 = rng[d][0], e1 = rng[d][1];
+        for (uint32_t i = tid; i < F2; i += 256) h[i] = 0;
+        __syncthreads();
+        const uint64_t k0 = lbase[d] + (e0 >> 40), k1 = lbase[d] + (e1 >> 40);
+        for (uint64_t k = k0 + wave; k < k1; k += 4 * U) {
+            uint4 q[U];
+            uint32_t fill[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint64_t kk = k + 4 * u;
+                const uint64_t en = kk < k1 ? list[kk] : 0ull;
+                fill[u] = (uint32_t)(en >> 32);
+                q[u] = lane * 4 < fill[u] ? *reinterpret_cast<const uint4 *>(keys + (uint64_t)(uint32_t)en * kBlk + lane * 4)
+                                          : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t w[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (lane * 4 + j < fill[u]) atomicAdd(&h[(w[j] >> shift2) & (F2 - 1)], 1u);
+            }
+        }
+        __syncthreads();
+        for (uint32_t i = tid; i < F2; i += 256) chain[((uint64_t)d * nseg + g) * F2 + i] = h[i];
+        __syncthreads();
+    }
+}
+
+hipError_t launch_chain_fix(const uint64_t *cnt, const uint64_t *tot, uint32_t nseg, uint32_t bits1, uint32_t bits2,
+                            const uint64_t *lbase, const uint64_t *list, const uint32_t *keys, uint32_t shift2,
+                            uint32_t *chain, hipStream_t s) {
+    if (nseg == 0) return hipSuccess;
+    if (bits2 > 9) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_chain_fix, dim3(nseg), dim3(256), 0, s, cnt, tot, nseg, 1u << bits1, 1u << bits2, lbase, list,
+                       keys, shift2, chain);
+    return hipGetLastError();
+}
+
 // --------------------------------------------------------------- scatter ---
 // Partition copy of one segment per workgroup (partition_copy, radix_join.cpp:659-697),
 // organised like the reference's software write-combining variant
@@ -454,6 +641,29 @@ struct ScatterLds {
     uint64_t ents[EXT == 2 ? kPass2Ents : 1];  // block-list input: phys block | fill << 32
     uint32_t pool_next;               // pooled: blocks taken from the segment's pool
 };
+
+// Chain histograms (pooled pass 1 of keys, F2 > 0): every chain's histogram of pass-2
+// digits, two u16 counts per LDS word, counted in phase C while the tile is in
+// registers (replacing the digit side stream and the pass-2 histogram pass over it),
+// stored as u32 [d][g][F2] at the segment's end.  A count wraps only in a chain of more
+// than 65,535 elements (a heavily skewed digit); launch_chain_fix recounts those chains
+// from their blocks (checking the chain records), so no flush sits in the scatter's
+// loop, which has no register to spare.
+struct ChainState {
+    uint32_t *h2;   // LDS [F][F2 / 2]
+    uint32_t *out;  // global [F][nseg][F2] (u32)
+    uint32_t g, nseg, shift2;
+};
+
+// The table out, after the segment's last tile (not inlined: its registers stay out of
+// the scatter's loop).
+template <int F, int F2, int NT>
+__device__ __noinline__ void chain_store(const uint32_t *h2, uint32_t *__restrict__ out, uint32_t g, uint32_t nseg) {
+    for (uint32_t i = threadIdx.x; i < F * F2 / 2; i += NT) {
+        const uint32_t d = i / (F2 / 2), j = i % (F2 / 2), w = h2[i];
+        *reinterpret_cast<uint2 *>(out + ((uint64_t)d * nseg + g) * F2 + 2 * j) = make_uint2(w & 0xFFFFu, w >> 16);
+    }
+}
 
 // Pooled output, per owner thread (digit): its chain's current block and length.
 struct PoolState {
@@ -534,11 +744,12 @@ __device__ __forceinline__ void block_scan2(uint32_t a, uint32_t b, uint32_t (&w
 // tn: valid tuples of the tile (items tid + k * NT < tn); with block-list input (EXT 2)
 // a bit mask instead, bit k = item k valid.  ps: the owner thread's chain (EXT 1).
 // FULL: every item is valid (no per-item checks; callers take it for full tiles).
-template <int BITS, int ITEMS, int NT, int EXT = 0, typename T = uint64_t, bool FULL = false>
+template <int BITS, int ITEMS, int NT, int EXT = 0, typename T = uint64_t, bool FULL = false, int F2 = 0>
 __device__ __forceinline__ uint32_t scatter_tile_sort(ScatterLds<BITS, ITEMS, NT, EXT, T> &L, uint64_t &pend,
                                                       uint32_t &carried, const T (&v)[ITEMS],
                                                       T *__restrict__ out, uint32_t tn, uint32_t shift,
-                                                      uint64_t tbase_global, PoolState *ps = nullptr) {
+                                                      uint64_t tbase_global, PoolState *ps = nullptr,
+                                                      ChainState *cs = nullptr) {
     constexpr uint32_t F = 1u << BITS, mask = F - 1, NW = NT / kWave;
     constexpr uint32_t G = ScatterLds<BITS, ITEMS, NT, EXT, T>::G, GPB = ScatterLds<BITS, ITEMS, NT, EXT, T>::GPB;
     const uint32_t tid = threadIdx.x;
@@ -551,7 +762,8 @@ __device__ __forceinline__ uint32_t scatter_tile_sort(ScatterLds<BITS, ITEMS, NT
 #endif
     (void)tbase_global;
     (void)ps;
-    // A. slot of every tuple inside its digit
+    (void)cs;
+    // A. slot of every tuple inside its digit (chain histograms: and its pass-2 digit's count)
     uint32_t slot[ITEMS];
 #pragma unroll
     for (int k = 0; k < ITEMS; ++k)
@@ -605,12 +817,17 @@ __device__ __forceinline__ uint32_t scatter_tile_sort(ScatterLds<BITS, ITEMS, NT
         carried = r;
     }
     __syncthreads();
-    // C. the tile, digit-sorted
+    // C. the tile, digit-sorted (chain histograms: each key's pass-2 digit counted here,
+    // where its rank's register is free again; in phase A the count spilled registers)
 #pragma unroll
     for (int k = 0; k < ITEMS; ++k) {
         if (valid(k)) {
             const uint32_t d = ((uint32_t)v[k] >> shift) & mask;
             L.tile[L.tbase[d] + slot[k]] = v[k];
+            if constexpr (F2 > 0) {
+                const uint32_t d2 = ((uint32_t)v[k] >> cs->shift2) & (uint32_t)(F2 - 1);
+                atomicAdd(&cs->h2[d * (F2 / 2) + (d2 >> 1)], 1u << ((d2 & 1u) * 16u));
+            }
         }
     }
     __syncthreads();
@@ -990,7 +1207,7 @@ __device__ __forceinline__ uint32_t load_tile_blk(const char *__restrict__ in,
 // EXT 1: contiguous segment g of `in` -> pooled output (po), digit side stream.
 // EXT 2: block-list segment g (list) -> `out` at the segment-major cursors cur_init.
 // T: the element written (tuple or key); IS: the input element size in bytes.
-template <int BITS, int ITEMS, int NT, int EXT, typename T, int IS>
+template <int BITS, int ITEMS, int NT, int EXT, typename T, int IS, int F2 = 0>
 __device__ __forceinline__ void scatter_segment_ext(ScatterLds<BITS, ITEMS, NT, EXT, T> &L, uint32_t g,
                                                     const char *__restrict__ in, T *__restrict__ out,
                                                     const SegMap &m, uint32_t shift,
@@ -998,11 +1215,13 @@ __device__ __forceinline__ void scatter_segment_ext(ScatterLds<BITS, ITEMS, NT, 
                                                     const uint64_t *__restrict__ list, const PoolOut &po,
                                                     uint8_t *__restrict__ side, uint32_t shift2, uint32_t mask2,
                                                     HistLayout layout = kSegMajor, uint32_t nseg_stride = 0,
-                                                    const uint64_t *__restrict__ digit_base = nullptr) {
+                                                    const uint64_t *__restrict__ digit_base = nullptr,
+                                                    ChainState *cs = nullptr) {
     using LdsT = ScatterLds<BITS, ITEMS, NT, EXT, T>;
     constexpr uint32_t TILE = NT * ITEMS, BPT = TILE / kBlk;
     constexpr uint32_t F = 1u << BITS, G = LdsT::G, GPB = LdsT::GPB, NG = NT / G, CS = G - 1;
-    constexpr bool SIDE = EXT == 1;
+    constexpr bool SIDE = EXT == 1 && F2 == 0;  // chain histograms replace the side stream
+    static_assert(F2 == 0 || (EXT == 1 && sizeof(T) == 4), "chain histograms: pooled keys");
     static_assert(F <= NT, "one owner thread per digit");
     static_assert(sizeof(T) <= IS, "elements are the input elements or their key words");
     uint32_t r;
@@ -1019,6 +1238,9 @@ __device__ __forceinline__ void scatter_segment_ext(ScatterLds<BITS, ITEMS, NT, 
         L.cnt[tid] = 0;
     }
     if (tid == 0) L.pool_next = 0;
+    if constexpr (F2 > 0) {
+        for (uint32_t i = tid; i < F * F2 / 2; i += NT) cs->h2[i] = 0;
+    }
     uint32_t nent = 0;
     if constexpr (EXT == 2) {
         nent = (uint32_t)(e - b);  // <= kPass2Ents (the plan's segment size)
@@ -1052,7 +1274,8 @@ __device__ __forceinline__ void scatter_segment_ext(ScatterLds<BITS, ITEMS, NT, 
     const auto sort = [&](T(&v)[ITEMS], uint32_t tn) -> uint32_t {
         if (EXT != 1 && is_full(tn))
             return scatter_tile_sort<BITS, ITEMS, NT, EXT, T, true>(L, pend, carried, v, out, tn, shift, 0, &ps);
-        return scatter_tile_sort<BITS, ITEMS, NT, EXT, T, false>(L, pend, carried, v, out, tn, shift, 0, &ps);
+        return scatter_tile_sort<BITS, ITEMS, NT, EXT, T, false, F2>(L, pend, carried, v, out, tn, shift, 0, &ps,
+                                                                     cs);
     };
     // the two-tiles-in-flight pipeline of scatter_segment
     T va[ITEMS], vb[ITEMS];
@@ -1107,15 +1330,24 @@ __device__ __forceinline__ void scatter_segment_ext(ScatterLds<BITS, ITEMS, NT, 
             if (SIDE) side[L.pend[d] + lane] = (uint8_t)(((uint32_t)x >> shift2) & mask2);
         }
     }
+    if constexpr (F2 > 0) chain_store<F, F2, NT>(cs->h2, cs->out, g, cs->nseg);
 }
 
-template <int BITS, int ITEMS, int NT, typename T, int IS>
+template <int BITS, int ITEMS, int NT, typename T, int IS, int F2 = 0>
 __global__ __launch_bounds__(NT, (scatter_waves_per_simd<BITS, ITEMS, NT, 1, T>())) void k_scatter_pool(
     const char *__restrict__ in, T *__restrict__ out, SegMap m, uint32_t shift, PoolOut po,
-    uint8_t *__restrict__ side, uint32_t shift2, uint32_t mask2) {
+    uint8_t *__restrict__ side, uint32_t shift2, uint32_t mask2, uint32_t *__restrict__ chain) {
     __shared__ ScatterLds<BITS, ITEMS, NT, 1, T> L;
-    scatter_segment_ext<BITS, ITEMS, NT, 1, T, IS>(L, xcd_contiguous(blockIdx.x, gridDim.x), in, out, m, shift,
-                                                   nullptr, nullptr, po, side, shift2, mask2);
+    const uint32_t g = xcd_contiguous(blockIdx.x, gridDim.x);
+    if constexpr (F2 > 0) {
+        __shared__ uint32_t h2[(1u << BITS) * F2 / 2];
+        ChainState cs{h2, chain, g, po.nseg, shift2};
+        scatter_segment_ext<BITS, ITEMS, NT, 1, T, IS, F2>(L, g, in, out, m, shift, nullptr, nullptr, po, side, shift2,
+                                                           mask2, kSegMajor, 0, nullptr, &cs);
+    } else {
+        scatter_segment_ext<BITS, ITEMS, NT, 1, T, IS>(L, g, in, out, m, shift, nullptr, nullptr, po, side, shift2,
+                                                       mask2);
+    }
 }
 
 // The one-pass scatter with cursors (k_scatter) writing the key words of the tuples.
@@ -1153,6 +1385,10 @@ __global__ __launch_bounds__(NT, (scatter_waves_per_simd<BITS, ITEMS, NT, 2, T>(
 // same workgroup moments later (in its XCD's L2); only the runs' ends at segment
 // boundaries are written as partial lines by two workgroups.  The next tile's keys
 // load while a tile is sorted and written (two register sets).
+// List entries staged in LDS: a fixed-size segment (kPass2Ents) or a chain-aligned one
+// (launch_chain_scan: up to kPass2Ents blocks + one chain); longer segments (one chain
+// of a heavily skewed digit) read their entries from the list itself.
+constexpr uint32_t kSortEnts = 1024;
 template <int BITS, int NT, int ITEMS>
 struct SortBlkLds {
     static constexpr uint32_t F = 1u << BITS, TILE = NT * ITEMS;
@@ -1160,7 +1396,7 @@ struct SortBlkLds {
         uint32_t sbase[kMaxF + 1];  // segment table (seg_lookup, before the first tile)
         uint32_t sorted[TILE];      // the tile's keys, digit-sorted
     };
-    uint64_t ents[kPass2Ents];  // the segment's block list: physical block | fill << 32
+    uint64_t ents[kSortEnts];   // the segment's block list: physical block | fill << 32
     uint64_t dbase[F];          // next output position of digit d in this segment
     uint64_t off[F];            // destination of sorted position q with digit d: off[d] + q
     uint32_t cnt[F];            // tile histogram (phase A), zero between tiles
@@ -1202,8 +1438,10 @@ __global__ __launch_bounds__(NT, NT * SGXAMD_SORT_WGS / 256) void k_sort_blk(con
     uint32_t r;
     uint64_t b, e;
     if (!seg_lookup(m, g, L.sbase, r, b, e)) return;
-    const uint32_t nent = (uint32_t)(e - b);  // <= kPass2Ents (the plan's segment size)
-    for (uint32_t i = tid; i < nent; i += NT) L.ents[i] = list[b + i];
+    const uint32_t nent = (uint32_t)(e - b);
+    const bool big = nent > kSortEnts;  // workgroup-uniform
+    if (!big)
+        for (uint32_t i = tid; i < nent; i += NT) L.ents[i] = list[b + i];
     if (tid < F) {
         L.dbase[tid] = cursors[(uint64_t)g * F + tid];
         L.cnt[tid] = 0;
@@ -1220,7 +1458,8 @@ __global__ __launch_bounds__(NT, NT * SGXAMD_SORT_WGS / 256) void k_sort_blk(con
 #pragma unroll
         for (int u = 0; u < (int)ITEMS; ++u) {
             const uint32_t idx = ti * BPT + (uint32_t)u * (NT / kBlk) + h;
-            const uint64_t en = idx < nent ? L.ents[idx] : 0ull;  // one address per wave: a broadcast
+            // one address per wave: a broadcast
+            const uint64_t en = idx < nent ? (big ? list[b + idx] : L.ents[idx]) : 0ull;
             const uint32_t phys = __builtin_amdgcn_readfirstlane((uint32_t)en);
             const uint32_t fill = __builtin_amdgcn_readfirstlane((uint32_t)(en >> 32));
             const __amdgpu_buffer_rsrc_t rs = make_rsrc(in + (uint64_t)phys * kBlk, fill * 4u);
@@ -1309,16 +1548,31 @@ constexpr int items_of() {
 
 template <typename T, int IS>
 hipError_t launch_scatter_pool_t(const void *in, void *out, const SegMap &m, uint32_t grid, uint32_t shift,
-                                 uint32_t bits, const PoolOut &po, const DigitSide &ds, hipStream_t s) {
+                                 uint32_t bits, const PoolOut &po, const DigitSide &ds, hipStream_t s,
+                                 uint32_t *chain) {
     constexpr int ITEMS = items_of<T, 1>(), NT = kScatterThreads;
     const char *ib = static_cast<const char *>(in);
     T *o = static_cast<T *>(out);
     const uint32_t mask2 = (1u << ds.bits2) - 1u;
+    if (chain) {  // chain histograms (keys, chain_hist_supported): 7-bit pass 1, 6- or 7-bit pass 2
+        if constexpr (sizeof(T) == 4) {
+            if (bits == 7 && ds.bits2 == 7)
+                hipLaunchKernelGGL((k_scatter_pool<7, ITEMS, NT, T, IS, 128>), dim3(grid), dim3(NT), 0, s, ib, o, m,
+                                   shift, po, nullptr, ds.shift2, mask2, chain);
+            else if (bits == 7 && ds.bits2 == 6)
+                hipLaunchKernelGGL((k_scatter_pool<7, ITEMS, NT, T, IS, 64>), dim3(grid), dim3(NT), 0, s, ib, o, m,
+                                   shift, po, nullptr, ds.shift2, mask2, chain);
+            else
+                return hipErrorInvalidValue;
+            return hipGetLastError();
+        }
+        return hipErrorInvalidValue;
+    }
 #define POOL_CASE(B)                                                                                             \
     case B:                                                                                                      \
         if constexpr (sizeof(ScatterLds<B, ITEMS, NT, 1, T>) <= 160 * 1024 && (1 << B) <= NT) {                   \
             hipLaunchKernelGGL((k_scatter_pool<B, ITEMS, NT, T, IS>), dim3(grid), dim3(NT), 0, s, ib, o, m, shift, \
-                               po, ds.side, ds.shift2, mask2);                                                   \
+                               po, ds.side, ds.shift2, mask2, nullptr);                                          \
             break;                                                                                               \
         } else {                                                                                                 \
             return hipErrorInvalidValue;                                                                         \
@@ -1342,13 +1596,18 @@ hipError_t launch_scatter_pool_t(const void *in, void *out, const SegMap &m, uin
 
 hipError_t launch_scatter_pool(const void *in, uint32_t in_size, void *out, uint32_t out_size, const SegMap &m,
                                uint32_t grid, uint32_t shift, uint32_t bits, const PoolOut &po, const DigitSide &ds,
-                               hipStream_t s) {
+                               hipStream_t s, uint32_t *chain) {
     if (grid == 0) return hipSuccess;
-    if (in_size == 8 && out_size == 8) return launch_scatter_pool_t<uint64_t, 8>(in, out, m, grid, shift, bits, po, ds, s);
-    if (in_size == 8 && out_size == 4) return launch_scatter_pool_t<uint32_t, 8>(in, out, m, grid, shift, bits, po, ds, s);
-    if (in_size == 4 && out_size == 4) return launch_scatter_pool_t<uint32_t, 4>(in, out, m, grid, shift, bits, po, ds, s);
+    if (in_size == 8 && out_size == 8 && !chain)
+        return launch_scatter_pool_t<uint64_t, 8>(in, out, m, grid, shift, bits, po, ds, s, nullptr);
+    if (in_size == 8 && out_size == 4)
+        return launch_scatter_pool_t<uint32_t, 8>(in, out, m, grid, shift, bits, po, ds, s, chain);
+    if (in_size == 4 && out_size == 4)
+        return launch_scatter_pool_t<uint32_t, 4>(in, out, m, grid, shift, bits, po, ds, s, chain);
     return hipErrorInvalidValue;
 }
+
+bool chain_hist_supported(uint32_t bits1, uint32_t bits2) { return bits1 == 7 && (bits2 == 6 || bits2 == 7); }
 
 // SGXAMD_SORT2 (development A/B switch, read once): 1 (default) = key partitions' pass 2
 // as the LDS counting sort k_sort_blk; 0 = the write-combining k_scatter_blk.
@@ -1455,7 +1714,7 @@ hipError_t launch_scatter_blk(const void *in, const uint64_t *list, void *out, u
 __global__ __launch_bounds__(1024) void k_pool_layout(const uint64_t *__restrict__ totals, uint32_t F,
                                                       uint64_t *__restrict__ start, uint64_t *__restrict__ count,
                                                       uint64_t *__restrict__ lbase, uint64_t *__restrict__ lcount,
-                                                      uint32_t *__restrict__ seg_base) {
+                                                      uint32_t *__restrict__ seg_base, uint32_t chain_nseg) {
     __shared__ uint64_t scratch[1024 / kWave + 1];
     const uint32_t d = threadIdx.x;
     const uint64_t v = d < F ? totals[d] : 0;
@@ -1463,7 +1722,9 @@ __global__ __launch_bounds__(1024) void k_pool_layout(const uint64_t *__restrict
     uint64_t tot;
     const uint64_t ex_t = block_excl_scan_u64(tup, scratch, &tot);
     const uint64_t ex_b = block_excl_scan_u64(blk, scratch, &tot);
-    const uint64_t ns = (blk + kPass2Ents - 1) / kPass2Ents;
+    // chain-aligned slots (chain_nseg > 0: launch_chain_scan) or kPass2Ents-block segments
+    const uint32_t T = chain_nseg ? chain_slot_target(blk, chain_nseg) : kPass2Ents;
+    const uint64_t ns = (blk + T - 1) / T;
     const uint64_t ex_s = block_excl_scan_u64(ns, scratch, &tot);
     if (d < F) {
         start[d] = ex_t;
@@ -1476,13 +1737,15 @@ __global__ __launch_bounds__(1024) void k_pool_layout(const uint64_t *__restrict
 }
 
 hipError_t launch_pool_layout(uint64_t *cnt, uint32_t nseg, uint32_t bits, uint64_t *totals, uint64_t *start,
-                              uint64_t *count, uint64_t *lbase, uint64_t *lcount, uint32_t *seg_base, hipStream_t s) {
+                              uint64_t *count, uint64_t *lbase, uint64_t *lcount, uint32_t *seg_base, hipStream_t s,
+                              bool chain_slots) {
     const uint32_t F = 1u << bits;
     hipLaunchKernelGGL(k_scan_cols, dim3(F), dim3(kBlock), 0, s, cnt, nseg, totals);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const uint32_t threads = F < 64 ? 64 : F;
-    hipLaunchKernelGGL(k_pool_layout, dim3(1), dim3(threads), 0, s, totals, F, start, count, lbase, lcount, seg_base);
+    hipLaunchKernelGGL(k_pool_layout, dim3(1), dim3(threads), 0, s, totals, F, start, count, lbase, lcount, seg_base,
+                       chain_slots ? nseg : 0u);
     return hipGetLastError();
 }
 
@@ -1942,6 +2205,7 @@ struct JoinLdsX {
     uint32_t head[RCAP];
     uint32_t link[RCAP + 1];  // 1-based: link[0] = 0, the end of every chain, is never written
     uint64_t red[NW + 2];
+    uint32_t nxt[3];  // task tickets (SGXAMD_JOIN_TICKETS): successors of tasks j (nxt[j & 1]), a skip
 };
 
 __device__ __forceinline__ uint32_t key_tag16(uint32_t k, uint32_t tshift) {
@@ -1954,6 +2218,7 @@ __device__ __forceinline__ uint32_t key_tag16(uint32_t k, uint32_t tshift) {
 struct XCursor {
     uint64_t t, nR, nS, rc, off, r_base, s_base;
     uint32_t phase;
+    uint32_t j;  // the workgroup's task ordinal (task tickets)
 };
 
 // A uniform value kept in SGPRs.  readfirstlane returns int: each half goes through
@@ -1965,9 +2230,21 @@ __device__ __forceinline__ uint64_t uni_u64(uint64_t v) {
     return ((uint64_t)hi << 32) | lo;
 }
 
+// Task order: grid stride, or (SGXAMD_JOIN_TICKETS, tick != null) task tickets: a
+// workgroup's first task is blockIdx.x, each later one the next value of a device
+// counter (+ gridDim.x), so that workgroups take tasks as they finish (Zipf: a few
+// partitions hold 33x the mean S, and a static stride leaves some workgroups with far
+// more than others).  The ticket for task j's successor is taken by thread 0 when the
+// cursor enters task j and lands in LDS (nxt[j & 1]) before task j's first build strip,
+// whose barriers publish it; the cursor reads it when it leaves task j.
+#ifndef SGXAMD_JOIN_TICKETS
+#define SGXAMD_JOIN_TICKETS 0
+#endif
 struct XTasks {
     const uint64_t *r_start, *r_count, *s_start, *s_count, *over;
     uint64_t P, T, s_chunk;
+    uint32_t *tick;  // null: grid stride
+    uint32_t *nxt;   // LDS: JoinLdsX::nxt
 };
 
 template <int RCAP>
@@ -1976,11 +2253,19 @@ __device__ __forceinline__ uint32_t x_nrc(const XCursor &c) {
     return d < (uint64_t)RCAP ? (uint32_t)d : (uint32_t)RCAP;
 }
 
-// the first task at or after c.t with work (c.t >= T: none)
-__device__ __forceinline__ void x_seek(XCursor &c, const XTasks &k) {
-    for (; c.t < k.T; c.t += gridDim.x) {
+// the first task at or after c.t with work (c.t >= T: none); with tickets, tkv (thread
+// 0) receives the ticket of its successor
+__device__ __forceinline__ void x_seek(XCursor &c, const XTasks &k, uint32_t &tkv) {
+    for (; c.t < k.T;) {
         uint64_t p, chunk;
-        decode_task(uni_u64(c.t), k.P, k.over, p, chunk);
+        // tickets take the further S chunks of the large partitions first (position
+        // c.t < n_over: over[c.t]), then the partitions: the largest tasks start first
+        // instead of finishing last
+        uint64_t t = uni_u64(c.t);
+#if SGXAMD_JOIN_TICKETS
+        if (k.tick != nullptr) t = t < k.T - k.P ? k.P + t : t - (k.T - k.P);
+#endif
+        decode_task(t, k.P, k.over, p, chunk);
         p = uni_u64(p);
         chunk = uni_u64(chunk);
         const uint64_t nR = uni_u64(k.r_count[p]), nSp = uni_u64(k.s_count[p]);
@@ -1995,13 +2280,26 @@ __device__ __forceinline__ void x_seek(XCursor &c, const XTasks &k) {
             c.phase = 0;
             c.r_base = uni_u64(k.r_start[p]);
             c.s_base = uni_u64(k.s_start[p]) + s_lo;
+#if SGXAMD_JOIN_TICKETS
+            if (k.tick != nullptr && threadIdx.x == 0) tkv = atomicAdd(k.tick, 1u);
+#endif
             return;
         }
+#if SGXAMD_JOIN_TICKETS
+        if (k.tick != nullptr) {  // a task without work (no R or no S tuples): the next ticket now
+            __syncthreads();
+            if (threadIdx.x == 0) k.nxt[2] = atomicAdd(k.tick, 1u) + gridDim.x;
+            __syncthreads();
+            c.t = (uint32_t)__builtin_amdgcn_readfirstlane(k.nxt[2]);
+            continue;
+        }
+#endif
+        c.t += gridDim.x;
     }
 }
 
 template <int RCAP, uint32_t STRIP>
-__device__ __forceinline__ void x_advance(XCursor &c, const XTasks &k) {
+__device__ __forceinline__ void x_advance(XCursor &c, const XTasks &k, uint32_t &tkv) {
     c.off += STRIP;
     if (c.phase == 0) {
         if (c.off >= x_nrc<RCAP>(c)) {
@@ -2013,8 +2311,13 @@ __device__ __forceinline__ void x_advance(XCursor &c, const XTasks &k) {
         c.off = 0;
         c.phase = 0;
         if (c.rc >= c.nR) {
+#if SGXAMD_JOIN_TICKETS
+            c.t = k.tick != nullptr ? (uint32_t)__builtin_amdgcn_readfirstlane(k.nxt[c.j & 1]) : c.t + gridDim.x;
+#else
             c.t += gridDim.x;
-            x_seek(c, k);
+#endif
+            ++c.j;
+            x_seek(c, k, tkv);
         }
     }
 }
@@ -2138,19 +2441,31 @@ __global__ __launch_bounds__(BLOCK, 1) void k_join_x(
     const uint64_t *__restrict__ r_count, const uint64_t *__restrict__ s_start, const uint64_t *__restrict__ s_count,
     uint64_t P, const uint64_t *__restrict__ over, const uint32_t *__restrict__ n_over, uint32_t hash_shift,
     uint64_t s_chunk, uint64_t *__restrict__ counts, uint64_t *__restrict__ cyc, uint64_t *__restrict__ red_result,
-    uint64_t *__restrict__ red_ticket, uint32_t ncounts) {
+    uint64_t *__restrict__ red_ticket, uint32_t ncounts, uint32_t *__restrict__ tickets) {
     constexpr int NW = BLOCK / kWave;
     constexpr uint32_t STRIP = BLOCK * UP;
     __shared__ JoinLdsX<RCAP, NW> L;
     const uint32_t tid = threadIdx.x, lane = __lane_id();
-    const XTasks tk{r_start, r_count, s_start, s_count, over, P, uni_u64(P + *n_over), s_chunk};
+    const XTasks tk{r_start, r_count, s_start, s_count, over, P, uni_u64(P + *n_over), s_chunk, tickets, L.nxt};
     const uint32_t *rkeys = reinterpret_cast<const uint32_t *>(R);
     const uint32_t *skeys = reinterpret_cast<const uint32_t *>(S);
     uint64_t matches = 0, bcyc = 0, pcyc = 0;
     if (tid == 0) L.link[0] = 0;  // visible after the first build strip's barriers
+    uint32_t tkv = 0;  // thread 0: the ticket of the current task's successor (in flight)
+    // before the first build strip of a task: its successor's ticket into LDS (the
+    // strip's barriers publish it; the ticket was taken a strip earlier, and the wait
+    // for this strip's keys, issued after it, has already covered it)
+    const auto publish = [&](const XCursor &c) {
+#if SGXAMD_JOIN_TICKETS
+        if (tk.tick != nullptr && tid == 0 && c.t < tk.T && c.phase == 0 && c.rc == 0 && c.off == 0)
+            L.nxt[c.j & 1] = tkv + gridDim.x;
+#else
+        (void)c;
+#endif
+    };
 
-    XCursor ca{(uint64_t)blockIdx.x, 0, 0, 0, 0, 0, 0, 0}, cb{};
-    x_seek(ca, tk);
+    XCursor ca{(uint64_t)blockIdx.x, 0, 0, 0, 0, 0, 0, 0, 0}, cb{};
+    x_seek(ca, tk, tkv);
     uint32_t ka[UP], kb[UP];
     x_load<RCAP, BLOCK, UP, KS>(ca, tk, rkeys, skeys, ka);
     // two register sets, the loop unrolled by two so that no set is ever copied (a copy
@@ -2159,20 +2474,22 @@ __global__ __launch_bounds__(BLOCK, 1) void k_join_x(
     // compiler's wait count is exactly UP
     while (ca.t < tk.T) {
         cb = ca;
-        x_advance<RCAP, STRIP>(cb, tk);
+        x_advance<RCAP, STRIP>(cb, tk, tkv);
         x_load<RCAP, BLOCK, UP, KS>(cb, tk, rkeys, skeys, kb);
 #pragma unroll
         for (int u = 0; u < UP; ++u) asm volatile("" ::"v"(ka[u]));
+        publish(ca);
         uint64_t dt;
         matches += x_step<RCAP, BLOCK, UP, KS>(L, ca, cb, ka, rkeys, hash_shift, dt);
         bcyc += ca.phase == 0 ? dt : 0;
         pcyc += ca.phase == 0 ? 0 : dt;
         if (cb.t >= tk.T) break;
         ca = cb;
-        x_advance<RCAP, STRIP>(ca, tk);
+        x_advance<RCAP, STRIP>(ca, tk, tkv);
         x_load<RCAP, BLOCK, UP, KS>(ca, tk, rkeys, skeys, ka);
 #pragma unroll
         for (int u = 0; u < UP; ++u) asm volatile("" ::"v"(kb[u]));
+        publish(cb);
         matches += x_step<RCAP, BLOCK, UP, KS>(L, cb, ca, kb, rkeys, hash_shift, dt);
         bcyc += cb.phase == 0 ? dt : 0;
         pcyc += cb.phase == 0 ? 0 : dt;
@@ -2582,7 +2899,7 @@ hipError_t launch_join_keys(const void *R, const void *S, const uint64_t *r_star
                             const uint64_t *s_start, const uint64_t *s_count, uint64_t P, const uint64_t *over,
                             const uint32_t *n_over, uint32_t hash_shift, uint32_t rcap, uint64_t s_chunk,
                             uint32_t grid, int mode, int algo, uint64_t *counts, uint64_t *cyc, hipStream_t s,
-                            const JoinReduce *reduce) {
+                            const JoinReduce *reduce, uint32_t *tickets) {
     if (mode != kJoinCount) return hipErrorInvalidValue;
     const uint64_t *R64 = static_cast<const uint64_t *>(R);
     const uint64_t *S64 = static_cast<const uint64_t *>(S);
@@ -2613,7 +2930,7 @@ hipError_t launch_join_keys(const void *R, const void *S, const uint64_t *r_star
     if (rcap == kBigRcap) {  // one workgroup per CU (128 KiB table), strips of 8 keys per thread
         hipLaunchKernelGGL((k_join_x<kBigRcap, 1024, 8, 1>), dim3(std::min<uint32_t>(grid, cu_count())), dim3(1024), 0,
                            s, R64, S64, r_start, r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts,
-                           cyc, rres, rtick, grid);
+                           cyc, rres, rtick, grid, tickets);
         return hipGetLastError();
     }
 #define KEYS_CASE(RC)                                                                                                   case RC:                                                                                                                hipLaunchKernelGGL((k_join<RC, kJoinCount, kBlock, 1>), dim3(grid), dim3(kBlock), 0, s, R64, S64, r_start,                            r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts, nullptr, nullptr,                             cyc, rres, rtick);                                                                               break;
@@ -2632,9 +2949,9 @@ hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, 
                        const uint64_t *s_start, const uint64_t *s_count, uint64_t P, const uint64_t *over,
                        const uint32_t *n_over, uint32_t hash_shift, uint32_t rcap, uint64_t s_chunk, uint32_t grid,
                        int mode, int algo, uint64_t *counts, const uint64_t *task_off, output_triple_t *out,
-                       uint64_t *cyc, hipStream_t s, const JoinReduce *reduce, int key_stride) {
+                       uint64_t *cyc, hipStream_t s, const JoinReduce *reduce, int key_stride, uint32_t *tickets) {
     if (key_stride == 1) return launch_join_keys(R, S, r_start, r_count, s_start, s_count, P, over, n_over, hash_shift,
-                                                 rcap, s_chunk, grid, mode, algo, counts, cyc, s, reduce);
+                                                 rcap, s_chunk, grid, mode, algo, counts, cyc, s, reduce, tickets);
     const uint64_t *R64 = reinterpret_cast<const uint64_t *>(R);
     const uint64_t *S64 = reinterpret_cast<const uint64_t *>(S);
     uint64_t *rres = (reduce && mode == kJoinCount) ? reduce->result : nullptr;
@@ -2667,7 +2984,7 @@ hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, 
         if (mode != kJoinCount) return hipErrorInvalidValue;
         hipLaunchKernelGGL((k_join_x<kBigRcap, 1024, 8, 2>), dim3(std::min<uint32_t>(grid, cu_count())), dim3(1024), 0,
                            s, R64, S64, r_start, r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts,
-                           cyc, rres, rtick, grid);
+                           cyc, rres, rtick, grid, tickets);
     } else if (mode == kJoinCount && grid <= 512 && rcap <= 4096) {
         // few tasks (small joins: one workgroup per CU at most): 1,024 threads per table
         // instead of 256, so that a CU holds 16 waves to hide the load latencies
@@ -2738,7 +3055,7 @@ __global__ __launch_bounds__(kBlock) void k_make_tasks(const uint64_t *__restric
 
 hipError_t launch_make_tasks(const uint64_t *r_count, const uint64_t *s_count, uint64_t P, uint64_t *over,
                              uint32_t over_cap, uint64_t *meta, uint64_t s_chunk, hipStream_t s) {
-    hipError_t e = hipMemsetAsync(meta, 0, 3 * sizeof(uint64_t), s);
+    hipError_t e = hipMemsetAsync(meta, 0, 6 * sizeof(uint64_t), s);
     if (e != hipSuccess) return e;
     uint32_t *n_over = reinterpret_cast<uint32_t *>(meta + 2);
     uint64_t blocks = (P + kBlock - 1) / kBlock;

@@ -143,6 +143,7 @@ class multi_stats(C.Structure):  # sgxamd/multi.h
         ("ms_allreduce", C.c_double),
         ("local", rho_stats),
         ("elem_bytes", C.c_uint32),
+        ("ms_tail", C.c_double),
     ]
 
     def as_dict(self) -> dict:

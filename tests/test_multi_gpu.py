@@ -77,7 +77,7 @@ def test_keys_only_exchange(sgx, orc, gpu, g, n, kw):
     res = multi(sgx, R, S, g, **kw)
     assert res.matches == exp
     st = res.stats
-    assert st["elem_bytes"] == 4 and st["local"]["layout"] == 2
+    assert st["elem_bytes"] == 4 and st["local"]["layout"] in (2, 3)
     # every key of a rank except those it keeps goes out once, 4 bytes each
     assert 4 * (2 * n) * (g - 1) // g * 0.9 < st["sent_bytes"] <= 4 * 2 * n
     # RHT counts over key partitions too (SGXAMD_KEYS=0 in test_paths_gpu keeps tuples)
@@ -218,7 +218,7 @@ def test_config4_rehearsal_full_size(sgx, gpu):
         res = sgx.rho_join_multi(R, nR, S, nS, g, transport="rehearsal")
         st = res.stats
         assert res.matches == nS
-        assert st["world"] == g and st["elem_bytes"] == 4 and st["local"]["layout"] == 2
+        assert st["world"] == g and st["elem_bytes"] == 4 and st["local"]["layout"] in (2, 3)
         assert st["recv_r_max"] == st["recv_r_min"] == nR // g
         assert st["recv_s_max"] == st["recv_s_min"] == nS // g
         sent = _slices_sent(R & 0xFFFFFFFF, g, 4) + _slices_sent(S & 0xFFFFFFFF, g, 4)

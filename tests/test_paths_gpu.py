@@ -9,7 +9,8 @@ with a pass-1 histogram and cursors instead of the pooled pass 1 and block-list 
 SGXAMD_POOL_SEGS sets the pooled pass-1 workgroups: 3 gives large pools, 100000 one
 tile per segment), SGXAMD_KEYS=0 (counting joins move whole tuples instead of keys),
 SGXAMD_SORT2=0 (pass 2 of key partitions with the write-combining scatter instead of
-the LDS counting sort).  The switches are read
+the LDS counting sort), SGXAMD_CHAIN_HIST=0 (the digit side stream and its histogram pass
+instead of the chain histograms counted in pass 1).  The switches are read
 once per process, so each setting runs in a child process against the oracle (the
 TPC-H selections ride along: they share the library's workspace)."""
 import os
@@ -28,7 +29,7 @@ import numpy as np
 import sgxamd, oracle
 R, S = sgxamd.reference_relations(1 << 20, 1 << 20, selectivity=50)
 exp, _ = oracle.rho_join(R, S, 2)
-for bits, passes in [(12, 2), (16, 2), (18, 2), (5, 1)]:
+for bits, passes in [(12, 2), (13, 2), (14, 2), (16, 2), (18, 2), (5, 1)]:
     got = sgxamd.rho_join(R, len(R), S, len(S), radix_bits=bits, passes=passes).matches
     assert got == exp, (bits, passes, got, exp)
 rng = np.random.default_rng(5)
@@ -77,10 +78,44 @@ print("paths ok")
                                  {"SGXAMD_DIGIT_SIDE": "1", "SGXAMD_BIG_JOIN": "1"},
                                  {"SGXAMD_SMALL_JOIN": "0"},
                                  {"SGXAMD_POOL": "0"}, {"SGXAMD_POOL_SEGS": "3"}, {"SGXAMD_POOL_SEGS": "100000"},
-                                 {"SGXAMD_KEYS": "0"}, {"SGXAMD_SORT2": "0"}])
+                                 {"SGXAMD_KEYS": "0"}, {"SGXAMD_SORT2": "0"}, {"SGXAMD_CHAIN_HIST": "0"}])
 def test_switch_paths_match_oracle(env):
     e = dict(os.environ, **env)
     e["PYTHONPATH"] = os.pathsep.join([os.path.join(PKG, "python"), os.path.join(ROOT, "oracle"),
                                        e.get("PYTHONPATH", "")])
     r = subprocess.run([sys.executable, "-c", CHILD], env=e, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and "paths ok" in r.stdout, (env, r.stdout[-2000:], r.stderr[-2000:])
+
+
+# Chain histograms under skew (rho_kernels.hip launch_chain_fix / k_sort_blk's list path):
+# every S key has the same pass-1 digit, so with 8 pass-1 workgroups each chain holds
+# 2^19 keys (u16 counts wrap: the chain is recounted from its blocks) and a pass-2
+# segment is one chain of 2,048 blocks (more than the LDS copy of the list holds).
+CHAIN_CHILD = r"""
+import numpy as np
+import sgxamd, oracle
+dt = np.dtype([("key", "<u4"), ("payload", "<u4")])
+rng = np.random.default_rng(3)
+R = np.zeros(1 << 20, dtype=dt); R["key"] = rng.permutation(1 << 20).astype(np.uint32)
+S = np.zeros((1 << 22) + 777, dtype=dt); S["key"] = (rng.integers(0, 8192, len(S)) * 128 + 5).astype(np.uint32)
+for bits in (13, 14):
+    for algo in ("RHO", "RHT"):
+        r = sgxamd.rho_join(R, len(R), S, len(S), radix_bits=bits, passes=2, algorithm=algo)
+        assert r.matches == len(S), (bits, algo, r.matches)
+        assert r.stats["layout"] == 3, r.stats["layout"]
+# and two hot digits among uniform ones, against the sort counter
+S2 = np.zeros(1 << 22, dtype=dt)
+S2["key"] = np.where(rng.random(len(S2)) < 0.6, rng.integers(0, 8192, len(S2)) * 128 + 9,
+                     rng.integers(0, 1 << 21, len(S2))).astype(np.uint32)
+assert sgxamd.rho_join(R, len(R), S2, len(S2), radix_bits=14, passes=2).matches == oracle.count_join_sort(R, S2)
+print("chain ok")
+"""
+
+
+@pytest.mark.parametrize("segs", ["8", "512"])
+def test_chain_histograms_skewed(segs):
+    e = dict(os.environ, SGXAMD_POOL_SEGS=segs)
+    e["PYTHONPATH"] = os.pathsep.join([os.path.join(PKG, "python"), os.path.join(ROOT, "oracle"),
+                                       e.get("PYTHONPATH", "")])
+    r = subprocess.run([sys.executable, "-c", CHAIN_CHILD], env=e, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "chain ok" in r.stdout, (segs, r.stdout[-2000:], r.stderr[-2000:])
