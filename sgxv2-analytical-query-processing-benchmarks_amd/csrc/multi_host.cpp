@@ -490,6 +490,18 @@ class RehearsalTransport final : public Transport {
 // ---------------------------------------------------------------- one rank's join
 std::atomic<int> g_pieces{4};
 
+// Tests (SGXAMD_DEBUG_EXCHANGE_DELAY_US, read once): the communication stream waits this
+// long before every piece, so that a local pass that does not wait for its piece's event
+// reads a receive buffer that has not landed (test_multi_gpu.py::test_late_pieces).
+uint32_t exchange_delay_us() {
+    static const uint32_t us = [] {
+        const char *e = std::getenv("SGXAMD_DEBUG_EXCHANGE_DELAY_US");
+        const long v = e ? std::atol(e) : 0;
+        return (uint32_t)(v > 0 && v < 1000000 ? v : 0);
+    }();
+    return us;
+}
+
 // Communication stream and piece events of a context (created on first use).
 struct RankStreams {
     hipStream_t comm = nullptr;
@@ -580,7 +592,7 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
     }
     RankStreams *rs = nullptr;
     // this rank's first error, kept until the next collective reports it
-    int fail_rc = pre_fail != MI355_OK ? pre_fail : rank_streams(ctx, 2 * K + 2, &rs);
+    int fail_rc = pre_fail != MI355_OK ? pre_fail : rank_streams(ctx, 3 * K + 2, &rs);
     std::string fail_msg = fail_rc ? last_error() : "";
     auto fail = [&](int rc) {
         if (rc != MI355_OK && fail_rc == MI355_OK) {
@@ -669,6 +681,7 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
     // the counts went out unflagged, so every piece is posted whatever happens now; a
     // failure from here on is flagged at the final all-reduce
     uint64_t total[2] = {0, 0};
+    std::vector<uint64_t> s_piece(K, 0);  // S tuples landing per piece (S's local pass 1 runs per piece)
     for (int j = 0; j < M; ++j) {
         const int rel = j / K;
         char *snd = (rel ? ctx->xsendS : ctx->xsendR).as<char>() + pa[j] * elem;
@@ -676,12 +689,16 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
         if (fail_rc == MI355_OK) fail(rho::shard_scatter_piece(ctx, s, j, snd));
         hipEvent_t ready = rs->ev[j];
         hip_ok(hipEventRecord(ready, s), "hipEventRecord (piece ready)");
+        if (const uint32_t us = exchange_delay_us())  // tests: every piece lands late
+            hip_ok(rho::launch_spin(us, rs->comm), "launch_spin (exchange delay)");
         const uint64_t *scj = sc.data() + (size_t)j * G, *rcj = rc.data() + (size_t)j * G;
         MH_RC(transport_rc(T.post_exchange(rank, rs->comm, ready, snd, scj, rcv, rcj, elem)));
         for (int q = 0; q < G; ++q) {
             total[rel] += rcj[q];
+            if (rel) s_piece[j - K] += rcj[q];
             if (q != rank) o.sent += scj[q] * elem;
         }
+        if (rel) hip_ok(hipEventRecord(rs->ev[2 * K + 2 + (j - K)], rs->comm), "hipEventRecord (S piece landed)");
         if ((j + 1) % K == 0)
             hip_ok(hipEventRecord(rs->ev[2 * K + rel], rs->comm), "hipEventRecord (relation landed)");
     }
@@ -696,11 +713,14 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
     if (fail_rc == MI355_OK) {
         const bool waited = hip_ok(hipStreamWaitEvent(s, rs->ev[2 * K], 0), "hipStreamWaitEvent (R landed)");
         if (waited && total[0] && total[1]) {
+            // S's pass 1 runs per piece as it lands (each launch waits for its piece's
+            // event); pass 2 and the build/probe follow the last one
             int lrc = injected(rank, kFailLocal) ? MI355_ERR_OOM
                                                  : rho::join_pipelined_begin(ctx, s, ctx->xrecvR.ptr, total[0],
-                                                                             total[1], &lo, (uint32_t)elem);
-            if (lrc == MI355_OK && hip_ok(hipStreamWaitEvent(s, rs->ev[2 * K + 1], 0), "hipStreamWaitEvent (S landed)"))
-                lrc = rho::join_pipelined_finish(ctx, ctx->xrecvS.ptr, total[1], &o.st);
+                                                                             total[1], &lo, (uint32_t)elem,
+                                                                             s_piece.data(), K);
+            if (lrc == MI355_OK)
+                lrc = rho::join_pipelined_finish(ctx, ctx->xrecvS.ptr, total[1], &o.st, &rs->ev[2 * K + 2]);
             fail(lrc);
             o.local = lrc == MI355_OK ? o.st.matches : 0;
         } else if (waited) {

@@ -32,14 +32,22 @@ int shard_count_pieces(Context *ctx, hipStream_t s, const row_t *const *in, cons
                        uint32_t key_shift, uint32_t dest_bits, uint32_t out_elem, uint64_t *counts);
 int shard_scatter_piece(Context *ctx, hipStream_t s, int j, void *out);
 // in_elem 8: dR / dS are row_t relations; 4: packed keys (needs keys_exchange_plan's plan).
+// s_piece_n[0..s_pieces): S arrives in contiguous pieces of these sizes (they add up to
+// nS); a pooled S pass 1 then runs per piece, each launch after its event in
+// s_landed[i] (finish; null: no waits), so that only the last piece's pass 1, the pool
+// layout, pass 2 and the build/probe follow S's last piece.
 int join_pipelined_begin(Context *ctx, hipStream_t s, const void *dR, uint64_t nR, uint64_t nS,
-                         const mi355_rho_opts *opts, uint32_t in_elem = 8);
-int join_pipelined_finish(Context *ctx, const void *dS, uint64_t nS, mi355_rho_stats *st);
+                         const mi355_rho_opts *opts, uint32_t in_elem = 8, const uint64_t *s_piece_n = nullptr,
+                         int s_pieces = 0);
+int join_pipelined_finish(Context *ctx, const void *dS, uint64_t nS, mi355_rho_stats *st,
+                          const hipEvent_t *s_landed = nullptr);
 // Whether a multi-GPU counting join can exchange keys only: fixes lo's local policy
 // (radix bits / passes) from the expected local sizes nR / nS when the caller left it
 // open, and checks that this policy takes the pooled keys layout for any local size up
 // to cap_r / cap_s (the receive capacities).  SGXAMD_KEYS=0 disables it.
 bool keys_exchange_plan(uint64_t nR, uint64_t nS, uint64_t cap_r, uint64_t cap_s, mi355_rho_opts *lo);
+// Tests: enqueue `us` microseconds of waiting on stream s (rho_kernels.hip k_spin).
+hipError_t launch_spin(uint32_t us, hipStream_t s);
 // What mi355_last_join_stats reports for this thread's last join (multi-GPU calls).
 void set_last_join_stats(const mi355_rho_stats &st);
 

@@ -155,13 +155,25 @@ inline bool keys_enabled() {
 // pass-2 digits in the pass-1 scatter (chain histograms, rho_internal.hpp
 // launch_scatter_pool): no digit side stream is written or read, and the pass-2
 // histogram pass becomes one scan over the chain histograms (launch_chain_scan).
-// SGXAMD_CHAIN_HIST=0 keeps the side stream (development A/B switch; results identical).
+// Off by default: the chain-aligned pass-2 segments made k_sort_blk 0.05 ms slower per
+// relation than the histogram pass they replace saves (r04k).
+// SGXAMD_CHAIN_HIST=1 takes them (development A/B switch; results identical).
 inline bool chain_enabled() {
     static const bool on = [] {
         const char *e = std::getenv("SGXAMD_CHAIN_HIST");
-        return !(e && std::atoi(e) == 0);
+        return e && std::atoi(e) == 1;
     }();
     return on;
+}
+// Slot targets of the chain-aligned pass-2 segments (launch_chain_scan): 1 = kPass2Ents
+// less two mean chains, 2 = less the region's longest chain.  SGXAMD_CHAIN_SLOTS (A/B).
+inline uint32_t chain_slot_mode() {
+    static const uint32_t m = [] {
+        const char *e = std::getenv("SGXAMD_CHAIN_SLOTS");
+        const int v = e ? std::atoi(e) : 2;
+        return (uint32_t)(v == 1 ? 1 : 2);
+    }();
+    return m;
 }
 constexpr uint32_t kPoolSegs = 512;  // two 512-thread workgroups per CU: one wave of workgroups
 inline uint32_t pool_segs() {
@@ -196,6 +208,12 @@ struct RelPlan {
     size_t hist1, tot1, start1, cnt1, segbase2, hist2, pstart, pcnt;
     size_t binfo, used, lbase, lcount, list;
     size_t chist, seglb, segle, segc0;  // chain histograms [F1][nseg1][F2], pass-2 segment ranges
+    // pooled pass 1 per input piece (the multi-GPU exchange's received pieces): piece i is
+    // elements [piece_off[i], + piece_n[i]), its segments start at piece_g0[i]; its launch
+    // waits for piece_ev[i] (null: no wait)
+    std::vector<uint64_t> piece_off, piece_n;
+    std::vector<uint32_t> piece_g0;
+    std::vector<hipEvent_t> piece_ev;
 };
 
 #define RHO_HIP(call)                                                                      \
@@ -220,16 +238,33 @@ int partition_relation_pooled(Context *ctx, hipStream_t s, Timer &tm, const std:
     uint64_t *list = A.at<uint64_t>(rp.list);
     const uint32_t F1 = 1u << pol.b1;
     if (!pass2_now) {
-        const SegMap m1{nullptr, nullptr, nullptr, 1, rp.seg1, rp.n};
-        const PoolOut po{A.at<uint32_t>(rp.binfo), A.at<uint64_t>(rp.hist1), A.at<uint32_t>(rp.used), rp.pool_blocks,
-                         rp.nseg1};
+        PoolOut po{A.at<uint32_t>(rp.binfo), A.at<uint64_t>(rp.hist1), A.at<uint32_t>(rp.used), rp.pool_blocks,
+                   rp.nseg1};
         const DigitSide ds{rp.chain ? nullptr : side, key_shift + pol.b1, pol.b2};
+        uint32_t *chist = rp.chain ? A.at<uint32_t>(rp.chist) : nullptr;
         tm.mark((t + "pass1_scatter").c_str());
-        RHO_HIP(launch_scatter_pool(in, rp.in_size, t1, rp.keys ? 4u : 8u, m1, rp.nseg1, key_shift, pol.b1, po, ds,
-                                    s, rp.chain ? A.at<uint32_t>(rp.chist) : nullptr));
+        if (rp.piece_n.empty()) {
+            const SegMap m1{nullptr, nullptr, nullptr, 1, rp.seg1, rp.n};
+            RHO_HIP(launch_scatter_pool(in, rp.in_size, t1, rp.keys ? 4u : 8u, m1, rp.nseg1, key_shift, pol.b1, po, ds,
+                                        s, chist));
+        } else {
+            // one launch per piece as it lands, its segments numbered after the earlier
+            // pieces' (one pool layout over all of them)
+            const char *ib = reinterpret_cast<const char *>(in);
+            for (size_t i = 0; i < rp.piece_n.size(); ++i) {
+                if (i < rp.piece_ev.size() && rp.piece_ev[i]) RHO_HIP(hipStreamWaitEvent(s, rp.piece_ev[i], 0));
+                const uint64_t n = rp.piece_n[i];
+                if (!n) continue;
+                const SegMap mi{nullptr, nullptr, nullptr, 1, rp.seg1, n};
+                po.g0 = rp.piece_g0[i];
+                RHO_HIP(launch_scatter_pool(ib + rp.piece_off[i] * rp.in_size, rp.in_size, t1, rp.keys ? 4u : 8u, mi,
+                                            (uint32_t)((n + rp.seg1 - 1) / rp.seg1), key_shift, pol.b1, po, ds, s,
+                                            chist));
+            }
+        }
         tm.mark((t + "pass1_scan").c_str());
         RHO_HIP(launch_pool_layout(po.cnt, rp.nseg1, pol.b1, A.at<uint64_t>(rp.tot1), start1, cnt1, lbase, lcount,
-                                   segbase2, s, rp.chain));
+                                   segbase2, s, rp.chain ? chain_slot_mode() : 0u));
         RHO_HIP(launch_block_list(po, lbase, list, s));
         *final_rel = t1;
         *pstart = start1;
@@ -248,7 +283,8 @@ int partition_relation_pooled(Context *ctx, hipStream_t s, Timer &tm, const std:
         RHO_HIP(launch_chain_fix(A.at<uint64_t>(rp.hist1), A.at<uint64_t>(rp.tot1), rp.nseg1, pol.b1, pol.b2, lbase,
                                  list, reinterpret_cast<const uint32_t *>(t1), key_shift + pol.b1,
                                  A.at<uint32_t>(rp.chist), s));
-        RHO_HIP(launch_chain_scan(A.at<uint64_t>(rp.hist1), rp.nseg1, A.at<uint32_t>(rp.chist), pol.b1, pol.b2,
+        RHO_HIP(launch_chain_scan(A.at<uint64_t>(rp.hist1), rp.nseg1, chain_slot_mode(), A.at<uint32_t>(rp.chist),
+                                  pol.b1, pol.b2,
                                   start1, lbase, lcount, segbase2, hist2, seglb, segle, A.at<uint32_t>(rp.segc0), ps,
                                   pc, s));
         SegMap mc = m2;
@@ -321,6 +357,9 @@ int partition_relation(Context *ctx, hipStream_t s, Timer &tm, const char *tag, 
     const bool use_side = side != nullptr && uses_digit_side(pol);
     if (rp.pooled) return partition_relation_pooled(ctx, s, tm, t, in, t1, t2, side, rp, pol, key_shift, final_rel,
                                                     pstart, pcnt, pass2_now);
+    if (!pass2_now)  // pieces (multi-GPU exchange): an unpooled pass reads the whole input at once
+        for (hipEvent_t e : rp.piece_ev)
+            if (e) RHO_HIP(hipStreamWaitEvent(s, e, 0));
     if (!pass2_now) {
         int rc = pass1_counts(ctx, s, tm, t, in, rp, pol, key_shift);
         if (!rc) rc = pass1_scatter(ctx, s, tm, t, in, t1, use_side ? side : nullptr, rp, pol, key_shift);
@@ -358,15 +397,16 @@ inline uint64_t pool_seg_size(uint64_t n) {
 }
 // Whether a relation of n tuples can take the pooled plan: a two-pass plan with the
 // digit side stream, and block counts that fit the 24-bit chain records.
-inline bool pool_fits(uint64_t n, const Policy &pol) {
+inline bool pool_fits(uint64_t n, const Policy &pol, uint64_t extra_segs = 0) {
     if (!(pol.passes == 2 && uses_digit_side(pol) && pool_enabled())) return false;
-    const uint64_t seg = pool_seg_size(n), nseg = (n + seg - 1) / seg;
+    const uint64_t seg = pool_seg_size(n), nseg = (n + seg - 1) / seg + extra_segs;
     const uint64_t pb = (seg + kBlk - 1) / kBlk + (1u << pol.b1);
     return n / kBlk + nseg * (1u << pol.b1) < (1ull << 24) && nseg * pb < (1ull << 27);
 }
 enum PoolMode : int { kNoPool = 0, kPoolTuples = 1, kPoolKeys = 2 };
 
-void plan_relation(Arena &A, RelPlan &rp, uint64_t n, const Policy &pol, int pool = kNoPool) {
+void plan_relation(Arena &A, RelPlan &rp, uint64_t n, const Policy &pol, int pool = kNoPool,
+                   const std::vector<uint64_t> *pieces = nullptr) {
     rp.n = n;
     rp.seg1 = seg_size_for(n);
     rp.nseg1 = (uint32_t)((n + rp.seg1 - 1) / rp.seg1);
@@ -378,12 +418,32 @@ void plan_relation(Arena &A, RelPlan &rp, uint64_t n, const Policy &pol, int poo
     rp.keys = false;
     rp.chain = false;
     rp.in_size = sizeof(row_t);
+    rp.piece_off.clear();
+    rp.piece_n.clear();
+    rp.piece_g0.clear();
+    rp.piece_ev.clear();
+    if (pieces && !pieces->empty()) {  // the input arrives in pieces (every plan waits for them)
+        uint64_t off = 0;
+        for (uint64_t pn : *pieces) {
+            rp.piece_off.push_back(off);
+            rp.piece_n.push_back(pn);
+            rp.piece_g0.push_back(0);
+            off += pn;
+        }
+    }
     if (pool != kNoPool) {
         // pass-1 segments of whole tiles, about pool_segs() of them; every digit of a
         // segment fills ceil(elements / kBlk) blocks, so a pool of ceil(seg1 / kBlk) + F1
         // blocks always suffices.  Chain records pack blocks << 40 | elements.
         const uint64_t seg = pool_seg_size(n);
-        const uint32_t nseg = (uint32_t)((n + seg - 1) / seg);
+        uint32_t nseg = (uint32_t)((n + seg - 1) / seg);
+        if (!rp.piece_n.empty()) {  // segments never straddle two pieces
+            nseg = 0;
+            for (size_t i = 0; i < rp.piece_n.size(); ++i) {
+                rp.piece_g0[i] = nseg;
+                nseg += (uint32_t)((rp.piece_n[i] + seg - 1) / seg);
+            }
+        }
         const uint64_t pb = (seg + kBlk - 1) / kBlk + F1;
         const uint64_t max_blocks = n / kBlk + (uint64_t)nseg * F1;
         rp.pooled = true;
@@ -460,7 +520,8 @@ PendingJoin &pending_of(const Context *ctx) {
 // may start after S has been produced later in the stream order of s (multi-GPU:
 // R's local passes run while S is still being exchanged).  Caller holds ctx->mu.
 // Policy, workspace and scratch layout of a join of nR x nS tuples (no launches).
-int plan_join(Context *ctx, hipStream_t s, uint64_t nR, uint64_t nS, const mi355_rho_opts *opts, PendingJoin &pj) {
+int plan_join(Context *ctx, hipStream_t s, uint64_t nR, uint64_t nS, const mi355_rho_opts *opts, PendingJoin &pj,
+              const std::vector<uint64_t> *s_pieces = nullptr) {
     pj = PendingJoin{};
     pj.s = s;
     pj.nR = nR;
@@ -479,11 +540,12 @@ int plan_join(Context *ctx, hipStream_t s, uint64_t nR, uint64_t nS, const mi355
     // both relations take the same layout (the build/probe reads both alike)
     // counting joins (RHO and RHT) move 4-byte keys after the input read
     const bool counting = !pj.materialize;
-    const int pool = !(pool_fits(nR, pol) && pool_fits(nS, pol)) ? kNoPool
-                     : (counting && keys_enabled())              ? kPoolKeys
-                                                                  : kPoolTuples;
+    const uint64_t ks = s_pieces ? s_pieces->size() : 0;
+    const int pool = !(pool_fits(nR, pol) && pool_fits(nS, pol, ks)) ? kNoPool
+                     : (counting && keys_enabled())                  ? kPoolKeys
+                                                                      : kPoolTuples;
     plan_relation(A, pj.pr, nR, pol, pool);
-    plan_relation(A, pj.ps, nS, pol, pool);
+    plan_relation(A, pj.ps, nS, pol, pool, s_pieces);
     const uint64_t c1R = pj.pr.t1_tuples, c1S = pj.ps.t1_tuples;  // pooled pass 1 needs room for its pools
     RHO_HIP(ctx->t1R.ensure(std::max<uint64_t>(c1R, 1) * sizeof(row_t)));
     RHO_HIP(ctx->t1S.ensure(std::max<uint64_t>(c1S, 1) * sizeof(row_t)));
@@ -531,8 +593,8 @@ int plan_join(Context *ctx, hipStream_t s, uint64_t nR, uint64_t nS, const mi355
 // may start after S has been produced later in the stream order of s (multi-GPU:
 // R's local passes run while S is still being exchanged).  Caller holds ctx->mu.
 int join_begin(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, uint64_t nS, const mi355_rho_opts *opts,
-               PendingJoin &pj, uint32_t in_elem = sizeof(row_t)) {
-    int prc = plan_join(ctx, s, nR, nS, opts, pj);
+               PendingJoin &pj, uint32_t in_elem = sizeof(row_t), const std::vector<uint64_t> *s_pieces = nullptr) {
+    int prc = plan_join(ctx, s, nR, nS, opts, pj, s_pieces);
     if (prc) return prc;
     if (in_elem != sizeof(row_t)) {  // key input: only the pooled keys layout reads it
         if (!(pj.pr.keys && pj.ps.keys)) {
@@ -836,7 +898,10 @@ int join_small(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const 
     RHO_HIP(launch_hist_pair(dR, mR, pj.pr.nseg1, dS, mS, pj.ps.nseg1, pj.key_shift, pol.b1, offsR, offsS, startR, cntR,
                              startS, cntS, sync, over, pj.over_cap, result + 1, pj.s_chunk, s));
     tm.mark("RS_pass1_scatter");
-    RHO_HIP(launch_scatter_pair(dR, oR, mR, pj.pr.nseg1, offsR, startR, dS, oS, mS, pj.ps.nseg1, offsS, startS,
+    // cursors: each segment's offset inside its copy of the digit totals + that copy's
+    // digit start (sync words written by k_hist_pair's last segment of each relation)
+    RHO_HIP(launch_scatter_pair(dR, oR, mR, pj.pr.nseg1, offsR, sync + kSyncStartR, dS, oS, mS, pj.ps.nseg1, offsS,
+                                sync + kSyncStartS,
                                 pj.key_shift, pol.b1, s));
     tm.mark("join_build_probe");
     const uint64_t P = 1ull << pol.bits;
@@ -889,19 +954,33 @@ int join_device(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const
 }
 
 int join_pipelined_begin(Context *ctx, hipStream_t s, const void *dR, uint64_t nR, uint64_t nS,
-                         const mi355_rho_opts *opts, uint32_t in_elem) {
+                         const mi355_rho_opts *opts, uint32_t in_elem, const uint64_t *s_piece_n, int s_pieces) {
     PendingJoin &pj = pending_of(ctx);
     if (pj.active) {
         set_last_error("a pipelined join is already pending on this context");
         return MI355_ERR_INVALID;
     }
-    const int rc = join_begin(ctx, s, static_cast<const row_t *>(dR), nR, nS, opts, pj, in_elem);
+    std::vector<uint64_t> pieces;
+    if (s_piece_n && s_pieces > 0) {
+        pieces.assign(s_piece_n, s_piece_n + s_pieces);
+        uint64_t sum = 0;
+        for (uint64_t x : pieces) sum += x;
+        if (sum != nS) {
+            set_last_error("join_pipelined_begin: the S pieces do not add up to |S|");
+            return MI355_ERR_INVALID;
+        }
+    }
+    const int rc = join_begin(ctx, s, static_cast<const row_t *>(dR), nR, nS, opts, pj, in_elem,
+                              pieces.empty() ? nullptr : &pieces);
     if (rc) pj.active = false;
     return rc;
 }
 
-int join_pipelined_finish(Context *ctx, const void *dS, uint64_t nS, mi355_rho_stats *st) {
-    return join_finish(ctx, pending_of(ctx), static_cast<const row_t *>(dS), nS, st, nullptr, 0, nullptr, true);
+int join_pipelined_finish(Context *ctx, const void *dS, uint64_t nS, mi355_rho_stats *st, const hipEvent_t *s_landed) {
+    PendingJoin &pj = pending_of(ctx);
+    pj.ps.piece_ev.clear();
+    if (s_landed) pj.ps.piece_ev.assign(s_landed, s_landed + pj.ps.piece_n.size());
+    return join_finish(ctx, pj, static_cast<const row_t *>(dS), nS, st, nullptr, 0, nullptr, true);
 }
 
 bool keys_exchange_plan(uint64_t nR, uint64_t nS, uint64_t cap_r, uint64_t cap_s, mi355_rho_opts *lo) {

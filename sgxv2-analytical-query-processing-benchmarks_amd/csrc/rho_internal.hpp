@@ -64,19 +64,34 @@ constexpr uint32_t kSyncTicketR = 0, kSyncTicketS = 1, kSyncTicket2 = 2, kSyncTi
 // synchronising the stream.
 constexpr uint32_t kSyncHostResult = kSyncTicketJoin + 1, kSyncT0 = kSyncTicketJoin + 2;
 constexpr uint32_t kHostJoinSpan = 6, kHostJoinDone = 7, kHostJoinWords = 8;
-constexpr uint32_t kSyncTotR = 8, kSyncTotS = kSyncTotR + kMaxF, kSyncWords = kSyncTotS + kMaxF;
+// Hand-offs spread over kSyncSpread groups of workgroups (segment or workgroup index mod
+// kSyncSpread), so that no device-scope atomic address takes more than 1/kSyncSpread of
+// the grid's updates: the digit totals are kSyncSpread copies [c][kMaxF] (a segment's
+// offset is its place inside its copy; the copies' digit starts [c][kMaxF] add the
+// copies before it), and a ticket of n arrivals is kSyncSpread sub-tickets
+// (sync[ticket + kSyncSub + kNumTickets * c]) whose last arrivers take the ticket itself.
+#ifndef SGXAMD_SMALL_SPREAD
+#define SGXAMD_SMALL_SPREAD 8
+#endif
+constexpr uint32_t kSyncSpread = SGXAMD_SMALL_SPREAD, kNumTickets = 4;
+constexpr uint32_t kSyncTotR = 8, kSyncTotS = kSyncTotR + kSyncSpread * kMaxF;
+constexpr uint32_t kSyncSub = kSyncTotS + kSyncSpread * kMaxF;  // relative to a ticket's word
+constexpr uint32_t kSyncStartR = kSyncSub + kNumTickets * kSyncSpread, kSyncStartS = kSyncStartR + kSyncSpread * kMaxF;
+constexpr uint32_t kSyncWords = kSyncStartS + kSyncSpread * kMaxF;
 
 // Small one-pass joins: histograms of R and S, digit starts / counts and the build/probe
 // task list (meta as launch_make_tasks) in one launch.  offs: [d][g] segment offsets
-// inside digit d (cursors for launch_scatter_pair with the starts as digit_base).
+// inside the segment's copy (g mod kSyncSpread) of digit d's total; the copies' digit
+// starts land in sync[kSyncStartR / kSyncStartS] (the bases of launch_scatter_pair).
 hipError_t launch_hist_pair(const row_t *R, const SegMap &mR, uint32_t gridR, const row_t *S, const SegMap &mS,
                             uint32_t gridS, uint32_t shift, uint32_t bits, uint64_t *offsR, uint64_t *offsS,
                             uint64_t *startR, uint64_t *cntR, uint64_t *startS, uint64_t *cntS, uint64_t *sync,
                             uint64_t *over, uint32_t over_cap, uint64_t *meta, uint64_t s_chunk, hipStream_t s);
-// Both relations' one-pass scatters in one launch (digit-major cursors + digit starts).
+// Both relations' one-pass scatters in one launch (digit-major cursors + the digit starts
+// of each segment's totals copy, cstart [kSyncSpread][kMaxF]).
 hipError_t launch_scatter_pair(const row_t *R, row_t *outR, const SegMap &mR, uint32_t gridR, const uint64_t *offsR,
-                               const uint64_t *startR, const row_t *S, row_t *outS, const SegMap &mS, uint32_t gridS,
-                               const uint64_t *offsS, const uint64_t *startS, uint32_t shift, uint32_t bits,
+                               const uint64_t *cstartR, const row_t *S, row_t *outS, const SegMap &mS, uint32_t gridS,
+                               const uint64_t *offsS, const uint64_t *cstartS, uint32_t shift, uint32_t bits,
                                hipStream_t s);
 
 // Digit side stream of a two-pass partition: the pass-1 scatter also writes, for the
@@ -112,6 +127,7 @@ struct PoolOut {
     uint32_t *used;        // per segment: blocks taken from its pool
     uint32_t pool_blocks;  // blocks per segment pool
     uint32_t nseg;
+    uint32_t g0 = 0;       // this launch's first segment (a pass 1 launched per input piece)
 };
 // Pass 1 of a pooled plan: contiguous input segments (m), pooled output in out, digit
 // side stream ds beside every stored element.  Elements: in_size-byte input
@@ -136,12 +152,13 @@ hipError_t launch_chain_fix(const uint64_t *cnt, const uint64_t *tot, uint32_t n
 // Chain-histogram plans: one workgroup per region from the column-scanned chain records
 // (po.cnt) and the chain histograms: the pass-2 segments, cut at chain boundaries (slot k
 // of region d holds the chains whose first block lies in [T*k, T*(k+1)) of d's list, T a
-// little below kPass2Ents (rho_kernels.hip chain_slot_target), so a segment is T blocks
+// little below kPass2Ents (mode 1: less two mean chains, rho_kernels.hip
+// chain_slot_target; mode 2: less the region's longest chain), so a segment is T blocks
 // + the rest of one chain; empty slots are holes), as list
 // ranges seg_lb / seg_le; the pass-2 cursors [slot][F2] (the histogram + scan of
 // launch_hist_side_blk + launch_scan_regions, without reading the elements) and the
 // partition table part_start / part_count [d][F2].  seg_c0: scratch, one u32 per slot.
-hipError_t launch_chain_scan(const uint64_t *cnt, uint32_t nseg, const uint32_t *chain, uint32_t bits1,
+hipError_t launch_chain_scan(const uint64_t *cnt, uint32_t nseg, uint32_t mode, const uint32_t *chain, uint32_t bits1,
                              uint32_t bits2, const uint64_t *region_start, const uint64_t *lbase,
                              const uint64_t *lcount, const uint32_t *seg_base, uint64_t *cursors, uint32_t *seg_lb,
                              uint32_t *seg_le, uint32_t *seg_c0, uint64_t *part_start, uint64_t *part_count,
@@ -149,10 +166,10 @@ hipError_t launch_chain_scan(const uint64_t *cnt, uint32_t nseg, const uint32_t 
 // After launch_scan_single-style column scans of po.cnt (k_scan_cols, in place): region
 // tuple starts / counts (the pass-2 output layout), region block-list bases / lengths
 // and the pass-2 segment table (kPass2Ents blocks per segment).
-// chain_slots: the slots of chain-aligned segments (launch_chain_scan) instead.
+// chain_mode 1 / 2: the slots of chain-aligned segments (launch_chain_scan) instead.
 hipError_t launch_pool_layout(uint64_t *cnt, uint32_t nseg, uint32_t bits, uint64_t *totals, uint64_t *start,
                               uint64_t *count, uint64_t *lbase, uint64_t *lcount, uint32_t *seg_base, hipStream_t s,
-                              bool chain_slots = false);
+                              uint32_t chain_mode = 0);
 // The block list: region d's blocks at [lbase[d], lbase[d] + lcount[d]) as
 // physical block | fill << 32.
 hipError_t launch_block_list(const PoolOut &po, const uint64_t *lbase, uint64_t *list, hipStream_t s);

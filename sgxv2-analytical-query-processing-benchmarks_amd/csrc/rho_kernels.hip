@@ -139,6 +139,40 @@ __device__ __forceinline__ bool arrive_last(uint64_t *ticket, uint64_t n, uint32
     return *lds_flag != 0;
 }
 
+// The same over kSyncSpread groups (rho_internal.hpp): arrival idx (a segment or
+// workgroup index < n) takes its group's sub-ticket (idx mod groups); the last of each
+// group takes the ticket.  At most n / groups + groups serialised device atomics per
+// address instead of n.
+__device__ __forceinline__ bool arrive_last_spread(uint64_t *ticket, uint64_t n, uint32_t idx, uint32_t *lds_flag) {
+    const uint32_t groups = n < kSyncSpread ? (uint32_t)n : kSyncSpread;
+    if (groups <= 1) return arrive_last(ticket, n, lds_flag);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t grp = idx % groups;
+        const uint64_t members = (n - grp + groups - 1) / groups;
+        uint64_t *sub = ticket + kSyncSub + kNumTickets * grp;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        bool last = false;
+        if (__hip_atomic_fetch_add(sub, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == members - 1) {
+            __hip_atomic_store(sub, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // the group's writes (acquired) pass on with this workgroup's release
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (__hip_atomic_fetch_add(ticket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == groups - 1) {
+                __hip_atomic_store(ticket, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                last = true;
+            }
+        }
+        *lds_flag = last ? 1u : 0u;
+    }
+    __syncthreads();
+    return *lds_flag != 0;
+}
+
 __device__ __forceinline__ uint64_t ld_agent(const uint64_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -160,11 +194,12 @@ struct HistPairRel {
     SegMap m;
     uint32_t grid;        // segments of the relation
     uint32_t shift;
-    uint64_t *offs;       // [d][g] (stride grid): segment g's offset inside digit d
-    uint64_t *tot;        // F digit totals, zero at entry (reset by the last segment)
+    uint64_t *offs;       // [d][g] (stride grid): segment g's offset inside its copy of digit d
+    uint64_t *tot;        // [kSyncSpread][kMaxF] digit totals, zero at entry (reset by the last segment)
     uint64_t *start;      // F digit starts
     uint64_t *cnt;        // F digit counts
     uint64_t *ticket;
+    uint64_t *cstart;     // [kSyncSpread][kMaxF]: digit starts of each copy's segments (the scatter's bases)
 };
 
 __global__ __launch_bounds__(kBlock) void k_hist_pair(HistPairRel A, HistPairRel B, uint32_t bits,
@@ -182,23 +217,35 @@ __global__ __launch_bounds__(kBlock) void k_hist_pair(HistPairRel A, HistPairRel
     if (blockIdx.x == 0 && threadIdx.x == 0)  // the call's start (small-join device span)
         ticket2[kSyncT0 - kSyncTicket2] = wall_clock64();
     const bool any = hist_segment(H.in, H.m, g, H.shift, bits, h, sbase);
+    uint64_t *tot_c = H.tot + (uint64_t)(g % kSyncSpread) * kMaxF;  // this segment's copy of the totals
     for (uint32_t d = threadIdx.x; d < F; d += kBlock) {
         const uint32_t v = any ? h[d] : 0u;
         H.offs[(uint64_t)d * H.grid + g] =
-            v ? __hip_atomic_fetch_add(&H.tot[d], (uint64_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+            v ? __hip_atomic_fetch_add(&tot_c[d], (uint64_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
     }
-    if (!arrive_last(H.ticket, H.grid, &flag)) return;
-    // the relation's last segment: digit starts and counts
+    if (!arrive_last_spread(H.ticket, H.grid, g, &flag)) return;
+    // the relation's last segment: digit starts and counts, and each copy's bases
     uint64_t carry = 0;
     for (uint32_t d0 = 0; d0 < F; d0 += kBlock) {
         const uint32_t d = d0 + threadIdx.x;
-        const uint64_t v = d < F ? ld_agent(&H.tot[d]) : 0ull;
+        uint64_t v = 0, part[kSyncSpread];
+#pragma unroll
+        for (uint32_t c = 0; c < kSyncSpread; ++c) {
+            part[c] = d < F ? ld_agent(&H.tot[(uint64_t)c * kMaxF + d]) : 0ull;
+            v += part[c];
+        }
         uint64_t tot;
         const uint64_t ex = block_excl_scan_u64(v, scratch, &tot);
         if (d < F) {
             H.start[d] = carry + ex;
             H.cnt[d] = v;
-            st_agent(&H.tot[d], 0ull);
+            uint64_t b = carry + ex;
+#pragma unroll
+            for (uint32_t c = 0; c < kSyncSpread; ++c) {
+                H.cstart[(uint64_t)c * kMaxF + d] = b;
+                b += part[c];
+                st_agent(&H.tot[(uint64_t)c * kMaxF + d], 0ull);
+            }
         }
         carry += tot;
     }
@@ -230,9 +277,9 @@ hipError_t launch_hist_pair(const row_t *R, const SegMap &mR, uint32_t gridR, co
                             uint64_t *startR, uint64_t *cntR, uint64_t *startS, uint64_t *cntS, uint64_t *sync,
                             uint64_t *over, uint32_t over_cap, uint64_t *meta, uint64_t s_chunk, hipStream_t s) {
     const HistPairRel A{reinterpret_cast<const uint32_t *>(R), mR, gridR, shift, offsR, sync + kSyncTotR, startR,
-                        cntR, sync + kSyncTicketR};
+                        cntR, sync + kSyncTicketR, sync + kSyncStartR};
     const HistPairRel B{reinterpret_cast<const uint32_t *>(S), mS, gridS, shift, offsS, sync + kSyncTotS, startS,
-                        cntS, sync + kSyncTicketS};
+                        cntS, sync + kSyncTicketS, sync + kSyncStartS};
     hipLaunchKernelGGL(k_hist_pair, dim3(gridR + gridS), dim3(kBlock), 0, s, A, B, bits, sync + kSyncTicket2, over,
                        over_cap, meta, s_chunk);
     return hipGetLastError();
@@ -404,10 +451,12 @@ hipError_t launch_scan_regions(uint64_t *hist, const uint32_t *seg_base, const u
 
 // Chain-aligned pass-2 segments (chain histograms): slot k of a region holds the chains
 // whose first block lies in [T*k, T*(k+1)) of its list, so a segment is T blocks plus the
-// part of its last chain past the boundary.  T = kPass2Ents less two mean chains of the
-// region (at least half of kPass2Ents): k_sort_blk's 64-block tiles then stay at four
-// per segment, where T = kPass2Ents made 4.25 (a fifth, nearly empty tile: pass 2 5 %
-// slower, r04f).
+// part of its last chain past the boundary, less the part of its first chain before it:
+// shorter than T + L for chains of at most L blocks.  Slot mode 1: T = kPass2Ents less
+// two mean chains of the region (at least half of kPass2Ents); mode 2: T = kPass2Ents
+// less the region's longest chain (k_chain_scan), so that no segment passes kPass2Ents
+// blocks (k_sort_blk's four 64-block tiles; T = kPass2Ents made 4.25 per segment, a
+// fifth nearly empty tile).  The layout reserves slots for T = kPass2Ents / 2 in mode 2.
 __host__ __device__ __forceinline__ uint32_t chain_slot_target(uint64_t blocks, uint32_t nseg) {
 #ifdef SGXAMD_CHAIN_T_FIXED
     (void)blocks, (void)nseg;
@@ -422,7 +471,7 @@ __host__ __device__ __forceinline__ uint32_t chain_slot_target(uint64_t blocks, 
 // (pass-1 digit).  cnt: the chain records [r][g] after the column scan (exclusive
 // prefixes blocks << 40 | elements of the chains before g); chain: u32 [r][g][F2].
 constexpr uint32_t kChainLds = 4096;  // chain starts / slot chains staged in LDS (more: read in place)
-__global__ __launch_bounds__(1024) void k_chain_scan(const uint64_t *__restrict__ cnt, uint32_t nseg,
+__global__ __launch_bounds__(1024) void k_chain_scan(const uint64_t *__restrict__ cnt, uint32_t nseg, uint32_t mode,
                                                      const uint32_t *__restrict__ chain, uint32_t F2,
                                                      const uint64_t *__restrict__ region_start,
                                                      const uint64_t *__restrict__ lbase,
@@ -442,10 +491,19 @@ __global__ __launch_bounds__(1024) void k_chain_scan(const uint64_t *__restrict_
     const uint32_t *ch = chain + (uint64_t)r * nseg * F2;
     const uint32_t s0 = seg_base[r], ns = seg_base[r + 1] - s0;
     const uint64_t B = lcount[r], lb0 = lbase[r];
-    const uint32_t T = chain_slot_target(B, nseg);
     const bool lds_c = nseg <= kChainLds, lds_s = ns <= kChainLds;  // workgroup-uniform
-    if (lds_c)
-        for (uint32_t g = tid; g < nseg; g += 1024) cst[g] = (uint32_t)(rec[g] >> 40);
+    uint64_t lmax = 0;  // the region's longest chain (blocks)
+    for (uint32_t g = tid; g < nseg; g += 1024) {
+        const uint32_t a = (uint32_t)(rec[g] >> 40);
+        const uint64_t b = g + 1 < nseg ? (rec[g + 1] >> 40) : B;
+        lmax = max(lmax, b - a);
+        if (lds_c) cst[g] = a;
+    }
+    uint32_t T = chain_slot_target(B, nseg);
+    if (mode == 2) {
+        lmax = block_max_u64(lmax, scratch);
+        T = (uint32_t)max<uint64_t>(kPass2Ents / 2, lmax < kPass2Ents ? kPass2Ents - lmax : 0);
+    }
     __syncthreads();
     const auto start_of = [&](uint32_t g) -> uint32_t { return lds_c ? cst[g] : (uint32_t)(rec[g] >> 40); };
     const auto first_at = [&](uint64_t x) -> uint32_t {  // first chain whose blocks start at or after x
@@ -502,14 +560,14 @@ __global__ __launch_bounds__(1024) void k_chain_scan(const uint64_t *__restrict_
     }
 }
 
-hipError_t launch_chain_scan(const uint64_t *cnt, uint32_t nseg, const uint32_t *chain, uint32_t bits1,
+hipError_t launch_chain_scan(const uint64_t *cnt, uint32_t nseg, uint32_t mode, const uint32_t *chain, uint32_t bits1,
                              uint32_t bits2, const uint64_t *region_start, const uint64_t *lbase,
                              const uint64_t *lcount, const uint32_t *seg_base, uint64_t *cursors, uint32_t *seg_lb,
                              uint32_t *seg_le, uint32_t *seg_c0, uint64_t *part_start, uint64_t *part_count,
                              hipStream_t s) {
     const uint32_t F2 = 1u << bits2;
     if (F2 < 2 || F2 > 1024 || 1024 % F2) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_chain_scan, dim3(1u << bits1), dim3(1024), 0, s, cnt, nseg, chain, F2, region_start, lbase,
+    hipLaunchKernelGGL(k_chain_scan, dim3(1u << bits1), dim3(1024), 0, s, cnt, nseg, mode, chain, F2, region_start, lbase,
                        lcount, seg_base, cursors, seg_lb, seg_le, seg_c0, part_start, part_count);
     return hipGetLastError();
 }
@@ -1062,7 +1120,7 @@ struct ScatterPairRel {
     SegMap m;
     uint32_t grid;
     const uint64_t *offs;
-    const uint64_t *start;
+    const uint64_t *cstart;  // [kSyncSpread][kMaxF]: digit starts of each totals copy (k_hist_pair)
 };
 
 template <int BITS, int ITEMS, int NT>
@@ -1072,8 +1130,8 @@ __global__ __launch_bounds__(NT, (scatter_waves_per_simd<BITS, ITEMS, NT>())) vo
     const bool isB = blockIdx.x >= A.grid;
     const ScatterPairRel &P = isB ? B : A;
     const uint32_t g = isB ? blockIdx.x - A.grid : blockIdx.x;
-    scatter_segment<BITS, ITEMS, NT, false>(L, g, P.in, P.out, P.m, shift, P.offs, kDigitMajor, P.grid, P.start,
-                                            nullptr, 0, 0);
+    scatter_segment<BITS, ITEMS, NT, false>(L, g, P.in, P.out, P.m, shift, P.offs, kDigitMajor, P.grid,
+                                            P.cstart + (uint64_t)(g % kSyncSpread) * kMaxF, nullptr, 0, 0);
 }
 
 hipError_t launch_scatter_pair(const row_t *R, row_t *outR, const SegMap &mR, uint32_t gridR, const uint64_t *offsR,
@@ -1230,7 +1288,8 @@ __device__ __forceinline__ void scatter_segment_ext(ScatterLds<BITS, ITEMS, NT, 
     uint64_t pend = 0;
     uint32_t carried = 0;
     const uint32_t tid = threadIdx.x;
-    PoolState ps{0u, 0u, EXT == 1 ? g * po.pool_blocks : 0u, po.binfo};
+    const uint32_t gp = EXT == 1 ? g + po.g0 : g;  // pooled: the segment's id among all launches' segments
+    PoolState ps{0u, 0u, EXT == 1 ? gp * po.pool_blocks : 0u, po.binfo};
     if (tid < F) {
         if constexpr (EXT != 1)
             pend = cur_init[hist_index(layout, g, tid, F, nseg_stride)] +
@@ -1313,7 +1372,7 @@ __device__ __forceinline__ void scatter_segment_ext(ScatterLds<BITS, ITEMS, NT, 
             }
             const uint64_t Tn = pend + carried;  // elements of digit tid in this segment
             if (ps.nb) po.binfo[ps.cur] = tid | ((uint32_t)(Tn - (uint64_t)(ps.nb - 1) * kBlk) << 16);
-            po.cnt[(uint64_t)tid * po.nseg + g] = ((uint64_t)ps.nb << 40) | Tn;
+            po.cnt[(uint64_t)tid * po.nseg + gp] = ((uint64_t)ps.nb << 40) | Tn;
             L.pend[tid] = (uint64_t)gran * G;
         } else {
             L.pend[tid] = pend;
@@ -1321,7 +1380,7 @@ __device__ __forceinline__ void scatter_segment_ext(ScatterLds<BITS, ITEMS, NT, 
         L.cnt[tid] = carried;
     }
     __syncthreads();
-    if (EXT == 1 && tid == 0) po.used[g] = L.pool_next;
+    if (EXT == 1 && tid == 0) po.used[gp] = L.pool_next;
     const uint32_t lane = tid & (G - 1);
     for (uint32_t d = tid / G; d < F; d += NG) {
         if (lane < L.cnt[d]) {
@@ -1330,7 +1389,7 @@ __device__ __forceinline__ void scatter_segment_ext(ScatterLds<BITS, ITEMS, NT, 
             if (SIDE) side[L.pend[d] + lane] = (uint8_t)(((uint32_t)x >> shift2) & mask2);
         }
     }
-    if constexpr (F2 > 0) chain_store<F, F2, NT>(cs->h2, cs->out, g, cs->nseg);
+    if constexpr (F2 > 0) chain_store<F, F2, NT>(cs->h2, cs->out, gp, cs->nseg);
 }
 
 template <int BITS, int ITEMS, int NT, typename T, int IS, int F2 = 0>
@@ -1341,7 +1400,7 @@ __global__ __launch_bounds__(NT, (scatter_waves_per_simd<BITS, ITEMS, NT, 1, T>(
     const uint32_t g = xcd_contiguous(blockIdx.x, gridDim.x);
     if constexpr (F2 > 0) {
         __shared__ uint32_t h2[(1u << BITS) * F2 / 2];
-        ChainState cs{h2, chain, g, po.nseg, shift2};
+        ChainState cs{h2, chain, g + po.g0, po.nseg, shift2};
         scatter_segment_ext<BITS, ITEMS, NT, 1, T, IS, F2>(L, g, in, out, m, shift, nullptr, nullptr, po, side, shift2,
                                                            mask2, kSegMajor, 0, nullptr, &cs);
     } else {
@@ -1714,7 +1773,8 @@ hipError_t launch_scatter_blk(const void *in, const uint64_t *list, void *out, u
 __global__ __launch_bounds__(1024) void k_pool_layout(const uint64_t *__restrict__ totals, uint32_t F,
                                                       uint64_t *__restrict__ start, uint64_t *__restrict__ count,
                                                       uint64_t *__restrict__ lbase, uint64_t *__restrict__ lcount,
-                                                      uint32_t *__restrict__ seg_base, uint32_t chain_nseg) {
+                                                      uint32_t *__restrict__ seg_base, uint32_t chain_nseg,
+                                                      uint32_t chain_mode) {
     __shared__ uint64_t scratch[1024 / kWave + 1];
     const uint32_t d = threadIdx.x;
     const uint64_t v = d < F ? totals[d] : 0;
@@ -1722,8 +1782,9 @@ __global__ __launch_bounds__(1024) void k_pool_layout(const uint64_t *__restrict
     uint64_t tot;
     const uint64_t ex_t = block_excl_scan_u64(tup, scratch, &tot);
     const uint64_t ex_b = block_excl_scan_u64(blk, scratch, &tot);
-    // chain-aligned slots (chain_nseg > 0: launch_chain_scan) or kPass2Ents-block segments
-    const uint32_t T = chain_nseg ? chain_slot_target(blk, chain_nseg) : kPass2Ents;
+    // chain-aligned slots (chain_mode > 0: launch_chain_scan; mode 2 reserves slots for
+    // its smallest target) or kPass2Ents-block segments
+    const uint32_t T = chain_mode == 2 ? kPass2Ents / 2 : chain_mode ? chain_slot_target(blk, chain_nseg) : kPass2Ents;
     const uint64_t ns = (blk + T - 1) / T;
     const uint64_t ex_s = block_excl_scan_u64(ns, scratch, &tot);
     if (d < F) {
@@ -1738,14 +1799,14 @@ __global__ __launch_bounds__(1024) void k_pool_layout(const uint64_t *__restrict
 
 hipError_t launch_pool_layout(uint64_t *cnt, uint32_t nseg, uint32_t bits, uint64_t *totals, uint64_t *start,
                               uint64_t *count, uint64_t *lbase, uint64_t *lcount, uint32_t *seg_base, hipStream_t s,
-                              bool chain_slots) {
+                              uint32_t chain_mode) {
     const uint32_t F = 1u << bits;
     hipLaunchKernelGGL(k_scan_cols, dim3(F), dim3(kBlock), 0, s, cnt, nseg, totals);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const uint32_t threads = F < 64 ? 64 : F;
     hipLaunchKernelGGL(k_pool_layout, dim3(1), dim3(threads), 0, s, totals, F, start, count, lbase, lcount, seg_base,
-                       chain_slots ? nseg : 0u);
+                       nseg, chain_mode);
     return hipGetLastError();
 }
 
@@ -1931,7 +1992,7 @@ __device__ __forceinline__ void join_reduce_last(const uint64_t *__restrict__ co
                                                  uint64_t *__restrict__ result, uint64_t *__restrict__ ticket,
                                                  uint64_t *red) {
     const uint32_t nw = blockDim.x / kWave;
-    if (!arrive_last(ticket, gridDim.x, reinterpret_cast<uint32_t *>(red + nw + 1))) return;
+    if (!arrive_last_spread(ticket, gridDim.x, blockIdx.x, reinterpret_cast<uint32_t *>(red + nw + 1))) return;
     uint64_t acc = 0, b = 0, p = 0;
     for (uint32_t i = threadIdx.x; i < gridDim.x; i += blockDim.x) {
         acc += counts[i];
@@ -3081,6 +3142,22 @@ __global__ __launch_bounds__(1024) void k_excl_scan(const uint64_t *__restrict__
         carry += tot;
     }
     if (threadIdx.x == 0) *total = carry;
+}
+
+// Tests: one thread holding a stream for a while (multi_host.cpp's exchange delay,
+// SGXAMD_DEBUG_EXCHANGE_DELAY_US, so that a consumer missing its wait reads early).
+__global__ void k_spin(uint64_t ticks) {
+    const uint64_t t0 = wall_clock64();
+    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(16);
+}
+
+hipError_t launch_spin(uint32_t us, hipStream_t s) {
+    int dev = 0, khz = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0)
+        khz = 100000;
+    hipLaunchKernelGGL(k_spin, dim3(1), dim3(1), 0, s, (uint64_t)us * (uint64_t)khz / 1000);
+    return hipGetLastError();
 }
 
 hipError_t launch_excl_scan(const uint64_t *in, const uint32_t *n_extra, uint64_t n_base, uint64_t *out,

@@ -9,8 +9,8 @@ with a pass-1 histogram and cursors instead of the pooled pass 1 and block-list 
 SGXAMD_POOL_SEGS sets the pooled pass-1 workgroups: 3 gives large pools, 100000 one
 tile per segment), SGXAMD_KEYS=0 (counting joins move whole tuples instead of keys),
 SGXAMD_SORT2=0 (pass 2 of key partitions with the write-combining scatter instead of
-the LDS counting sort), SGXAMD_CHAIN_HIST=0 (the digit side stream and its histogram pass
-instead of the chain histograms counted in pass 1).  The switches are read
+the LDS counting sort), SGXAMD_CHAIN_HIST=1 (the chain histograms counted in pass 1
+instead of the digit side stream and its histogram pass; measured slower, r04k).  The switches are read
 once per process, so each setting runs in a child process against the oracle (the
 TPC-H selections ride along: they share the library's workspace)."""
 import os
@@ -78,7 +78,8 @@ print("paths ok")
                                  {"SGXAMD_DIGIT_SIDE": "1", "SGXAMD_BIG_JOIN": "1"},
                                  {"SGXAMD_SMALL_JOIN": "0"},
                                  {"SGXAMD_POOL": "0"}, {"SGXAMD_POOL_SEGS": "3"}, {"SGXAMD_POOL_SEGS": "100000"},
-                                 {"SGXAMD_KEYS": "0"}, {"SGXAMD_SORT2": "0"}, {"SGXAMD_CHAIN_HIST": "0"}])
+                                 {"SGXAMD_KEYS": "0"}, {"SGXAMD_SORT2": "0"}, {"SGXAMD_CHAIN_HIST": "1"},
+                                 {"SGXAMD_CHAIN_HIST": "1", "SGXAMD_CHAIN_SLOTS": "1"}])
 def test_switch_paths_match_oracle(env):
     e = dict(os.environ, **env)
     e["PYTHONPATH"] = os.pathsep.join([os.path.join(PKG, "python"), os.path.join(ROOT, "oracle"),
@@ -114,7 +115,7 @@ print("chain ok")
 
 @pytest.mark.parametrize("segs", ["8", "512"])
 def test_chain_histograms_skewed(segs):
-    e = dict(os.environ, SGXAMD_POOL_SEGS=segs)
+    e = dict(os.environ, SGXAMD_POOL_SEGS=segs, SGXAMD_CHAIN_HIST="1")
     e["PYTHONPATH"] = os.pathsep.join([os.path.join(PKG, "python"), os.path.join(ROOT, "oracle"),
                                        e.get("PYTHONPATH", "")])
     r = subprocess.run([sys.executable, "-c", CHAIN_CHILD], env=e, capture_output=True, text=True, timeout=110)
