@@ -459,7 +459,8 @@ void plan_relation(Arena &A, RelPlan &rp, uint64_t n, const Policy &pol, int poo
         // blocks (chain_slot_target), at most one partial slot per region either way
         rp.grid2 = (uint32_t)(max_blocks / (rp.chain ? kPass2Ents / 2 : kPass2Ents)) + F1 + 1;
     }
-    rp.hist1 = A.reserve(sizeof(uint64_t) * (size_t)F1 * std::max<uint32_t>(rp.nseg1, 1));
+    // (+ 1: a small join's histogram workgroups write two offsets per 2-tile segment)
+    rp.hist1 = A.reserve(sizeof(uint64_t) * (size_t)F1 * (std::max<uint32_t>(rp.nseg1, 1) + 1));
     rp.tot1 = A.reserve(sizeof(uint64_t) * F1);
     rp.start1 = A.reserve(sizeof(uint64_t) * F1);
     rp.cnt1 = A.reserve(sizeof(uint64_t) * F1);
@@ -870,26 +871,42 @@ int join_small(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const 
     }
     Timer &tm = thread_timer();
     const bool per_kernel = thread_timing_enabled() || (opts && opts->timing);
+    // development: per-workgroup stamps of the three kernels (SGXAMD_DEBUG_STAMPS)
+    static DeviceBuffer stamps;
+    static const bool want_stamps = std::getenv("SGXAMD_DEBUG_STAMPS") != nullptr;
+    if (want_stamps) {
+        RHO_HIP(stamps.ensure(12 * kStampWgs * sizeof(uint64_t)));
+        RHO_HIP(hipMemsetAsync(stamps.ptr, 0, 12 * kStampWgs * sizeof(uint64_t), s));
+        RHO_HIP(set_debug_stamps(stamps.as<uint64_t>()));
+    }
     tm.begin_call(s, per_kernel);  // without per-kernel events the kernels time the call
     volatile uint64_t *hj = ctx->host_join;
     hj[kHostJoinDone] = 0;
     // segments of at least 8192 tuples: fewer digit-total atomics per address (2^20 x 2^20:
     // 4096 / 8192 / 16384 / 32768-tuple segments 67.9 / 58.5 / 64.6 / 85.3 us per join;
     // SGXAMD_SMALL_SEG overrides, development)
+    // a histogram workgroup takes two scatter segments (whole tiles each), so a segment
+    // is an even number of tiles
     static const uint64_t small_seg = [] {
         const char *e = std::getenv("SGXAMD_SMALL_SEG");
         const uint64_t v = e ? std::strtoull(e, nullptr, 10) : 8192;
-        return std::max<uint64_t>(kTile, (v + kTile - 1) / kTile * kTile);
+        return std::max<uint64_t>(2 * kTile, (v + 2 * kTile - 1) / (2 * kTile) * (2 * kTile));
     }();
     for (RelPlan *rp : {&pj.pr, &pj.ps}) {
+        const uint32_t cap = rp->nseg1 + 1;  // the plan's offset table holds F1 x (nseg1 + 1)
         rp->seg1 = std::max<uint64_t>(rp->seg1, small_seg);
         rp->nseg1 = (uint32_t)((rp->n + rp->seg1 - 1) / rp->seg1);
+        if (2 * rp->nseg1 > cap) {
+            set_last_error("small join: segment offsets do not fit the plan's table");
+            return MI355_ERR_INVALID;
+        }
     }
     Arena &A = ctx->scratch;
     uint64_t *sync = ctx->sync.as<uint64_t>();
     uint64_t *result = A.at<uint64_t>(pj.off_result);
     uint64_t *over = A.at<uint64_t>(pj.off_over);
-    const SegMap mR{nullptr, nullptr, nullptr, 1, pj.pr.seg1, nR}, mS{nullptr, nullptr, nullptr, 1, pj.ps.seg1, nS};
+    // the scatter's segments: halves of the histogram workgroups' segments
+    const SegMap mR{nullptr, nullptr, nullptr, 1, pj.pr.seg1 / 2, nR}, mS{nullptr, nullptr, nullptr, 1, pj.ps.seg1 / 2, nS};
     uint64_t *offsR = A.at<uint64_t>(pj.pr.hist1), *offsS = A.at<uint64_t>(pj.ps.hist1);
     uint64_t *startR = A.at<uint64_t>(pj.pr.start1), *cntR = A.at<uint64_t>(pj.pr.cnt1);
     uint64_t *startS = A.at<uint64_t>(pj.ps.start1), *cntS = A.at<uint64_t>(pj.ps.cnt1);
@@ -900,8 +917,8 @@ int join_small(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const 
     tm.mark("RS_pass1_scatter");
     // cursors: each segment's offset inside its copy of the digit totals + that copy's
     // digit start (sync words written by k_hist_pair's last segment of each relation)
-    RHO_HIP(launch_scatter_pair(dR, oR, mR, pj.pr.nseg1, offsR, sync + kSyncStartR, dS, oS, mS, pj.ps.nseg1, offsS,
-                                sync + kSyncStartS,
+    RHO_HIP(launch_scatter_pair(dR, oR, mR, 2 * pj.pr.nseg1, offsR, sync + kSyncStartR, dS, oS, mS, 2 * pj.ps.nseg1,
+                                offsS, sync + kSyncStartS,
                                 pj.key_shift, pol.b1, s));
     tm.mark("join_build_probe");
     const uint64_t P = 1ull << pol.bits;
@@ -924,6 +941,37 @@ int join_small(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const 
     for (int i = 0; i < 6; ++i) ctx->host_result[i] = hj[i];
     tm.collect();
     fill_join_stats(ctx, pj, tm, span, st);
+    if (want_stamps) {
+        RHO_HIP(hipStreamSynchronize(s));
+        RHO_HIP(set_debug_stamps(nullptr));
+        std::vector<uint64_t> h(12 * (size_t)kStampWgs);
+        RHO_HIP(hipMemcpy(h.data(), stamps.ptr, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+        uint64_t t0 = UINT64_MAX;
+        for (uint64_t v : h)
+            if (v) t0 = std::min(t0, v);
+        const double us = 1000.0 / wall_clock_khz();
+        std::fprintf(stderr, "[stamps]");
+        for (int k = 0; k < 4; ++k) {
+            uint64_t e_min = UINT64_MAX, e_max = 0, x_max = 0, h_max = 0;
+            std::vector<double> body;
+            for (uint32_t w = 0; w < kStampWgs; ++w) {
+                const uint64_t e = h[(k * 3 + 0) * kStampWgs + w], m = h[(k * 3 + 1) * kStampWgs + w],
+                               x = h[(k * 3 + 2) * kStampWgs + w];
+                if (!e) continue;
+                e_min = std::min(e_min, e);
+                e_max = std::max(e_max, e);
+                x_max = std::max(x_max, x);
+                if (m) h_max = std::max(h_max, m);
+                if (m) body.push_back((double)(m - e) * us);
+            }
+            std::sort(body.begin(), body.end());
+            std::fprintf(stderr, " k%d: first entry %.1f last entry %.1f body med %.1f max %.1f last pre-handoff %.1f exit %.1f |",
+                         k, (double)(e_min - t0) * us, (double)(e_max - t0) * us,
+                         body.empty() ? 0.0 : body[body.size() / 2], body.empty() ? 0.0 : body.back(),
+                         h_max ? (double)(h_max - t0) * us : 0.0, (double)(x_max - t0) * us);
+        }
+        std::fprintf(stderr, "\n");
+    }
     return MI355_OK;
 }
 

@@ -80,9 +80,16 @@ constexpr uint32_t kSyncTotR = 8, kSyncTotS = kSyncTotR + kSyncSpread * kMaxF;
 constexpr uint32_t kSyncSub = kSyncTotS + kSyncSpread * kMaxF;  // relative to a ticket's word
 constexpr uint32_t kSyncStartR = kSyncSub + kNumTickets * kSyncSpread, kSyncStartS = kSyncStartR + kSyncSpread * kMaxF;
 constexpr uint32_t kSyncWords = kSyncStartS + kSyncSpread * kMaxF;
+// Development: small-join workgroup stamps (rho_kernels.hip dbg_stamp), 3 kernels + the
+// build/probe reduction x 3
+// stamps x kStampWgs u64; null turns them off.
+constexpr uint32_t kStampWgs = 1024;
+hipError_t set_debug_stamps(uint64_t *p);
 
 // Small one-pass joins: histograms of R and S, digit starts / counts and the build/probe
-// task list (meta as launch_make_tasks) in one launch.  offs: [d][g] segment offsets
+// task list (meta as launch_make_tasks) in one launch.  gridR / gridS workgroups each
+// take two segments of mR / mS (2g, 2g + 1; the scatter's segments).  offs: [d][2 grid]
+// segment offsets
 // inside the segment's copy (g mod kSyncSpread) of digit d's total; the copies' digit
 // starts land in sync[kSyncStartR / kSyncStartS] (the bases of launch_scatter_pair).
 hipError_t launch_hist_pair(const row_t *R, const SegMap &mR, uint32_t gridR, const row_t *S, const SegMap &mS,

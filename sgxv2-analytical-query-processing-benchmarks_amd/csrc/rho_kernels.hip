@@ -20,6 +20,17 @@ namespace rho {
 
 constexpr int kWaves = kBlock / kWave;
 
+// Development (SGXAMD_DEBUG_STAMPS, rho_host.cpp join_small): wall-clock stamps of the
+// small join's workgroups, [kernel][stamp][workgroup] — 0: entry, 1: before the
+// hand-off, 2: exit; null (the default) records nothing.
+__device__ uint64_t *g_stamps = nullptr;
+__device__ __forceinline__ void dbg_stamp(uint32_t kernel, uint32_t which) {
+    uint64_t *p = g_stamps;
+    if (p != nullptr && threadIdx.x == 0)
+        p[(kernel * 3 + which) * kStampWgs + min(blockIdx.x, kStampWgs - 1)] = wall_clock64();
+}
+hipError_t set_debug_stamps(uint64_t *p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &p, sizeof(p)); }
+
 // Segment g -> [b, e) of the input and its region r.  Block-uniform; contains a
 // __syncthreads() (every thread of the block must call it).
 __device__ __forceinline__ bool seg_lookup(const SegMap &m, uint32_t g, uint32_t *lds_base, uint32_t &r,
@@ -96,6 +107,50 @@ __device__ __forceinline__ bool hist_segment(const uint32_t *__restrict__ in_wor
         atomicAdd(&h[(q.z >> shift) & mask], 1u);
     }
     if (((e - b2) & 1) && threadIdx.x == 0) atomicAdd(&h[(in_words[2 * (e - 1)] >> shift) & mask], 1u);
+    __syncthreads();
+    return true;
+}
+
+// Histograms of two consecutive segments of a single-region map (2g and 2g + 1, even
+// starts) into h / h2 with both segments' 16-B loads in flight together (one memory round
+// trip per step instead of one per segment).  false: both empty.
+__device__ __forceinline__ bool hist_two_segments(const uint32_t *__restrict__ in_words, const SegMap &m, uint32_t g,
+                                                  uint32_t shift, uint32_t bits, uint32_t *h, uint32_t *h2) {
+    const uint64_t n = m.single_n, seg = m.seg_size;
+    const uint64_t bA = min<uint64_t>(2ull * g * seg, n), eA = min<uint64_t>(bA + seg, n), eB = min<uint64_t>(eA + seg, n);
+    if (bA >= eB) return false;
+    const uint32_t F = 1u << bits, mask = F - 1;
+    for (uint32_t d = threadIdx.x; d < F; d += blockDim.x) h[d] = h2[d] = 0;
+    __syncthreads();
+    const uint64_t *in64 = reinterpret_cast<const uint64_t *>(in_words);
+    const uint4 *pa = reinterpret_cast<const uint4 *>(in64 + bA), *pb = reinterpret_cast<const uint4 *>(in64 + eA);
+    const uint64_t npa = (eA - bA) / 2, npb = (eB - eA) / 2, np = npa > npb ? npa : npb;
+    constexpr int U = 8;
+    for (uint64_t i = threadIdx.x; i < np; i += U * kBlock) {
+        uint4 qa[U], qb[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t k = i + u * kBlock;
+            qa[u] = k < npa ? ld_nt(pa + k) : make_uint4(0, 0, 0, 0);
+            qb[u] = k < npb ? ld_nt(pb + k) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t k = i + u * kBlock;
+            if (k < npa) {
+                atomicAdd(&h[(qa[u].x >> shift) & mask], 1u);
+                atomicAdd(&h[(qa[u].z >> shift) & mask], 1u);
+            }
+            if (k < npb) {
+                atomicAdd(&h2[(qb[u].x >> shift) & mask], 1u);
+                atomicAdd(&h2[(qb[u].z >> shift) & mask], 1u);
+            }
+        }
+    }
+    if (threadIdx.x == 0) {  // odd trailing tuples (segments start at even offsets)
+        if ((eA - bA) & 1) atomicAdd(&h[(in_words[2 * (eA - 1)] >> shift) & mask], 1u);
+        if ((eB - eA) & 1) atomicAdd(&h2[(in_words[2 * (eB - 1)] >> shift) & mask], 1u);
+    }
     __syncthreads();
     return true;
 }
@@ -206,23 +261,29 @@ __global__ __launch_bounds__(kBlock) void k_hist_pair(HistPairRel A, HistPairRel
                                                       uint64_t *__restrict__ ticket2, uint64_t *__restrict__ over,
                                                       uint32_t over_cap, uint64_t *__restrict__ meta,
                                                       uint64_t s_chunk) {
-    __shared__ uint32_t h[kMaxF];
-    __shared__ uint32_t sbase[kMaxF + 1];
+    __shared__ uint32_t h[kMaxF], h2[kMaxF];
     __shared__ uint64_t scratch[kWaves + 1];
     __shared__ uint32_t flag;
     const bool isB = blockIdx.x >= A.grid;
     const HistPairRel &H = isB ? B : A;
-    const uint32_t g = isB ? blockIdx.x - A.grid : blockIdx.x;
+    const uint32_t g = isB ? blockIdx.x - A.grid : blockIdx.x;  // segment g = scatter segments 2g, 2g + 1
     const uint32_t F = 1u << bits;
     if (blockIdx.x == 0 && threadIdx.x == 0)  // the call's start (small-join device span)
         ticket2[kSyncT0 - kSyncTicket2] = wall_clock64();
-    const bool any = hist_segment(H.in, H.m, g, H.shift, bits, h, sbase);
+    dbg_stamp(0, 0);
+    // segment g is two scatter segments (H.m's, halves 2g and 2g + 1: one tile each, so
+    // that the scatter's workgroups each load, sort and write one tile): one histogram
+    // each, their sum to the totals, the second half's offset after the first half's
+    const bool any = hist_two_segments(H.in, H.m, g, H.shift, bits, h, h2);
     uint64_t *tot_c = H.tot + (uint64_t)(g % kSyncSpread) * kMaxF;  // this segment's copy of the totals
     for (uint32_t d = threadIdx.x; d < F; d += kBlock) {
-        const uint32_t v = any ? h[d] : 0u;
-        H.offs[(uint64_t)d * H.grid + g] =
+        const uint32_t a = any ? h[d] : 0u, v = a + (any ? h2[d] : 0u);
+        const uint64_t off =
             v ? __hip_atomic_fetch_add(&tot_c[d], (uint64_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+        H.offs[(uint64_t)d * 2 * H.grid + 2 * g] = off;
+        H.offs[(uint64_t)d * 2 * H.grid + 2 * g + 1] = off + a;
     }
+    dbg_stamp(0, 1);
     if (!arrive_last_spread(H.ticket, H.grid, g, &flag)) return;
     // the relation's last segment: digit starts and counts, and each copy's bases
     uint64_t carry = 0;
@@ -270,6 +331,7 @@ __global__ __launch_bounds__(kBlock) void k_hist_pair(HistPairRel A, HistPairRel
         meta[1] = ms;
         meta[2] = base;  // n_over (u32, low word; the high word is 0)
     }
+    dbg_stamp(0, 2);
 }
 
 hipError_t launch_hist_pair(const row_t *R, const SegMap &mR, uint32_t gridR, const row_t *S, const SegMap &mS,
@@ -1130,8 +1192,10 @@ __global__ __launch_bounds__(NT, (scatter_waves_per_simd<BITS, ITEMS, NT>())) vo
     const bool isB = blockIdx.x >= A.grid;
     const ScatterPairRel &P = isB ? B : A;
     const uint32_t g = isB ? blockIdx.x - A.grid : blockIdx.x;
+    dbg_stamp(1, 0);
     scatter_segment<BITS, ITEMS, NT, false>(L, g, P.in, P.out, P.m, shift, P.offs, kDigitMajor, P.grid,
                                             P.cstart + (uint64_t)(g % kSyncSpread) * kMaxF, nullptr, 0, 0);
+    dbg_stamp(1, 2);
 }
 
 hipError_t launch_scatter_pair(const row_t *R, row_t *outR, const SegMap &mR, uint32_t gridR, const uint64_t *offsR,
@@ -1990,23 +2054,44 @@ hipError_t launch_hist_side_blk(const uint8_t *side, const uint64_t *list, const
 // result[0] / [4] / [5].  red: NW + 2 u64 of LDS (NW = waves per workgroup).
 __device__ __forceinline__ void join_reduce_last(const uint64_t *__restrict__ counts, const uint64_t *__restrict__ cyc,
                                                  uint64_t *__restrict__ result, uint64_t *__restrict__ ticket,
-                                                 uint64_t *red) {
+                                                 uint64_t *red, uint64_t tasks) {
     const uint32_t nw = blockDim.x / kWave;
-    if (!arrive_last_spread(ticket, gridDim.x, blockIdx.x, reinterpret_cast<uint32_t *>(red + nw + 1))) return;
+    // workgroups without a task (blockIdx >= tasks; their count slots are 0) do not take
+    // a ticket: every arrival is a device atomic on one address, serialised (≈ 14 ns each)
+    const uint64_t n = tasks < gridDim.x ? tasks : gridDim.x;
+    if (blockIdx.x >= n && n > 0) return;
+    if (!arrive_last_spread(ticket, n > 0 ? n : gridDim.x, blockIdx.x, reinterpret_cast<uint32_t *>(red + nw + 1)))
+        return;
+    dbg_stamp(3, 0);
     uint64_t acc = 0, b = 0, p = 0;
-    for (uint32_t i = threadIdx.x; i < gridDim.x; i += blockDim.x) {
+    // only the arrivals' slots (an idle workgroup's slot was never released to this one)
+    const uint32_t na = (uint32_t)(n > 0 ? n : gridDim.x);
+    for (uint32_t i = threadIdx.x; i < na; i += blockDim.x) {
         acc += counts[i];
         if (cyc) {
             b += cyc[2 * i];
             p += cyc[2 * i + 1];
         }
     }
-    uint64_t t, tb = 0, tp = 0;
-    (void)block_excl_scan_u64(acc, red, &t);
-    if (cyc) {
-        (void)block_excl_scan_u64(b, red, &tb);
-        (void)block_excl_scan_u64(p, red, &tp);
+    // the three sums in one block reduction (wave sums, one barrier, thread 0 adds)
+    acc = wave_sum_u64(acc);
+    b = wave_sum_u64(b);
+    p = wave_sum_u64(p);
+    __shared__ uint64_t wsum[3][1024 / kWave];
+    if (__lane_id() == 0) {
+        wsum[0][threadIdx.x / kWave] = acc;
+        wsum[1][threadIdx.x / kWave] = b;
+        wsum[2][threadIdx.x / kWave] = p;
     }
+    __syncthreads();
+    uint64_t t = 0, tb = 0, tp = 0;
+    if (threadIdx.x == 0)
+        for (uint32_t w = 0; w < nw; ++w) {
+            t += wsum[0][w];
+            tb += wsum[1][w];
+            tp += wsum[2][w];
+        }
+    dbg_stamp(3, 1);
     if (threadIdx.x == 0) {
         result[0] = t;
         if (cyc) {
@@ -2015,7 +2100,8 @@ __device__ __forceinline__ void join_reduce_last(const uint64_t *__restrict__ co
         }
         // the call's result block in mapped host memory (kSyncHostResult): all six words
         // (result[1..3] come from the launches before this one), the device span, then
-        // the done flag the host spins on -- the kernel's last memory operation
+        // the done flag the host spins on -- the kernel's last memory operation (the
+        // kernel's end releases it; one system fence orders the words before it)
         volatile uint64_t *h = reinterpret_cast<volatile uint64_t *>(ticket[kSyncHostResult - kSyncTicketJoin]);
         if (h) {
             h[0] = t;
@@ -2027,9 +2113,9 @@ __device__ __forceinline__ void join_reduce_last(const uint64_t *__restrict__ co
             h[kHostJoinSpan] = wall_clock64() - ticket[kSyncT0 - kSyncTicketJoin];
             __threadfence_system();
             h[kHostJoinDone] = 1;
-            __threadfence_system();
         }
     }
+    dbg_stamp(3, 2);
 }
 
 __device__ __forceinline__ void tmatch_add(uint64_t &m, bool hit) { m += hit ? 1u : 0u; }
@@ -2088,6 +2174,7 @@ __global__ __launch_bounds__(BLOCK) void k_join(const uint64_t *__restrict__ R, 
     __shared__ JoinLds<RCAP, MODE, NW> L;
     const uint32_t *Rk = reinterpret_cast<const uint32_t *>(R), *Sk = reinterpret_cast<const uint32_t *>(S);
     const uint32_t tid = threadIdx.x, lane = __lane_id();
+    dbg_stamp(2, 0);
     const uint64_t T = P + *n_over;
     uint64_t matches = 0;
     uint64_t bcyc = 0, pcyc = 0;  // build / probe wall-clock ticks of this workgroup
@@ -2239,9 +2326,11 @@ __global__ __launch_bounds__(BLOCK) void k_join(const uint64_t *__restrict__ R, 
         cyc[2 * blockIdx.x] = bcyc;
         cyc[2 * blockIdx.x + 1] = pcyc;
     }
+    dbg_stamp(2, 1);
     if constexpr (MODE == kJoinCount) {
-        if (red_ticket) join_reduce_last(counts, cyc, red_result, red_ticket, L.red);
+        if (red_ticket) join_reduce_last(counts, cyc, red_result, red_ticket, L.red, T);
     }
+    dbg_stamp(2, 2);
 }
 
 // ------------------------------ 16,384-key counting table with exchange links (X) ---
@@ -2573,7 +2662,7 @@ __global__ __launch_bounds__(BLOCK, 1) void k_join_x(
         counts[i] = 0;
         if (cyc) cyc[2 * i] = cyc[2 * i + 1] = 0;
     }
-    if (red_ticket) join_reduce_last(counts, cyc, red_result, red_ticket, L.red);
+    if (red_ticket) join_reduce_last(counts, cyc, red_result, red_ticket, L.red, tk.T);
 }
 
 // ------------------------------------------------------- histogram join (RHT) ---
@@ -2784,7 +2873,7 @@ __global__ __launch_bounds__(BLOCK) void k_join_hist(const uint64_t *__restrict_
         cyc[2 * blockIdx.x + 1] = pcyc;
     }
     if constexpr (MODE == kJoinCount) {
-        if (red_ticket) join_reduce_last(counts, cyc, red_result, red_ticket, L.red);
+        if (red_ticket) join_reduce_last(counts, cyc, red_result, red_ticket, L.red, T);
     }
 }
 
@@ -2940,7 +3029,7 @@ __global__ __launch_bounds__(1024, 8) void k_join_hist_big(
         cyc[2 * blockIdx.x] = bcyc;
         cyc[2 * blockIdx.x + 1] = pcyc;
     }
-    if (red_ticket) join_reduce_last(counts, cyc, red_result, red_ticket, L.red);
+    if (red_ticket) join_reduce_last(counts, cyc, red_result, red_ticket, L.red, T);
 }
 
 // Multiprocessors of the current device: k_join_x runs one workgroup per CU.
