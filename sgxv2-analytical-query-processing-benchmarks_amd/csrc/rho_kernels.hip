@@ -1592,6 +1592,15 @@ __global__ __launch_bounds__(NT, NT * SGXAMD_SORT_WGS / 256) void k_sort_blk(con
         return vm;
     };
     const auto sort_write = [&](const uint32_t(&k)[ITEMS], uint32_t vm) {
+#if SGXAMD_ABLATE_SORT2 == 1  // development ablation: the tile's keys copied in load order (no sort)
+        {
+            const uint64_t base = ((uint64_t)g * 4 * TILE) % (1ull << 27);
+#pragma unroll
+            for (int u = 0; u < (int)ITEMS; ++u)
+                if ((vm >> u) & 1u) out[base + tid + (uint32_t)u * NT] = k[u];
+            return;
+        }
+#endif
         // A. rank of every key inside its digit (tile histogram at once)
         uint32_t rd[ITEMS];
 #pragma unroll
@@ -1634,7 +1643,11 @@ __global__ __launch_bounds__(NT, NT * SGXAMD_SORT_WGS / 256) void k_sort_blk(con
                 const uint32_t x = L.sorted[q];
                 // a plain (write-back) store: the lines a store leaves partial are
                 // completed in L2 by the next wave or tile, not sent to HBM in pieces
+#if SGXAMD_ABLATE_SORT2 == 2  // development ablation: the sort without its stores
+                if (x == 0xFFFFFFFFu) out[L.off[(x >> shift) & mask] + q] = x;
+#else
                 out[L.off[(x >> shift) & mask] + q] = x;
+#endif
             }
         }
         // the next tile's phase A touches only cnt (zeroed in B); its C comes after a barrier
@@ -1743,7 +1756,6 @@ bool sort2_enabled() {
     }();
     return on;
 }
-
 template <typename T>
 hipError_t launch_scatter_blk_t(const void *in, const uint64_t *list, void *out, const SegMap &m, uint32_t grid,
                                 uint32_t shift, uint32_t bits, const uint64_t *cursors, hipStream_t s) {
