@@ -265,7 +265,7 @@ int partition_relation_pooled(Context *ctx, hipStream_t s, Timer &tm, const std:
         tm.mark((t + "pass1_scan").c_str());
         RHO_HIP(launch_pool_layout(po.cnt, rp.nseg1, pol.b1, A.at<uint64_t>(rp.tot1), start1, cnt1, lbase, lcount,
                                    segbase2, s, rp.chain ? chain_slot_mode() : 0u));
-        RHO_HIP(launch_block_list(po, lbase, list, s));
+        RHO_HIP(launch_block_list(po, lbase, list, pol.b1, s));
         *final_rel = t1;
         *pstart = start1;
         *pcnt = cnt1;

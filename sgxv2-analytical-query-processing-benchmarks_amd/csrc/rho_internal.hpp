@@ -181,7 +181,7 @@ hipError_t launch_pool_layout(uint64_t *cnt, uint32_t nseg, uint32_t bits, uint6
                               uint32_t chain_mode = 0);
 // The block list: region d's blocks at [lbase[d], lbase[d] + lcount[d]) as
 // physical block | fill << 32.
-hipError_t launch_block_list(const PoolOut &po, const uint64_t *lbase, uint64_t *list, hipStream_t s);
+hipError_t launch_block_list(const PoolOut &po, const uint64_t *lbase, uint64_t *list, uint32_t bits, hipStream_t s);
 // Pass-2 histogram / scatter over block-list segments (m: reg_start = lbase,
 // reg_count = lcount, seg_size = kPass2Ents).
 hipError_t launch_hist_side_blk(const uint8_t *side, const uint64_t *list, const SegMap &m, uint32_t grid,
