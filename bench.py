@@ -250,15 +250,18 @@ def spawn_ranks(args, argv: list[str]) -> int:
 
 
 def algorithmic_bytes(kernel: str, nR: int, nS: int, passes: int = 2, pass2_bits: int = 8, elem: int = 8,
-                      layout: int = 2) -> int:
+                      layout: int = 2, narrow: int = 0) -> int:
     """Bytes a kernel must move per launch (DESIGN.md 'Kernels and their rooflines').
 
     Two-pass plans: the pass-1 scatter also writes one pass-2 digit byte per tuple (the
     digit side stream) and the pass-2 histogram reads those bytes, not the tuples.
     elem: bytes per partitioned element after the input read — 8 (row_t tuples) or 4
     (counting joins move keys only: the pass-1 scatter reads 8-byte tuples and
-    writes 4-byte keys, pass 2 and the build/probe read and write keys)."""
+    writes 4-byte keys, pass 2 and the build/probe read and write keys).
+    narrow (mi355_rho_stats.narrow, bit 0 R / bit 1 S): that relation's final partitions
+    hold 2-byte key residuals — its pass 2 writes 2 bytes per key, the build/probe reads 2."""
     n = nR if kernel.startswith("R_") else nS
+    nar = bool(narrow & (1 if kernel.startswith("R_") else 2))
     # uses_digit_side(); layout 3 (chain histograms) writes and reads no side stream
     side = (passes == 2 and pass2_bits <= 8 and os.environ.get("SGXAMD_DIGIT_SIDE", "1") != "0" and layout != 3)
     if kernel.endswith("pass2_hist") and side:
@@ -268,10 +271,16 @@ def algorithmic_bytes(kernel: str, nR: int, nS: int, passes: int = 2, pass2_bits
     if kernel.endswith("pass1_scatter"):
         return (8 + elem + (1 if side else 0)) * n  # read the tuple, write the element (+ its digit byte)
     if kernel.endswith("_scatter"):
-        return 2 * elem * n   # read + write every element
-    if kernel == "join_build_probe":
-        return elem * (nR + nS)  # every partitioned element read once
+        return (elem + (2 if nar else elem)) * n  # read + write every element
+    if kernel == "join_build_probe":  # every partitioned element read once
+        return (2 if narrow & 1 else elem) * nR + (2 if narrow & 2 else elem) * nS
     return 0
+
+
+def plan_of(ls: dict) -> tuple:
+    """algorithmic_bytes' plan arguments from a join's statistics."""
+    return (ls.get("passes") or 2, ls.get("pass2_bits") or 0, ls.get("elem_bytes") or 8, ls.get("layout") or 0,
+            ls.get("narrow") or 0)
 
 
 def main():
@@ -495,8 +504,7 @@ def main():
     nR = results[-1].recv_r
     nS = results[-1].recv_s
     avg = {k: statistics.mean(v) for k, v in per_kernel.items()}
-    plan = (results[-1].local_stats.get("passes") or 2, results[-1].local_stats.get("pass2_bits") or 0,
-            results[-1].local_stats.get("elem_bytes") or 8, results[-1].local_stats.get("layout") or 0)
+    plan = plan_of(results[-1].local_stats)
     byte_kernels = {k: v for k, v in avg.items() if algorithmic_bytes(k, nR, nS, *plan) > 0}
     dom = max(byte_kernels, key=byte_kernels.get)
     achieved = algorithmic_bytes(dom, nR, nS, *plan) / (avg[dom] * 1e-3) / 1e9
@@ -525,6 +533,9 @@ def main():
         "partition_overlap": bool(args.partition_overlap),
         "radix_bits": ls.get("radix_bits"), "passes": ls.get("passes"),
         "partition_layout": LAYOUTS.get(ls.get("layout"), "unknown"),
+        "narrow_partitions": {"R": bool((ls.get("narrow") or 0) & 1), "S": bool((ls.get("narrow") or 0) & 2),
+                              "what": "final partitions hold 2-byte key residuals (key >> radix bits): every "
+                                      "key's residual fits 16 bits (pass 1's key OR)"},
         "step_ms_breakdown": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in results[-1].ms.items()},
     }
     if args.workload == "c5":
@@ -542,8 +553,7 @@ def main():
             sgxamd.set_key_layout(True)
         avg_t = {k: statistics.mean(v) for k, v in pk_t.items()}
         ls_t = res_t[-1].local_stats
-        plan_t = (ls_t.get("passes") or 2, ls_t.get("pass2_bits") or 0, ls_t.get("elem_bytes") or 8,
-                  ls_t.get("layout") or 0)
+        plan_t = plan_of(ls_t)
         pb_t = algorithmic_bytes("join_build_probe", nR, nS, *plan_t) / (avg_t["join_build_probe"] * 1e-3) / 1e9
         rho_info["tuple_layout"] = {
             "partition_layout": LAYOUTS.get(ls_t.get("layout"), "unknown"), "timed": "untimed for value; own K steps",
@@ -575,8 +585,7 @@ def main():
             avg_w = {k: statistics.mean(v) for k, v in pk_w.items()}
             nRw, nSw = res_w[-1].recv_r, res_w[-1].recv_s
             ls_w = res_w[-1].local_stats
-            plan_w = (ls_w.get("passes") or 2, ls_w.get("pass2_bits") or 0, ls_w.get("elem_bytes") or 8,
-                      ls_w.get("layout") or 0)
+            plan_w = plan_of(ls_w)
             pb = algorithmic_bytes("join_build_probe", nRw, nSw, *plan_w) / (avg_w["join_build_probe"] * 1e-3) / 1e9
             configs_info[wl] = {
                 "workload": desc_w, "generator": gen_w, "scaling": "strong", "global_R": gRw, "global_S": gSw,

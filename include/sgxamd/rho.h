@@ -83,6 +83,10 @@ typedef struct mi355_rho_stats {
      * 3 = as 2, with the pass-2 digits counted per chain in pass 1 (no digit side stream) */
     uint32_t layout;
     uint32_t elem_bytes;      /* bytes per partitioned element after the input read (8 or 4) */
+    /* bit 0 / bit 1: R's / S's final partitions hold 16-bit key residuals (key >> radix
+     * bits, when every key's residual fits; counting RHO over key partitions) */
+    uint32_t narrow;
+    uint32_t reserved0;
 } mi355_rho_stats;
 
 /* Number of gfx950 devices visible (0 on a CPU-only host). */

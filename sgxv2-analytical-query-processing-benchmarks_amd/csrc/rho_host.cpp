@@ -158,6 +158,17 @@ inline bool keys_enabled() {
 // Off by default: the chain-aligned pass-2 segments made k_sort_blk 0.05 ms slower per
 // relation than the histogram pass they replace saves (r04k).
 // SGXAMD_CHAIN_HIST=1 takes them (development A/B switch; results identical).
+// Narrow key partitions (counting RHO with the 16,384-key table over key partitions):
+// pass 1 ORs every key, and when the residuals above the radix bits fit 16 bits, pass 2
+// writes them as u16 and the build/probe reads 2 instead of 4 bytes per key
+// (launch_scatter_blk).  SGXAMD_NARROW=0 keeps 4-byte keys (development A/B switch).
+inline bool narrow_enabled() {
+    static const bool on = [] {
+        const char *e = std::getenv("SGXAMD_NARROW");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return on;
+}
 inline bool chain_enabled() {
     static const bool on = [] {
         const char *e = std::getenv("SGXAMD_CHAIN_HIST");
@@ -208,6 +219,8 @@ struct RelPlan {
     size_t hist1, tot1, start1, cnt1, segbase2, hist2, pstart, pcnt;
     size_t binfo, used, lbase, lcount, list;
     size_t chist, seglb, segle, segc0;  // chain histograms [F1][nseg1][F2], pass-2 segment ranges
+    size_t kor;    // pooled keys: the segments' key ORs, then the relation's ([nseg1])
+    bool narrow;   // pass 2 writes u16 residuals when the key OR allows (plan_join)
     // pooled pass 1 per input piece (the multi-GPU exchange's received pieces): piece i is
     // elements [piece_off[i], + piece_n[i]), its segments start at piece_g0[i]; its launch
     // waits for piece_ev[i] (null: no wait)
@@ -240,6 +253,7 @@ int partition_relation_pooled(Context *ctx, hipStream_t s, Timer &tm, const std:
     if (!pass2_now) {
         PoolOut po{A.at<uint32_t>(rp.binfo), A.at<uint64_t>(rp.hist1), A.at<uint32_t>(rp.used), rp.pool_blocks,
                    rp.nseg1};
+        po.kor = rp.narrow ? A.at<uint32_t>(rp.kor) : nullptr;
         const DigitSide ds{rp.chain ? nullptr : side, key_shift + pol.b1, pol.b2};
         uint32_t *chist = rp.chain ? A.at<uint32_t>(rp.chist) : nullptr;
         tm.mark((t + "pass1_scatter").c_str());
@@ -264,7 +278,7 @@ int partition_relation_pooled(Context *ctx, hipStream_t s, Timer &tm, const std:
         }
         tm.mark((t + "pass1_scan").c_str());
         RHO_HIP(launch_pool_layout(po.cnt, rp.nseg1, pol.b1, A.at<uint64_t>(rp.tot1), start1, cnt1, lbase, lcount,
-                                   segbase2, s, rp.chain ? chain_slot_mode() : 0u));
+                                   segbase2, s, rp.chain ? chain_slot_mode() : 0u, po.kor));
         RHO_HIP(launch_block_list(po, lbase, list, pol.b1, s));
         *final_rel = t1;
         *pstart = start1;
@@ -275,6 +289,7 @@ int partition_relation_pooled(Context *ctx, hipStream_t s, Timer &tm, const std:
     uint64_t *ps = A.at<uint64_t>(rp.pstart);
     uint64_t *pc = A.at<uint64_t>(rp.pcnt);
     const SegMap m2{lbase, lcount, segbase2, F1, kPass2Ents, rp.n};
+    const uint32_t *narrow = rp.narrow ? A.at<uint32_t>(rp.kor) + rp.nseg1 : nullptr;
     if (rp.chain) {
         // the chain histograms (recounted where a count may have wrapped) give the
         // chain-aligned pass-2 segments, their cursors and the partition table
@@ -291,7 +306,7 @@ int partition_relation_pooled(Context *ctx, hipStream_t s, Timer &tm, const std:
         mc.seg_lb = seglb;
         mc.seg_le = segle;
         tm.mark((t + "pass2_scatter").c_str());
-        RHO_HIP(launch_scatter_blk(t1, list, t2, 4u, mc, rp.grid2, key_shift + pol.b1, pol.b2, hist2, s));
+        RHO_HIP(launch_scatter_blk(t1, list, t2, 4u, mc, rp.grid2, key_shift + pol.b1, pol.b2, hist2, s, narrow));
         *final_rel = t2;
         *pstart = ps;
         *pcnt = pc;
@@ -302,7 +317,8 @@ int partition_relation_pooled(Context *ctx, hipStream_t s, Timer &tm, const std:
     tm.mark((t + "pass2_scan").c_str());
     RHO_HIP(launch_scan_regions(hist2, segbase2, start1, F1, pol.b2, ps, pc, s));
     tm.mark((t + "pass2_scatter").c_str());
-    RHO_HIP(launch_scatter_blk(t1, list, t2, rp.keys ? 4u : 8u, m2, rp.grid2, key_shift + pol.b1, pol.b2, hist2, s));
+    RHO_HIP(launch_scatter_blk(t1, list, t2, rp.keys ? 4u : 8u, m2, rp.grid2, key_shift + pol.b1, pol.b2, hist2, s,
+                               narrow));
     *final_rel = t2;
     *pstart = ps;
     *pcnt = pc;
@@ -417,6 +433,8 @@ void plan_relation(Arena &A, RelPlan &rp, uint64_t n, const Policy &pol, int poo
     rp.pooled = false;
     rp.keys = false;
     rp.chain = false;
+    rp.narrow = false;
+    rp.kor = 0;
     rp.in_size = sizeof(row_t);
     rp.piece_off.clear();
     rp.piece_n.clear();
@@ -476,6 +494,7 @@ void plan_relation(Arena &A, RelPlan &rp, uint64_t n, const Policy &pol, int poo
         rp.lbase = A.reserve(sizeof(uint64_t) * F1);
         rp.lcount = A.reserve(sizeof(uint64_t) * F1);
         rp.list = A.reserve(sizeof(uint64_t) * (size_t)(rp.n / kBlk + (uint64_t)rp.nseg1 * F1));
+        if (rp.keys) rp.kor = A.reserve(sizeof(uint32_t) * ((size_t)rp.nseg1 + 1));
     }
     if (rp.chain) {
         rp.chist = A.reserve(sizeof(uint32_t) * (size_t)F1 * rp.nseg1 * F2);
@@ -573,6 +592,11 @@ int plan_join(Context *ctx, hipStream_t s, uint64_t nR, uint64_t nS, const mi355
         // and 5) the 32,768-key chunks split hot partitions finer (Zipf: 0.544 vs 0.56 ms)
         pj.s_chunk = avgS >= kBigSPart ? kBigSPart : kBigSChunk;
     }
+    // narrow key partitions: the counting chaining join over key partitions with the
+    // 16,384-key table (k_sort_blk writes them, k_join_x reads them)
+    const bool narrow = pool == kPoolKeys && counting && pj.algo == kAlgoChaining && pj.pol.rcap == kBigRcap &&
+                        pol.passes == 2 && sort2_enabled() && narrow_enabled();
+    pj.pr.narrow = pj.ps.narrow = narrow;
     pj.over_cap = (uint32_t)(nS / pj.s_chunk + 1);
     // one workgroup per task up to 2048 (few partitions with a large S — a tiny build
     // side — still spread their S chunks over the chip)
@@ -642,6 +666,8 @@ void fill_join_stats(const Context *ctx, const PendingJoin &pj, const Timer &tm,
         st->pass2_bits = pol.b2;
         st->layout = pj.pr.chain ? 3u : (pj.pr.keys ? 2u : (pj.pr.pooled ? 1u : 0u));
         st->elem_bytes = pj.pr.keys ? 4u : 8u;
+        // (k_join_x: the high word of result[6] = 1 | narrow R << 1 | narrow S << 2)
+        st->narrow = (uint32_t)(ctx->host_result[6] >> 33) & 3u;
         st->num_partitions = P;
         st->num_tasks = P + (uint32_t)ctx->host_result[3];
         st->max_part_r = ctx->host_result[1];
@@ -731,7 +757,9 @@ int join_finish(Context *ctx, PendingJoin &pj, const row_t *dS, uint64_t nS, mi3
         tm.mark("join_build_probe");
         RHO_HIP(launch_join(fR, fS, psR, pcR, psS, pcS, P, over, n_over, hash_shift, pol.rcap, pj.s_chunk, join_grid,
                             kJoinCount, algo, counts, nullptr, nullptr, cyc, s, nullptr, pj.pr.keys ? 1 : 2,
-                            reinterpret_cast<uint32_t *>(result + 6)));
+                            reinterpret_cast<uint32_t *>(result + 6),
+                            pj.pr.narrow ? A.at<uint32_t>(pj.pr.kor) + pj.pr.nseg1 : nullptr,
+                            pj.ps.narrow ? A.at<uint32_t>(pj.ps.kor) + pj.ps.nseg1 : nullptr));
         tm.mark("join_reduce");
         RHO_HIP(launch_reduce(counts, join_grid, result, cyc, join_grid, s));
     } else {
@@ -763,7 +791,7 @@ int join_finish(Context *ctx, PendingJoin &pj, const row_t *dS, uint64_t nS, mi3
     }
     tm.end_call();
     if (s2) RHO_HIP(hipEventRecord(ctx->ev_t1, s));
-    RHO_HIP(hipMemcpyAsync(ctx->host_result, result, 6 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    RHO_HIP(hipMemcpyAsync(ctx->host_result, result, 7 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     RHO_HIP(hipStreamSynchronize(s));
     if (std::getenv("SGXAMD_DEBUG_WG_TICKS") && !pj.materialize) {
         // development: the build/probe workgroups' wall-clock ticks (load balance)
@@ -939,6 +967,7 @@ int join_small(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const 
         span = (float)((double)hj[kHostJoinSpan] / wall_clock_khz());
     }
     for (int i = 0; i < 6; ++i) ctx->host_result[i] = hj[i];
+    ctx->host_result[6] = 0;  // (no narrow partitions in a small join)
     tm.collect();
     fill_join_stats(ctx, pj, tm, span, st);
     if (want_stamps) {

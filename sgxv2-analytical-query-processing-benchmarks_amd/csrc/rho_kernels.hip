@@ -760,6 +760,7 @@ struct ScatterLds {
                                       //          first granule of the blocks d took for this tile}
     uint64_t ents[EXT == 2 ? kPass2Ents : 1];  // block-list input: phys block | fill << 32
     uint32_t pool_next;               // pooled: blocks taken from the segment's pool
+    uint32_t kor;                     // pooled keys: the OR of the segment's keys
 };
 
 // Chain histograms (pooled pass 1 of keys, F2 > 0): every chain's histogram of pass-2
@@ -1360,7 +1361,10 @@ __device__ __forceinline__ void scatter_segment_ext(ScatterLds<BITS, ITEMS, NT, 
                    (digit_base ? digit_base[(uint64_t)r * F + tid] : 0);
         L.cnt[tid] = 0;
     }
-    if (tid == 0) L.pool_next = 0;
+    if (tid == 0) {
+        L.pool_next = 0;
+        L.kor = 0;
+    }
     if constexpr (F2 > 0) {
         for (uint32_t i = tid; i < F * F2 / 2; i += NT) cs->h2[i] = 0;
     }
@@ -1400,12 +1404,23 @@ __device__ __forceinline__ void scatter_segment_ext(ScatterLds<BITS, ITEMS, NT, 
         return scatter_tile_sort<BITS, ITEMS, NT, EXT, T, false, F2>(L, pend, carried, v, out, tn, shift, 0, &ps,
                                                                      cs);
     };
+    // pooled keys: the OR of the segment's keys (lanes past its end load 0), whether pass
+    // 2 may write 16-bit residuals (k_sort_blk)
+    constexpr bool KOR = EXT == 1 && sizeof(T) == 4;
+    uint32_t kor = 0;
+    const auto key_or = [&](const T(&v)[ITEMS]) {
+        if constexpr (KOR) {
+#pragma unroll
+            for (int k = 0; k < ITEMS; ++k) kor |= (uint32_t)v[k];
+        }
+    };
     // the two-tiles-in-flight pipeline of scatter_segment
     T va[ITEMS], vb[ITEMS];
     uint32_t ma = load(0, va);
     uint32_t mb = load(1, vb);
 #pragma unroll
     for (int k = 0; k < ITEMS; ++k) asm volatile("" ::"v"(va[k]));
+    key_or(va);
     uint32_t gt = sort(va, tn_of(0, ma));
     for (uint32_t ti = 0;; ti += 2) {
         ma = load(ti + 2, va);
@@ -1413,14 +1428,17 @@ __device__ __forceinline__ void scatter_segment_ext(ScatterLds<BITS, ITEMS, NT, 
         for (int k = 0; k < ITEMS; ++k) asm volatile("" ::"v"(vb[k]));
         scatter_tile_write<BITS, ITEMS, NT, SIDE, EXT, T>(L, out, gt, side, shift2, mask2);
         if (ti + 1 >= ntiles) break;
+        key_or(vb);
         gt = sort(vb, tn_of(ti + 1, mb));
         mb = load(ti + 3, vb);
 #pragma unroll
         for (int k = 0; k < ITEMS; ++k) asm volatile("" ::"v"(va[k]));
         scatter_tile_write<BITS, ITEMS, NT, SIDE, EXT, T>(L, out, gt, side, shift2, mask2);
         if (ti + 2 >= ntiles) break;
+        key_or(va);
         gt = sort(va, tn_of(ti + 2, ma));
     }
+    if (KOR && kor) atomicOr(&L.kor, kor);
     // flush the carried (partial) granules; pooled: close every chain
     __syncthreads();
     if (tid < F) {
@@ -1444,7 +1462,10 @@ __device__ __forceinline__ void scatter_segment_ext(ScatterLds<BITS, ITEMS, NT, 
         L.cnt[tid] = carried;
     }
     __syncthreads();
-    if (EXT == 1 && tid == 0) po.used[gp] = L.pool_next;
+    if (EXT == 1 && tid == 0) {
+        po.used[gp] = L.pool_next;
+        if (KOR && po.kor) po.kor[gp] = L.kor;
+    }
     const uint32_t lane = tid & (G - 1);
     for (uint32_t d = tid / G; d < F; d += NG) {
         if (lane < L.cnt[d]) {
@@ -1547,17 +1568,21 @@ struct SortBlkLds {
 #ifndef SGXAMD_SORT_UNROLL
 #define SGXAMD_SORT_UNROLL 16
 #endif
-template <int BITS, int NT, int ITEMS>
-__global__ __launch_bounds__(NT, NT * SGXAMD_SORT_WGS / 256) void k_sort_blk(const uint32_t *__restrict__ in, const uint64_t *__restrict__ list,
-                                                    uint32_t *__restrict__ out, SegMap m, uint32_t shift,
-                                                    const uint64_t *__restrict__ cursors) {
+// NAR: narrow partitions — every key's residual above the radix bits fits 16 bits (the
+// relation's key OR from pass 1), so the output holds those u16 residuals.  The kernel
+// picks the body once (one copy of the loop each, no store branches inside it).
+template <int BITS, int NT, int ITEMS, bool NAR>
+__device__ __forceinline__ void sort_blk_body(SortBlkLds<BITS, NT, ITEMS> &L, const uint32_t *__restrict__ in,
+                                              const uint64_t *__restrict__ list, uint32_t *__restrict__ out, SegMap m,
+                                              uint32_t shift, const uint64_t *__restrict__ cursors) {
     using LdsT = SortBlkLds<BITS, NT, ITEMS>;
     constexpr uint32_t F = LdsT::F, TILE = LdsT::TILE, BPT = TILE / kBlk, mask = F - 1, NW = NT / kWave;
     constexpr uint32_t WPB = kBlk / kWave;  // waves per block row: item u of wave w reads block u * (NT / kBlk) + w / WPB
     static_assert(TILE % kBlk == 0 && NT % kBlk == 0 && F <= NT && ITEMS <= 32 && TILE <= 65536, "tile geometry");
-    __shared__ LdsT L;
     const uint32_t tid = threadIdx.x, lane = __lane_id(), wave = tid / kWave;
     const uint32_t g = blockIdx.x;
+    const uint32_t rshift = shift + BITS;
+    uint16_t *__restrict__ out16 = reinterpret_cast<uint16_t *>(out);
     uint32_t r;
     uint64_t b, e;
     if (!seg_lookup(m, g, L.sbase, r, b, e)) return;
@@ -1636,6 +1661,17 @@ __global__ __launch_bounds__(NT, NT * SGXAMD_SORT_WGS / 256) void k_sort_blk(con
         __syncthreads();
         // D. sorted position q -> off[d] + q: consecutive lanes, consecutive addresses
         const uint32_t tn = L.wsum[NW];
+        if constexpr (NAR) {
+#pragma unroll SGXAMD_SORT_UNROLL
+            for (int u = 0; u < (int)ITEMS; ++u) {
+                const uint32_t q = tid + (uint32_t)u * NT;
+                if (q < tn) {
+                    const uint32_t x = L.sorted[q];
+                    out16[L.off[(x >> shift) & mask] + q] = (uint16_t)(x >> rshift);
+                }
+            }
+            return;
+        }
 #pragma unroll SGXAMD_SORT_UNROLL
         for (int u = 0; u < (int)ITEMS; ++u) {
             const uint32_t q = tid + (uint32_t)u * NT;
@@ -1666,6 +1702,18 @@ __global__ __launch_bounds__(NT, NT * SGXAMD_SORT_WGS / 256) void k_sort_blk(con
         sort_write(kb, mb);
         if (ti + 2 >= ntiles) break;
     }
+}
+
+template <int BITS, int NT, int ITEMS>
+__global__ __launch_bounds__(NT, NT * SGXAMD_SORT_WGS / 256) void k_sort_blk(const uint32_t *__restrict__ in, const uint64_t *__restrict__ list,
+                                                    uint32_t *__restrict__ out, SegMap m, uint32_t shift,
+                                                    const uint64_t *__restrict__ cursors,
+                                                    const uint32_t *__restrict__ narrow) {
+    __shared__ SortBlkLds<BITS, NT, ITEMS> L;
+    if (narrow != nullptr && ((*narrow >> (shift + BITS)) >> 16) == 0)
+        sort_blk_body<BITS, NT, ITEMS, true>(L, in, list, out, m, shift, cursors);
+    else
+        sort_blk_body<BITS, NT, ITEMS, false>(L, in, list, out, m, shift, cursors);
 }
 
 // Elements per thread per tile: 8 tuples (32 KiB tiles); keys: 12 in the pooled pass 1
@@ -1758,7 +1806,8 @@ bool sort2_enabled() {
 }
 template <typename T>
 hipError_t launch_scatter_blk_t(const void *in, const uint64_t *list, void *out, const SegMap &m, uint32_t grid,
-                                uint32_t shift, uint32_t bits, const uint64_t *cursors, hipStream_t s) {
+                                uint32_t shift, uint32_t bits, const uint64_t *cursors, hipStream_t s,
+                                const uint32_t *narrow) {
     if constexpr (sizeof(T) == 4) {
         if (sort2_enabled()) {
             const uint32_t *ik = static_cast<const uint32_t *>(in);
@@ -1766,7 +1815,7 @@ hipError_t launch_scatter_blk_t(const void *in, const uint64_t *list, void *out,
 #define SORT_CASE(B)                                                                                              \
     case B:                                                                                                       \
         hipLaunchKernelGGL((k_sort_blk<B, SGXAMD_SORT_NT, SGXAMD_SORT_ITEMS>), dim3(grid), dim3(SGXAMD_SORT_NT), 0, s, \
-                           ik, list, ok, m, shift, cursors);                                                      \
+                           ik, list, ok, m, shift, cursors, narrow);                                              \
         break;
             switch (bits) {
                 SORT_CASE(1)
@@ -1836,10 +1885,13 @@ hipError_t launch_scatter_keys(const row_t *in, uint32_t *out, const SegMap &m, 
 }
 
 hipError_t launch_scatter_blk(const void *in, const uint64_t *list, void *out, uint32_t elem_size, const SegMap &m,
-                              uint32_t grid, uint32_t shift, uint32_t bits, const uint64_t *cursors, hipStream_t s) {
+                              uint32_t grid, uint32_t shift, uint32_t bits, const uint64_t *cursors, hipStream_t s,
+                              const uint32_t *narrow) {
     if (grid == 0) return hipSuccess;
-    if (elem_size == 8) return launch_scatter_blk_t<uint64_t>(in, list, out, m, grid, shift, bits, cursors, s);
-    if (elem_size == 4) return launch_scatter_blk_t<uint32_t>(in, list, out, m, grid, shift, bits, cursors, s);
+    // narrow residuals: key partitions through k_sort_blk only
+    if (narrow && !(elem_size == 4 && sort2_enabled())) return hipErrorInvalidValue;
+    if (elem_size == 8) return launch_scatter_blk_t<uint64_t>(in, list, out, m, grid, shift, bits, cursors, s, nullptr);
+    if (elem_size == 4) return launch_scatter_blk_t<uint32_t>(in, list, out, m, grid, shift, bits, cursors, s, narrow);
     return hipErrorInvalidValue;
 }
 
@@ -1850,9 +1902,11 @@ __global__ __launch_bounds__(1024) void k_pool_layout(const uint64_t *__restrict
                                                       uint64_t *__restrict__ start, uint64_t *__restrict__ count,
                                                       uint64_t *__restrict__ lbase, uint64_t *__restrict__ lcount,
                                                       uint32_t *__restrict__ seg_base, uint32_t chain_nseg,
-                                                      uint32_t chain_mode) {
+                                                      uint32_t chain_mode, uint32_t *__restrict__ kor) {
     __shared__ uint64_t scratch[1024 / kWave + 1];
+    __shared__ uint32_t kor_all;
     const uint32_t d = threadIdx.x;
+    if (d == 0) kor_all = 0;
     const uint64_t v = d < F ? totals[d] : 0;
     const uint64_t tup = v & ((1ull << 40) - 1), blk = v >> 40;
     uint64_t tot;
@@ -1871,18 +1925,25 @@ __global__ __launch_bounds__(1024) void k_pool_layout(const uint64_t *__restrict
         seg_base[d] = (uint32_t)ex_s;
     }
     if (d == 0) seg_base[F] = (uint32_t)tot;
+    if (kor) {  // (chain_nseg: the pass-1 segments) the relation's key OR into kor[nseg]
+        uint32_t x = 0;
+        for (uint32_t i = d; i < chain_nseg; i += blockDim.x) x |= kor[i];
+        if (x) atomicOr(&kor_all, x);
+        __syncthreads();
+        if (d == 0) kor[chain_nseg] = kor_all;
+    }
 }
 
 hipError_t launch_pool_layout(uint64_t *cnt, uint32_t nseg, uint32_t bits, uint64_t *totals, uint64_t *start,
                               uint64_t *count, uint64_t *lbase, uint64_t *lcount, uint32_t *seg_base, hipStream_t s,
-                              uint32_t chain_mode) {
+                              uint32_t chain_mode, uint32_t *kor) {
     const uint32_t F = 1u << bits;
     hipLaunchKernelGGL(k_scan_cols, dim3(F), dim3(kBlock), 0, s, cnt, nseg, totals);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const uint32_t threads = F < 64 ? 64 : F;
     hipLaunchKernelGGL(k_pool_layout, dim3(1), dim3(threads), 0, s, totals, F, start, count, lbase, lcount, seg_base,
-                       nseg, chain_mode);
+                       nseg, chain_mode, kor);
     return hipGetLastError();
 }
 
@@ -2505,9 +2566,11 @@ __device__ __forceinline__ void x_advance(XCursor &c, const XTasks &k, uint32_t 
 // end read 0 (hardware bounds check, applied to the VGPR offset, which therefore holds
 // the whole offset), so every load is issued unconditionally and the wait for a strip
 // never covers the loads of the strip after it.
-template <int RCAP, int BLOCK, int UP, int KS>
+// The keys arrive as their residuals above the radix bits (key >> hash_shift; NR / NS:
+// R's / S's partitions hold them as u16, launch_scatter_blk's narrow partitions).
+template <int RCAP, int BLOCK, int UP, int KS, bool NR, bool NS>
 __device__ __forceinline__ void x_load(const XCursor &c, const XTasks &k, const uint32_t *rkeys,
-                                       const uint32_t *skeys, uint32_t (&v)[UP]) {
+                                       const uint32_t *skeys, uint32_t hash_shift, uint32_t (&v)[UP]) {
     constexpr uint32_t STRIP = BLOCK * UP;
     uint64_t base = 0, n = 0;
     const uint32_t *src = rkeys;
@@ -2522,25 +2585,38 @@ __device__ __forceinline__ void x_load(const XCursor &c, const XTasks &k, const 
         }
     }
     const uint32_t cnt = n < STRIP ? (uint32_t)n : STRIP;
-    const __amdgpu_buffer_rsrc_t rs = make_rsrc(src + base * KS, cnt * 4u * KS);
+    // (NR == NS: one width for both phases, no branch between the loads and their use)
+    const bool nar = NR == NS ? NR : (c.phase == 0 ? NR : NS);
+    if (nar) {
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(reinterpret_cast<const uint16_t *>(src) + base, cnt * 2u);
 #pragma unroll
-    for (int u = 0; u < UP; ++u)
-        v[u] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)((threadIdx.x + u * BLOCK) * 4u * KS), 0, 2);
+        for (int u = 0; u < UP; ++u)
+            v[u] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(rs, (int)((threadIdx.x + u * BLOCK) * 2u), 0, 2);
+    } else {
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(src + base * KS, cnt * 4u * KS);
+#pragma unroll
+        for (int u = 0; u < UP; ++u)
+            v[u] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)((threadIdx.x + u * BLOCK) * 4u * KS), 0, 2) >>
+                   hash_shift;
+    }
 }
 
 // One strip: clear the table at a chunk's first R strip, insert (phase 0) or probe
 // (phase 1) the strip's keys; a barrier after a chunk's last R strip (nx: the strip
 // after this one).  Returns the strip's matches (this thread).
-template <int RCAP, int BLOCK, int UP, int KS>
+// k: residuals (x_load); rbits: the residuals' width (16 when both relations are narrow,
+// else 32 - hash_shift).  The bucket is HASH_BIT_MODULO(key, N-1 << bits, bits) = the
+// residual's low lgN bits, the tag its next 16.
+template <int RCAP, int BLOCK, int UP, int KS, bool NR>
 __device__ __forceinline__ uint32_t x_step(JoinLdsX<RCAP, BLOCK / kWave> &L, const XCursor &c, const XCursor &nx,
                                            const uint32_t (&k)[UP], const uint32_t *rkeys, uint32_t hash_shift,
-                                           uint64_t &cyc2) {
+                                           uint32_t rbits, uint64_t &cyc2) {
     const uint32_t tid = threadIdx.x;
     const uint64_t c0 = wall_clock64();
     const uint32_t nrc = x_nrc<RCAP>(c);
     const uint32_t lgN = nrc <= 1 ? 0u : 32u - __builtin_clz(nrc - 1);  // N = NEXT_POW_2(numR)
     const uint32_t hmask = (1u << lgN) - 1;
-    const uint32_t tshift = hash_shift + lgN;
+    const uint32_t tshift = lgN;
     uint32_t m = 0;
     if (c.phase == 0) {  // BUILD-LOOP (:407-411)
         if (c.off == 0) {
@@ -2555,7 +2631,7 @@ __device__ __forceinline__ uint32_t x_step(JoinLdsX<RCAP, BLOCK / kWave> &L, con
 #pragma unroll
             for (int u = 0; u < UP; ++u) {
                 const uint32_t i = (uint32_t)c.off + tid + u * BLOCK;
-                old[u] = atomicExch(&L.head[(k[u] >> hash_shift) & hmask], (i + 1) | (key_tag16(k[u], tshift) << 16));
+                old[u] = atomicExch(&L.head[k[u] & hmask], (i + 1) | (key_tag16(k[u], tshift) << 16));
             }
 #pragma unroll
             for (int u = 0; u < UP; ++u) L.link[(uint32_t)c.off + tid + u * BLOCK + 1] = old[u];
@@ -2565,8 +2641,7 @@ __device__ __forceinline__ uint32_t x_step(JoinLdsX<RCAP, BLOCK / kWave> &L, con
                 const uint32_t j = tid + u * BLOCK;
                 if (j < lim) {
                     const uint32_t i = (uint32_t)c.off + j;
-                    const uint32_t b = (k[u] >> hash_shift) & hmask;
-                    L.link[i + 1] = atomicExch(&L.head[b], (i + 1) | (key_tag16(k[u], tshift) << 16));
+                    L.link[i + 1] = atomicExch(&L.head[k[u] & hmask], (i + 1) | (key_tag16(k[u], tshift) << 16));
                 }
             }
         }
@@ -2576,10 +2651,10 @@ __device__ __forceinline__ uint32_t x_step(JoinLdsX<RCAP, BLOCK / kWave> &L, con
         uint32_t w[UP];
 #pragma unroll
         for (int u = 0; u < UP; ++u) {
-            const uint32_t h = L.head[(k[u] >> hash_shift) & hmask];
+            const uint32_t h = L.head[k[u] & hmask];
             w[u] = vsel(tid + u * BLOCK < lim, h, 0u);
         }
-        if (tshift + 16 >= 32) {
+        if (tshift + 16 >= rbits) {
             // the tag is every remaining key bit: chain steps without branches, all UP link
             // reads in flight at once (a finished walk re-reads link[0], a broadcast)
             bool more = true;
@@ -2593,8 +2668,9 @@ __device__ __forceinline__ uint32_t x_step(JoinLdsX<RCAP, BLOCK / kWave> &L, con
                     more |= w[u] != 0;
                 }
             }
-        } else {  // a tag match is confirmed against the R key (an L2 hit)
+        } else {  // a tag match is confirmed against the R key's residual (an L2 hit)
             const uint32_t *rkc = rkeys + (c.r_base + c.rc) * KS;
+            const uint16_t *rkc16 = reinterpret_cast<const uint16_t *>(rkeys) + (c.r_base + c.rc);
             bool more = true;
             while (more) {
                 more = false;
@@ -2602,7 +2678,9 @@ __device__ __forceinline__ uint32_t x_step(JoinLdsX<RCAP, BLOCK / kWave> &L, con
                 for (int u = 0; u < UP; ++u) {
                     if (w[u] != 0) {
                         const uint32_t e = w[u] & 0xFFFFu;
-                        if ((w[u] >> 16) == key_tag16(k[u], tshift) && rkc[KS * (e - 1)] == k[u]) ++m;
+                        if ((w[u] >> 16) == key_tag16(k[u], tshift) &&
+                            (NR ? (uint32_t)rkc16[e - 1] : rkc[KS * (e - 1)] >> hash_shift) == k[u])
+                            ++m;
                         w[u] = L.link[e];
                         more |= w[u] != 0;
                     }
@@ -2614,16 +2692,19 @@ __device__ __forceinline__ uint32_t x_step(JoinLdsX<RCAP, BLOCK / kWave> &L, con
     return m;
 }
 
-template <int RCAP, int BLOCK, int UP, int KS = 1>
-__global__ __launch_bounds__(BLOCK, 1) void k_join_x(
-    const uint64_t *__restrict__ R, const uint64_t *__restrict__ S, const uint64_t *__restrict__ r_start,
-    const uint64_t *__restrict__ r_count, const uint64_t *__restrict__ s_start, const uint64_t *__restrict__ s_count,
-    uint64_t P, const uint64_t *__restrict__ over, const uint32_t *__restrict__ n_over, uint32_t hash_shift,
-    uint64_t s_chunk, uint64_t *__restrict__ counts, uint64_t *__restrict__ cyc, uint64_t *__restrict__ red_result,
-    uint64_t *__restrict__ red_ticket, uint32_t ncounts, uint32_t *__restrict__ tickets) {
+// The kernel body for one pair of key widths (NR / NS: R / S hold u16 residuals); the
+// kernel picks it once, from the relations' key ORs, so no branch sits inside the loop.
+template <int RCAP, int BLOCK, int UP, int KS, bool NR, bool NS>
+__device__ __forceinline__ void join_x_body(
+    JoinLdsX<RCAP, BLOCK / kWave> &L, const uint64_t *__restrict__ R, const uint64_t *__restrict__ S,
+    const uint64_t *__restrict__ r_start, const uint64_t *__restrict__ r_count, const uint64_t *__restrict__ s_start,
+    const uint64_t *__restrict__ s_count, uint64_t P, const uint64_t *__restrict__ over,
+    const uint32_t *__restrict__ n_over, uint32_t hash_shift, uint64_t s_chunk, uint64_t *__restrict__ counts,
+    uint64_t *__restrict__ cyc, uint64_t *__restrict__ red_result, uint64_t *__restrict__ red_ticket,
+    uint32_t ncounts, uint32_t *__restrict__ tickets) {
     constexpr int NW = BLOCK / kWave;
     constexpr uint32_t STRIP = BLOCK * UP;
-    __shared__ JoinLdsX<RCAP, NW> L;
+    const uint32_t rbits = NR && NS ? 16u : 32u - hash_shift;
     const uint32_t tid = threadIdx.x, lane = __lane_id();
     const XTasks tk{r_start, r_count, s_start, s_count, over, P, uni_u64(P + *n_over), s_chunk, tickets, L.nxt};
     const uint32_t *rkeys = reinterpret_cast<const uint32_t *>(R);
@@ -2646,7 +2727,7 @@ __global__ __launch_bounds__(BLOCK, 1) void k_join_x(
     XCursor ca{(uint64_t)blockIdx.x, 0, 0, 0, 0, 0, 0, 0, 0}, cb{};
     x_seek(ca, tk, tkv);
     uint32_t ka[UP], kb[UP];
-    x_load<RCAP, BLOCK, UP, KS>(ca, tk, rkeys, skeys, ka);
+    x_load<RCAP, BLOCK, UP, KS, NR, NS>(ca, tk, rkeys, skeys, hash_shift, ka);
     // two register sets, the loop unrolled by two so that no set is ever copied (a copy
     // of a set still in flight would wait for it); the empty asm uses wait for a set
     // right after the next set's loads are issued, in straight-line code, where the
@@ -2654,22 +2735,22 @@ __global__ __launch_bounds__(BLOCK, 1) void k_join_x(
     while (ca.t < tk.T) {
         cb = ca;
         x_advance<RCAP, STRIP>(cb, tk, tkv);
-        x_load<RCAP, BLOCK, UP, KS>(cb, tk, rkeys, skeys, kb);
+        x_load<RCAP, BLOCK, UP, KS, NR, NS>(cb, tk, rkeys, skeys, hash_shift, kb);
 #pragma unroll
         for (int u = 0; u < UP; ++u) asm volatile("" ::"v"(ka[u]));
         publish(ca);
         uint64_t dt;
-        matches += x_step<RCAP, BLOCK, UP, KS>(L, ca, cb, ka, rkeys, hash_shift, dt);
+        matches += x_step<RCAP, BLOCK, UP, KS, NR>(L, ca, cb, ka, rkeys, hash_shift, rbits, dt);
         bcyc += ca.phase == 0 ? dt : 0;
         pcyc += ca.phase == 0 ? 0 : dt;
         if (cb.t >= tk.T) break;
         ca = cb;
         x_advance<RCAP, STRIP>(ca, tk, tkv);
-        x_load<RCAP, BLOCK, UP, KS>(ca, tk, rkeys, skeys, ka);
+        x_load<RCAP, BLOCK, UP, KS, NR, NS>(ca, tk, rkeys, skeys, hash_shift, ka);
 #pragma unroll
         for (int u = 0; u < UP; ++u) asm volatile("" ::"v"(kb[u]));
         publish(cb);
-        matches += x_step<RCAP, BLOCK, UP, KS>(L, cb, ca, kb, rkeys, hash_shift, dt);
+        matches += x_step<RCAP, BLOCK, UP, KS, NR>(L, cb, ca, kb, rkeys, hash_shift, rbits, dt);
         bcyc += cb.phase == 0 ? dt : 0;
         pcyc += cb.phase == 0 ? 0 : dt;
     }
@@ -2692,6 +2773,35 @@ __global__ __launch_bounds__(BLOCK, 1) void k_join_x(
         if (cyc) cyc[2 * i] = cyc[2 * i + 1] = 0;
     }
     if (red_ticket) join_reduce_last(counts, cyc, red_result, red_ticket, L.red, tk.T);
+}
+
+template <int RCAP, int BLOCK, int UP, int KS = 1>
+__global__ __launch_bounds__(BLOCK, 1) void k_join_x(
+    const uint64_t *__restrict__ R, const uint64_t *__restrict__ S, const uint64_t *__restrict__ r_start,
+    const uint64_t *__restrict__ r_count, const uint64_t *__restrict__ s_start, const uint64_t *__restrict__ s_count,
+    uint64_t P, const uint64_t *__restrict__ over, const uint32_t *__restrict__ n_over, uint32_t hash_shift,
+    uint64_t s_chunk, uint64_t *__restrict__ counts, uint64_t *__restrict__ cyc, uint64_t *__restrict__ red_result,
+    uint64_t *__restrict__ red_ticket, uint32_t ncounts, uint32_t *__restrict__ tickets,
+    const uint32_t *__restrict__ narrow_r, const uint32_t *__restrict__ narrow_s) {
+    __shared__ JoinLdsX<RCAP, BLOCK / kWave> L;
+    // (the same test as k_sort_blk's, which wrote the partitions)
+    const bool nr = narrow_r != nullptr && ((*narrow_r >> hash_shift) >> 16) == 0;
+    const bool ns = narrow_s != nullptr && ((*narrow_s >> hash_shift) >> 16) == 0;
+    // the widths taken, for the caller's statistics (the ticket word's high half, zeroed by
+    // launch_make_tasks)
+    if (tickets && blockIdx.x == 0 && threadIdx.x == 0) tickets[1] = 1u | (nr ? 2u : 0u) | (ns ? 4u : 0u);
+#define JOIN_X_BODY(A, B)                                                                                          \
+    join_x_body<RCAP, BLOCK, UP, KS, A, B>(L, R, S, r_start, r_count, s_start, s_count, P, over, n_over, hash_shift, \
+                                           s_chunk, counts, cyc, red_result, red_ticket, ncounts, tickets)
+    if constexpr (KS == 1) {
+        if (nr && ns) JOIN_X_BODY(true, true);
+        else if (nr) JOIN_X_BODY(true, false);
+        else if (ns) JOIN_X_BODY(false, true);
+        else JOIN_X_BODY(false, false);
+    } else {
+        JOIN_X_BODY(false, false);
+    }
+#undef JOIN_X_BODY
 }
 
 // ------------------------------------------------------- histogram join (RHT) ---
@@ -3078,8 +3188,11 @@ hipError_t launch_join_keys(const void *R, const void *S, const uint64_t *r_star
                             const uint64_t *s_start, const uint64_t *s_count, uint64_t P, const uint64_t *over,
                             const uint32_t *n_over, uint32_t hash_shift, uint32_t rcap, uint64_t s_chunk,
                             uint32_t grid, int mode, int algo, uint64_t *counts, uint64_t *cyc, hipStream_t s,
-                            const JoinReduce *reduce, uint32_t *tickets) {
+                            const JoinReduce *reduce, uint32_t *tickets, const uint32_t *narrow_r,
+                            const uint32_t *narrow_s) {
     if (mode != kJoinCount) return hipErrorInvalidValue;
+    // narrow partitions are read by the 16,384-key chaining table only
+    if ((narrow_r || narrow_s) && !(algo == kAlgoChaining && rcap == kBigRcap)) return hipErrorInvalidValue;
     const uint64_t *R64 = static_cast<const uint64_t *>(R);
     const uint64_t *S64 = static_cast<const uint64_t *>(S);
     uint64_t *rres = reduce ? reduce->result : nullptr;
@@ -3109,7 +3222,7 @@ hipError_t launch_join_keys(const void *R, const void *S, const uint64_t *r_star
     if (rcap == kBigRcap) {  // one workgroup per CU (128 KiB table), strips of 8 keys per thread
         hipLaunchKernelGGL((k_join_x<kBigRcap, 1024, 8, 1>), dim3(std::min<uint32_t>(grid, cu_count())), dim3(1024), 0,
                            s, R64, S64, r_start, r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts,
-                           cyc, rres, rtick, grid, tickets);
+                           cyc, rres, rtick, grid, tickets, narrow_r, narrow_s);
         return hipGetLastError();
     }
 #define KEYS_CASE(RC)                                                                                                   case RC:                                                                                                                hipLaunchKernelGGL((k_join<RC, kJoinCount, kBlock, 1>), dim3(grid), dim3(kBlock), 0, s, R64, S64, r_start,                            r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts, nullptr, nullptr,                             cyc, rres, rtick);                                                                               break;
@@ -3128,9 +3241,12 @@ hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, 
                        const uint64_t *s_start, const uint64_t *s_count, uint64_t P, const uint64_t *over,
                        const uint32_t *n_over, uint32_t hash_shift, uint32_t rcap, uint64_t s_chunk, uint32_t grid,
                        int mode, int algo, uint64_t *counts, const uint64_t *task_off, output_triple_t *out,
-                       uint64_t *cyc, hipStream_t s, const JoinReduce *reduce, int key_stride, uint32_t *tickets) {
-    if (key_stride == 1) return launch_join_keys(R, S, r_start, r_count, s_start, s_count, P, over, n_over, hash_shift,
-                                                 rcap, s_chunk, grid, mode, algo, counts, cyc, s, reduce, tickets);
+                       uint64_t *cyc, hipStream_t s, const JoinReduce *reduce, int key_stride, uint32_t *tickets,
+                       const uint32_t *narrow_r, const uint32_t *narrow_s) {
+    if (key_stride == 1)
+        return launch_join_keys(R, S, r_start, r_count, s_start, s_count, P, over, n_over, hash_shift, rcap, s_chunk,
+                                grid, mode, algo, counts, cyc, s, reduce, tickets, narrow_r, narrow_s);
+    if (narrow_r || narrow_s) return hipErrorInvalidValue;
     const uint64_t *R64 = reinterpret_cast<const uint64_t *>(R);
     const uint64_t *S64 = reinterpret_cast<const uint64_t *>(S);
     uint64_t *rres = (reduce && mode == kJoinCount) ? reduce->result : nullptr;
@@ -3163,7 +3279,7 @@ hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, 
         if (mode != kJoinCount) return hipErrorInvalidValue;
         hipLaunchKernelGGL((k_join_x<kBigRcap, 1024, 8, 2>), dim3(std::min<uint32_t>(grid, cu_count())), dim3(1024), 0,
                            s, R64, S64, r_start, r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts,
-                           cyc, rres, rtick, grid, tickets);
+                           cyc, rres, rtick, grid, tickets, nullptr, nullptr);
     } else if (mode == kJoinCount && grid <= 512 && rcap <= 4096) {
         // few tasks (small joins: one workgroup per CU at most): 1,024 threads per table
         // instead of 256, so that a CU holds 16 waves to hide the load latencies

@@ -117,6 +117,8 @@ class rho_stats(C.Structure):
         ("ms_probe", C.c_double),
         ("layout", C.c_uint32),
         ("elem_bytes", C.c_uint32),
+        ("narrow", C.c_uint32),
+        ("reserved0", C.c_uint32),
     ]
 
     def as_dict(self) -> dict:

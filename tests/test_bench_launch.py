@@ -81,3 +81,14 @@ def test_algorithmic_bytes_keys_layout(kernel, expect):
     n = 1 << 20
     per = bench.algorithmic_bytes(kernel, n, n, 2, 7, 4) / (n * (2 if kernel == "join_build_probe" else 1))
     assert per == expect
+
+
+@pytest.mark.parametrize("kernel,narrow,expect", [("R_pass2_scatter", 3, 6), ("S_pass2_scatter", 1, 8),
+                                                  ("S_pass2_scatter", 2, 6), ("R_pass1_scatter", 3, 13),
+                                                  ("join_build_probe", 3, 2), ("join_build_probe", 1, 3)])
+def test_algorithmic_bytes_narrow(kernel, narrow, expect):
+    """Narrow partitions (stats narrow bit 0 R / bit 1 S): pass 2 writes and the build/probe
+    reads 2-byte residuals; pass 1 is unchanged."""
+    n = 1 << 20
+    per = bench.algorithmic_bytes(kernel, n, n, 2, 7, 4, 2, narrow) / (n * (2 if kernel == "join_build_probe" else 1))
+    assert per == expect

@@ -10,7 +10,8 @@ SGXAMD_POOL_SEGS sets the pooled pass-1 workgroups: 3 gives large pools, 100000 
 tile per segment), SGXAMD_KEYS=0 (counting joins move whole tuples instead of keys),
 SGXAMD_SORT2=0 (pass 2 of key partitions with the write-combining scatter instead of
 the LDS counting sort), SGXAMD_CHAIN_HIST=1 (the chain histograms counted in pass 1
-instead of the digit side stream and its histogram pass; measured slower, r04k).  The switches are read
+instead of the digit side stream and its histogram pass; measured slower, r04k),
+SGXAMD_NARROW=0 (key partitions stay 4-byte keys where u16 residuals would fit).  The switches are read
 once per process, so each setting runs in a child process against the oracle (the
 TPC-H selections ride along: they share the library's workspace)."""
 import os
@@ -78,7 +79,7 @@ print("paths ok")
                                  {"SGXAMD_DIGIT_SIDE": "1", "SGXAMD_BIG_JOIN": "1"},
                                  {"SGXAMD_SMALL_JOIN": "0"},
                                  {"SGXAMD_POOL": "0"}, {"SGXAMD_POOL_SEGS": "3"}, {"SGXAMD_POOL_SEGS": "100000"},
-                                 {"SGXAMD_KEYS": "0"}, {"SGXAMD_SORT2": "0"}, {"SGXAMD_CHAIN_HIST": "1"},
+                                 {"SGXAMD_KEYS": "0"}, {"SGXAMD_SORT2": "0"}, {"SGXAMD_NARROW": "0"}, {"SGXAMD_CHAIN_HIST": "1"},
                                  {"SGXAMD_CHAIN_HIST": "1", "SGXAMD_CHAIN_SLOTS": "1"}])
 def test_switch_paths_match_oracle(env):
     e = dict(os.environ, **env)

@@ -234,6 +234,8 @@ def test_full_size_config2_property(sgx, gpu):
     assert res.matches == n
     # 2^14 partitions of 16,384 R tuples (7 + 7 bits), one 16,384-tuple table each
     assert res.stats["radix_bits"] == 14 and res.stats["passes"] == 2
+    # keys 1..2^28: residuals above 14 bits fit 16 bits, both final partitions are u16
+    assert res.stats["narrow"] == 3
     del R, S
     torch.cuda.empty_cache()
 
