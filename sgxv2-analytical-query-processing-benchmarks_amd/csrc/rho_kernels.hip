@@ -2775,6 +2775,11 @@ __device__ __forceinline__ void join_x_body(
     if (red_ticket) join_reduce_last(counts, cyc, red_result, red_ticket, L.red, tk.T);
 }
 
+// Keys per thread per strip when both relations are narrow (2-byte keys: the same bytes
+// in flight per strip as 8 four-byte keys at 16)
+#ifndef SGXAMD_JOIN_UP_NARROW
+#define SGXAMD_JOIN_UP_NARROW 16
+#endif
 template <int RCAP, int BLOCK, int UP, int KS = 1>
 __global__ __launch_bounds__(BLOCK, 1) void k_join_x(
     const uint64_t *__restrict__ R, const uint64_t *__restrict__ S, const uint64_t *__restrict__ r_start,
@@ -2790,11 +2795,12 @@ __global__ __launch_bounds__(BLOCK, 1) void k_join_x(
     // the widths taken, for the caller's statistics (the ticket word's high half, zeroed by
     // launch_make_tasks)
     if (tickets && blockIdx.x == 0 && threadIdx.x == 0) tickets[1] = 1u | (nr ? 2u : 0u) | (ns ? 4u : 0u);
-#define JOIN_X_BODY(A, B)                                                                                          \
-    join_x_body<RCAP, BLOCK, UP, KS, A, B>(L, R, S, r_start, r_count, s_start, s_count, P, over, n_over, hash_shift, \
-                                           s_chunk, counts, cyc, red_result, red_ticket, ncounts, tickets)
+#define JOIN_X_BODY_U(U, A, B)                                                                                     \
+    join_x_body<RCAP, BLOCK, U, KS, A, B>(L, R, S, r_start, r_count, s_start, s_count, P, over, n_over, hash_shift, \
+                                          s_chunk, counts, cyc, red_result, red_ticket, ncounts, tickets)
+#define JOIN_X_BODY(A, B) JOIN_X_BODY_U(UP, A, B)
     if constexpr (KS == 1) {
-        if (nr && ns) JOIN_X_BODY(true, true);
+        if (nr && ns) JOIN_X_BODY_U(SGXAMD_JOIN_UP_NARROW, true, true);
         else if (nr) JOIN_X_BODY(true, false);
         else if (ns) JOIN_X_BODY(false, true);
         else JOIN_X_BODY(false, false);
@@ -2802,6 +2808,7 @@ __global__ __launch_bounds__(BLOCK, 1) void k_join_x(
         JOIN_X_BODY(false, false);
     }
 #undef JOIN_X_BODY
+#undef JOIN_X_BODY_U
 }
 
 // ------------------------------------------------------- histogram join (RHT) ---
