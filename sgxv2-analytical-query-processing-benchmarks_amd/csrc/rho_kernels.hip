@@ -2442,8 +2442,16 @@ __global__ __launch_bounds__(BLOCK) void k_join(const uint64_t *__restrict__ R, 
 // 80 KiB table instead overlaps two workgroups' phases).
 template <int RCAP, int NW>
 struct JoinLdsX {
-    uint32_t head[RCAP];
-    uint32_t link[RCAP + 1];  // 1-based: link[0] = 0, the end of every chain, is never written
+    union {
+        struct {
+            uint32_t head[RCAP];
+            uint32_t link[RCAP + 1];  // 1-based: link[0] = 0, the end of every chain, is never written
+        };
+        // narrow relations (x_step DIRECT): the count of R keys per 16-bit residual, two
+        // u16 counters per word (a chunk holds at most RCAP <= 65535 keys: no carry)
+        uint32_t cnt2[1u << 15];
+    };
+    static_assert(RCAP <= 65535 && 2 * RCAP >= (1u << 15), "direct count table inside the chain table");
     uint64_t red[NW + 2];
     uint32_t nxt[3];  // task tickets (SGXAMD_JOIN_TICKETS): successors of tasks j (nxt[j & 1]), a skip
 };
@@ -2607,13 +2615,62 @@ __device__ __forceinline__ void x_load(const XCursor &c, const XTasks &k, const 
 // k: residuals (x_load); rbits: the residuals' width (16 when both relations are narrow,
 // else 32 - hash_shift).  The bucket is HASH_BIT_MODULO(key, N-1 << bits, bits) = the
 // residual's low lgN bits, the tag its next 16.
-template <int RCAP, int BLOCK, int UP, int KS, bool NR>
+// DIRECT (either relation narrow): the residuals that can match lie below 2^16, so the
+// table has one bucket per residual value — every chain holds one key value, and the
+// count a probe takes from it is the chain's length: the table keeps that length (a u16
+// counter per residual, cnt2) instead of the chain.  Build: one LDS add per R key;
+// probe: one LDS read per S key; a residual at or above 2^16 (the wide relation's)
+// matches nothing on the narrow side and is skipped.
+#ifndef SGXAMD_JOIN_DIRECT  // development A/B: 0 keeps the chain table for narrow relations
+#define SGXAMD_JOIN_DIRECT 1
+#endif
+#ifndef SGXAMD_ABLATE_JOIN
+#define SGXAMD_ABLATE_JOIN 0
+#endif
+template <int RCAP, int BLOCK, int UP, int KS, bool NR, bool NS = false>
 __device__ __forceinline__ uint32_t x_step(JoinLdsX<RCAP, BLOCK / kWave> &L, const XCursor &c, const XCursor &nx,
                                            const uint32_t (&k)[UP], const uint32_t *rkeys, uint32_t hash_shift,
                                            uint32_t rbits, uint64_t &cyc2) {
     const uint32_t tid = threadIdx.x;
     const uint64_t c0 = wall_clock64();
     const uint32_t nrc = x_nrc<RCAP>(c);
+    if constexpr (SGXAMD_JOIN_DIRECT && (NR || NS)) {
+        uint32_t m = 0;
+        if (c.phase == 0) {
+            if (c.off == 0) {
+                __syncthreads();  // the previous chunk's probe is done with the table
+#if SGXAMD_ABLATE_JOIN != 1  // development ablation 1: no clear (wrong counts)
+                for (uint32_t i = tid; i < (1u << 15) / 4; i += BLOCK)
+                    reinterpret_cast<uint4 *>(L.cnt2)[i] = make_uint4(0, 0, 0, 0);
+#endif
+                __syncthreads();
+            }
+            const uint32_t lim = nrc - (uint32_t)c.off;
+#pragma unroll
+            for (int u = 0; u < UP; ++u) {
+                const uint32_t r = k[u];
+#if SGXAMD_ABLATE_JOIN == 2  // development ablation 2: plain stores instead of the adds (wrong counts)
+                if (tid + u * BLOCK < lim && (NR || r < (1u << 16))) L.cnt2[r >> 1] = r;
+#elif SGXAMD_ABLATE_JOIN == 3  // development ablation 3: no table writes (wrong counts)
+                if (tid + u * BLOCK < lim && r == 0xFFFFFFFFu) L.cnt2[r >> 1] = r;
+#else
+                if (tid + u * BLOCK < lim && (NR || r < (1u << 16))) atomicAdd(&L.cnt2[r >> 1], 1u << ((r & 1u) << 4));
+#endif
+            }
+            if (nx.phase != 0 || nx.t != c.t || nx.rc != c.rc) __syncthreads();  // the chunk's table is complete
+        } else {
+            const uint64_t lim = c.nS - c.off;
+#pragma unroll
+            for (int u = 0; u < UP; ++u) {
+                const uint32_t r = k[u];
+                const bool ok = tid + u * BLOCK < lim && (NS || r < (1u << 16));
+                const uint32_t w = L.cnt2[(ok ? r : 0u) >> 1];
+                m += ok ? (w >> ((r & 1u) << 4)) & 0xFFFFu : 0u;
+            }
+        }
+        cyc2 = wall_clock64() - c0;
+        return m;
+    }
     const uint32_t lgN = nrc <= 1 ? 0u : 32u - __builtin_clz(nrc - 1);  // N = NEXT_POW_2(numR)
     const uint32_t hmask = (1u << lgN) - 1;
     const uint32_t tshift = lgN;
@@ -2740,7 +2797,7 @@ __device__ __forceinline__ void join_x_body(
         for (int u = 0; u < UP; ++u) asm volatile("" ::"v"(ka[u]));
         publish(ca);
         uint64_t dt;
-        matches += x_step<RCAP, BLOCK, UP, KS, NR>(L, ca, cb, ka, rkeys, hash_shift, rbits, dt);
+        matches += x_step<RCAP, BLOCK, UP, KS, NR, NS>(L, ca, cb, ka, rkeys, hash_shift, rbits, dt);
         bcyc += ca.phase == 0 ? dt : 0;
         pcyc += ca.phase == 0 ? 0 : dt;
         if (cb.t >= tk.T) break;
@@ -2750,7 +2807,7 @@ __device__ __forceinline__ void join_x_body(
 #pragma unroll
         for (int u = 0; u < UP; ++u) asm volatile("" ::"v"(kb[u]));
         publish(cb);
-        matches += x_step<RCAP, BLOCK, UP, KS, NR>(L, cb, ca, kb, rkeys, hash_shift, rbits, dt);
+        matches += x_step<RCAP, BLOCK, UP, KS, NR, NS>(L, cb, ca, kb, rkeys, hash_shift, rbits, dt);
         bcyc += cb.phase == 0 ? dt : 0;
         pcyc += cb.phase == 0 ? 0 : dt;
     }
