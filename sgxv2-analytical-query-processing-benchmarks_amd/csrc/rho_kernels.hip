@@ -2630,17 +2630,19 @@ __device__ __forceinline__ void x_load(const XCursor &c, const XTasks &k, const 
 template <int RCAP, int BLOCK, int UP, int KS, bool NR, bool NS = false>
 __device__ __forceinline__ uint32_t x_step(JoinLdsX<RCAP, BLOCK / kWave> &L, const XCursor &c, const XCursor &nx,
                                            const uint32_t (&k)[UP], const uint32_t *rkeys, uint32_t hash_shift,
-                                           uint32_t rbits, uint64_t &cyc2) {
+                                           uint32_t rbits, uint32_t tlim, uint64_t &cyc2) {
     const uint32_t tid = threadIdx.x;
     const uint64_t c0 = wall_clock64();
     const uint32_t nrc = x_nrc<RCAP>(c);
+    // (DIRECT: tlim = the counters in use, 2^(the narrower relation's residual bits): a
+    // residual at or above it matches nothing; only their words are cleared per chunk)
     if constexpr (SGXAMD_JOIN_DIRECT && (NR || NS)) {
         uint32_t m = 0;
         if (c.phase == 0) {
             if (c.off == 0) {
                 __syncthreads();  // the previous chunk's probe is done with the table
 #if SGXAMD_ABLATE_JOIN != 1  // development ablation 1: no clear (wrong counts)
-                for (uint32_t i = tid; i < (1u << 15) / 4; i += BLOCK)
+                for (uint32_t i = tid; i < (tlim + 7) / 8; i += BLOCK)
                     reinterpret_cast<uint4 *>(L.cnt2)[i] = make_uint4(0, 0, 0, 0);
 #endif
                 __syncthreads();
@@ -2650,11 +2652,11 @@ __device__ __forceinline__ uint32_t x_step(JoinLdsX<RCAP, BLOCK / kWave> &L, con
             for (int u = 0; u < UP; ++u) {
                 const uint32_t r = k[u];
 #if SGXAMD_ABLATE_JOIN == 2  // development ablation 2: plain stores instead of the adds (wrong counts)
-                if (tid + u * BLOCK < lim && (NR || r < (1u << 16))) L.cnt2[r >> 1] = r;
+                if (tid + u * BLOCK < lim && r < tlim) L.cnt2[r >> 1] = r;
 #elif SGXAMD_ABLATE_JOIN == 3  // development ablation 3: no table writes (wrong counts)
                 if (tid + u * BLOCK < lim && r == 0xFFFFFFFFu) L.cnt2[r >> 1] = r;
 #else
-                if (tid + u * BLOCK < lim && (NR || r < (1u << 16))) atomicAdd(&L.cnt2[r >> 1], 1u << ((r & 1u) << 4));
+                if (tid + u * BLOCK < lim && r < tlim) atomicAdd(&L.cnt2[r >> 1], 1u << ((r & 1u) << 4));
 #endif
             }
             if (nx.phase != 0 || nx.t != c.t || nx.rc != c.rc) __syncthreads();  // the chunk's table is complete
@@ -2663,7 +2665,7 @@ __device__ __forceinline__ uint32_t x_step(JoinLdsX<RCAP, BLOCK / kWave> &L, con
 #pragma unroll
             for (int u = 0; u < UP; ++u) {
                 const uint32_t r = k[u];
-                const bool ok = tid + u * BLOCK < lim && (NS || r < (1u << 16));
+                const bool ok = tid + u * BLOCK < lim && r < tlim;
                 const uint32_t w = L.cnt2[(ok ? r : 0u) >> 1];
                 m += ok ? (w >> ((r & 1u) << 4)) & 0xFFFFu : 0u;
             }
@@ -2758,7 +2760,7 @@ __device__ __forceinline__ void join_x_body(
     const uint64_t *__restrict__ s_count, uint64_t P, const uint64_t *__restrict__ over,
     const uint32_t *__restrict__ n_over, uint32_t hash_shift, uint64_t s_chunk, uint64_t *__restrict__ counts,
     uint64_t *__restrict__ cyc, uint64_t *__restrict__ red_result, uint64_t *__restrict__ red_ticket,
-    uint32_t ncounts, uint32_t *__restrict__ tickets) {
+    uint32_t ncounts, uint32_t *__restrict__ tickets, uint32_t tlim) {
     constexpr int NW = BLOCK / kWave;
     constexpr uint32_t STRIP = BLOCK * UP;
     const uint32_t rbits = NR && NS ? 16u : 32u - hash_shift;
@@ -2797,7 +2799,7 @@ __device__ __forceinline__ void join_x_body(
         for (int u = 0; u < UP; ++u) asm volatile("" ::"v"(ka[u]));
         publish(ca);
         uint64_t dt;
-        matches += x_step<RCAP, BLOCK, UP, KS, NR, NS>(L, ca, cb, ka, rkeys, hash_shift, rbits, dt);
+        matches += x_step<RCAP, BLOCK, UP, KS, NR, NS>(L, ca, cb, ka, rkeys, hash_shift, rbits, tlim, dt);
         bcyc += ca.phase == 0 ? dt : 0;
         pcyc += ca.phase == 0 ? 0 : dt;
         if (cb.t >= tk.T) break;
@@ -2807,7 +2809,7 @@ __device__ __forceinline__ void join_x_body(
 #pragma unroll
         for (int u = 0; u < UP; ++u) asm volatile("" ::"v"(kb[u]));
         publish(cb);
-        matches += x_step<RCAP, BLOCK, UP, KS, NR, NS>(L, cb, ca, kb, rkeys, hash_shift, rbits, dt);
+        matches += x_step<RCAP, BLOCK, UP, KS, NR, NS>(L, cb, ca, kb, rkeys, hash_shift, rbits, tlim, dt);
         bcyc += cb.phase == 0 ? dt : 0;
         pcyc += cb.phase == 0 ? 0 : dt;
     }
@@ -2849,12 +2851,23 @@ __global__ __launch_bounds__(BLOCK, 1) void k_join_x(
     // (the same test as k_sort_blk's, which wrote the partitions)
     const bool nr = narrow_r != nullptr && ((*narrow_r >> hash_shift) >> 16) == 0;
     const bool ns = narrow_s != nullptr && ((*narrow_s >> hash_shift) >> 16) == 0;
+    // the direct table's counters: residuals below 2^(the fewest residual bits of a narrow
+    // relation; 16 for a wide one) — BASELINE config 2's keys 1..2^28 over 14 bits: 2^14
+    const auto res_bits = [&](bool n, const uint32_t *kor) -> uint32_t {
+        const uint32_t x = n ? (*kor >> hash_shift) : 0xFFFFu;
+        return x ? 32u - (uint32_t)__builtin_clz(x) : 0u;
+    };
+#ifdef SGXAMD_JOIN_FULL_TABLE  // development A/B: all 2^16 counters
+    const uint32_t tlim = 1u << 16;
+#else
+    const uint32_t tlim = 1u << min(res_bits(nr, narrow_r), res_bits(ns, narrow_s));
+#endif
     // the widths taken, for the caller's statistics (the ticket word's high half, zeroed by
     // launch_make_tasks)
     if (tickets && blockIdx.x == 0 && threadIdx.x == 0) tickets[1] = 1u | (nr ? 2u : 0u) | (ns ? 4u : 0u);
 #define JOIN_X_BODY_U(U, A, B)                                                                                     \
     join_x_body<RCAP, BLOCK, U, KS, A, B>(L, R, S, r_start, r_count, s_start, s_count, P, over, n_over, hash_shift, \
-                                          s_chunk, counts, cyc, red_result, red_ticket, ncounts, tickets)
+                                          s_chunk, counts, cyc, red_result, red_ticket, ncounts, tickets, tlim)
 #define JOIN_X_BODY(A, B) JOIN_X_BODY_U(UP, A, B)
     if constexpr (KS == 1) {
         if (nr && ns) JOIN_X_BODY_U(SGXAMD_JOIN_UP_NARROW, true, true);

@@ -35,6 +35,10 @@ def case_relations(case, rng):
         R = keys_below(rng, nR, BOUND // 4)
         S = keys_below(rng, nS, BOUND // 4)
         return R, S, 3
+    if case == "uneven":  # both narrow, R's residuals 9 bits wide, S's 16: S keys above R's range skip
+        R = keys_below(rng, nR, 1 << (BITS + 9))
+        S = np.concatenate([keys_below(rng, nS // 2, BOUND), keys_below(rng, nS - nS // 2, 1 << (BITS + 9))])
+        return R, S, 3
     if case == "boundary":  # the largest narrow key on both sides (residual 0xFFFF)
         R = keys_below(rng, nR, BOUND)
         S = np.concatenate([keys_below(rng, nS - 3, BOUND), np.full(3, BOUND - 1, np.uint32)])
@@ -65,7 +69,7 @@ def case_relations(case, rng):
     return R, S, 0
 
 
-CASES = ["narrow", "boundary", "wide_s", "wide_r", "wide"]
+CASES = ["narrow", "uneven", "boundary", "wide_s", "wide_r", "wide"]
 
 
 @pytest.mark.parametrize("case", CASES)
