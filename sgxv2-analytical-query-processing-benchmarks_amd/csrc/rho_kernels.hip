@@ -2751,6 +2751,11 @@ __device__ __forceinline__ uint32_t x_step(JoinLdsX<RCAP, BLOCK / kWave> &L, con
     return m;
 }
 
+// Keys per thread per strip when both relations are narrow (2-byte keys: the same bytes
+// in flight per strip as 8 four-byte keys at 16)
+#ifndef SGXAMD_JOIN_UP_NARROW
+#define SGXAMD_JOIN_UP_NARROW 16
+#endif
 // The kernel body for one pair of key widths (NR / NS: R / S hold u16 residuals); the
 // kernel picks it once, from the relations' key ORs, so no branch sits inside the loop.
 template <int RCAP, int BLOCK, int UP, int KS, bool NR, bool NS>
@@ -2834,11 +2839,6 @@ __device__ __forceinline__ void join_x_body(
     if (red_ticket) join_reduce_last(counts, cyc, red_result, red_ticket, L.red, tk.T);
 }
 
-// Keys per thread per strip when both relations are narrow (2-byte keys: the same bytes
-// in flight per strip as 8 four-byte keys at 16)
-#ifndef SGXAMD_JOIN_UP_NARROW
-#define SGXAMD_JOIN_UP_NARROW 16
-#endif
 template <int RCAP, int BLOCK, int UP, int KS = 1>
 __global__ __launch_bounds__(BLOCK, 1) void k_join_x(
     const uint64_t *__restrict__ R, const uint64_t *__restrict__ S, const uint64_t *__restrict__ r_start,
