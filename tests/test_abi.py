@@ -131,3 +131,26 @@ def test_multi_rejects_bad_world(sgx):
             assert e.code == sgx.MI355_ERR_INVALID
         else:
             raise AssertionError(g)
+
+
+def test_stats_structs_match_ctypes(sgx, tmp_path):
+    """The ctypes mirrors of mi355_rho_stats / mi355_multi_stats (python/sgxamd) have the C
+    headers' size and field offsets: a C program compiled against include/ prints them."""
+    structs = {"mi355_rho_stats": sgx.rho_stats, "mi355_multi_stats": sgx.multi_stats}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "sgxamd/rho.h"', '#include "sgxamd/multi.h"',
+             "int main(void) {"]
+    for cname, py in structs.items():
+        lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
+        for f, _ in py._fields_:
+            lines.append(f'printf("{cname} {f} %zu\\n", offsetof({cname}, {f}));')
+    lines.append("return 0; }")
+    src = tmp_path / "stats_layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "stats_layout"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split("\n")
+    got = {tuple(line.split()[:2]): int(line.split()[2]) for line in out if line}
+    for cname, py in structs.items():
+        assert got[(cname, "size")] == C.sizeof(py), cname
+        for f, _ in py._fields_:
+            assert got[(cname, f)] == getattr(py, f).offset, (cname, f)
