@@ -121,3 +121,27 @@ def test_chain_histograms_skewed(segs):
                                        e.get("PYTHONPATH", "")])
     r = subprocess.run([sys.executable, "-c", CHAIN_CHILD], env=e, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and "chain ok" in r.stdout, (segs, r.stdout[-2000:], r.stderr[-2000:])
+
+
+# Chain histograms (layout 3) with narrow partitions: BASELINE config 2's 2^28 pk/fk keys
+# over the 14 = 7 + 7-bit plan, pass 2 over chain-aligned segments writing 2-byte residuals.
+CHAIN_NARROW_CHILD = r"""
+import torch
+import sgxamd
+n = 1 << 28
+R = torch.empty(n, dtype=torch.int64, device="cuda:0")
+S = torch.empty(n, dtype=torch.int64, device="cuda:0")
+sgxamd.gen_pk_dev(R, n, 0, n, 11111)
+sgxamd.gen_fk_dev(S, n, 0, n, 22222)
+r = sgxamd.rho_join(R, n, S, n)
+assert r.matches == n, r.matches
+assert r.stats["layout"] == 3 and r.stats["narrow"] == 3, (r.stats["layout"], r.stats["narrow"])
+print("chain narrow ok")
+"""
+
+
+def test_chain_histograms_narrow_full_size():
+    e = dict(os.environ, SGXAMD_CHAIN_HIST="1")
+    e["PYTHONPATH"] = os.pathsep.join([os.path.join(PKG, "python"), e.get("PYTHONPATH", "")])
+    r = subprocess.run([sys.executable, "-c", CHAIN_NARROW_CHILD], env=e, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "chain narrow ok" in r.stdout, (r.stdout[-2000:], r.stderr[-2000:])
