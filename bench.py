@@ -528,7 +528,12 @@ def main():
         "M_rec_per_s_reference_formula": round((gR + gS) * args.steps / elapsed / 1e6, 1),
         "probe_phase_M_probed_tuples_per_s": round(nS / (avg["join_build_probe"] * 1e-3) / 1e6, 1),
         "probe_roofline": {"achieved": round(probe_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                           "frac": round(probe_gbs / HBM_PEAK_GBS, 4)},
+                           "frac": round(probe_gbs / HBM_PEAK_GBS, 4),
+                           "bytes": algorithmic_bytes("join_build_probe", nR, nS, *plan),
+                           "bytes_are": ("the bytes the build/probe reads: 2 per key of a narrow relation (16-bit "
+                                         "residuals), 4 per key otherwise; BASELINE.md's probe-phase definition "
+                                         "(8 B per tuple of R and S) is priced on the whole-tuple leg, "
+                                         "rho.tuple_layout.probe_roofline")},
         "kernel_ms_avg": phase, "kernel_times_from": kernel_times,
         "partition_overlap": bool(args.partition_overlap),
         "radix_bits": ls.get("radix_bits"), "passes": ls.get("passes"),
