@@ -159,7 +159,7 @@ inline bool keys_enabled() {
 // relation than the histogram pass they replace saves (r04k).
 // SGXAMD_CHAIN_HIST=1 takes them (development A/B switch; results identical).
 // Narrow key partitions (counting RHO with the 16,384-key table over key partitions):
-// pass 1 ORs every key, and when the residuals above the radix bits fit 16 bits, pass 2
+// pass 1 takes the largest key, and when the residuals above the radix bits fit 16 bits, pass 2
 // writes them as u16 and the build/probe reads 2 instead of 4 bytes per key
 // (launch_scatter_blk).  SGXAMD_NARROW=0 keeps 4-byte keys (development A/B switch).
 inline bool narrow_enabled() {
@@ -219,8 +219,8 @@ struct RelPlan {
     size_t hist1, tot1, start1, cnt1, segbase2, hist2, pstart, pcnt;
     size_t binfo, used, lbase, lcount, list;
     size_t chist, seglb, segle, segc0;  // chain histograms [F1][nseg1][F2], pass-2 segment ranges
-    size_t kor;    // pooled keys: the segments' key ORs, then the relation's ([nseg1])
-    bool narrow;   // pass 2 writes u16 residuals when the key OR allows (plan_join)
+    size_t kmax;   // pooled keys: the segments' largest keys, then the relation's ([nseg1])
+    bool narrow;   // pass 2 writes u16 residuals when the largest key allows (plan_join)
     // pooled pass 1 per input piece (the multi-GPU exchange's received pieces): piece i is
     // elements [piece_off[i], + piece_n[i]), its segments start at piece_g0[i]; its launch
     // waits for piece_ev[i] (null: no wait)
@@ -253,7 +253,7 @@ int partition_relation_pooled(Context *ctx, hipStream_t s, Timer &tm, const std:
     if (!pass2_now) {
         PoolOut po{A.at<uint32_t>(rp.binfo), A.at<uint64_t>(rp.hist1), A.at<uint32_t>(rp.used), rp.pool_blocks,
                    rp.nseg1};
-        po.kor = rp.narrow ? A.at<uint32_t>(rp.kor) : nullptr;
+        po.kmax = rp.narrow ? A.at<uint32_t>(rp.kmax) : nullptr;
         const DigitSide ds{rp.chain ? nullptr : side, key_shift + pol.b1, pol.b2};
         uint32_t *chist = rp.chain ? A.at<uint32_t>(rp.chist) : nullptr;
         tm.mark((t + "pass1_scatter").c_str());
@@ -278,7 +278,7 @@ int partition_relation_pooled(Context *ctx, hipStream_t s, Timer &tm, const std:
         }
         tm.mark((t + "pass1_scan").c_str());
         RHO_HIP(launch_pool_layout(po.cnt, rp.nseg1, pol.b1, A.at<uint64_t>(rp.tot1), start1, cnt1, lbase, lcount,
-                                   segbase2, s, rp.chain ? chain_slot_mode() : 0u, po.kor));
+                                   segbase2, s, rp.chain ? chain_slot_mode() : 0u, po.kmax));
         RHO_HIP(launch_block_list(po, lbase, list, pol.b1, s));
         *final_rel = t1;
         *pstart = start1;
@@ -289,7 +289,7 @@ int partition_relation_pooled(Context *ctx, hipStream_t s, Timer &tm, const std:
     uint64_t *ps = A.at<uint64_t>(rp.pstart);
     uint64_t *pc = A.at<uint64_t>(rp.pcnt);
     const SegMap m2{lbase, lcount, segbase2, F1, kPass2Ents, rp.n};
-    const uint32_t *narrow = rp.narrow ? A.at<uint32_t>(rp.kor) + rp.nseg1 : nullptr;
+    const uint32_t *narrow = rp.narrow ? A.at<uint32_t>(rp.kmax) + rp.nseg1 : nullptr;
     if (rp.chain) {
         // the chain histograms (recounted where a count may have wrapped) give the
         // chain-aligned pass-2 segments, their cursors and the partition table
@@ -434,7 +434,7 @@ void plan_relation(Arena &A, RelPlan &rp, uint64_t n, const Policy &pol, int poo
     rp.keys = false;
     rp.chain = false;
     rp.narrow = false;
-    rp.kor = 0;
+    rp.kmax = 0;
     rp.in_size = sizeof(row_t);
     rp.piece_off.clear();
     rp.piece_n.clear();
@@ -494,7 +494,7 @@ void plan_relation(Arena &A, RelPlan &rp, uint64_t n, const Policy &pol, int poo
         rp.lbase = A.reserve(sizeof(uint64_t) * F1);
         rp.lcount = A.reserve(sizeof(uint64_t) * F1);
         rp.list = A.reserve(sizeof(uint64_t) * (size_t)(rp.n / kBlk + (uint64_t)rp.nseg1 * F1));
-        if (rp.keys) rp.kor = A.reserve(sizeof(uint32_t) * ((size_t)rp.nseg1 + 1));
+        if (rp.keys) rp.kmax = A.reserve(sizeof(uint32_t) * ((size_t)rp.nseg1 + 1));
     }
     if (rp.chain) {
         rp.chist = A.reserve(sizeof(uint32_t) * (size_t)F1 * rp.nseg1 * F2);
@@ -752,14 +752,18 @@ int join_finish(Context *ctx, PendingJoin &pj, const row_t *dS, uint64_t nS, mi3
     uint32_t *n_over = reinterpret_cast<uint32_t *>(result + 3);
     const uint32_t hash_shift = pj.key_shift + pol.bits;
     tm.mark("join_tasks");
-    RHO_HIP(launch_make_tasks(pcR, pcS, P, over, pj.over_cap, result + 1, pj.s_chunk, s));
+    // narrow plans: k_join_n adds into the count and tick slots, zeroed here
+    const bool nar = !pj.materialize && (pj.pr.narrow || pj.ps.narrow) && narrow_join_enabled();
+    RHO_HIP(launch_make_tasks(pcR, pcS, P, over, pj.over_cap, result + 1, pj.s_chunk, s, nar ? counts : nullptr, cyc,
+                              join_grid));
     if (!pj.materialize) {
         tm.mark("join_build_probe");
         RHO_HIP(launch_join(fR, fS, psR, pcR, psS, pcS, P, over, n_over, hash_shift, pol.rcap, pj.s_chunk, join_grid,
                             kJoinCount, algo, counts, nullptr, nullptr, cyc, s, nullptr, pj.pr.keys ? 1 : 2,
                             reinterpret_cast<uint32_t *>(result + 6),
-                            pj.pr.narrow ? A.at<uint32_t>(pj.pr.kor) + pj.pr.nseg1 : nullptr,
-                            pj.ps.narrow ? A.at<uint32_t>(pj.ps.kor) + pj.ps.nseg1 : nullptr));
+                            pj.pr.narrow ? A.at<uint32_t>(pj.pr.kmax) + pj.pr.nseg1 : nullptr,
+                            pj.ps.narrow ? A.at<uint32_t>(pj.ps.kmax) + pj.ps.nseg1 : nullptr,
+                            (uint32_t)std::min<uint64_t>(P + pj.over_cap - 1, 0xFFFFFFFFull)));
         tm.mark("join_reduce");
         RHO_HIP(launch_reduce(counts, join_grid, result, cyc, join_grid, s));
     } else {

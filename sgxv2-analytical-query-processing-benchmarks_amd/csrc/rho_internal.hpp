@@ -137,7 +137,7 @@ struct PoolOut {
     uint32_t pool_blocks;  // blocks per segment pool
     uint32_t nseg;
     uint32_t g0 = 0;       // this launch's first segment (a pass 1 launched per input piece)
-    uint32_t *kor = nullptr;  // keys (nullable): per segment, the OR of its keys (narrow residuals)
+    uint32_t *kmax = nullptr;  // keys (nullable): per segment, its largest key (narrow residuals)
 };
 // Pass 1 of a pooled plan: contiguous input segments (m), pooled output in out, digit
 // side stream ds beside every stored element.  Elements: in_size-byte input
@@ -177,12 +177,12 @@ hipError_t launch_chain_scan(const uint64_t *cnt, uint32_t nseg, uint32_t mode, 
 // tuple starts / counts (the pass-2 output layout), region block-list bases / lengths
 // and the pass-2 segment table (kPass2Ents blocks per segment).
 // chain_mode 1 / 2: the slots of chain-aligned segments (launch_chain_scan) instead.
-// kor (nullable): the segments' key ORs (PoolOut::kor), folded into kor[nseg] — the OR
-// of every key of the relation, which tells pass 2 and the build/probe whether the key
+// kmax (nullable): the segments' largest keys (PoolOut::kmax), folded into kmax[nseg] —
+// the relation's largest key, which tells pass 2 and the build/probe whether the key
 // residuals above the radix bits fit 16 bits (narrow partitions, launch_scatter_blk).
 hipError_t launch_pool_layout(uint64_t *cnt, uint32_t nseg, uint32_t bits, uint64_t *totals, uint64_t *start,
                               uint64_t *count, uint64_t *lbase, uint64_t *lcount, uint32_t *seg_base, hipStream_t s,
-                              uint32_t chain_mode = 0, uint32_t *kor = nullptr);
+                              uint32_t chain_mode = 0, uint32_t *kmax = nullptr);
 // The block list: region d's blocks at [lbase[d], lbase[d] + lcount[d]) as
 // physical block | fill << 32.
 hipError_t launch_block_list(const PoolOut &po, const uint64_t *lbase, uint64_t *list, uint32_t bits, hipStream_t s);
@@ -190,7 +190,7 @@ hipError_t launch_block_list(const PoolOut &po, const uint64_t *lbase, uint64_t 
 // reg_count = lcount, seg_size = kPass2Ents).
 hipError_t launch_hist_side_blk(const uint8_t *side, const uint64_t *list, const SegMap &m, uint32_t grid,
                                 uint32_t bits, uint64_t *hist, hipStream_t s);
-// narrow (nullable; key partitions through k_sort_blk only): the relation's key OR
+// narrow (nullable; key partitions through k_sort_blk only): the relation's largest key
 // (launch_pool_layout).  When every key's residual above the radix bits (key >>
 // (shift + bits)) fits 16 bits, the partitions are written as those u16 residuals —
 // the build/probe (launch_join with the same word) compares residuals, which within
@@ -237,8 +237,11 @@ enum JoinAlgo : int { kAlgoChaining = 0, kAlgoHistogram = 1 };
 // meta (zeroed here): [0] = largest R partition, [1] = largest S partition,
 // [2] = the number of extra tasks (u32 n_over, read by launch_join / launch_excl_scan),
 // [3..5] zero as well ([5]: launch_join's task tickets).
+// zero / zero2 (nullable): nzero / 2 nzero u64 words zeroed as well (k_join_n's count
+// and tick slots).
 hipError_t launch_make_tasks(const uint64_t *r_count, const uint64_t *s_count, uint64_t P, uint64_t *over,
-                             uint32_t over_cap, uint64_t *meta, uint64_t s_chunk, hipStream_t s);
+                             uint32_t over_cap, uint64_t *meta, uint64_t s_chunk, hipStream_t s,
+                             uint64_t *zero = nullptr, uint64_t *zero2 = nullptr, uint32_t nzero = 0);
 // reduce (mode 0, nullable): the last workgroup to finish sums the partial counts and
 // ticks into reduce->result as launch_reduce does (reduce->ticket: a Context::sync word).
 struct JoinReduce {
@@ -251,15 +254,19 @@ hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, 
                        int mode, int algo, uint64_t *counts, const uint64_t *task_off, output_triple_t *out,
                        uint64_t *cyc, hipStream_t s, const JoinReduce *reduce = nullptr, int key_stride = 2,
                        uint32_t *tickets = nullptr, const uint32_t *narrow_r = nullptr,
-                       const uint32_t *narrow_s = nullptr);
+                       const uint32_t *narrow_s = nullptr, uint32_t tasks_max = 0);
 // key_stride 2: R / S are row_t partitions; 1: packed u32 keys (counting RHO only —
 // the partitions of a counting join carry keys only after the input read).
 // tickets (nullable; a u32 that is zero at the launch, e.g. meta[5] of launch_make_tasks):
 // the 16,384-key counting table takes its tasks by ticket (k_join_x, SGXAMD_JOIN_TICKETS
 // builds) instead of by grid stride.
-// narrow_r / narrow_s (nullable; the 16,384-key counting table, key_stride 1): the key
-// ORs given to launch_scatter_blk for R / S — a relation whose residuals fit 16 bits
-// was written as u16 residuals.
+// narrow_r / narrow_s (nullable; the 16,384-key counting table, key_stride 1): the
+// largest keys given to launch_scatter_blk for R / S — a relation whose residuals fit 16
+// bits was written as u16 residuals.  Then the join runs in k_join_n (SGXAMD_JOIN_N),
+// one workgroup per task: tasks_max (>= P + *n_over) workgroups, their counts and
+// ticks added into counts[0 .. grid) / cyc[0 .. 2 grid), which must be zero (the zero
+// words of launch_make_tasks).
+bool narrow_join_enabled();
 // One-block exclusive scan of n_base + *n_extra values; *total = their sum.
 hipError_t launch_excl_scan(const uint64_t *in, const uint32_t *n_extra, uint64_t n_base, uint64_t *out,
                             uint64_t *total, hipStream_t s);

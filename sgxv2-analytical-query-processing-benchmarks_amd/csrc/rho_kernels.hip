@@ -760,7 +760,7 @@ struct ScatterLds {
                                       //          first granule of the blocks d took for this tile}
     uint64_t ents[EXT == 2 ? kPass2Ents : 1];  // block-list input: phys block | fill << 32
     uint32_t pool_next;               // pooled: blocks taken from the segment's pool
-    uint32_t kor;                     // pooled keys: the OR of the segment's keys
+    uint32_t kmax;                    // pooled keys: the largest key of the segment
 };
 
 // Chain histograms (pooled pass 1 of keys, F2 > 0): every chain's histogram of pass-2
@@ -1363,7 +1363,7 @@ __device__ __forceinline__ void scatter_segment_ext(ScatterLds<BITS, ITEMS, NT, 
     }
     if (tid == 0) {
         L.pool_next = 0;
-        L.kor = 0;
+        L.kmax = 0;
     }
     if constexpr (F2 > 0) {
         for (uint32_t i = tid; i < F * F2 / 2; i += NT) cs->h2[i] = 0;
@@ -1404,14 +1404,14 @@ __device__ __forceinline__ void scatter_segment_ext(ScatterLds<BITS, ITEMS, NT, 
         return scatter_tile_sort<BITS, ITEMS, NT, EXT, T, false, F2>(L, pend, carried, v, out, tn, shift, 0, &ps,
                                                                      cs);
     };
-    // pooled keys: the OR of the segment's keys (lanes past its end load 0), whether pass
-    // 2 may write 16-bit residuals (k_sort_blk)
+    // pooled keys: the largest key of the segment (lanes past its end load 0): whether
+    // pass 2 may write 16-bit residuals (k_sort_blk), and the build/probe's table size
     constexpr bool KOR = EXT == 1 && sizeof(T) == 4;
-    uint32_t kor = 0;
-    const auto key_or = [&](const T(&v)[ITEMS]) {
+    uint32_t kmax = 0;
+    const auto key_max = [&](const T(&v)[ITEMS]) {
         if constexpr (KOR) {
 #pragma unroll
-            for (int k = 0; k < ITEMS; ++k) kor |= (uint32_t)v[k];
+            for (int k = 0; k < ITEMS; ++k) kmax = max(kmax, (uint32_t)v[k]);
         }
     };
     // the two-tiles-in-flight pipeline of scatter_segment
@@ -1420,7 +1420,7 @@ __device__ __forceinline__ void scatter_segment_ext(ScatterLds<BITS, ITEMS, NT, 
     uint32_t mb = load(1, vb);
 #pragma unroll
     for (int k = 0; k < ITEMS; ++k) asm volatile("" ::"v"(va[k]));
-    key_or(va);
+    key_max(va);
     uint32_t gt = sort(va, tn_of(0, ma));
     for (uint32_t ti = 0;; ti += 2) {
         ma = load(ti + 2, va);
@@ -1428,17 +1428,17 @@ __device__ __forceinline__ void scatter_segment_ext(ScatterLds<BITS, ITEMS, NT, 
         for (int k = 0; k < ITEMS; ++k) asm volatile("" ::"v"(vb[k]));
         scatter_tile_write<BITS, ITEMS, NT, SIDE, EXT, T>(L, out, gt, side, shift2, mask2);
         if (ti + 1 >= ntiles) break;
-        key_or(vb);
+        key_max(vb);
         gt = sort(vb, tn_of(ti + 1, mb));
         mb = load(ti + 3, vb);
 #pragma unroll
         for (int k = 0; k < ITEMS; ++k) asm volatile("" ::"v"(va[k]));
         scatter_tile_write<BITS, ITEMS, NT, SIDE, EXT, T>(L, out, gt, side, shift2, mask2);
         if (ti + 2 >= ntiles) break;
-        key_or(va);
+        key_max(va);
         gt = sort(va, tn_of(ti + 2, ma));
     }
-    if (KOR && kor) atomicOr(&L.kor, kor);
+    if (KOR && kmax) atomicMax(&L.kmax, kmax);
     // flush the carried (partial) granules; pooled: close every chain
     __syncthreads();
     if (tid < F) {
@@ -1464,7 +1464,7 @@ __device__ __forceinline__ void scatter_segment_ext(ScatterLds<BITS, ITEMS, NT, 
     __syncthreads();
     if (EXT == 1 && tid == 0) {
         po.used[gp] = L.pool_next;
-        if (KOR && po.kor) po.kor[gp] = L.kor;
+        if (KOR && po.kmax) po.kmax[gp] = L.kmax;
     }
     const uint32_t lane = tid & (G - 1);
     for (uint32_t d = tid / G; d < F; d += NG) {
@@ -1569,7 +1569,7 @@ struct SortBlkLds {
 #define SGXAMD_SORT_UNROLL 16
 #endif
 // NAR: narrow partitions — every key's residual above the radix bits fits 16 bits (the
-// relation's key OR from pass 1), so the output holds those u16 residuals.  The kernel
+// relation's largest key from pass 1), so the output holds those u16 residuals.  The kernel
 // picks the body once (one copy of the loop each, no store branches inside it).
 template <int BITS, int NT, int ITEMS, bool NAR>
 __device__ __forceinline__ void sort_blk_body(SortBlkLds<BITS, NT, ITEMS> &L, const uint32_t *__restrict__ in,
@@ -1902,11 +1902,11 @@ __global__ __launch_bounds__(1024) void k_pool_layout(const uint64_t *__restrict
                                                       uint64_t *__restrict__ start, uint64_t *__restrict__ count,
                                                       uint64_t *__restrict__ lbase, uint64_t *__restrict__ lcount,
                                                       uint32_t *__restrict__ seg_base, uint32_t chain_nseg,
-                                                      uint32_t chain_mode, uint32_t *__restrict__ kor) {
+                                                      uint32_t chain_mode, uint32_t *__restrict__ kmax) {
     __shared__ uint64_t scratch[1024 / kWave + 1];
-    __shared__ uint32_t kor_all;
+    __shared__ uint32_t kmax_all;
     const uint32_t d = threadIdx.x;
-    if (d == 0) kor_all = 0;
+    if (d == 0) kmax_all = 0;
     const uint64_t v = d < F ? totals[d] : 0;
     const uint64_t tup = v & ((1ull << 40) - 1), blk = v >> 40;
     uint64_t tot;
@@ -1925,25 +1925,25 @@ __global__ __launch_bounds__(1024) void k_pool_layout(const uint64_t *__restrict
         seg_base[d] = (uint32_t)ex_s;
     }
     if (d == 0) seg_base[F] = (uint32_t)tot;
-    if (kor) {  // (chain_nseg: the pass-1 segments) the relation's key OR into kor[nseg]
+    if (kmax) {  // (chain_nseg: the pass-1 segments) the relation's largest key into kmax[nseg]
         uint32_t x = 0;
-        for (uint32_t i = d; i < chain_nseg; i += blockDim.x) x |= kor[i];
-        if (x) atomicOr(&kor_all, x);
+        for (uint32_t i = d; i < chain_nseg; i += blockDim.x) x = max(x, kmax[i]);
+        if (x) atomicMax(&kmax_all, x);
         __syncthreads();
-        if (d == 0) kor[chain_nseg] = kor_all;
+        if (d == 0) kmax[chain_nseg] = kmax_all;
     }
 }
 
 hipError_t launch_pool_layout(uint64_t *cnt, uint32_t nseg, uint32_t bits, uint64_t *totals, uint64_t *start,
                               uint64_t *count, uint64_t *lbase, uint64_t *lcount, uint32_t *seg_base, hipStream_t s,
-                              uint32_t chain_mode, uint32_t *kor) {
+                              uint32_t chain_mode, uint32_t *kmax) {
     const uint32_t F = 1u << bits;
     hipLaunchKernelGGL(k_scan_cols, dim3(F), dim3(kBlock), 0, s, cnt, nseg, totals);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const uint32_t threads = F < 64 ? 64 : F;
     hipLaunchKernelGGL(k_pool_layout, dim3(1), dim3(threads), 0, s, totals, F, start, count, lbase, lcount, seg_base,
-                       nseg, chain_mode, kor);
+                       nseg, chain_mode, kmax);
     return hipGetLastError();
 }
 
@@ -2757,7 +2757,7 @@ __device__ __forceinline__ uint32_t x_step(JoinLdsX<RCAP, BLOCK / kWave> &L, con
 #define SGXAMD_JOIN_UP_NARROW 16
 #endif
 // The kernel body for one pair of key widths (NR / NS: R / S hold u16 residuals); the
-// kernel picks it once, from the relations' key ORs, so no branch sits inside the loop.
+// kernel picks it once, from the relations' largest keys, so no branch sits inside the loop.
 template <int RCAP, int BLOCK, int UP, int KS, bool NR, bool NS>
 __device__ __forceinline__ void join_x_body(
     JoinLdsX<RCAP, BLOCK / kWave> &L, const uint64_t *__restrict__ R, const uint64_t *__restrict__ S,
@@ -2846,15 +2846,16 @@ __global__ __launch_bounds__(BLOCK, 1) void k_join_x(
     uint64_t P, const uint64_t *__restrict__ over, const uint32_t *__restrict__ n_over, uint32_t hash_shift,
     uint64_t s_chunk, uint64_t *__restrict__ counts, uint64_t *__restrict__ cyc, uint64_t *__restrict__ red_result,
     uint64_t *__restrict__ red_ticket, uint32_t ncounts, uint32_t *__restrict__ tickets,
-    const uint32_t *__restrict__ narrow_r, const uint32_t *__restrict__ narrow_s) {
+    const uint32_t *__restrict__ narrow_r, const uint32_t *__restrict__ narrow_s, uint32_t skip_narrow) {
     __shared__ JoinLdsX<RCAP, BLOCK / kWave> L;
     // (the same test as k_sort_blk's, which wrote the partitions)
     const bool nr = narrow_r != nullptr && ((*narrow_r >> hash_shift) >> 16) == 0;
     const bool ns = narrow_s != nullptr && ((*narrow_s >> hash_shift) >> 16) == 0;
+    if (skip_narrow && (nr || ns)) return;  // k_join_n, launched beside it, joins them
     // the direct table's counters: residuals below 2^(the fewest residual bits of a narrow
     // relation; 16 for a wide one) — BASELINE config 2's keys 1..2^28 over 14 bits: 2^14
-    const auto res_bits = [&](bool n, const uint32_t *kor) -> uint32_t {
-        const uint32_t x = n ? (*kor >> hash_shift) : 0xFFFFu;
+    const auto res_bits = [&](bool n, const uint32_t *kmax) -> uint32_t {
+        const uint32_t x = n ? (*kmax >> hash_shift) : 0xFFFFu;
         return x ? 32u - (uint32_t)__builtin_clz(x) : 0u;
     };
 #ifdef SGXAMD_JOIN_FULL_TABLE  // development A/B: all 2^16 counters
@@ -2879,6 +2880,273 @@ __global__ __launch_bounds__(BLOCK, 1) void k_join_x(
     }
 #undef JOIN_X_BODY
 #undef JOIN_X_BODY_U
+}
+
+// ------------------------------------------- narrow build/probe (round 5) ---
+// k_join_n: bucket_chaining_join (radix_join.cpp:359-458) over narrow partitions as a
+// direct count table (x_step DIRECT's table: one counter per residual, since a chain of
+// the one-bucket-per-residual table holds one key value and a probe counts its length),
+// with an LDS footprint sized to the residuals instead of k_join_x's 128 KiB chain
+// table, and one task per workgroup: two to four workgroups share a CU, so one task's
+// clear and barriers overlap another's loads (k_join_x, one workgroup per CU, left the
+// CU's memory queue idle at every per-chunk clear and build->probe barrier).
+//
+// Table: kNarrowCap counters (2^14 + 64: BASELINE config 2's keys 1..2^28 over 14 radix
+// bits leave residuals 0..2^14 -- the relations' largest keys, pass 1's kmax words, give
+// the bound) and two dump slots: DR takes the R keys that do not go into the table
+// (outside the strip, or, in the general body, outside the window), DS -- never written
+// -- is the counter the S keys outside read (0).  C16: u16 counters, two per word
+// (a chunk holds at most kBigRcap keys: no carry into the neighbour).
+//
+// Keys stream in strips of L 16-byte loads per thread (8 u16 residuals or 4 u32 keys per
+// load), through a buffer resource from the 16-byte boundary at or below the range's
+// first key; lanes whose 16 bytes straddle the range's ends replace the keys outside it
+// with the dump slot (only the first and last strip check, a branch only those lanes
+// take), so the loops themselves hold no per-key test.
+//
+// Fast body (both relations narrow, every residual below kNarrowCap): per key one LDS
+// add (build) or one LDS read (probe) and its address.  General body (one relation
+// wide, or residuals up to 2^16): the matching residual range [0, lim) (the narrow
+// relations' largest residual + 1) in windows of kNarrowCap, each key mapped to its
+// window's counter or the dump slot; the strips of a chunk are read once per window.
+constexpr uint32_t kNarrowCap = (1u << 14) + 64;
+
+template <int BLOCK, bool C16>
+struct JoinLdsN {
+    static constexpr uint32_t DR = kNarrowCap, DS = C16 ? kNarrowCap + 2 : kNarrowCap + 1;
+    static constexpr uint32_t WORDS = ((C16 ? kNarrowCap / 2 + 2 : kNarrowCap + 2) + 3) & ~3u;
+    uint32_t cnt[WORDS];
+    uint64_t red[BLOCK / kWave];
+};
+
+// One relation's range of a task: 16-byte aligned byte base, the keys before the range
+// start inside the first 16 bytes (h), the keys (n), strips of SB bytes.
+struct NRange {
+    const char *p;
+    uint32_t h, n, strips, bytes;
+};
+
+template <int ESZ, uint32_t SB>
+__device__ __forceinline__ NRange n_range(const void *keys, uint64_t first, uint32_t n) {
+    const uint64_t b = first * ESZ, a = b & ~15ull;
+    NRange r;
+    r.p = static_cast<const char *>(keys) + a;
+    r.h = (uint32_t)(b - a) / ESZ;
+    r.n = n;
+    // whole 16-byte units (the buffers hold at least 15 bytes past any range: the
+    // partitions of |X| keys sit in a buffer of 8 |X| bytes)
+    r.bytes = ((r.h + n) * ESZ + 15u) & ~15u;
+    r.strips = (r.bytes + SB - 1) / SB;
+    return r;
+}
+
+// (bytes = 0: no strip, every load reads 0; issued all the same, so that no branch
+// stands between a strip's loads and the wait for them)
+template <int BLOCK, int L>
+__device__ __forceinline__ void n_load(const char *p, uint32_t bytes, uint32_t k, uint4 (&v)[L]) {
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(p, bytes);
+#pragma unroll
+    for (int j = 0; j < L; ++j)
+        v[j] = buf_ld_nt_u128(rs, (k * (uint32_t)(BLOCK * L) + threadIdx.x + (uint32_t)j * BLOCK) * 16u, 0);
+}
+
+// The u16 residuals of one 16-byte load outside [h, h + n) (element q0 = the load's
+// first) replaced by the dump slot D (a u16 value: kNarrowCap + 2 < 2^16).
+__device__ __forceinline__ void n_fix16(uint4 &w, uint32_t q0, uint32_t h, uint32_t n, uint32_t D) {
+    uint32_t c[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const bool lo = q0 + 2 * i - h < n, hi = q0 + 2 * i + 1 - h < n;
+        c[i] = (lo ? c[i] & 0xFFFFu : D) | (hi ? c[i] & 0xFFFF0000u : D << 16);
+    }
+    w = make_uint4(c[0], c[1], c[2], c[3]);
+}
+
+template <bool C16>
+__device__ __forceinline__ void n_add(uint32_t *cnt, uint32_t k) {
+    if constexpr (C16) atomicAdd(&cnt[k >> 1], 1u << ((k & 1u) << 4));
+    else atomicAdd(&cnt[k], 1u);
+}
+template <bool C16>
+__device__ __forceinline__ uint32_t n_get(const uint32_t *cnt, uint32_t k) {
+    if constexpr (C16) return reinterpret_cast<const uint16_t *>(cnt)[k];
+    else return cnt[k];
+}
+
+// One strip of a relation: build (BUILD: adds) or probe (returns the matches).
+// NAR: u16 residuals; else u32 keys (residual = key >> hash_shift).  GEN: the general
+// body's window mapping (wb: the window's first residual, wl: its counters in use).
+template <int BLOCK, int L, bool C16, bool NAR, bool BUILD, bool GEN>
+__device__ __forceinline__ uint32_t n_strip(uint32_t *cnt, const NRange &r, uint32_t k, uint4 (&v)[L],
+                                            uint32_t hash_shift, uint32_t wb, uint32_t wl) {
+    constexpr uint32_t KPL = NAR ? 8 : 4;
+    constexpr uint32_t D = BUILD ? JoinLdsN<BLOCK, C16>::DR : JoinLdsN<BLOCK, C16>::DS;
+    // the strip's first and last units may straddle the range's ends (uniform test)
+    const uint32_t u0 = k * (uint32_t)(BLOCK * L);
+    const bool edge = (k == 0 && r.h != 0) || (u0 + BLOCK * L) * KPL > r.h + r.n;
+    uint32_t m = 0;
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+        const uint32_t q0 = (u0 + threadIdx.x + (uint32_t)j * BLOCK) * KPL;
+        if constexpr (!GEN) {  // (both narrow, every residual inside the table)
+            if (edge && (q0 < r.h || q0 + KPL > r.h + r.n)) n_fix16(v[j], q0, r.h, r.n, D);
+            const uint32_t c[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t a = c[i] & 0xFFFFu, b = c[i] >> 16;
+                if constexpr (BUILD) {
+                    n_add<C16>(cnt, a);
+                    n_add<C16>(cnt, b);
+                } else {
+                    m += n_get<C16>(cnt, a) + n_get<C16>(cnt, b);
+                }
+            }
+        } else {
+            const uint32_t c[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+#pragma unroll
+            for (int i = 0; i < (int)KPL; ++i) {
+                const uint32_t key = NAR ? ((c[i / 2] >> ((i & 1) * 16)) & 0xFFFFu) : (c[i] >> hash_shift);
+                const uint32_t x = key - wb;
+                const uint32_t e = (q0 + (uint32_t)i - r.h < r.n && x < wl) ? x : D;
+                if constexpr (BUILD) n_add<C16>(cnt, e);
+                else m += n_get<C16>(cnt, e);
+            }
+        }
+    }
+    return m;
+}
+
+// One task (a partition's S chunk): per R chunk of kBigRcap keys and per window, clear,
+// build from R's strips, probe S's strips; the strips of one (chunk, window) pass are
+// one sequence with the next strip's loads in flight while one is processed.
+template <int BLOCK, int L, bool C16, bool NR, bool NS, bool GEN>
+__device__ __forceinline__ uint64_t join_n_task(JoinLdsN<BLOCK, C16> &Ls, const void *rk, const void *sk,
+                                                uint64_t r_base, uint64_t nR, uint64_t s_base, uint32_t nS,
+                                                uint32_t hash_shift, uint32_t lim, uint64_t &bt, uint64_t &pt) {
+    constexpr uint32_t SB = BLOCK * L * 16u;
+    constexpr int ER = NR ? 2 : 4, ES = NS ? 2 : 4;
+    const uint32_t nwin = GEN ? (lim + kNarrowCap - 1) / kNarrowCap : 1u;
+    const NRange sr = n_range<ES, SB>(sk, s_base, nS);
+    uint64_t m = 0;
+    bool first = true;
+    for (uint64_t rc = 0; rc < nR; rc += kBigRcap) {
+        const NRange rr = n_range<ER, SB>(rk, r_base + rc, (uint32_t)min(nR - rc, (uint64_t)kBigRcap));
+        const uint32_t nsr = rr.strips, ns = nsr + sr.strips;
+        for (uint32_t w = 0; w < nwin; ++w) {
+            const uint32_t wb = w * kNarrowCap, wl = GEN ? min(kNarrowCap, lim - wb) : kNarrowCap;
+            const uint64_t t0 = wall_clock64();
+            uint4 va[L], vb[L];
+            const auto load = [&](uint32_t i, uint4(&v)[L]) {
+                const bool isr = i < nsr;
+                n_load<BLOCK, L>(isr ? rr.p : sr.p, isr ? rr.bytes : (i < ns ? sr.bytes : 0u), isr ? i : i - nsr, v);
+            };
+            uint64_t tb = t0;
+            const auto step = [&](uint32_t i, uint4(&v)[L]) {
+                if (i < nsr) {
+                    n_strip<BLOCK, L, C16, NR, true, GEN>(Ls.cnt, rr, i, v, hash_shift, wb, wl);
+                    if (i + 1 == nsr) {
+                        __syncthreads();  // the table is complete
+                        tb = wall_clock64();
+                    }
+                } else {
+                    m += n_strip<BLOCK, L, C16, NS, false, GEN>(Ls.cnt, sr, i - nsr, v, hash_shift, wb, wl);
+                }
+            };
+            load(0, va);
+            if (!first) __syncthreads();  // the previous pass's probe is done with the table
+            first = false;
+            for (uint32_t i = threadIdx.x; i < JoinLdsN<BLOCK, C16>::WORDS / 4; i += BLOCK)
+                reinterpret_cast<uint4 *>(Ls.cnt)[i] = make_uint4(0, 0, 0, 0);
+            __syncthreads();
+            // two register sets, the loop unrolled by two (no copy of a set in flight)
+            for (uint32_t i = 0;; i += 2) {
+                load(i + 1, vb);
+#pragma unroll
+                for (int j = 0; j < L; ++j) asm volatile("" ::"v"(va[j].x), "v"(va[j].y), "v"(va[j].z), "v"(va[j].w));
+                step(i, va);
+                if (i + 1 >= ns) break;
+                load(i + 2, va);
+#pragma unroll
+                for (int j = 0; j < L; ++j) asm volatile("" ::"v"(vb[j].x), "v"(vb[j].y), "v"(vb[j].z), "v"(vb[j].w));
+                step(i + 1, vb);
+                if (i + 2 >= ns) break;
+            }
+            bt += tb - t0;
+            pt += wall_clock64() - tb;
+        }
+    }
+    return m;
+}
+
+// Geometry: BLOCK threads, L 16-byte loads per thread and strip, C16 u16 counters,
+// WPC workgroups per CU (occupancy hint).
+#ifndef SGXAMD_JN_BLOCK
+#define SGXAMD_JN_BLOCK 512
+#endif
+#ifndef SGXAMD_JN_L
+#define SGXAMD_JN_L 4
+#endif
+#ifndef SGXAMD_JN_C16
+#define SGXAMD_JN_C16 0
+#endif
+#ifndef SGXAMD_JN_WPC
+#define SGXAMD_JN_WPC 2
+#endif
+
+// grid = an upper bound of the tasks (P + over_cap - 1); workgroup t takes task t
+// (decode_task: the partitions, then the further S chunks of large ones).  Counts and
+// build / probe ticks go to slot t mod nslots (device atomics, the slots zeroed by
+// launch_make_tasks).  Nothing to do unless a relation is narrow (k_join_x, launched
+// beside it, takes that case).
+template <int BLOCK, int L, bool C16>
+__global__ __launch_bounds__(BLOCK, BLOCK *SGXAMD_JN_WPC / 256) void k_join_n(
+    const void *__restrict__ R, const void *__restrict__ S, const uint64_t *__restrict__ r_start,
+    const uint64_t *__restrict__ r_count, const uint64_t *__restrict__ s_start, const uint64_t *__restrict__ s_count,
+    uint64_t P, const uint64_t *__restrict__ over, const uint32_t *__restrict__ n_over, uint32_t hash_shift,
+    uint64_t s_chunk, uint64_t *__restrict__ counts, uint64_t *__restrict__ cyc, uint32_t nslots,
+    uint32_t *__restrict__ tickets, const uint32_t *__restrict__ narrow_r, const uint32_t *__restrict__ narrow_s) {
+    __shared__ JoinLdsN<BLOCK, C16> Ls;
+    // the largest residual of each relation (k_sort_blk's test: narrow below 2^16)
+    const uint32_t xr = narrow_r ? (*narrow_r >> hash_shift) : 0xFFFFFFFFu;
+    const uint32_t xs = narrow_s ? (*narrow_s >> hash_shift) : 0xFFFFFFFFu;
+    const bool nr = xr < 0x10000u, ns = xs < 0x10000u;
+    if (!nr && !ns) return;
+    if (tickets && blockIdx.x == 0 && threadIdx.x == 0) tickets[1] = 1u | (nr ? 2u : 0u) | (ns ? 4u : 0u);
+    const uint64_t t = blockIdx.x;
+    if (t >= P + *n_over) return;
+    uint64_t p, chunk;
+    decode_task(t, P, over, p, chunk);
+    const uint64_t nR = r_count[p], nSp = s_count[p];
+    const uint64_t s_lo = chunk * s_chunk;
+    const uint64_t rem = nSp > s_lo ? nSp - s_lo : 0;
+    const uint32_t nS = nR == 0 ? 0u : (uint32_t)(rem < s_chunk ? rem : s_chunk);
+    if (nS == 0) return;
+    const uint64_t rb = r_start[p], sb = s_start[p] + s_lo;
+    // the residuals that can match: [0, lim), lim = the narrow relations' smallest
+    // (largest residual + 1)
+    const uint32_t lim = min(nr ? xr + 1 : 0xFFFFFFFFu, ns ? xs + 1 : 0xFFFFFFFFu);
+    uint64_t bt = 0, pt = 0, m;
+    if (nr && ns && xr < kNarrowCap && xs < kNarrowCap)
+        m = join_n_task<BLOCK, L, C16, true, true, false>(Ls, R, S, rb, nR, sb, nS, hash_shift, lim, bt, pt);
+    else if (nr && ns)
+        m = join_n_task<BLOCK, L, C16, true, true, true>(Ls, R, S, rb, nR, sb, nS, hash_shift, lim, bt, pt);
+    else if (nr)
+        m = join_n_task<BLOCK, L, C16, true, false, true>(Ls, R, S, rb, nR, sb, nS, hash_shift, lim, bt, pt);
+    else
+        m = join_n_task<BLOCK, L, C16, false, true, true>(Ls, R, S, rb, nR, sb, nS, hash_shift, lim, bt, pt);
+    m = wave_sum_u64(m);
+    if (__lane_id() == 0) Ls.red[threadIdx.x / kWave] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t acc = 0;
+        for (int w = 0; w < BLOCK / kWave; ++w) acc += Ls.red[w];
+        const uint32_t slot = (uint32_t)(t % nslots);
+        if (acc) atomicAdd((unsigned long long *)&counts[slot], (unsigned long long)acc);
+        if (cyc) {
+            atomicAdd((unsigned long long *)&cyc[2 * slot], (unsigned long long)bt);
+            atomicAdd((unsigned long long *)&cyc[2 * slot + 1], (unsigned long long)pt);
+        }
+    }
 }
 
 // ------------------------------------------------------- histogram join (RHT) ---
@@ -3260,13 +3528,24 @@ uint32_t cu_count() {
     return n;
 }
 
+// SGXAMD_JOIN_N (development A/B switch, read once): 1 (default) = narrow relations'
+// build/probe in k_join_n (one task per workgroup, the table sized to the residuals);
+// 0 = k_join_x's direct table (one workgroup per CU).
+bool narrow_join_enabled() {
+    static const bool on = [] {
+        const char *e = std::getenv("SGXAMD_JOIN_N");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return on;
+}
+
 // Counting build/probe over packed keys (key-only partitions, KS = 1).
 hipError_t launch_join_keys(const void *R, const void *S, const uint64_t *r_start, const uint64_t *r_count,
                             const uint64_t *s_start, const uint64_t *s_count, uint64_t P, const uint64_t *over,
                             const uint32_t *n_over, uint32_t hash_shift, uint32_t rcap, uint64_t s_chunk,
                             uint32_t grid, int mode, int algo, uint64_t *counts, uint64_t *cyc, hipStream_t s,
                             const JoinReduce *reduce, uint32_t *tickets, const uint32_t *narrow_r,
-                            const uint32_t *narrow_s) {
+                            const uint32_t *narrow_s, uint32_t tasks_max) {
     if (mode != kJoinCount) return hipErrorInvalidValue;
     // narrow partitions are read by the 16,384-key chaining table only
     if ((narrow_r || narrow_s) && !(algo == kAlgoChaining && rcap == kBigRcap)) return hipErrorInvalidValue;
@@ -3297,9 +3576,23 @@ hipError_t launch_join_keys(const void *R, const void *S, const uint64_t *r_star
     }
     if (algo != kAlgoChaining) return hipErrorInvalidValue;
     if (rcap == kBigRcap) {  // one workgroup per CU (128 KiB table), strips of 8 keys per thread
+        // narrow relations: k_join_n, one task per workgroup (tasks_max of them), its
+        // counts and ticks added into the grid's slots (zeroed by launch_make_tasks);
+        // k_join_x takes the join only when neither relation is narrow (the width is
+        // known on the device only: both are launched, one returns at once)
+        const bool nar = (narrow_r || narrow_s) && narrow_join_enabled();
+        if (nar) {
+            if (reduce) return hipErrorInvalidValue;
+            hipLaunchKernelGGL((k_join_n<SGXAMD_JN_BLOCK, SGXAMD_JN_L, SGXAMD_JN_C16 != 0>),
+                               dim3(std::max<uint32_t>(tasks_max, 1)), dim3(SGXAMD_JN_BLOCK), 0, s, R, S, r_start,
+                               r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts, cyc, grid,
+                               tickets, narrow_r, narrow_s);
+            const hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return e;
+        }
         hipLaunchKernelGGL((k_join_x<kBigRcap, 1024, 8, 1>), dim3(std::min<uint32_t>(grid, cu_count())), dim3(1024), 0,
                            s, R64, S64, r_start, r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts,
-                           cyc, rres, rtick, grid, tickets, narrow_r, narrow_s);
+                           cyc, rres, rtick, grid, tickets, narrow_r, narrow_s, nar ? 1u : 0u);
         return hipGetLastError();
     }
 #define KEYS_CASE(RC)                                                                                                   case RC:                                                                                                                hipLaunchKernelGGL((k_join<RC, kJoinCount, kBlock, 1>), dim3(grid), dim3(kBlock), 0, s, R64, S64, r_start,                            r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts, nullptr, nullptr,                             cyc, rres, rtick);                                                                               break;
@@ -3319,10 +3612,10 @@ hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, 
                        const uint32_t *n_over, uint32_t hash_shift, uint32_t rcap, uint64_t s_chunk, uint32_t grid,
                        int mode, int algo, uint64_t *counts, const uint64_t *task_off, output_triple_t *out,
                        uint64_t *cyc, hipStream_t s, const JoinReduce *reduce, int key_stride, uint32_t *tickets,
-                       const uint32_t *narrow_r, const uint32_t *narrow_s) {
+                       const uint32_t *narrow_r, const uint32_t *narrow_s, uint32_t tasks_max) {
     if (key_stride == 1)
         return launch_join_keys(R, S, r_start, r_count, s_start, s_count, P, over, n_over, hash_shift, rcap, s_chunk,
-                                grid, mode, algo, counts, cyc, s, reduce, tickets, narrow_r, narrow_s);
+                                grid, mode, algo, counts, cyc, s, reduce, tickets, narrow_r, narrow_s, tasks_max);
     if (narrow_r || narrow_s) return hipErrorInvalidValue;
     const uint64_t *R64 = reinterpret_cast<const uint64_t *>(R);
     const uint64_t *S64 = reinterpret_cast<const uint64_t *>(S);
@@ -3356,7 +3649,7 @@ hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, 
         if (mode != kJoinCount) return hipErrorInvalidValue;
         hipLaunchKernelGGL((k_join_x<kBigRcap, 1024, 8, 2>), dim3(std::min<uint32_t>(grid, cu_count())), dim3(1024), 0,
                            s, R64, S64, r_start, r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts,
-                           cyc, rres, rtick, grid, tickets, nullptr, nullptr);
+                           cyc, rres, rtick, grid, tickets, nullptr, nullptr, 0u);
     } else if (mode == kJoinCount && grid <= 512 && rcap <= 4096) {
         // few tasks (small joins: one workgroup per CU at most): 1,024 threads per table
         // instead of 256, so that a CU holds 16 waves to hide the load latencies
@@ -3393,7 +3686,12 @@ __global__ __launch_bounds__(kBlock) void k_make_tasks(const uint64_t *__restric
                                                        const uint64_t *__restrict__ s_count, uint64_t P,
                                                        uint64_t *__restrict__ over, uint32_t over_cap,
                                                        uint32_t *__restrict__ n_over, uint64_t *__restrict__ max_rs,
-                                                       uint64_t s_chunk) {
+                                                       uint64_t s_chunk, uint64_t *__restrict__ zero,
+                                                       uint64_t *__restrict__ zero2, uint32_t nzero) {
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < nzero; i += gridDim.x * kBlock) {
+        zero[i] = 0;
+        zero2[2 * i] = zero2[2 * i + 1] = 0;
+    }
     uint64_t mr = 0, ms = 0;  // largest partitions (diagnostics), folded into this pass over the counts
     for (uint64_t p = blockIdx.x * (uint64_t)kBlock + threadIdx.x; p < P; p += (uint64_t)gridDim.x * kBlock) {
         const uint64_t nS = s_count[p], nR = r_count[p];
@@ -3426,14 +3724,15 @@ __global__ __launch_bounds__(kBlock) void k_make_tasks(const uint64_t *__restric
 }
 
 hipError_t launch_make_tasks(const uint64_t *r_count, const uint64_t *s_count, uint64_t P, uint64_t *over,
-                             uint32_t over_cap, uint64_t *meta, uint64_t s_chunk, hipStream_t s) {
+                             uint32_t over_cap, uint64_t *meta, uint64_t s_chunk, hipStream_t s, uint64_t *zero,
+                             uint64_t *zero2, uint32_t nzero) {
     hipError_t e = hipMemsetAsync(meta, 0, 6 * sizeof(uint64_t), s);
     if (e != hipSuccess) return e;
     uint32_t *n_over = reinterpret_cast<uint32_t *>(meta + 2);
     uint64_t blocks = (P + kBlock - 1) / kBlock;
     if (blocks > 1024) blocks = 1024;
     hipLaunchKernelGGL(k_make_tasks, dim3((uint32_t)blocks), dim3(kBlock), 0, s, r_count, s_count, P, over, over_cap,
-                       n_over, meta, s_chunk);
+                       n_over, meta, s_chunk, zero, zero2, zero && zero2 ? nzero : 0u);
     return hipGetLastError();
 }
 

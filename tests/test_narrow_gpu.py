@@ -16,6 +16,7 @@ pytestmark = pytest.mark.gpu
 DT = np.dtype([("key", "<u4"), ("payload", "<u4")])
 BITS = 9
 BOUND = 1 << (BITS + 16)  # first key whose residual needs 17 bits
+CAP = (1 << 14) + 64  # k_join_n's counters (rho_kernels.hip kNarrowCap)
 
 
 def rel(keys):
@@ -44,6 +45,24 @@ def case_relations(case, rng):
         S = np.concatenate([keys_below(rng, nS - 3, BOUND), np.full(3, BOUND - 1, np.uint32)])
         R[:5] = BOUND - 1
         return R, S, 3
+    if case == "cap":  # residuals up to k_join_n's table end (kNarrowCap - 1: the fast body)
+        R = keys_below(rng, nR, CAP << BITS)
+        S = keys_below(rng, nS, CAP << BITS)
+        R[:3] = (CAP << BITS) - 1
+        S[:2] = (CAP << BITS) - 1
+        return R, S, 3
+    if case == "cap_over":  # one residual past the table on both sides: two windows
+        R = keys_below(rng, nR, CAP << BITS)
+        S = keys_below(rng, nS, CAP << BITS)
+        R[7] = CAP << BITS
+        S[11:14] = CAP << BITS
+        return R, S, 3
+    if case == "hot_r":  # an R partition of four 16,384-key chunks (40,000 copies of one key, hot in S too)
+        R = keys_below(rng, nR, BOUND // 4)
+        S = keys_below(rng, nS, BOUND // 4)
+        R[:40_000] = 77 << BITS | 5
+        S[:3000] = 77 << BITS | 5
+        return R, S, 3
     if case == "wide_s":
         # R narrow, S holds keys of 17+ bit residuals: among them, for R keys of sparse
         # partitions (few R keys: a short table, whose 16-bit tags stop below the top
@@ -69,12 +88,12 @@ def case_relations(case, rng):
     return R, S, 0
 
 
-CASES = ["narrow", "uneven", "boundary", "wide_s", "wide_r", "wide"]
+CASES = ["narrow", "uneven", "boundary", "cap", "cap_over", "hot_r", "wide_s", "wide_r", "wide"]
 
 
 @pytest.mark.parametrize("case", CASES)
 def test_narrow_partitions_match_oracle(sgx, orc, gpu, case):
-    rng = np.random.default_rng(40 + CASES.index(case))
+    rng = np.random.default_rng(40 + CASES.index(case))  # (seeds of the first three kept from round 4)
     Rk, Sk, narrow = case_relations(case, rng)
     R, S = rel(Rk), rel(Sk)
     exp = orc.count_join_sort(R, S)
