@@ -165,8 +165,12 @@ LAYOUTS = {
 
 
 def visible_gpus() -> int:
-    """GPUs this process could use, counted without initialising HIP (on this image
-    torch.cuda.device_count() does not initialise the GPU)."""
+    """GPUs this process could use (torch.cuda.device_count(), which on ROCm goes through
+    hipGetDeviceCount and so initialises the HIP runtime in this parent process).  That
+    is harmless here: the rank processes are started with Popen (fresh processes, no
+    fork of an initialised runtime), and this process never launches GPU work when it
+    spawns ranks.  The sysfs KFD topology is not used instead: it lists every GPU of the
+    host, including ones this container cannot open."""
     import torch
 
     return torch.cuda.device_count()
@@ -523,6 +527,20 @@ def main():
     probe_gbs = algorithmic_bytes("join_build_probe", nR, nS, *plan) / (avg["join_build_probe"] * 1e-3) / 1e9
     phase = {k: round(v, 4) for k, v in sorted(avg.items())}
     ls = results[-1].local_stats
+    # the north-star probe phase and the whole step as scalars of `roofline` (the block
+    # the driver's record keeps): the build/probe launch priced at the bytes it reads,
+    # and every kernel of one join at its algorithmic bytes over the measured step time
+    step_bytes = sum(algorithmic_bytes(k, nR, nS, *plan) for k in avg)
+    roofline.update({
+        "probe_kernel": ("k_join_n" if (ls.get("narrow") or 0) and os.environ.get("SGXAMD_JOIN_N", "1") != "0"
+                         else "k_join_x" if args.algorithm == "RHO" else "k_join_hist_big"),
+        "probe_bytes": algorithmic_bytes("join_build_probe", nR, nS, *plan),
+        "probe_avg_ms": round(avg["join_build_probe"], 4),
+        "probe_frac": round(probe_gbs / HBM_PEAK_GBS, 4),
+        "probe_frac_tuple_layout": None,
+        "step_algorithmic_bytes": step_bytes,
+        "step_frac": round(step_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+    })
     rho_info = {
         "matches_ok": ok, "matches": results[-1].matches, "generator": gen_desc,
         "M_rec_per_s_reference_formula": round((gR + gS) * args.steps / elapsed / 1e6, 1),
@@ -540,7 +558,7 @@ def main():
         "partition_layout": LAYOUTS.get(ls.get("layout"), "unknown"),
         "narrow_partitions": {"R": bool((ls.get("narrow") or 0) & 1), "S": bool((ls.get("narrow") or 0) & 2),
                               "what": "final partitions hold 2-byte key residuals (key >> radix bits): every "
-                                      "key's residual fits 16 bits (pass 1's key OR)"},
+                                      "key's residual fits 16 bits (pass 1's largest key)"},
         "step_ms_breakdown": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in results[-1].ms.items()},
     }
     if args.workload == "c5":
@@ -560,6 +578,7 @@ def main():
         ls_t = res_t[-1].local_stats
         plan_t = plan_of(ls_t)
         pb_t = algorithmic_bytes("join_build_probe", nR, nS, *plan_t) / (avg_t["join_build_probe"] * 1e-3) / 1e9
+        roofline["probe_frac_tuple_layout"] = round(pb_t / HBM_PEAK_GBS, 4)
         rho_info["tuple_layout"] = {
             "partition_layout": LAYOUTS.get(ls_t.get("layout"), "unknown"), "timed": "untimed for value; own K steps",
             "ms_per_step": round(el_t / args.steps * 1e3, 4),

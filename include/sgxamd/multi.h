@@ -69,7 +69,8 @@ typedef struct mi355_multi_stats {
                                   counting join whose local join reads keys) */
     double ms_tail;            /* device time from S's last piece landing to the local join's
                                   end (max over the ranks seen; the part of the join that no
-                                  exchange hides) */
+                                  exchange hides); -1 when no rank measured it (a world of
+                                  one, a failed or untimed tail) */
 } mi355_multi_stats;
 
 /* Single process, `ngpus` ranks driven by one host thread each.  R and S are host or

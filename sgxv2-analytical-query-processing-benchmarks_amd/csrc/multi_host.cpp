@@ -578,8 +578,10 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
     lo.stream = nullptr;
     lo.out = nullptr;
     lo.out_capacity = 0;
-    if (G == 1) {  // nothing to exchange
+    if (G == 1) {  // nothing to exchange: no collective to leave, so a failure is local
+        o.together = true;
         if (pre_fail != MI355_OK) return pre_fail;
+        if (injected(rank, kFailLocal)) return MI355_ERR_OOM;
         if (nR && nS) {
             MH_RC(rho::join_pipelined_begin(ctx, s, R, nR, nS, &lo));
             MH_RC(rho::join_pipelined_finish(ctx, S, nS, &o.st));
@@ -809,6 +811,7 @@ void fill_stats(mi355_multi_stats *st, const std::vector<RankOut> &outs, int G, 
     st->pieces = std::max(1, std::min(64, g_pieces.load()));
     st->rank = rank;
     st->recv_r_min = st->recv_s_min = UINT64_MAX;
+    st->ms_tail = -1;  // not measured (a failed or untimed tail), unless a rank measured it
     for (const RankOut &o : outs) {
         st->matches = o.global;
         st->recv_r_max = std::max(st->recv_r_max, o.recv_r);
@@ -992,9 +995,12 @@ void destroy_own_context(std::unique_ptr<Context> &c) {
         if (it != g_streams.end()) {
             if (it->second.comm) (void)hipStreamSynchronize(it->second.comm), (void)hipStreamDestroy(it->second.comm);
             for (hipEvent_t e : it->second.ev) (void)hipEventDestroy(e);
+            for (hipEvent_t e : {it->second.t_land, it->second.t_done})
+                if (e) (void)hipEventDestroy(e);
             g_streams.erase(it);
         }
     }
+    rho::forget_context(c.get());
     (void)hipStreamDestroy(c->stream);
     if (c->host_result) (void)hipHostFree(c->host_result);
     c.reset();
@@ -1108,9 +1114,22 @@ int mi355_multi_comm_init(const void *id128, int nranks, int rank, void **comm) 
     MH_HIP(hipGetDevice(&h->device));
     ncclUniqueId id;
     std::memcpy(&id, id128, sizeof(id));
-    MH_NCCL(lib.CommInitRank(&h->comm, nranks, id, rank));
+    // counted before the communicator exists (under g_all_mu, the lock
+    // mi355_multi_set_rccl_library checks it under), so the library cannot be swapped
+    // while this init runs; rolled back if the init fails
+    {
+        std::lock_guard<std::mutex> lk(multi::g_all_mu);
+        ++multi::g_live_handles;
+    }
+    const ncclResult_t ir = lib.CommInitRank(&h->comm, nranks, id, rank);
+    if (ir != ncclSuccess) {
+        --multi::g_live_handles;
+        set_last_error(std::string("ncclCommInitRank: ") + lib.ErrorString(ir));
+        return MI355_ERR_COMM;
+    }
     const ncclResult_t sr = lib.CommSplit(h->comm, 0, rank, &h->ccomm, nullptr);
     if (sr != ncclSuccess) {
+        --multi::g_live_handles;
         set_last_error(std::string("ncclCommSplit (count communicator): ") + lib.ErrorString(sr));
         h->abort_comms();
         return MI355_ERR_COMM;
@@ -1131,7 +1150,6 @@ int mi355_multi_comm_init(const void *id128, int nranks, int rank, void **comm) 
     }
     // without a context the rank still takes part in the joins' collectives, flagged as
     // failed (mi355_rho_join_sharded), so the communicator is kept
-    ++multi::g_live_handles;
     *comm = h.release();
     return MI355_OK;
 }

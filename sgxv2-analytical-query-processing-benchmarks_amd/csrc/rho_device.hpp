@@ -31,6 +31,9 @@ int shard_partition_device(Context *ctx, hipStream_t s, const row_t *in, uint64_
 int shard_count_pieces(Context *ctx, hipStream_t s, const row_t *const *in, const uint64_t *n, int npieces,
                        uint32_t key_shift, uint32_t dest_bits, uint32_t out_elem, uint64_t *counts);
 int shard_scatter_piece(Context *ctx, hipStream_t s, int j, void *out);
+// Drops the per-context state of the shard and pipelined-join calls (the pinned count
+// block of the shard pieces): called when a context of its own is destroyed.
+void forget_context(const Context *ctx);
 // in_elem 8: dR / dS are row_t relations; 4: packed keys (needs keys_exchange_plan's plan).
 // s_piece_n[0..s_pieces): S arrives in contiguous pieces of these sizes (they add up to
 // nS); a pooled S pass 1 then runs per piece, each launch after its event in

@@ -318,7 +318,7 @@ int partition_relation_pooled(Context *ctx, hipStream_t s, Timer &tm, const std:
     RHO_HIP(launch_scan_regions(hist2, segbase2, start1, F1, pol.b2, ps, pc, s));
     tm.mark((t + "pass2_scatter").c_str());
     RHO_HIP(launch_scatter_blk(t1, list, t2, rp.keys ? 4u : 8u, m2, rp.grid2, key_shift + pol.b1, pol.b2, hist2, s,
-                               narrow));
+                               narrow, ps, pc));
     *final_rel = t2;
     *pstart = ps;
     *pcnt = pc;
@@ -1123,6 +1123,19 @@ ShardPieces &shard_of(const Context *ctx) {
     return g_shard[ctx];
 }
 }  // namespace
+
+void forget_context(const Context *ctx) {
+    {
+        std::lock_guard<std::mutex> lk(g_shard_mu);
+        auto it = g_shard.find(ctx);
+        if (it != g_shard.end()) {
+            if (it->second.host) (void)hipHostFree(it->second.host);
+            g_shard.erase(it);
+        }
+    }
+    std::lock_guard<std::mutex> lk(g_pending_mu);
+    g_pending.erase(ctx);
+}
 
 int shard_count_pieces(Context *ctx, hipStream_t s, const row_t *const *in, const uint64_t *n, int npieces,
                        uint32_t key_shift, uint32_t dest_bits, uint32_t out_elem, uint64_t *counts) {

@@ -195,9 +195,14 @@ hipError_t launch_hist_side_blk(const uint8_t *side, const uint64_t *list, const
 // (shift + bits)) fits 16 bits, the partitions are written as those u16 residuals —
 // the build/probe (launch_join with the same word) compares residuals, which within
 // one partition are equal exactly when the keys are.
+// part_start / part_count (nullable; fixed-size segments, launch_scan_regions' partition
+// table [region][digit]): with them a narrow relation's pass 2 is the segment placement
+// k_place_seg, each segment's digit counts taken from consecutive cursors.
 hipError_t launch_scatter_blk(const void *in, const uint64_t *list, void *out, uint32_t elem_size, const SegMap &m,
                               uint32_t grid, uint32_t shift, uint32_t bits, const uint64_t *cursors, hipStream_t s,
-                              const uint32_t *narrow = nullptr);
+                              const uint32_t *narrow = nullptr, const uint64_t *part_start = nullptr,
+                              const uint64_t *part_count = nullptr);
+bool place_enabled();
 // launch_scatter's one-pass cursor scatter writing only the key word of every tuple
 // (the multi-GPU shard partition of a counting join, whose exchange moves keys).
 hipError_t launch_scatter_keys(const row_t *in, uint32_t *out, const SegMap &m, uint32_t grid, uint32_t shift,

@@ -31,6 +31,15 @@ __device__ __forceinline__ void dbg_stamp(uint32_t kernel, uint32_t which) {
 }
 hipError_t set_debug_stamps(uint64_t *p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &p, sizeof(p)); }
 
+// A uniform value kept in SGPRs.  readfirstlane returns int: each half goes through
+// uint32_t, or a low word >= 2^31 would sign-extend over the high word (element
+// indices past 2^31: test_max_size_pk_fk).
+__device__ __forceinline__ uint64_t uni_u64(uint64_t v) {
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+    return ((uint64_t)hi << 32) | lo;
+}
+
 // Segment g -> [b, e) of the input and its region r.  Block-uniform; contains a
 // __syncthreads() (every thread of the block must call it).
 __device__ __forceinline__ bool seg_lookup(const SegMap &m, uint32_t g, uint32_t *lds_base, uint32_t &r,
@@ -1557,16 +1566,19 @@ struct SortBlkLds {
 // the next-tile prefetch (64 VGPRs), or with the ranks taken by a second LDS atomic in
 // phase C, measured equal (0.52-0.55); 512-key segments (SGXAMD_PASS2_ENTS=512) 0.54-0.57.
 #ifndef SGXAMD_SORT_NT
-#define SGXAMD_SORT_NT 1024
+#define SGXAMD_SORT_NT 512
 #endif
 #ifndef SGXAMD_SORT_ITEMS
-#define SGXAMD_SORT_ITEMS 16
+#define SGXAMD_SORT_ITEMS 32
 #endif
 #ifndef SGXAMD_SORT_WGS
-#define SGXAMD_SORT_WGS 1
+#define SGXAMD_SORT_WGS 2
 #endif
 #ifndef SGXAMD_SORT_UNROLL
 #define SGXAMD_SORT_UNROLL 16
+#endif
+#ifndef SGXAMD_SORT_CRANK
+#define SGXAMD_SORT_CRANK 1
 #endif
 // NAR: narrow partitions — every key's residual above the radix bits fits 16 bits (the
 // relation's largest key from pass 1), so the output holds those u16 residuals.  The kernel
@@ -1626,13 +1638,21 @@ __device__ __forceinline__ void sort_blk_body(SortBlkLds<BITS, NT, ITEMS> &L, co
             return;
         }
 #endif
-        // A. rank of every key inside its digit (tile histogram at once)
+        // A. rank of every key inside its digit (tile histogram at once); SGXAMD_SORT_CRANK:
+        // the histogram alone (no returned ranks: no rank registers across the scan), the
+        // ranks taken in C from the digit starts
+#if SGXAMD_SORT_CRANK
+#pragma unroll
+        for (int u = 0; u < (int)ITEMS; ++u)
+            if ((vm >> u) & 1u) atomicAdd(&L.cnt[(k[u] >> shift) & mask], 1u);
+#else
         uint32_t rd[ITEMS];
 #pragma unroll
         for (int u = 0; u < (int)ITEMS; ++u) {
             const uint32_t d = (k[u] >> shift) & mask;
             rd[u] = ((vm >> u) & 1u) ? (atomicAdd(&L.cnt[d], 1u) | (d << 16)) : 0u;
         }
+#endif
         __syncthreads();
         // B. digit starts (block scan over F counters), destinations, next cursors
         uint32_t c = 0, incl = 0;
@@ -1655,9 +1675,15 @@ __device__ __forceinline__ void sort_blk_body(SortBlkLds<BITS, NT, ITEMS> &L, co
         }
         __syncthreads();
         // C. the tile, digit-sorted
+#if SGXAMD_SORT_CRANK
+#pragma unroll
+        for (int u = 0; u < (int)ITEMS; ++u)
+            if ((vm >> u) & 1u) L.sorted[atomicAdd(&L.start[(k[u] >> shift) & mask], 1u)] = k[u];
+#else
 #pragma unroll
         for (int u = 0; u < (int)ITEMS; ++u)
             if ((vm >> u) & 1u) L.sorted[L.start[rd[u] >> 16] + (rd[u] & 0xFFFFu)] = k[u];
+#endif
         __syncthreads();
         // D. sorted position q -> off[d] + q: consecutive lanes, consecutive addresses
         const uint32_t tn = L.wsum[NW];
@@ -1708,12 +1734,156 @@ template <int BITS, int NT, int ITEMS>
 __global__ __launch_bounds__(NT, NT * SGXAMD_SORT_WGS / 256) void k_sort_blk(const uint32_t *__restrict__ in, const uint64_t *__restrict__ list,
                                                     uint32_t *__restrict__ out, SegMap m, uint32_t shift,
                                                     const uint64_t *__restrict__ cursors,
-                                                    const uint32_t *__restrict__ narrow) {
+                                                    const uint32_t *__restrict__ narrow, uint32_t skip_narrow) {
     __shared__ SortBlkLds<BITS, NT, ITEMS> L;
-    if (narrow != nullptr && ((*narrow >> (shift + BITS)) >> 16) == 0)
+    if (narrow != nullptr && ((*narrow >> (shift + BITS)) >> 16) == 0) {
+        if (skip_narrow) return;  // k_place_seg, launched beside it, places them
         sort_blk_body<BITS, NT, ITEMS, true>(L, in, list, out, m, shift, cursors);
-    else
-        sort_blk_body<BITS, NT, ITEMS, false>(L, in, list, out, m, shift, cursors);
+        return;
+    }
+    sort_blk_body<BITS, NT, ITEMS, false>(L, in, list, out, m, shift, cursors);
+}
+
+#ifndef SGXAMD_PLACE_WGS  // workgroups per CU of k_place_seg (its LDS holds a segment)
+#define SGXAMD_PLACE_WGS (SGXAMD_PASS2_ENTS <= 128 ? 2 : 1)
+#endif
+#ifndef SGXAMD_PLACE_NT
+#define SGXAMD_PLACE_NT (1024 / SGXAMD_PLACE_WGS)
+#endif
+#ifndef SGXAMD_PLACE_ITEMS
+#define SGXAMD_PLACE_ITEMS 16
+#endif
+// Pass 2 of narrow key partitions as one placement per segment (k_place_seg, round 5).
+// radix_cluster (radix_join.cpp:715-761) scatters a region by its pass-2 digit at
+// cursors from a histogram; here the pass-2 histogram (k_hist_side_blk, over the digit
+// side stream) already holds every segment's digit counts -- k_scan_regions turned them
+// into the segment's cursors in place, and the counts come back as the difference of
+// two consecutive segments' cursors (the region's last segment: its partition ends) --
+// so the segment's digit-sorted layout is known before its first key is read.  Each key
+// is placed as it arrives: one LDS add (its slot in its digit's run) and one 2-byte LDS
+// store of its residual; after the segment's last key, the runs leave for their
+// partitions with consecutive lanes on consecutive addresses.  Against k_sort_blk's
+// per-16,384-key tile sort (a histogram pass, a scan, a placement and a sorted read per
+// tile, four barriers): no per-tile histogram or scan, two barriers per segment, three
+// LDS accesses per key instead of five, and digit runs of a whole segment (65,536 keys:
+// 512 on average, 1 KiB of output) instead of a tile's (128).
+// The segment's residuals are staged in LDS (kPass2Ents * 256 u16: 128 KiB at 256
+// blocks, one workgroup per CU; 64 KiB at 128 blocks, two).  Only narrow relations
+// (16-bit residuals); k_sort_blk, launched beside it, takes the others.
+template <int BITS, int NT>
+struct PlaceLds {
+    static constexpr uint32_t F = 1u << BITS, CAP = kPass2Ents * kBlk;
+    union {
+        uint32_t sbase[kMaxF + 1];  // segment table (seg_lookup, before the first key)
+        uint16_t res[CAP];          // the segment's residuals, digit-sorted
+    };
+    uint64_t ents[kPass2Ents];  // the segment's block list: physical block | fill << 32
+    uint64_t dst[F];            // output position of digit d's run
+    uint32_t pos[F];            // next free slot of d's run in res
+    uint32_t st[F + 1];         // run start of d in res; st[F] = the segment's keys
+    uint32_t wsum[NT / kWave];
+    uint32_t last;              // the segment is its region's last
+};
+
+template <int BITS, int NT, int ITEMS>
+__global__ __launch_bounds__(NT, NT *SGXAMD_PLACE_WGS / 256) void k_place_seg(
+    const uint32_t *__restrict__ in, const uint64_t *__restrict__ list, uint16_t *__restrict__ out, SegMap m,
+    uint32_t shift, const uint64_t *__restrict__ cursors, const uint64_t *__restrict__ part_start,
+    const uint64_t *__restrict__ part_count, const uint32_t *__restrict__ narrow) {
+    using LdsT = PlaceLds<BITS, NT>;
+    constexpr uint32_t F = LdsT::F, mask = F - 1, NW = NT / kWave, WPB = kBlk / kWave, TILE = NT * ITEMS;
+    constexpr uint32_t BPT = TILE / kBlk;
+    static_assert(TILE % kBlk == 0 && NT % kBlk == 0 && F <= NT && LdsT::CAP % TILE == 0, "placement geometry");
+    __shared__ LdsT L;
+    if (narrow == nullptr || ((*narrow >> (shift + BITS)) >> 16) != 0) return;  // wide: k_sort_blk
+    const uint32_t tid = threadIdx.x, lane = __lane_id(), wave = tid / kWave, g = blockIdx.x;
+    const uint32_t rshift = shift + BITS;
+    uint32_t r;
+    uint64_t b, e;
+    if (!seg_lookup(m, g, L.sbase, r, b, e)) return;
+    const uint32_t nent = (uint32_t)(e - b);  // <= kPass2Ents (fixed-size segments)
+    if (tid == 0) L.last = g + 1 == L.sbase[r + 1] ? 1u : 0u;
+    for (uint32_t i = tid; i < nent; i += NT) L.ents[i] = list[b + i];
+    __syncthreads();  // (last and ents; sbase is dead after the next barrier)
+    // the segment's digit counts: the next segment's cursors (or the partition ends) less
+    // its own; a block scan gives the runs' starts
+    uint32_t c = 0, incl = 0;
+    if (tid < F) {
+        const uint64_t cur = cursors[(uint64_t)g * F + tid];
+        const uint64_t nxt = L.last ? part_start[(uint64_t)r * F + tid] + part_count[(uint64_t)r * F + tid]
+                                    : cursors[(uint64_t)(g + 1) * F + tid];
+        c = (uint32_t)(nxt - cur);
+        L.dst[tid] = cur;
+        incl = wave_incl_scan_u32(c);
+        if (lane == kWave - 1 || tid == F - 1) L.wsum[wave] = incl;
+    }
+    __syncthreads();
+    if (tid < F) {
+        uint32_t pre = 0;
+        for (uint32_t w = 0; w < wave; ++w) pre += L.wsum[w];
+        L.st[tid] = L.pos[tid] = pre + incl - c;
+        if (tid == F - 1) L.st[F] = pre + incl;
+    }
+    const uint32_t ntiles = (nent + BPT - 1) / BPT;
+    const uint32_t o = tid & (kBlk - 1);
+    const uint32_t h = __builtin_amdgcn_readfirstlane(wave / WPB);
+    // tile ti's keys: item u = element o of block u * (NT / kBlk) + h of the tile (one
+    // block per wave and item, through a buffer resource over its fill: lanes past it
+    // read 0 and are masked out); returns the valid mask (bit u: item u)
+    const auto load = [&](uint32_t ti, uint32_t(&k)[ITEMS]) -> uint32_t {
+        uint32_t vm = 0;
+#pragma unroll
+        for (int u = 0; u < (int)ITEMS; ++u) {
+            const uint32_t idx = ti * BPT + (uint32_t)u * (NT / kBlk) + h;
+            const uint64_t en = idx < nent ? L.ents[idx] : 0ull;  // one address per wave: a broadcast
+            const uint32_t phys = __builtin_amdgcn_readfirstlane((uint32_t)en);
+            const uint32_t fill = __builtin_amdgcn_readfirstlane((uint32_t)(en >> 32));
+            const __amdgpu_buffer_rsrc_t rs = make_rsrc(in + (uint64_t)phys * kBlk, fill * 4u);
+            k[u] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)(o * 4u), 0, 2);
+            vm |= (o < fill ? 1u : 0u) << u;
+        }
+        return vm;
+    };
+    const auto place = [&](const uint32_t(&k)[ITEMS], uint32_t vm) {
+#pragma unroll
+        for (int u = 0; u < (int)ITEMS; ++u)
+            if ((vm >> u) & 1u) L.res[atomicAdd(&L.pos[(k[u] >> shift) & mask], 1u)] = (uint16_t)(k[u] >> rshift);
+    };
+    uint32_t ka[ITEMS], kb[ITEMS];
+    uint32_t ma = load(0, ka);
+    __syncthreads();  // the runs' starts (pos) are set
+    for (uint32_t ti = 0;; ti += 2) {
+        const uint32_t mb = load(ti + 1, kb);  // past the last tile: no blocks, all masked
+#pragma unroll
+        for (int u = 0; u < (int)ITEMS; ++u) asm volatile("" ::"v"(ka[u]));
+        place(ka, ma);
+        if (ti + 1 >= ntiles) break;
+        ma = load(ti + 2, ka);
+#pragma unroll
+        for (int u = 0; u < (int)ITEMS; ++u) asm volatile("" ::"v"(kb[u]));
+        place(kb, mb);
+        if (ti + 2 >= ntiles) break;
+    }
+    __syncthreads();  // the segment is placed
+    // the runs out: wave w takes positions [w C, (w + 1) C) of the digit-sorted segment
+    // and copies the part of every digit run inside them, 64 consecutive keys per step
+    // (run bounds and destinations wave-uniform: one LDS read per key)
+    const uint32_t total = L.st[F];
+    const uint32_t C = ((total + NW - 1) / NW + kWave - 1) & ~(kWave - 1);
+    const uint32_t q0 = wave * C, q1 = min(total, q0 + C);
+    if (q0 >= q1) return;
+    uint32_t lo = 0, hi = F;  // the run holding q0: the last d with st[d] <= q0
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (L.st[mid] <= q0) lo = mid; else hi = mid;
+    }
+    for (uint32_t d = __builtin_amdgcn_readfirstlane(lo); d < F; ++d) {
+        const uint32_t rs = __builtin_amdgcn_readfirstlane(L.st[d]), re = __builtin_amdgcn_readfirstlane(L.st[d + 1]);
+        if (rs >= q1) break;
+        const uint32_t a = max(rs, q0), z = min(re, q1);
+        const uint64_t o = uni_u64(L.dst[d]) - rs;
+        for (uint32_t q = a + lane; q < z; q += kWave) out[o + q] = L.res[q];
+    }
 }
 
 // Elements per thread per tile: 8 tuples (32 KiB tiles); keys: 12 in the pooled pass 1
@@ -1804,18 +1974,36 @@ bool sort2_enabled() {
     }();
     return on;
 }
+// SGXAMD_PLACE (development A/B switch, read once): 1 (default) = narrow relations' pass
+// 2 as the segment placement k_place_seg; 0 = k_sort_blk's tile sort.
+bool place_enabled() {
+    static const bool on = [] {
+        const char *e = std::getenv("SGXAMD_PLACE");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return on;
+}
 template <typename T>
 hipError_t launch_scatter_blk_t(const void *in, const uint64_t *list, void *out, const SegMap &m, uint32_t grid,
                                 uint32_t shift, uint32_t bits, const uint64_t *cursors, hipStream_t s,
-                                const uint32_t *narrow) {
+                                const uint32_t *narrow, const uint64_t *part_start, const uint64_t *part_count) {
     if constexpr (sizeof(T) == 4) {
         if (sort2_enabled()) {
             const uint32_t *ik = static_cast<const uint32_t *>(in);
             uint32_t *ok = static_cast<uint32_t *>(out);
+            // narrow relations: k_place_seg (fixed-size segments with their partition
+            // ends); k_sort_blk then returns at once for them (the width is known on the
+            // device only)
+            const bool place = narrow && part_start && part_count && m.seg_lb == nullptr && place_enabled();
+            const uint32_t skip = place ? 1u : 0u;
 #define SORT_CASE(B)                                                                                              \
     case B:                                                                                                       \
+        if (place)                                                                                                \
+            hipLaunchKernelGGL((k_place_seg<B, SGXAMD_PLACE_NT, SGXAMD_PLACE_ITEMS>), dim3(grid),                   \
+                               dim3(SGXAMD_PLACE_NT), 0, s, ik, list, reinterpret_cast<uint16_t *>(out), m, shift, \
+                               cursors, part_start, part_count, narrow);                                          \
         hipLaunchKernelGGL((k_sort_blk<B, SGXAMD_SORT_NT, SGXAMD_SORT_ITEMS>), dim3(grid), dim3(SGXAMD_SORT_NT), 0, s, \
-                           ik, list, ok, m, shift, cursors, narrow);                                              \
+                           ik, list, ok, m, shift, cursors, narrow, skip);                                        \
         break;
             switch (bits) {
                 SORT_CASE(1)
@@ -1886,12 +2074,16 @@ hipError_t launch_scatter_keys(const row_t *in, uint32_t *out, const SegMap &m, 
 
 hipError_t launch_scatter_blk(const void *in, const uint64_t *list, void *out, uint32_t elem_size, const SegMap &m,
                               uint32_t grid, uint32_t shift, uint32_t bits, const uint64_t *cursors, hipStream_t s,
-                              const uint32_t *narrow) {
+                              const uint32_t *narrow, const uint64_t *part_start, const uint64_t *part_count) {
     if (grid == 0) return hipSuccess;
-    // narrow residuals: key partitions through k_sort_blk only
+    // narrow residuals: key partitions through k_sort_blk / k_place_seg only
     if (narrow && !(elem_size == 4 && sort2_enabled())) return hipErrorInvalidValue;
-    if (elem_size == 8) return launch_scatter_blk_t<uint64_t>(in, list, out, m, grid, shift, bits, cursors, s, nullptr);
-    if (elem_size == 4) return launch_scatter_blk_t<uint32_t>(in, list, out, m, grid, shift, bits, cursors, s, narrow);
+    if (elem_size == 8)
+        return launch_scatter_blk_t<uint64_t>(in, list, out, m, grid, shift, bits, cursors, s, nullptr, nullptr,
+                                              nullptr);
+    if (elem_size == 4)
+        return launch_scatter_blk_t<uint32_t>(in, list, out, m, grid, shift, bits, cursors, s, narrow, part_start,
+                                              part_count);
     return hipErrorInvalidValue;
 }
 
@@ -2469,14 +2661,6 @@ struct XCursor {
     uint32_t j;  // the workgroup's task ordinal (task tickets)
 };
 
-// A uniform value kept in SGPRs.  readfirstlane returns int: each half goes through
-// uint32_t, or a low word >= 2^31 would sign-extend over the high word (element
-// indices past 2^31: test_max_size_pk_fk).
-__device__ __forceinline__ uint64_t uni_u64(uint64_t v) {
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
-    return ((uint64_t)hi << 32) | lo;
-}
 
 // Task order: grid stride, or (SGXAMD_JOIN_TICKETS, tick != null) task tickets: a
 // workgroup's first task is blockIdx.x, each later one the next value of a device
@@ -3081,16 +3265,16 @@ __device__ __forceinline__ uint64_t join_n_task(JoinLdsN<BLOCK, C16> &Ls, const 
 // Geometry: BLOCK threads, L 16-byte loads per thread and strip, C16 u16 counters,
 // WPC workgroups per CU (occupancy hint).
 #ifndef SGXAMD_JN_BLOCK
-#define SGXAMD_JN_BLOCK 512
+#define SGXAMD_JN_BLOCK 256
 #endif
 #ifndef SGXAMD_JN_L
 #define SGXAMD_JN_L 4
 #endif
 #ifndef SGXAMD_JN_C16
-#define SGXAMD_JN_C16 0
+#define SGXAMD_JN_C16 1
 #endif
 #ifndef SGXAMD_JN_WPC
-#define SGXAMD_JN_WPC 2
+#define SGXAMD_JN_WPC 4
 #endif
 
 // grid = an upper bound of the tasks (P + over_cap - 1); workgroup t takes task t

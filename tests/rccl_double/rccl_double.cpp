@@ -13,12 +13,16 @@
 //   - ncclSend/ncclRecv inside ncclGroupStart/End: at GroupEnd a rank publishes its
 //     sends (source, size, an event recorded on its stream), then for every receive
 //     takes the peer's next send on that channel, makes its stream wait for the
-//     sender's event and copies device to device on its own stream; the sender's stream
+//     sender's event and copies device to device on its own stream with a copy kernel
+//     (k_copy: RCCL's own p2p transfers are kernels on the communication stream, a
+//     workgroup per channel, so they compete with the join's kernels for CUs; a
+//     hipMemcpyAsync would use the DMA engines and hide that); the sender's stream
 //     then waits for the receiver's copy (the sender must not overwrite its buffer
 //     before the copy ran: RCCL's stream semantics).  Sizes must match (else
 //     ncclInvalidUsage), as RCCL's would;
 //   - ncclAllGather: every rank copies every rank's block into its receive buffer on its
-//     own stream after the owner's ready event; every stream then waits for every copy;
+//     own stream (k_copy) after the owner's ready event; every stream then waits for every
+//     copy;
 //   - ncclAllReduce: staged through the host (sum / max / min of integer and double
 //     types), synchronous with respect to the caller's stream.
 // Fault injection for the failure protocol tests: rccl_double_fail(rank, n) makes rank's
@@ -39,6 +43,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <map>
@@ -48,6 +53,41 @@
 #include <vector>
 
 namespace {
+
+// The transfer kernel: kCopyWgs workgroups (RCCL_DOUBLE_COPY_WGS; RCCL's p2p runs a
+// workgroup per channel, of the order of 16 per peer set) copying 16-byte words when
+// source, destination and size allow, 4-byte words, or bytes.
+int copy_wgs() {
+    static const int n = [] {
+        const char *e = std::getenv("RCCL_DOUBLE_COPY_WGS");
+        const int v = e ? std::atoi(e) : 16;
+        return v > 0 && v <= 1024 ? v : 16;
+    }();
+    return n;
+}
+
+__global__ __launch_bounds__(512) void k_copy(const char *__restrict__ src, char *__restrict__ dst, size_t bytes) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (size_t)gridDim.x * blockDim.x;
+    const uintptr_t al = reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst) | bytes;
+    if ((al & 15) == 0) {
+        const uint4 *s4 = reinterpret_cast<const uint4 *>(src);
+        uint4 *d4 = reinterpret_cast<uint4 *>(dst);
+        for (size_t i = t; i < bytes / 16; i += stride) d4[i] = s4[i];
+    } else if ((al & 3) == 0) {
+        const uint32_t *s1 = reinterpret_cast<const uint32_t *>(src);
+        uint32_t *d1 = reinterpret_cast<uint32_t *>(dst);
+        for (size_t i = t; i < bytes / 4; i += stride) d1[i] = s1[i];
+    } else {
+        for (size_t i = t; i < bytes; i += stride) dst[i] = src[i];
+    }
+}
+
+hipError_t copy_d2d(void *dst, const void *src, size_t bytes, hipStream_t s) {
+    if (!bytes) return hipSuccess;
+    hipLaunchKernelGGL(k_copy, dim3(copy_wgs()), dim3(512), 0, s, static_cast<const char *>(src),
+                       static_cast<char *>(dst), bytes);
+    return hipGetLastError();
+}
 
 struct SendPost {
     const void *src = nullptr;
@@ -194,7 +234,7 @@ ncclResult_t run_group(std::vector<Op> &ops) {
         bool ok = p->bytes == o.bytes;
         if (!ok) rc = ncclInvalidUsage;
         if (ok && (hipStreamWaitEvent(o.stream, p->ready, 0) != hipSuccess ||
-                   hipMemcpyAsync(o.buf, p->src, o.bytes, hipMemcpyDeviceToDevice, o.stream) != hipSuccess))
+                   copy_d2d(o.buf, p->src, o.bytes, o.stream) != hipSuccess))
             return ncclUnhandledCudaError;
         if (hipEventCreateWithFlags(&done, hipEventDisableTiming) != hipSuccess ||
             hipEventRecord(done, o.stream) != hipSuccess)
@@ -398,8 +438,7 @@ ncclResult_t ncclAllGather(const void *send, void *recv, size_t count, ncclDataT
     if (!w.barrier(lk)) return ncclSystemError;
     for (int q = 0; q < w.n; ++q)
         if (hipStreamWaitEvent(s, w.slots[q].ev, 0) != hipSuccess ||
-            hipMemcpyAsync(static_cast<char *>(recv) + q * bytes, w.slots[q].ptr, bytes, hipMemcpyDeviceToDevice,
-                           s) != hipSuccess)
+            copy_d2d(static_cast<char *>(recv) + q * bytes, w.slots[q].ptr, bytes, s) != hipSuccess)
             return ncclUnhandledCudaError;
     if (hipEventCreateWithFlags(&done, hipEventDisableTiming) != hipSuccess || hipEventRecord(done, s) != hipSuccess)
         return ncclUnhandledCudaError;

@@ -170,6 +170,30 @@ def test_rccl_comm_single_rank(sgx, orc, gpu):
         sgx.multi_comm_destroy(h)
 
 
+def test_rccl_single_rank_local_failure_keeps_handle(sgx, orc, gpu):
+    """A world of one has no collective to leave: a local failure (injected at the local
+    join) returns that error and leaves the communicator usable, so the next sharded
+    join on the same handle is exact (the handle is not marked broken)."""
+    import torch
+
+    h = sgx.multi_comm_init(sgx.multi_unique_id(), 1, 0)
+    try:
+        R, S = sgx.reference_relations(1 << 16, 1 << 16, selectivity=50)
+        dR = torch.from_numpy(R.view(np.int64)).to(gpu)
+        dS = torch.from_numpy(S.view(np.int64)).to(gpu)
+        sgx.multi_inject_failure(0, 3)
+        try:
+            with pytest.raises(sgx.Mi355Error, match="injected failure"):
+                sgx.rho_join_sharded(h, dR, len(R), dS, len(S))
+        finally:
+            sgx.multi_inject_failure(-1, 0)
+        res = sgx.rho_join_sharded(h, dR, len(R), dS, len(S))
+        assert res.matches == orc.rho_join(R, S, 4)[0]
+        assert res.stats["ms_tail"] == -1  # nothing exchanged: no tail measured
+    finally:
+        sgx.multi_comm_destroy(h)
+
+
 @pytest.mark.parametrize("step", [1, 2, 3])
 def test_failure_on_one_rank(sgx, orc, gpu, step):
     """A rank that fails (exchange buffers, a shard pass of S, its local join) flags it in
