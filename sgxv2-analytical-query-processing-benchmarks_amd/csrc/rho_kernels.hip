@@ -1750,8 +1750,8 @@ __global__ __launch_bounds__(NT, NT * SGXAMD_SORT_WGS / 256) void k_sort_blk(con
 #ifndef SGXAMD_PLACE_NT
 #define SGXAMD_PLACE_NT (1024 / SGXAMD_PLACE_WGS)
 #endif
-#ifndef SGXAMD_PLACE_ITEMS
-#define SGXAMD_PLACE_ITEMS 16
+#ifndef SGXAMD_PLACE_U  // 16-byte loads (4 keys) per thread and tile
+#define SGXAMD_PLACE_U 2
 #endif
 // Pass 2 of narrow key partitions as one placement per segment (k_place_seg, round 5).
 // radix_cluster (radix_join.cpp:715-761) scatters a region by its pass-2 digit at
@@ -1772,28 +1772,34 @@ __global__ __launch_bounds__(NT, NT * SGXAMD_SORT_WGS / 256) void k_sort_blk(con
 // (16-bit residuals); k_sort_blk, launched beside it, takes the others.
 template <int BITS, int NT>
 struct PlaceLds {
-    static constexpr uint32_t F = 1u << BITS, CAP = kPass2Ents * kBlk;
-    union {
+    static constexpr uint32_t F = 1u << BITS;
+    // d's run sits at st[d] inside a slot range of round_up8(count + 7) u16 that starts
+    // on a multiple of 8, with st[d] = dst[d] mod 8: the run's 16-byte pieces in LDS are
+    // the 16-byte pieces of its destination (whole-line copies)
+    static constexpr uint32_t CAP = kPass2Ents * kBlk + 14 * F;
+    union alignas(16) {
         uint32_t sbase[kMaxF + 1];  // segment table (seg_lookup, before the first key)
         uint16_t res[CAP];          // the segment's residuals, digit-sorted
     };
     uint64_t ents[kPass2Ents];  // the segment's block list: physical block | fill << 32
     uint64_t dst[F];            // output position of digit d's run
     uint32_t pos[F];            // next free slot of d's run in res
-    uint32_t st[F + 1];         // run start of d in res; st[F] = the segment's keys
+    uint32_t st[F];             // run start of d in res
+    uint32_t pb[F + 1];         // d's slot range starts (non-decreasing); pb[F] = the slots in use
+    uint32_t cnt[F];
     uint32_t wsum[NT / kWave];
     uint32_t last;              // the segment is its region's last
 };
 
-template <int BITS, int NT, int ITEMS>
+template <int BITS, int NT, int U>
 __global__ __launch_bounds__(NT, NT *SGXAMD_PLACE_WGS / 256) void k_place_seg(
     const uint32_t *__restrict__ in, const uint64_t *__restrict__ list, uint16_t *__restrict__ out, SegMap m,
     uint32_t shift, const uint64_t *__restrict__ cursors, const uint64_t *__restrict__ part_start,
     const uint64_t *__restrict__ part_count, const uint32_t *__restrict__ narrow) {
     using LdsT = PlaceLds<BITS, NT>;
-    constexpr uint32_t F = LdsT::F, mask = F - 1, NW = NT / kWave, WPB = kBlk / kWave, TILE = NT * ITEMS;
-    constexpr uint32_t BPT = TILE / kBlk;
-    static_assert(TILE % kBlk == 0 && NT % kBlk == 0 && F <= NT && LdsT::CAP % TILE == 0, "placement geometry");
+    constexpr uint32_t F = LdsT::F, mask = F - 1, NW = NT / kWave;
+    constexpr uint32_t BPT = NW * U;  // blocks per tile: U per wave, one 16-byte load per lane each
+    static_assert(kBlk == 4 * kWave && F <= NT, "placement geometry");
     __shared__ LdsT L;
     if (narrow == nullptr || ((*narrow >> (shift + BITS)) >> 16) != 0) return;  // wide: k_sort_blk
     const uint32_t tid = threadIdx.x, lane = __lane_id(), wave = tid / kWave, g = blockIdx.x;
@@ -1806,83 +1812,98 @@ __global__ __launch_bounds__(NT, NT *SGXAMD_PLACE_WGS / 256) void k_place_seg(
     for (uint32_t i = tid; i < nent; i += NT) L.ents[i] = list[b + i];
     __syncthreads();  // (last and ents; sbase is dead after the next barrier)
     // the segment's digit counts: the next segment's cursors (or the partition ends) less
-    // its own; a block scan gives the runs' starts
-    uint32_t c = 0, incl = 0;
+    // its own; a block scan of the slot ranges gives the runs' starts
+    uint32_t c = 0, slots = 0, incl = 0;
+    uint64_t cur = 0;
     if (tid < F) {
-        const uint64_t cur = cursors[(uint64_t)g * F + tid];
+        cur = cursors[(uint64_t)g * F + tid];
         const uint64_t nxt = L.last ? part_start[(uint64_t)r * F + tid] + part_count[(uint64_t)r * F + tid]
                                     : cursors[(uint64_t)(g + 1) * F + tid];
         c = (uint32_t)(nxt - cur);
+        slots = c ? (c + 7 + 7) & ~7u : 0u;
         L.dst[tid] = cur;
-        incl = wave_incl_scan_u32(c);
+        L.cnt[tid] = c;
+        incl = wave_incl_scan_u32(slots);
         if (lane == kWave - 1 || tid == F - 1) L.wsum[wave] = incl;
     }
     __syncthreads();
     if (tid < F) {
         uint32_t pre = 0;
         for (uint32_t w = 0; w < wave; ++w) pre += L.wsum[w];
-        L.st[tid] = L.pos[tid] = pre + incl - c;
-        if (tid == F - 1) L.st[F] = pre + incl;
+        L.pb[tid] = pre + incl - slots;
+        L.st[tid] = L.pos[tid] = pre + incl - slots + (uint32_t)(cur & 7);
+        if (tid == F - 1) L.pb[F] = pre + incl;
     }
     const uint32_t ntiles = (nent + BPT - 1) / BPT;
-    const uint32_t o = tid & (kBlk - 1);
-    const uint32_t h = __builtin_amdgcn_readfirstlane(wave / WPB);
-    // tile ti's keys: item u = element o of block u * (NT / kBlk) + h of the tile (one
-    // block per wave and item, through a buffer resource over its fill: lanes past it
-    // read 0 and are masked out); returns the valid mask (bit u: item u)
-    const auto load = [&](uint32_t ti, uint32_t(&k)[ITEMS]) -> uint32_t {
+    // tile ti: item u of wave w = block ti * BPT + u * NW + w, lane l its keys 4l..4l+3
+    // (a buffer resource over the block's fill: keys past it read 0 and are masked out)
+    const auto load = [&](uint32_t ti, uint4(&k)[U]) -> uint32_t {
         uint32_t vm = 0;
 #pragma unroll
-        for (int u = 0; u < (int)ITEMS; ++u) {
-            const uint32_t idx = ti * BPT + (uint32_t)u * (NT / kBlk) + h;
+        for (int u = 0; u < U; ++u) {
+            const uint32_t idx = ti * BPT + (uint32_t)u * NW + wave;
             const uint64_t en = idx < nent ? L.ents[idx] : 0ull;  // one address per wave: a broadcast
             const uint32_t phys = __builtin_amdgcn_readfirstlane((uint32_t)en);
             const uint32_t fill = __builtin_amdgcn_readfirstlane((uint32_t)(en >> 32));
-            const __amdgpu_buffer_rsrc_t rs = make_rsrc(in + (uint64_t)phys * kBlk, fill * 4u);
-            k[u] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)(o * 4u), 0, 2);
-            vm |= (o < fill ? 1u : 0u) << u;
+            k[u] = buf_ld_nt_u128(make_rsrc(in + (uint64_t)phys * kBlk, fill * 4u), lane * 16u, 0);
+            const uint32_t f = fill > 4 * lane ? min(fill - 4 * lane, 4u) : 0u;
+            vm |= ((1u << f) - 1u) << (4 * u);
         }
         return vm;
     };
-    const auto place = [&](const uint32_t(&k)[ITEMS], uint32_t vm) {
+    const auto place = [&](const uint4(&k)[U], uint32_t vm) {
 #pragma unroll
-        for (int u = 0; u < (int)ITEMS; ++u)
-            if ((vm >> u) & 1u) L.res[atomicAdd(&L.pos[(k[u] >> shift) & mask], 1u)] = (uint16_t)(k[u] >> rshift);
+        for (int u = 0; u < U; ++u) {
+            const uint32_t w[4] = {k[u].x, k[u].y, k[u].z, k[u].w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if ((vm >> (4 * u + j)) & 1u)
+                    L.res[atomicAdd(&L.pos[(w[j] >> shift) & mask], 1u)] = (uint16_t)(w[j] >> rshift);
+        }
     };
-    uint32_t ka[ITEMS], kb[ITEMS];
+    uint4 ka[U], kb[U];
     uint32_t ma = load(0, ka);
     __syncthreads();  // the runs' starts (pos) are set
     for (uint32_t ti = 0;; ti += 2) {
         const uint32_t mb = load(ti + 1, kb);  // past the last tile: no blocks, all masked
 #pragma unroll
-        for (int u = 0; u < (int)ITEMS; ++u) asm volatile("" ::"v"(ka[u]));
+        for (int u = 0; u < U; ++u) asm volatile("" ::"v"(ka[u].x), "v"(ka[u].y), "v"(ka[u].z), "v"(ka[u].w));
         place(ka, ma);
         if (ti + 1 >= ntiles) break;
         ma = load(ti + 2, ka);
 #pragma unroll
-        for (int u = 0; u < (int)ITEMS; ++u) asm volatile("" ::"v"(kb[u]));
+        for (int u = 0; u < U; ++u) asm volatile("" ::"v"(kb[u].x), "v"(kb[u].y), "v"(kb[u].z), "v"(kb[u].w));
         place(kb, mb);
         if (ti + 2 >= ntiles) break;
     }
     __syncthreads();  // the segment is placed
-    // the runs out: wave w takes positions [w C, (w + 1) C) of the digit-sorted segment
-    // and copies the part of every digit run inside them, 64 consecutive keys per step
-    // (run bounds and destinations wave-uniform: one LDS read per key)
-    const uint32_t total = L.st[F];
-    const uint32_t C = ((total + NW - 1) / NW + kWave - 1) & ~(kWave - 1);
+    // the runs out: wave w takes slots [w C, (w + 1) C) (C a multiple of 8) and copies the
+    // part of every run inside them: its 16-byte pieces one per lane (ds_read_b128, a
+    // 16-byte store on a 16-byte boundary of the output), the up to 7 keys before the
+    // first and after the last piece one per lane.  Run bounds are wave-uniform.
+    const uint32_t total = L.pb[F];
+    const uint32_t C = ((total + NW - 1) / NW + 7) & ~7u;
     const uint32_t q0 = wave * C, q1 = min(total, q0 + C);
     if (q0 >= q1) return;
-    uint32_t lo = 0, hi = F;  // the run holding q0: the last d with st[d] <= q0
+    uint32_t lo = 0, hi = F;  // the first run that may reach into [q0, q1): the last d with pb[d] <= q0
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
-        if (L.st[mid] <= q0) lo = mid; else hi = mid;
+        if (L.pb[mid] <= q0) lo = mid; else hi = mid;
     }
     for (uint32_t d = __builtin_amdgcn_readfirstlane(lo); d < F; ++d) {
-        const uint32_t rs = __builtin_amdgcn_readfirstlane(L.st[d]), re = __builtin_amdgcn_readfirstlane(L.st[d + 1]);
-        if (rs >= q1) break;
+        if (__builtin_amdgcn_readfirstlane(L.pb[d]) >= q1) break;
+        const uint32_t rs = __builtin_amdgcn_readfirstlane(L.st[d]);
+        const uint32_t re = rs + __builtin_amdgcn_readfirstlane(L.cnt[d]);
         const uint32_t a = max(rs, q0), z = min(re, q1);
-        const uint64_t o = uni_u64(L.dst[d]) - rs;
-        for (uint32_t q = a + lane; q < z; q += kWave) out[o + q] = L.res[q];
+        if (a >= z) continue;
+        // slot q -> output dst[d] + q - rs (o[q] below); o[8k] is 16-byte aligned
+        uint16_t *o = out + uni_u64(L.dst[d]);
+        o -= rs;
+        const uint32_t a8 = min((a + 7) & ~7u, z), z8 = max(z & ~7u, a8);
+        if (lane < a8 - a) o[a + lane] = L.res[a + lane];
+        if (lane < z - z8) o[z8 + lane] = L.res[z8 + lane];
+        for (uint32_t q = a8 + 8 * lane; q < z8; q += 8 * kWave)
+            *reinterpret_cast<uint4 *>(o + q) = *reinterpret_cast<const uint4 *>(&L.res[q]);
     }
 }
 
@@ -1999,7 +2020,7 @@ hipError_t launch_scatter_blk_t(const void *in, const uint64_t *list, void *out,
 #define SORT_CASE(B)                                                                                              \
     case B:                                                                                                       \
         if (place)                                                                                                \
-            hipLaunchKernelGGL((k_place_seg<B, SGXAMD_PLACE_NT, SGXAMD_PLACE_ITEMS>), dim3(grid),                   \
+            hipLaunchKernelGGL((k_place_seg<B, SGXAMD_PLACE_NT, SGXAMD_PLACE_U>), dim3(grid),                   \
                                dim3(SGXAMD_PLACE_NT), 0, s, ik, list, reinterpret_cast<uint16_t *>(out), m, shift, \
                                cursors, part_start, part_count, narrow);                                          \
         hipLaunchKernelGGL((k_sort_blk<B, SGXAMD_SORT_NT, SGXAMD_SORT_ITEMS>), dim3(grid), dim3(SGXAMD_SORT_NT), 0, s, \
