@@ -161,6 +161,9 @@ LAYOUTS = {
        "(the payloads are never read by the count; SGXAMD_KEYS=0 moves whole tuples)",
     3: "pooled pass 1 of 4-byte keys with per-chain pass-2 digit histograms counted in LDS (no digit side "
        "stream; chain-aligned pass-2 segments; SGXAMD_CHAIN_HIST=0 keeps the side stream)",
+    4: "pooled pass 1 of a narrow plan writing the keys' 16-bit residuals and their pass-2 digit bytes (a narrow "
+       "pool, 11 B per tuple; repeated as 4-byte keys when a residual does not fit); pass 2 places each segment "
+       "in LDS (opt-in: SGXAMD_NARROW_POOL=1; measured equal to layout 2, r05j)",
 }
 
 
@@ -263,7 +266,11 @@ def algorithmic_bytes(kernel: str, nR: int, nS: int, passes: int = 2, pass2_bits
     (counting joins move keys only: the pass-1 scatter reads 8-byte tuples and
     writes 4-byte keys, pass 2 and the build/probe read and write keys).
     narrow (mi355_rho_stats.narrow, bit 0 R / bit 1 S): that relation's final partitions
-    hold 2-byte key residuals — its pass 2 writes 2 bytes per key, the build/probe reads 2."""
+    hold 2-byte key residuals — its pass 2 writes 2 bytes per key, the build/probe reads 2.
+    layout 4 (the narrow pool): pass 1 of a narrow relation writes the 2-byte residuals and
+    the digit byte (11 B per tuple) and pass 2 reads both (5 B per key with its 2-byte
+    output); a relation that is not narrow pays that pass 1 and its repeat as keys
+    (`pass1_wide`, 13 B)."""
     n = nR if kernel.startswith("R_") else nS
     nar = bool(narrow & (1 if kernel.startswith("R_") else 2))
     # uses_digit_side(); layout 3 (chain histograms) writes and reads no side stream
@@ -273,8 +280,14 @@ def algorithmic_bytes(kernel: str, nR: int, nS: int, passes: int = 2, pass2_bits
     if kernel.endswith("_hist"):
         return 8 * n          # read every tuple once (key only used, AoS line read)
     if kernel.endswith("pass1_scatter"):
+        if layout == 4:
+            return 11 * n  # read the tuple, write its residual and digit byte
         return (8 + elem + (1 if side else 0)) * n  # read the tuple, write the element (+ its digit byte)
+    if kernel.endswith("pass1_wide"):
+        return 0 if (layout != 4 or nar) else (8 + elem + 1) * n  # the 4-byte pool's repeat
     if kernel.endswith("_scatter"):
+        if layout == 4 and nar:
+            return 5 * n  # read residual + digit byte, write the residual
         return (elem + (2 if nar else elem)) * n  # read + write every element
     if kernel == "join_build_probe":  # every partitioned element read once
         return (2 if narrow & 1 else elem) * nR + (2 if narrow & 2 else elem) * nS

@@ -32,7 +32,15 @@
  *                               device copies: the whole C++ path on one GPU, for tests;
  *   MI355_TRANSPORT_AUTO      — RCCL when G devices are visible, else rehearsal.
  *   SGXAMD_MULTI_TRANSPORT=rccl|rehearsal overrides AUTO.
- * G must be a power of two (1..256).  Counting joins only (MATERIALIZE stays on one GPU).
+ * G must be a power of two (1..256).
+ * Materialising joins (opts->materialize, radix_join.cpp:437-446): whole tuples travel
+ * (the payloads), each rank writes its matches as output_triple_t {key, R payload,
+ * S payload} into a growable buffer of its own -- its output chunk, as the reference's
+ * threads write theirs (ChunkedTable.cpp:98-171) -- and the chunks reach opts->out:
+ * mi355_rho_join_multi_ex concatenates every rank's (rank 0 first) into opts->out
+ * (host or device memory, out_capacity triples; MI355_ERR_CAPACITY with
+ * stats->matches = the triples needed when they do not fit); mi355_rho_join_sharded
+ * writes the calling rank's own chunk (stats->local_matches triples) to its opts->out.
  */
 #ifndef SGXAMD_MULTI_H
 #define SGXAMD_MULTI_H
@@ -76,8 +84,8 @@ typedef struct mi355_multi_stats {
 /* Single process, `ngpus` ranks driven by one host thread each.  R and S are host or
  * device memory (device memory of the current GPU); rank g joins the slice
  * [g*floor(n/G), ...) of each relation (the last rank takes the remainder), staged to
- * its GPU.  opts: algorithm / radix_bits / passes of the local joins (NULL = defaults);
- * key_shift, materialize and stream must be 0. */
+ * its GPU.  opts: algorithm / radix_bits / passes of the local joins (NULL = defaults),
+ * materialize / out / out_capacity (above); key_shift and stream must be 0. */
 int mi355_rho_join_multi_ex(const struct row_t *R, uint64_t nR, const struct row_t *S, uint64_t nS, int ngpus,
                             int transport, const mi355_rho_opts *opts, mi355_multi_stats *stats);
 

@@ -80,7 +80,9 @@ typedef struct mi355_rho_stats {
     double ms_probe;          /* "Join":   fused build+probe kernel measures per workgroup */
     /* partition layout: 0 = tuples, pass-1 histogram + cursors; 1 = pooled pass 1 (no
      * pass-1 histogram), tuples; 2 = pooled pass 1, 4-byte keys (counting joins, RHO and RHT);
-     * 3 = as 2, with the pass-2 digits counted per chain in pass 1 (no digit side stream) */
+     * 3 = as 2, with the pass-2 digits counted per chain in pass 1 (no digit side stream);
+     * 4 = as 2 for a narrow plan: pass 1 writes the keys' 16-bit residuals (and their pass-2
+     * digits beside them), repeated as 4-byte keys for a relation whose residuals do not fit */
     uint32_t layout;
     uint32_t elem_bytes;      /* bytes per partitioned element after the input read (8 or 4) */
     /* bit 0 / bit 1: R's / S's final partitions hold 16-bit key residuals (key >> radix

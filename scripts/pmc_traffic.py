@@ -33,6 +33,11 @@ ALIASES = {
     "k_join_x": ["join_build_probe"],
     "k_predicate": ["scan_count", "scan_bitvector"],
     "k_select": ["scan_select_index"],
+    # narrow plans (round 5): the segment placement and the one-task-per-workgroup
+    # build/probe; k_sort_blk / k_join_x are then launched beside them and return at once
+    # (their near-empty launches are skipped below)
+    "k_place_seg": ["R_pass2_scatter", "S_pass2_scatter"],
+    "k_join_n": ["join_build_probe"],
 }
 # kernels whose bench-size launches differ per pass, told apart by grid size (pass 2's
 # grid is its segments + one per pass-1 bin, larger than pass 1's): smallest grid first
@@ -96,7 +101,7 @@ def main():
                 for name in names:
                     bytes_per_launch[name] = vals[min(i, len(vals) - 1)]
     for k, names in ALIASES.items():
-        if k in per_kernel:
+        if k in per_kernel and per_kernel[k]["total_bytes"] > 1e6:
             for name in names:
                 bytes_per_launch[name] = per_kernel[k]["total_bytes"]
     json.dump({"log2n": log2n, "source": run, "commit": os.environ.get("COMMIT", "unknown"),

@@ -535,6 +535,7 @@ struct RankOut {
     double ms_post = 0, ms_local = 0, ms_allreduce = 0, ms_total = 0;
     double ms_tail = -1;  // device time from S's last piece landing to the local join's end
     mi355_rho_stats st{};
+    Context *ctx = nullptr;  // materialising joins: the rank's triples are in ctx->mat (local of them)
 };
 
 uint32_t log2_exact(int g) {
@@ -574,17 +575,23 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
     mi355_rho_opts lo{};
     if (opts) lo = *opts;
     lo.key_shift = dest_bits;
-    lo.materialize = 0;
+    // materialising joins (MATERIALIZE, radix_join.cpp:437-446): whole tuples travel (the
+    // payloads; keys_exchange_plan refuses keys), and each rank's triples stay in its
+    // context's growable buffer (ctx->mat), its output chunk (the reference's per-thread
+    // chunks of a ChunkedTable, ChunkedTable.cpp:98-171); the caller copies them out
+    lo.materialize = opts && opts->materialize ? 1 : 0;
     lo.stream = nullptr;
     lo.out = nullptr;
     lo.out_capacity = 0;
+    o.ctx = ctx;
+    DeviceBuffer *mat = lo.materialize && ctx ? &ctx->mat : nullptr;
     if (G == 1) {  // nothing to exchange: no collective to leave, so a failure is local
         o.together = true;
         if (pre_fail != MI355_OK) return pre_fail;
         if (injected(rank, kFailLocal)) return MI355_ERR_OOM;
         if (nR && nS) {
             MH_RC(rho::join_pipelined_begin(ctx, s, R, nR, nS, &lo));
-            MH_RC(rho::join_pipelined_finish(ctx, S, nS, &o.st));
+            MH_RC(rho::join_pipelined_finish(ctx, S, nS, &o.st, nullptr, mat));
         }
         o.global = o.local = o.st.matches;
         o.recv_r = nR;
@@ -722,7 +729,7 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
                                                                              total[1], &lo, (uint32_t)elem,
                                                                              s_piece.data(), K);
             if (lrc == MI355_OK)
-                lrc = rho::join_pipelined_finish(ctx, ctx->xrecvS.ptr, total[1], &o.st, &rs->ev[2 * K + 2]);
+                lrc = rho::join_pipelined_finish(ctx, ctx->xrecvS.ptr, total[1], &o.st, &rs->ev[2 * K + 2], mat);
             fail(lrc);
             o.local = lrc == MI355_OK ? o.st.matches : 0;
         } else if (waited) {
@@ -841,8 +848,8 @@ int join_multi(const row_t *R, uint64_t nR, const row_t *S, uint64_t nS, int G, 
         set_last_error("mi355_rho_join_multi: ngpus must be a power of two in 1..256, relations non-null");
         return MI355_ERR_INVALID;
     }
-    if (opts && (opts->key_shift || opts->materialize || opts->stream)) {
-        set_last_error("mi355_rho_join_multi: key_shift, materialize and stream must be 0");
+    if (opts && (opts->key_shift || opts->stream)) {
+        set_last_error("mi355_rho_join_multi: key_shift and stream must be 0");
         return MI355_ERR_INVALID;
     }
     int ndev = 0;
@@ -950,6 +957,26 @@ int join_multi(const row_t *R, uint64_t nR, const row_t *S, uint64_t nS, int G, 
         return rcs[first];
     }
     fill_stats(st, outs, G, kind, 0);
+    if (opts && opts->materialize) {
+        // the ranks' output chunks, rank 0's first, into the caller's buffer
+        uint64_t total = 0;
+        for (const RankOut &o : outs) total += o.local;
+        if (total > opts->out_capacity || (total && !opts->out)) {
+            set_last_error("materialisation output too small: " + std::to_string(total) + " triples needed");
+            return MI355_ERR_CAPACITY;
+        }
+        uint64_t off = 0;
+        for (int g = 0; g < G; ++g) {
+            const RankOut &o = outs[g];
+            if (!o.local) continue;
+            MH_HIP(hipSetDevice(o.ctx->device));
+            const hipError_t e = hipMemcpy(opts->out + off, o.ctx->mat.ptr, o.local * sizeof(output_triple_t),
+                                           hipMemcpyDefault);
+            (void)hipSetDevice(cur);
+            MH_HIP(e);
+            off += o.local;
+        }
+    }
     return MI355_OK;
 }
 
@@ -1203,8 +1230,8 @@ int mi355_rho_join_sharded(void *comm, const row_t *R, uint64_t nR, const row_t 
         set_last_error("mi355_rho_join_sharded needs device-resident slices");
         return MI355_ERR_INVALID;
     }
-    if (opts && (opts->key_shift || opts->materialize)) {
-        set_last_error("mi355_rho_join_sharded: key_shift and materialize must be 0");
+    if (opts && opts->key_shift) {
+        set_last_error("mi355_rho_join_sharded: key_shift must be 0");
         return MI355_ERR_INVALID;
     }
     if (h->broken) {
@@ -1247,6 +1274,15 @@ int mi355_rho_join_sharded(void *comm, const row_t *R, uint64_t nR, const row_t 
     mi355_rho_stats ls = outs[0].st;
     ls.matches = outs[0].global;
     rho::set_last_join_stats(ls);
+    if (opts && opts->materialize) {
+        // this rank's output chunk (its local_matches triples) into the caller's buffer
+        const uint64_t n = outs[0].local;
+        if (n > opts->out_capacity || (n && !opts->out)) {
+            set_last_error("materialisation output too small: " + std::to_string(n) + " triples needed (this rank)");
+            return MI355_ERR_CAPACITY;
+        }
+        if (n) MH_HIP(hipMemcpy(opts->out, outs[0].ctx->mat.ptr, n * sizeof(output_triple_t), hipMemcpyDefault));
+    }
     return MI355_OK;
 }
 

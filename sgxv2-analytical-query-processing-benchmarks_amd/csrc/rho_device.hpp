@@ -42,8 +42,10 @@ void forget_context(const Context *ctx);
 int join_pipelined_begin(Context *ctx, hipStream_t s, const void *dR, uint64_t nR, uint64_t nS,
                          const mi355_rho_opts *opts, uint32_t in_elem = 8, const uint64_t *s_piece_n = nullptr,
                          int s_pieces = 0);
+// mat (materialising joins, opts->materialize at begin): the triples go to this growable
+// device buffer (st->matches of them).
 int join_pipelined_finish(Context *ctx, const void *dS, uint64_t nS, mi355_rho_stats *st,
-                          const hipEvent_t *s_landed = nullptr);
+                          const hipEvent_t *s_landed = nullptr, DeviceBuffer *mat = nullptr);
 // Whether a multi-GPU counting join can exchange keys only: fixes lo's local policy
 // (radix bits / passes) from the expected local sizes nR / nS when the caller left it
 // open, and checks that this policy takes the pooled keys layout for any local size up

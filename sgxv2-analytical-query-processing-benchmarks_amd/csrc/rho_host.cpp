@@ -169,6 +169,18 @@ inline bool narrow_enabled() {
     }();
     return on;
 }
+// SGXAMD_NARROW_POOL=1 (development A/B switch, read once): narrow plans' pass 1 writes
+// the narrow pool (u16 residuals + the digit side stream, 11 B per tuple instead of 13;
+// repeated as 4-byte keys when a residual does not fit) instead of 4-byte keys.  Measured
+// and not the default (r05j): pass 1 takes the same 0.74 ms either way -- it is bound by
+// its tile sort in LDS, not by the bytes it writes -- and pass 2 gains 0.02 ms.
+inline bool narrow_pool_enabled() {
+    static const bool on = [] {
+        const char *e = std::getenv("SGXAMD_NARROW_POOL");
+        return e && std::atoi(e) == 1;
+    }();
+    return on;
+}
 inline bool chain_enabled() {
     static const bool on = [] {
         const char *e = std::getenv("SGXAMD_CHAIN_HIST");
@@ -221,6 +233,7 @@ struct RelPlan {
     size_t chist, seglb, segle, segc0;  // chain histograms [F1][nseg1][F2], pass-2 segment ranges
     size_t kmax;   // pooled keys: the segments' largest keys, then the relation's ([nseg1])
     bool narrow;   // pass 2 writes u16 residuals when the largest key allows (plan_join)
+    bool narrow16; // pass 1 writes a narrow pool first (u16 residuals, the 4-byte pool repeated if a residual does not fit)
     // pooled pass 1 per input piece (the multi-GPU exchange's received pieces): piece i is
     // elements [piece_off[i], + piece_n[i]), its segments start at piece_g0[i]; its launch
     // waits for piece_ev[i] (null: no wait)
@@ -256,30 +269,59 @@ int partition_relation_pooled(Context *ctx, hipStream_t s, Timer &tm, const std:
         po.kmax = rp.narrow ? A.at<uint32_t>(rp.kmax) : nullptr;
         const DigitSide ds{rp.chain ? nullptr : side, key_shift + pol.b1, pol.b2};
         uint32_t *chist = rp.chain ? A.at<uint32_t>(rp.chist) : nullptr;
-        tm.mark((t + "pass1_scatter").c_str());
-        if (rp.piece_n.empty()) {
-            const SegMap m1{nullptr, nullptr, nullptr, 1, rp.seg1, rp.n};
-            RHO_HIP(launch_scatter_pool(in, rp.in_size, t1, rp.keys ? 4u : 8u, m1, rp.nseg1, key_shift, pol.b1, po, ds,
-                                        s, chist));
-        } else {
-            // one launch per piece as it lands, its segments numbered after the earlier
-            // pieces' (one pool layout over all of them)
+        // pass 1 over the relation (one launch, or one per piece as it lands, its segments
+        // numbered after the earlier pieces' -- one pool layout over all of them)
+        const auto scatter = [&](PoolOut &p) -> int {
+            if (rp.piece_n.empty()) {
+                const SegMap m1{nullptr, nullptr, nullptr, 1, rp.seg1, rp.n};
+                RHO_HIP(launch_scatter_pool(in, rp.in_size, t1, rp.keys ? 4u : 8u, m1, rp.nseg1, key_shift, pol.b1, p,
+                                            ds, s, chist));
+                return MI355_OK;
+            }
             const char *ib = reinterpret_cast<const char *>(in);
             for (size_t i = 0; i < rp.piece_n.size(); ++i) {
                 if (i < rp.piece_ev.size() && rp.piece_ev[i]) RHO_HIP(hipStreamWaitEvent(s, rp.piece_ev[i], 0));
                 const uint64_t n = rp.piece_n[i];
                 if (!n) continue;
                 const SegMap mi{nullptr, nullptr, nullptr, 1, rp.seg1, n};
-                po.g0 = rp.piece_g0[i];
+                p.g0 = rp.piece_g0[i];
                 RHO_HIP(launch_scatter_pool(ib + rp.piece_off[i] * rp.in_size, rp.in_size, t1, rp.keys ? 4u : 8u, mi,
-                                            (uint32_t)((n + rp.seg1 - 1) / rp.seg1), key_shift, pol.b1, po, ds, s,
+                                            (uint32_t)((n + rp.seg1 - 1) / rp.seg1), key_shift, pol.b1, p, ds, s,
                                             chist));
             }
+            return MI355_OK;
+        };
+        const auto layout = [&](const PoolOut &p) -> int {
+            RHO_HIP(launch_pool_layout(p.cnt, rp.nseg1, pol.b1, A.at<uint64_t>(rp.tot1), start1, cnt1, lbase, lcount,
+                                       segbase2, s, rp.chain ? chain_slot_mode() : 0u, p.kmax, p.guard,
+                                       p.guard_shift));
+            RHO_HIP(launch_block_list(p, lbase, list, pol.b1, s));
+            return MI355_OK;
+        };
+        int rc;
+        if (rp.narrow16) {
+            // the narrow pool (u16 residuals + the side stream), then the 4-byte pool's
+            // launches guarded by the relation's largest key: they return at once when
+            // every residual fit (the guards read the word the narrow pool's layout wrote)
+            PoolOut pn = po;
+            pn.narrow16 = true;
+            pn.rshift = key_shift + pol.b1 + pol.b2;
+            tm.mark((t + "pass1_scatter").c_str());
+            if ((rc = scatter(pn))) return rc;
+            tm.mark((t + "pass1_scan").c_str());
+            if ((rc = layout(pn))) return rc;
+            PoolOut pw = po;
+            pw.guard = po.kmax + rp.nseg1;
+            pw.guard_shift = pn.rshift;
+            tm.mark((t + "pass1_wide").c_str());
+            if ((rc = scatter(pw))) return rc;
+            if ((rc = layout(pw))) return rc;
+        } else {
+            tm.mark((t + "pass1_scatter").c_str());
+            if ((rc = scatter(po))) return rc;
+            tm.mark((t + "pass1_scan").c_str());
+            if ((rc = layout(po))) return rc;
         }
-        tm.mark((t + "pass1_scan").c_str());
-        RHO_HIP(launch_pool_layout(po.cnt, rp.nseg1, pol.b1, A.at<uint64_t>(rp.tot1), start1, cnt1, lbase, lcount,
-                                   segbase2, s, rp.chain ? chain_slot_mode() : 0u, po.kmax));
-        RHO_HIP(launch_block_list(po, lbase, list, pol.b1, s));
         *final_rel = t1;
         *pstart = start1;
         *pcnt = cnt1;
@@ -318,7 +360,7 @@ int partition_relation_pooled(Context *ctx, hipStream_t s, Timer &tm, const std:
     RHO_HIP(launch_scan_regions(hist2, segbase2, start1, F1, pol.b2, ps, pc, s));
     tm.mark((t + "pass2_scatter").c_str());
     RHO_HIP(launch_scatter_blk(t1, list, t2, rp.keys ? 4u : 8u, m2, rp.grid2, key_shift + pol.b1, pol.b2, hist2, s,
-                               narrow, ps, pc));
+                               narrow, ps, pc, rp.narrow16 ? side : nullptr));
     *final_rel = t2;
     *pstart = ps;
     *pcnt = pc;
@@ -434,6 +476,7 @@ void plan_relation(Arena &A, RelPlan &rp, uint64_t n, const Policy &pol, int poo
     rp.keys = false;
     rp.chain = false;
     rp.narrow = false;
+    rp.narrow16 = false;
     rp.kmax = 0;
     rp.in_size = sizeof(row_t);
     rp.piece_off.clear();
@@ -597,6 +640,13 @@ int plan_join(Context *ctx, hipStream_t s, uint64_t nR, uint64_t nS, const mi355
     const bool narrow = pool == kPoolKeys && counting && pj.algo == kAlgoChaining && pj.pol.rcap == kBigRcap &&
                         pol.passes == 2 && sort2_enabled() && narrow_enabled();
     pj.pr.narrow = pj.ps.narrow = narrow;
+    // ... and pass 1 writes them first as a narrow pool (u16 residuals, read by
+    // k_place_seg with their digit side stream); the chain-histogram layout keeps keys,
+    // and so do pass-1 digits above 7 bits (the narrow pool's 64-residual granules keep
+    // up to 63 carried keys per digit in LDS: 64 KiB at 8 bits, one workgroup per CU)
+    const bool n16 = narrow && pol.b1 <= 7 && uses_digit_side(pol) && place_enabled() && narrow_pool_enabled();
+    pj.pr.narrow16 = n16 && !pj.pr.chain;
+    pj.ps.narrow16 = n16 && !pj.ps.chain;
     pj.over_cap = (uint32_t)(nS / pj.s_chunk + 1);
     // one workgroup per task up to 2048 (few partitions with a large S — a tiny build
     // side — still spread their S chunks over the chip)
@@ -664,7 +714,7 @@ void fill_join_stats(const Context *ctx, const PendingJoin &pj, const Timer &tm,
         st->passes = pol.passes;
         st->pass1_bits = pol.b1;
         st->pass2_bits = pol.b2;
-        st->layout = pj.pr.chain ? 3u : (pj.pr.keys ? 2u : (pj.pr.pooled ? 1u : 0u));
+        st->layout = pj.pr.chain ? 3u : pj.pr.narrow16 ? 4u : (pj.pr.keys ? 2u : (pj.pr.pooled ? 1u : 0u));
         st->elem_bytes = pj.pr.keys ? 4u : 8u;
         // (k_join_x: the high word of result[6] = 1 | narrow R << 1 | narrow S << 2)
         st->narrow = (uint32_t)(ctx->host_result[6] >> 33) & 3u;
@@ -1057,11 +1107,17 @@ int join_pipelined_begin(Context *ctx, hipStream_t s, const void *dR, uint64_t n
     return rc;
 }
 
-int join_pipelined_finish(Context *ctx, const void *dS, uint64_t nS, mi355_rho_stats *st, const hipEvent_t *s_landed) {
+int join_pipelined_finish(Context *ctx, const void *dS, uint64_t nS, mi355_rho_stats *st, const hipEvent_t *s_landed,
+                          DeviceBuffer *mat) {
     PendingJoin &pj = pending_of(ctx);
     pj.ps.piece_ev.clear();
     if (s_landed) pj.ps.piece_ev.assign(s_landed, s_landed + pj.ps.piece_n.size());
-    return join_finish(ctx, pj, static_cast<const row_t *>(dS), nS, st, nullptr, 0, nullptr, true);
+    if (pj.materialize && !mat) {
+        pj.active = false;
+        set_last_error("join_pipelined_finish: a materialising join needs an output buffer");
+        return MI355_ERR_INVALID;
+    }
+    return join_finish(ctx, pj, static_cast<const row_t *>(dS), nS, st, nullptr, 0, mat, true);
 }
 
 bool keys_exchange_plan(uint64_t nR, uint64_t nS, uint64_t cap_r, uint64_t cap_s, mi355_rho_opts *lo) {

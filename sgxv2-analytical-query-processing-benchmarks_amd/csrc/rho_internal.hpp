@@ -138,6 +138,15 @@ struct PoolOut {
     uint32_t nseg;
     uint32_t g0 = 0;       // this launch's first segment (a pass 1 launched per input piece)
     uint32_t *kmax = nullptr;  // keys (nullable): per segment, its largest key (narrow residuals)
+    // narrow pool (keys): the elements written are the residuals key >> rshift as u16
+    // (k_scatter_pool's OB 2), speculatively: kmax tells afterwards whether they fit
+    bool narrow16 = false;
+    uint32_t rshift = 0;
+    // the 4-byte pool repeated after a narrow pool: its launches (scatter, layout, block
+    // list) return at once when guard (the relation's largest key) >> guard_shift fits 16
+    // bits (nullable: unguarded)
+    const uint32_t *guard = nullptr;
+    uint32_t guard_shift = 0;
 };
 // Pass 1 of a pooled plan: contiguous input segments (m), pooled output in out, digit
 // side stream ds beside every stored element.  Elements: in_size-byte input
@@ -180,9 +189,12 @@ hipError_t launch_chain_scan(const uint64_t *cnt, uint32_t nseg, uint32_t mode, 
 // kmax (nullable): the segments' largest keys (PoolOut::kmax), folded into kmax[nseg] —
 // the relation's largest key, which tells pass 2 and the build/probe whether the key
 // residuals above the radix bits fit 16 bits (narrow partitions, launch_scatter_blk).
+// guard / gshift (nullable): the launches return at once when *guard >> gshift fits 16
+// bits (the 4-byte pool repeated after a narrow pool that stood, PoolOut::guard).
 hipError_t launch_pool_layout(uint64_t *cnt, uint32_t nseg, uint32_t bits, uint64_t *totals, uint64_t *start,
                               uint64_t *count, uint64_t *lbase, uint64_t *lcount, uint32_t *seg_base, hipStream_t s,
-                              uint32_t chain_mode = 0, uint32_t *kmax = nullptr);
+                              uint32_t chain_mode = 0, uint32_t *kmax = nullptr, const uint32_t *guard = nullptr,
+                              uint32_t gshift = 0);
 // The block list: region d's blocks at [lbase[d], lbase[d] + lcount[d]) as
 // physical block | fill << 32.
 hipError_t launch_block_list(const PoolOut &po, const uint64_t *lbase, uint64_t *list, uint32_t bits, hipStream_t s);
@@ -201,7 +213,11 @@ hipError_t launch_hist_side_blk(const uint8_t *side, const uint64_t *list, const
 hipError_t launch_scatter_blk(const void *in, const uint64_t *list, void *out, uint32_t elem_size, const SegMap &m,
                               uint32_t grid, uint32_t shift, uint32_t bits, const uint64_t *cursors, hipStream_t s,
                               const uint32_t *narrow = nullptr, const uint64_t *part_start = nullptr,
-                              const uint64_t *part_count = nullptr);
+                              const uint64_t *part_count = nullptr, const uint8_t *side16 = nullptr);
+// side16 (nullable): in is a narrow pool (launch_scatter_pool with PoolOut::narrow16)
+// whose digits are in this side stream: k_place_seg reads its u16 residuals, while
+// k_sort_blk (guarded by the largest key) reads the 4-byte pool repeated when a residual
+// did not fit.
 bool place_enabled();
 // launch_scatter's one-pass cursor scatter writing only the key word of every tuple
 // (the multi-GPU shard partition of a counting join, whose exchange moves keys).

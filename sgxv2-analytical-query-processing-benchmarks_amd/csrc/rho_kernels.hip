@@ -414,9 +414,14 @@ hipError_t launch_hist_side(const uint8_t *side, const SegMap &m, uint32_t grid,
 
 // ------------------------------------------------------------------ scans ---
 // One block per digit column: exclusive prefix over the segments (in place).
+// guard (nullable): nothing to do when *guard >> gshift fits 16 bits (the 4-byte pool
+// repeated after a narrow pool that stood, PoolOut::guard).
 __global__ __launch_bounds__(kBlock) void k_scan_cols(uint64_t *__restrict__ hist, uint32_t nseg,
-                                                      uint64_t *__restrict__ totals) {
+                                                      uint64_t *__restrict__ totals,
+                                                      const uint32_t *__restrict__ guard = nullptr,
+                                                      uint32_t gshift = 0) {
     __shared__ uint64_t scratch[kWaves + 1];
+    if (guard && ((*guard >> gshift) >> 16) == 0) return;
     uint64_t *col = hist + (uint64_t)blockIdx.x * nseg;
     uint64_t carry = 0;
     for (uint32_t base = 0; base < nseg; base += kBlock) {
@@ -745,12 +750,14 @@ __device__ __forceinline__ T lds_pick(bool c, const T *a, const T *b) {
 // EXT: 0 = cursor output, contiguous input; 1 = pooled output (PoolOut); 2 = block-list
 // input (the segment's list entries staged in ents).
 // T: the element moved (uint64_t tuple, or uint32_t key of a count-only join).
-template <int BITS, int ITEMS, int NT, int EXT = 0, typename T = uint64_t>
+// OB: bytes per element written (sizeof(T); 2: the pooled pass 1 of a narrow relation
+// writes the keys' 16-bit residuals, k_scatter_pool's narrow variant).
+template <int BITS, int ITEMS, int NT, int EXT = 0, typename T = uint64_t, int OB = (int)sizeof(T)>
 struct ScatterLds {
     static constexpr uint32_t F = 1u << BITS;
     static constexpr uint32_t TILE = NT * ITEMS;
     static constexpr uint32_t NW = NT / kWave;
-    static constexpr uint32_t G = 128 / sizeof(T);  // elements per 128-B granule
+    static constexpr uint32_t G = 128 / OB;  // elements per 128-B granule
     static constexpr uint32_t GPB = kBlk / G;       // granules per pool block
     static constexpr uint32_t MAXDESC = (TILE + (G - 1) * F) / G + F;
     union {
@@ -795,6 +802,13 @@ __device__ __noinline__ void chain_store(const uint32_t *h2, uint32_t *__restric
     }
 }
 
+// The 4-byte pool's launches after a speculative narrow pool (po.guard: the relation's
+// largest key; po.guard_shift: the residual shift): nothing to do when every residual fit
+// 16 bits.
+__device__ __forceinline__ bool pool_guard_skip(const PoolOut &po) {
+    return po.guard != nullptr && ((*po.guard >> po.guard_shift) >> 16) == 0;
+}
+
 // Pooled output, per owner thread (digit): its chain's current block and length.
 struct PoolState {
     uint32_t cur;
@@ -806,9 +820,9 @@ struct PoolState {
 // Waves per SIMD that the LDS footprint allows (__launch_bounds__ second argument:
 // k workgroups per CU of NT threads <=> k * NT / 256 waves per SIMD), so the
 // register allocation never becomes the tighter occupancy limit.
-template <int BITS, int ITEMS, int NT, int EXT = 0, typename T = uint64_t>
+template <int BITS, int ITEMS, int NT, int EXT = 0, typename T = uint64_t, int OB = (int)sizeof(T)>
 constexpr int scatter_waves_per_simd() {
-    constexpr int k = (160 * 1024) / (int)sizeof(ScatterLds<BITS, ITEMS, NT, EXT, T>);
+    constexpr int k = (160 * 1024) / (int)sizeof(ScatterLds<BITS, ITEMS, NT, EXT, T, OB>);
     constexpr int w = (k < 1 ? 1 : k) * NT / 256;
     // at most 4 waves/SIMD (128 VGPRs): fewer registers spill, and a scratch reload is
     // a vector-memory op whose wait would also wait for every store in flight
@@ -874,14 +888,15 @@ __device__ __forceinline__ void block_scan2(uint32_t a, uint32_t b, uint32_t (&w
 // tn: valid tuples of the tile (items tid + k * NT < tn); with block-list input (EXT 2)
 // a bit mask instead, bit k = item k valid.  ps: the owner thread's chain (EXT 1).
 // FULL: every item is valid (no per-item checks; callers take it for full tiles).
-template <int BITS, int ITEMS, int NT, int EXT = 0, typename T = uint64_t, bool FULL = false, int F2 = 0>
-__device__ __forceinline__ uint32_t scatter_tile_sort(ScatterLds<BITS, ITEMS, NT, EXT, T> &L, uint64_t &pend,
+template <int BITS, int ITEMS, int NT, int EXT = 0, typename T = uint64_t, bool FULL = false, int F2 = 0,
+          int OB = (int)sizeof(T)>
+__device__ __forceinline__ uint32_t scatter_tile_sort(ScatterLds<BITS, ITEMS, NT, EXT, T, OB> &L, uint64_t &pend,
                                                       uint32_t &carried, const T (&v)[ITEMS],
                                                       T *__restrict__ out, uint32_t tn, uint32_t shift,
                                                       uint64_t tbase_global, PoolState *ps = nullptr,
                                                       ChainState *cs = nullptr) {
     constexpr uint32_t F = 1u << BITS, mask = F - 1, NW = NT / kWave;
-    constexpr uint32_t G = ScatterLds<BITS, ITEMS, NT, EXT, T>::G, GPB = ScatterLds<BITS, ITEMS, NT, EXT, T>::GPB;
+    constexpr uint32_t G = ScatterLds<BITS, ITEMS, NT, EXT, T, OB>::G, GPB = ScatterLds<BITS, ITEMS, NT, EXT, T, OB>::GPB;
     const uint32_t tid = threadIdx.x;
     const auto valid = [&](int k) { return FULL || (EXT == 2 ? ((tn >> k) & 1u) != 0 : tid + k * NT < tn); };
 #ifdef SGXAMD_ABLATE_NOSORT  // development ablation (tools/part_bench): the memory pipeline alone
@@ -967,11 +982,12 @@ __device__ __forceinline__ uint32_t scatter_tile_sort(ScatterLds<BITS, ITEMS, NT
 // Phases D-E of the tile sorted by scatter_tile_sort (gtot = its granule count).
 // SIDE: every stored tuple's next-pass digit also goes to side[a] (a 16-lane group
 // writes 16 consecutive bytes next to its 128-B granule).
-template <int BITS, int ITEMS, int NT, bool SIDE, int EXT = 0, typename T = uint64_t>
-__device__ __forceinline__ void scatter_tile_write(ScatterLds<BITS, ITEMS, NT, EXT, T> &L, T *__restrict__ out,
+// OB 2 (narrow pool): the elements written are the keys' residuals key >> rshift, u16.
+template <int BITS, int ITEMS, int NT, bool SIDE, int EXT = 0, typename T = uint64_t, int OB = (int)sizeof(T)>
+__device__ __forceinline__ void scatter_tile_write(ScatterLds<BITS, ITEMS, NT, EXT, T, OB> &L, T *__restrict__ out,
                                                    uint32_t gtot, uint8_t *__restrict__ side, uint32_t shift2,
-                                                   uint32_t mask2) {
-    constexpr uint32_t G = ScatterLds<BITS, ITEMS, NT, EXT, T>::G;
+                                                   uint32_t mask2, uint32_t rshift = 0) {
+    constexpr uint32_t G = ScatterLds<BITS, ITEMS, NT, EXT, T, OB>::G;
     constexpr uint32_t F = 1u << BITS, NG = NT / G;
     constexpr uint32_t CS = G - 1;
     constexpr uint32_t TB = EXT == 1 ? 0xFFFFu : ~0u;  // tile offset bits of meta.x
@@ -981,7 +997,35 @@ __device__ __forceinline__ void scatter_tile_write(ScatterLds<BITS, ITEMS, NT, E
     const uint32_t tid = threadIdx.x;
     // D. whole granules, G lanes (one 128-B line) per granule
     const uint32_t lane = tid & (G - 1), grp = tid / G;
-    if constexpr (sizeof(T) == 4) {
+    if constexpr (OB == 2) {
+        // narrow pool (pooled, every granule whole): 16 lanes per 64-residual granule, four
+        // consecutive keys per lane -- one 8-byte store of their residuals and one 4-byte
+        // store of their next-pass digits
+        static_assert(EXT == 1 && sizeof(T) == 4 && SIDE, "narrow pool: pooled keys with the side stream");
+        constexpr uint32_t NG4 = NT / 16;
+        const uint32_t l4 = 4 * (tid & 15);
+        uint16_t *__restrict__ o16 = reinterpret_cast<uint16_t *>(out);
+        for (uint32_t j = tid / 16; j < gtot; j += NG4) {
+            const uint32_t d = L.desc[j];
+            const uint2 m = L.meta[d];
+            const uint32_t jj = j - L.gbase[d], cd = m.y & 0xFFu, tbx = m.x & TB;
+            const uint64_t gv = *reinterpret_cast<const uint64_t *>(&L.gaddr[d]);
+            const uint32_t g0 = m.x >> 16;
+            const uint32_t gb = jj < g0 ? (uint32_t)gv + jj : (uint32_t)(gv >> 32) + (jj - g0);
+            const uint64_t a = (uint64_t)gb * G + l4;
+            const uint32_t q = jj * G + l4;
+            uint32_t x[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                x[i] = (uint32_t)lds_pick(q + i < cd, &L.carry[d * CS + q + i], &L.tile[tbx + q + i - cd]);
+            const uint32_t r01 = ((x[0] >> rshift) & 0xFFFFu) | ((x[1] >> rshift) << 16);
+            const uint32_t r23 = ((x[2] >> rshift) & 0xFFFFu) | ((x[3] >> rshift) << 16);
+            st_nt(reinterpret_cast<uint64_t *>(o16 + a), (uint64_t)r01 | ((uint64_t)r23 << 32));
+            *reinterpret_cast<uint32_t *>(side + a) = ((x[0] >> shift2) & mask2) | (((x[1] >> shift2) & mask2) << 8) |
+                                                      (((x[2] >> shift2) & mask2) << 16) |
+                                                      (((x[3] >> shift2) & mask2) << 24);
+        }
+    } else if constexpr (sizeof(T) == 4) {
         // keys: 16 lanes per granule, two consecutive keys per lane (one 8-byte store and
         // one 2-byte side store), half the rounds and metadata reads of one key per lane
         constexpr uint32_t NG2 = NT / 16;
@@ -1339,8 +1383,8 @@ __device__ __forceinline__ uint32_t load_tile_blk(const char *__restrict__ in,
 // EXT 1: contiguous segment g of `in` -> pooled output (po), digit side stream.
 // EXT 2: block-list segment g (list) -> `out` at the segment-major cursors cur_init.
 // T: the element written (tuple or key); IS: the input element size in bytes.
-template <int BITS, int ITEMS, int NT, int EXT, typename T, int IS, int F2 = 0>
-__device__ __forceinline__ void scatter_segment_ext(ScatterLds<BITS, ITEMS, NT, EXT, T> &L, uint32_t g,
+template <int BITS, int ITEMS, int NT, int EXT, typename T, int IS, int F2 = 0, int OB = (int)sizeof(T)>
+__device__ __forceinline__ void scatter_segment_ext(ScatterLds<BITS, ITEMS, NT, EXT, T, OB> &L, uint32_t g,
                                                     const char *__restrict__ in, T *__restrict__ out,
                                                     const SegMap &m, uint32_t shift,
                                                     const uint64_t *__restrict__ cur_init,
@@ -1349,7 +1393,7 @@ __device__ __forceinline__ void scatter_segment_ext(ScatterLds<BITS, ITEMS, NT, 
                                                     HistLayout layout = kSegMajor, uint32_t nseg_stride = 0,
                                                     const uint64_t *__restrict__ digit_base = nullptr,
                                                     ChainState *cs = nullptr) {
-    using LdsT = ScatterLds<BITS, ITEMS, NT, EXT, T>;
+    using LdsT = ScatterLds<BITS, ITEMS, NT, EXT, T, OB>;
     constexpr uint32_t TILE = NT * ITEMS, BPT = TILE / kBlk;
     constexpr uint32_t F = 1u << BITS, G = LdsT::G, GPB = LdsT::GPB, NG = NT / G, CS = G - 1;
     constexpr bool SIDE = EXT == 1 && F2 == 0;  // chain histograms replace the side stream
@@ -1409,9 +1453,9 @@ __device__ __forceinline__ void scatter_segment_ext(ScatterLds<BITS, ITEMS, NT, 
     // (pooled pass 1, EXT 1, keeps one sort copy: a full-tile copy spills 3-5 VGPRs there)
     const auto sort = [&](T(&v)[ITEMS], uint32_t tn) -> uint32_t {
         if (EXT != 1 && is_full(tn))
-            return scatter_tile_sort<BITS, ITEMS, NT, EXT, T, true>(L, pend, carried, v, out, tn, shift, 0, &ps);
-        return scatter_tile_sort<BITS, ITEMS, NT, EXT, T, false, F2>(L, pend, carried, v, out, tn, shift, 0, &ps,
-                                                                     cs);
+            return scatter_tile_sort<BITS, ITEMS, NT, EXT, T, true, 0, OB>(L, pend, carried, v, out, tn, shift, 0, &ps);
+        return scatter_tile_sort<BITS, ITEMS, NT, EXT, T, false, F2, OB>(L, pend, carried, v, out, tn, shift, 0, &ps,
+                                                                         cs);
     };
     // pooled keys: the largest key of the segment (lanes past its end load 0): whether
     // pass 2 may write 16-bit residuals (k_sort_blk), and the build/probe's table size
@@ -1435,14 +1479,14 @@ __device__ __forceinline__ void scatter_segment_ext(ScatterLds<BITS, ITEMS, NT, 
         ma = load(ti + 2, va);
 #pragma unroll
         for (int k = 0; k < ITEMS; ++k) asm volatile("" ::"v"(vb[k]));
-        scatter_tile_write<BITS, ITEMS, NT, SIDE, EXT, T>(L, out, gt, side, shift2, mask2);
+        scatter_tile_write<BITS, ITEMS, NT, SIDE, EXT, T, OB>(L, out, gt, side, shift2, mask2, po.rshift);
         if (ti + 1 >= ntiles) break;
         key_max(vb);
         gt = sort(vb, tn_of(ti + 1, mb));
         mb = load(ti + 3, vb);
 #pragma unroll
         for (int k = 0; k < ITEMS; ++k) asm volatile("" ::"v"(va[k]));
-        scatter_tile_write<BITS, ITEMS, NT, SIDE, EXT, T>(L, out, gt, side, shift2, mask2);
+        scatter_tile_write<BITS, ITEMS, NT, SIDE, EXT, T, OB>(L, out, gt, side, shift2, mask2, po.rshift);
         if (ti + 2 >= ntiles) break;
         key_max(va);
         gt = sort(va, tn_of(ti + 2, ma));
@@ -1479,18 +1523,26 @@ __device__ __forceinline__ void scatter_segment_ext(ScatterLds<BITS, ITEMS, NT, 
     for (uint32_t d = tid / G; d < F; d += NG) {
         if (lane < L.cnt[d]) {
             const T x = L.carry[d * CS + lane];
-            out[L.pend[d] + lane] = x;
+            if constexpr (OB == 2)  // narrow pool: the residual
+                reinterpret_cast<uint16_t *>(out)[L.pend[d] + lane] = (uint16_t)((uint32_t)x >> po.rshift);
+            else
+                out[L.pend[d] + lane] = x;
             if (SIDE) side[L.pend[d] + lane] = (uint8_t)(((uint32_t)x >> shift2) & mask2);
         }
     }
     if constexpr (F2 > 0) chain_store<F, F2, NT>(cs->h2, cs->out, gp, cs->nseg);
 }
 
-template <int BITS, int ITEMS, int NT, typename T, int IS, int F2 = 0>
-__global__ __launch_bounds__(NT, (scatter_waves_per_simd<BITS, ITEMS, NT, 1, T>())) void k_scatter_pool(
+// OB 2: the narrow pool (keys' residuals, u16), written speculatively: the relation's
+// largest key (kmax, folded by launch_pool_layout) tells afterwards whether every residual
+// fit; if not, the launches are repeated as a 4-byte pool, guarded by po.guard (they
+// return at once when the narrow pool stood).
+template <int BITS, int ITEMS, int NT, typename T, int IS, int F2 = 0, int OB = (int)sizeof(T)>
+__global__ __launch_bounds__(NT, (scatter_waves_per_simd<BITS, ITEMS, NT, 1, T, OB>())) void k_scatter_pool(
     const char *__restrict__ in, T *__restrict__ out, SegMap m, uint32_t shift, PoolOut po,
     uint8_t *__restrict__ side, uint32_t shift2, uint32_t mask2, uint32_t *__restrict__ chain) {
-    __shared__ ScatterLds<BITS, ITEMS, NT, 1, T> L;
+    __shared__ ScatterLds<BITS, ITEMS, NT, 1, T, OB> L;
+    if (pool_guard_skip(po)) return;
     const uint32_t g = xcd_contiguous(blockIdx.x, gridDim.x);
     if constexpr (F2 > 0) {
         __shared__ uint32_t h2[(1u << BITS) * F2 / 2];
@@ -1498,8 +1550,8 @@ __global__ __launch_bounds__(NT, (scatter_waves_per_simd<BITS, ITEMS, NT, 1, T>(
         scatter_segment_ext<BITS, ITEMS, NT, 1, T, IS, F2>(L, g, in, out, m, shift, nullptr, nullptr, po, side, shift2,
                                                            mask2, kSegMajor, 0, nullptr, &cs);
     } else {
-        scatter_segment_ext<BITS, ITEMS, NT, 1, T, IS>(L, g, in, out, m, shift, nullptr, nullptr, po, side, shift2,
-                                                       mask2);
+        scatter_segment_ext<BITS, ITEMS, NT, 1, T, IS, 0, OB>(L, g, in, out, m, shift, nullptr, nullptr, po, side,
+                                                              shift2, mask2);
     }
 }
 
@@ -1791,11 +1843,14 @@ struct PlaceLds {
     uint32_t last;              // the segment is its region's last
 };
 
-template <int BITS, int NT, int U>
+// I16: the input is a narrow pool (k_scatter_pool OB 2): u16 residuals, the digits in the
+// side stream beside them; else 4-byte keys.
+template <int BITS, int NT, int U, bool I16>
 __global__ __launch_bounds__(NT, NT *SGXAMD_PLACE_WGS / 256) void k_place_seg(
-    const uint32_t *__restrict__ in, const uint64_t *__restrict__ list, uint16_t *__restrict__ out, SegMap m,
-    uint32_t shift, const uint64_t *__restrict__ cursors, const uint64_t *__restrict__ part_start,
-    const uint64_t *__restrict__ part_count, const uint32_t *__restrict__ narrow) {
+    const uint32_t *__restrict__ in, const uint8_t *__restrict__ side, const uint64_t *__restrict__ list,
+    uint16_t *__restrict__ out, SegMap m, uint32_t shift, const uint64_t *__restrict__ cursors,
+    const uint64_t *__restrict__ part_start, const uint64_t *__restrict__ part_count,
+    const uint32_t *__restrict__ narrow) {
     using LdsT = PlaceLds<BITS, NT>;
     constexpr uint32_t F = LdsT::F, mask = F - 1, NW = NT / kWave;
     constexpr uint32_t BPT = NW * U;  // blocks per tile: U per wave, one 16-byte load per lane each
@@ -1837,6 +1892,7 @@ __global__ __launch_bounds__(NT, NT *SGXAMD_PLACE_WGS / 256) void k_place_seg(
     const uint32_t ntiles = (nent + BPT - 1) / BPT;
     // tile ti: item u of wave w = block ti * BPT + u * NW + w, lane l its keys 4l..4l+3
     // (a buffer resource over the block's fill: keys past it read 0 and are masked out)
+    // (I16: .x/.y the four residuals, .z their four digits)
     const auto load = [&](uint32_t ti, uint4(&k)[U]) -> uint32_t {
         uint32_t vm = 0;
 #pragma unroll
@@ -1845,7 +1901,17 @@ __global__ __launch_bounds__(NT, NT *SGXAMD_PLACE_WGS / 256) void k_place_seg(
             const uint64_t en = idx < nent ? L.ents[idx] : 0ull;  // one address per wave: a broadcast
             const uint32_t phys = __builtin_amdgcn_readfirstlane((uint32_t)en);
             const uint32_t fill = __builtin_amdgcn_readfirstlane((uint32_t)(en >> 32));
-            k[u] = buf_ld_nt_u128(make_rsrc(in + (uint64_t)phys * kBlk, fill * 4u), lane * 16u, 0);
+            if constexpr (I16) {
+                // (ranges rounded up to whole dwords: the bounds check is per dword, and the
+                // elements past the fill are masked out)
+                const uint16_t *b16 = reinterpret_cast<const uint16_t *>(in) + (uint64_t)phys * kBlk;
+                const uint64_t r = buf_ld_nt_u64(make_rsrc(b16, (fill * 2u + 3u) & ~3u), lane * 8u, 0);
+                const uint32_t dg = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(
+                    make_rsrc(side + (uint64_t)phys * kBlk, (fill + 3u) & ~3u), (int)(lane * 4u), 0, 2);
+                k[u] = make_uint4((uint32_t)r, (uint32_t)(r >> 32), dg, 0u);
+            } else {
+                k[u] = buf_ld_nt_u128(make_rsrc(in + (uint64_t)phys * kBlk, fill * 4u), lane * 16u, 0);
+            }
             const uint32_t f = fill > 4 * lane ? min(fill - 4 * lane, 4u) : 0u;
             vm |= ((1u << f) - 1u) << (4 * u);
         }
@@ -1854,11 +1920,20 @@ __global__ __launch_bounds__(NT, NT *SGXAMD_PLACE_WGS / 256) void k_place_seg(
     const auto place = [&](const uint4(&k)[U], uint32_t vm) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint32_t w[4] = {k[u].x, k[u].y, k[u].z, k[u].w};
+            if constexpr (I16) {
+                const uint32_t rr[2] = {k[u].x, k[u].y};
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-                if ((vm >> (4 * u + j)) & 1u)
-                    L.res[atomicAdd(&L.pos[(w[j] >> shift) & mask], 1u)] = (uint16_t)(w[j] >> rshift);
+                for (int j = 0; j < 4; ++j)
+                    if ((vm >> (4 * u + j)) & 1u)
+                        L.res[atomicAdd(&L.pos[(k[u].z >> (8 * j)) & mask], 1u)] =
+                            (uint16_t)(rr[j >> 1] >> (16 * (j & 1)));
+            } else {
+                const uint32_t w[4] = {k[u].x, k[u].y, k[u].z, k[u].w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if ((vm >> (4 * u + j)) & 1u)
+                        L.res[atomicAdd(&L.pos[(w[j] >> shift) & mask], 1u)] = (uint16_t)(w[j] >> rshift);
+            }
         }
     };
     uint4 ka[U], kb[U];
@@ -1943,6 +2018,30 @@ hipError_t launch_scatter_pool_t(const void *in, void *out, const SegMap &m, uin
         }
         return hipErrorInvalidValue;
     }
+    if (po.narrow16) {  // the narrow pool: keys with the side stream, up to 8-bit digits
+        if constexpr (sizeof(T) == 4) {
+            if (!ds.side || po.guard) return hipErrorInvalidValue;
+#define NPOOL_CASE(B)                                                                                          \
+    case B:                                                                                                    \
+        hipLaunchKernelGGL((k_scatter_pool<B, ITEMS, NT, T, IS, 0, 2>), dim3(grid), dim3(NT), 0, s, ib, o, m, \
+                           shift, po, ds.side, ds.shift2, mask2, nullptr);                                     \
+        break;
+            switch (bits) {
+                NPOOL_CASE(1)
+                NPOOL_CASE(2)
+                NPOOL_CASE(3)
+                NPOOL_CASE(4)
+                NPOOL_CASE(5)
+                NPOOL_CASE(6)
+                NPOOL_CASE(7)
+                default:
+                    return hipErrorInvalidValue;
+            }
+#undef NPOOL_CASE
+            return hipGetLastError();
+        }
+        return hipErrorInvalidValue;
+    }
 #define POOL_CASE(B)                                                                                             \
     case B:                                                                                                      \
         if constexpr (sizeof(ScatterLds<B, ITEMS, NT, 1, T>) <= 160 * 1024 && (1 << B) <= NT) {                   \
@@ -2007,7 +2106,8 @@ bool place_enabled() {
 template <typename T>
 hipError_t launch_scatter_blk_t(const void *in, const uint64_t *list, void *out, const SegMap &m, uint32_t grid,
                                 uint32_t shift, uint32_t bits, const uint64_t *cursors, hipStream_t s,
-                                const uint32_t *narrow, const uint64_t *part_start, const uint64_t *part_count) {
+                                const uint32_t *narrow, const uint64_t *part_start, const uint64_t *part_count,
+                                const uint8_t *side16) {
     if constexpr (sizeof(T) == 4) {
         if (sort2_enabled()) {
             const uint32_t *ik = static_cast<const uint32_t *>(in);
@@ -2016,13 +2116,18 @@ hipError_t launch_scatter_blk_t(const void *in, const uint64_t *list, void *out,
             // ends); k_sort_blk then returns at once for them (the width is known on the
             // device only)
             const bool place = narrow && part_start && part_count && m.seg_lb == nullptr && place_enabled();
+            if (side16 && !place) return hipErrorInvalidValue;  // a narrow pool is read by k_place_seg only
             const uint32_t skip = place ? 1u : 0u;
 #define SORT_CASE(B)                                                                                              \
     case B:                                                                                                       \
-        if (place)                                                                                                \
-            hipLaunchKernelGGL((k_place_seg<B, SGXAMD_PLACE_NT, SGXAMD_PLACE_U>), dim3(grid),                   \
-                               dim3(SGXAMD_PLACE_NT), 0, s, ik, list, reinterpret_cast<uint16_t *>(out), m, shift, \
-                               cursors, part_start, part_count, narrow);                                          \
+        if (place && side16)                                                                                      \
+            hipLaunchKernelGGL((k_place_seg<B, SGXAMD_PLACE_NT, SGXAMD_PLACE_U, true>), dim3(grid),             \
+                               dim3(SGXAMD_PLACE_NT), 0, s, ik, side16, list, reinterpret_cast<uint16_t *>(out), m, \
+                               shift, cursors, part_start, part_count, narrow);                                   \
+        else if (place)                                                                                           \
+            hipLaunchKernelGGL((k_place_seg<B, SGXAMD_PLACE_NT, SGXAMD_PLACE_U, false>), dim3(grid),            \
+                               dim3(SGXAMD_PLACE_NT), 0, s, ik, nullptr, list, reinterpret_cast<uint16_t *>(out), \
+                               m, shift, cursors, part_start, part_count, narrow);                                \
         hipLaunchKernelGGL((k_sort_blk<B, SGXAMD_SORT_NT, SGXAMD_SORT_ITEMS>), dim3(grid), dim3(SGXAMD_SORT_NT), 0, s, \
                            ik, list, ok, m, shift, cursors, narrow, skip);                                        \
         break;
@@ -2095,16 +2200,17 @@ hipError_t launch_scatter_keys(const row_t *in, uint32_t *out, const SegMap &m, 
 
 hipError_t launch_scatter_blk(const void *in, const uint64_t *list, void *out, uint32_t elem_size, const SegMap &m,
                               uint32_t grid, uint32_t shift, uint32_t bits, const uint64_t *cursors, hipStream_t s,
-                              const uint32_t *narrow, const uint64_t *part_start, const uint64_t *part_count) {
+                              const uint32_t *narrow, const uint64_t *part_start, const uint64_t *part_count,
+                              const uint8_t *side16) {
     if (grid == 0) return hipSuccess;
     // narrow residuals: key partitions through k_sort_blk / k_place_seg only
     if (narrow && !(elem_size == 4 && sort2_enabled())) return hipErrorInvalidValue;
     if (elem_size == 8)
         return launch_scatter_blk_t<uint64_t>(in, list, out, m, grid, shift, bits, cursors, s, nullptr, nullptr,
-                                              nullptr);
+                                              nullptr, nullptr);
     if (elem_size == 4)
         return launch_scatter_blk_t<uint32_t>(in, list, out, m, grid, shift, bits, cursors, s, narrow, part_start,
-                                              part_count);
+                                              part_count, side16);
     return hipErrorInvalidValue;
 }
 
@@ -2115,9 +2221,11 @@ __global__ __launch_bounds__(1024) void k_pool_layout(const uint64_t *__restrict
                                                       uint64_t *__restrict__ start, uint64_t *__restrict__ count,
                                                       uint64_t *__restrict__ lbase, uint64_t *__restrict__ lcount,
                                                       uint32_t *__restrict__ seg_base, uint32_t chain_nseg,
-                                                      uint32_t chain_mode, uint32_t *__restrict__ kmax) {
+                                                      uint32_t chain_mode, uint32_t *__restrict__ kmax,
+                                                      const uint32_t *__restrict__ guard, uint32_t gshift) {
     __shared__ uint64_t scratch[1024 / kWave + 1];
     __shared__ uint32_t kmax_all;
+    if (guard && ((*guard >> gshift) >> 16) == 0) return;
     const uint32_t d = threadIdx.x;
     if (d == 0) kmax_all = 0;
     const uint64_t v = d < F ? totals[d] : 0;
@@ -2149,14 +2257,14 @@ __global__ __launch_bounds__(1024) void k_pool_layout(const uint64_t *__restrict
 
 hipError_t launch_pool_layout(uint64_t *cnt, uint32_t nseg, uint32_t bits, uint64_t *totals, uint64_t *start,
                               uint64_t *count, uint64_t *lbase, uint64_t *lcount, uint32_t *seg_base, hipStream_t s,
-                              uint32_t chain_mode, uint32_t *kmax) {
+                              uint32_t chain_mode, uint32_t *kmax, const uint32_t *guard, uint32_t gshift) {
     const uint32_t F = 1u << bits;
-    hipLaunchKernelGGL(k_scan_cols, dim3(F), dim3(kBlock), 0, s, cnt, nseg, totals);
+    hipLaunchKernelGGL(k_scan_cols, dim3(F), dim3(kBlock), 0, s, cnt, nseg, totals, guard, gshift);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const uint32_t threads = F < 64 ? 64 : F;
     hipLaunchKernelGGL(k_pool_layout, dim3(1), dim3(threads), 0, s, totals, F, start, count, lbase, lcount, seg_base,
-                       nseg, chain_mode, kmax);
+                       nseg, chain_mode, kmax, guard, gshift);
     return hipGetLastError();
 }
 
@@ -2167,6 +2275,7 @@ __global__ __launch_bounds__(kBlock) void k_block_list(PoolOut po, const uint64_
                                                        uint64_t *__restrict__ list, uint32_t F) {
     __shared__ uint32_t rank[kMaxF];
     __shared__ uint64_t pre[kMaxF];  // the segment's first list position per digit
+    if (pool_guard_skip(po)) return;
     const uint32_t g = blockIdx.x;
     for (uint32_t d = threadIdx.x; d < F; d += kBlock) {
         rank[d] = 0;

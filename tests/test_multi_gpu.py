@@ -78,7 +78,7 @@ def test_keys_only_exchange(sgx, orc, gpu, g, n, kw):
     res = multi(sgx, R, S, g, **kw)
     assert res.matches == exp
     st = res.stats
-    assert st["elem_bytes"] == 4 and st["local"]["layout"] in (2, 3)
+    assert st["elem_bytes"] == 4 and st["local"]["layout"] in (2, 3, 4)
     # every key of a rank except those it keeps goes out once, 4 bytes each
     assert 4 * (2 * n) * (g - 1) // g * 0.9 < st["sent_bytes"] <= 4 * 2 * n
     # RHT counts over key partitions too (SGXAMD_KEYS=0 in test_paths_gpu keeps tuples)
@@ -170,6 +170,51 @@ def test_rccl_comm_single_rank(sgx, orc, gpu):
         sgx.multi_comm_destroy(h)
 
 
+def sorted_triples(t):
+    t = np.asarray(t, dtype=np.uint32).reshape(-1, 3)
+    return t[np.lexsort((t[:, 2], t[:, 1], t[:, 0]))]
+
+
+def materialize_cases(sgx):
+    rng = np.random.default_rng(17)
+    dt = np.dtype([("key", "<u4"), ("payload", "<u4")])
+    R1, S1 = sgx.reference_relations(1 << 16, 1 << 16, selectivity=50)
+    R2 = np.empty(30_000, dtype=dt)
+    R2["key"] = rng.integers(0, 5000, len(R2))
+    R2["payload"] = np.arange(len(R2))
+    S2 = np.empty(40_003, dtype=dt)
+    S2["key"] = rng.integers(0, 5000, len(S2))
+    S2["payload"] = np.arange(len(S2)) + 7
+    return [(R1, S1), (R2, S2)]
+
+
+@pytest.mark.parametrize("g", [2, 4, 8])
+def test_materialize_multi_matches_oracle(sgx, orc, gpu, g):
+    """Multi-GPU MATERIALIZE (radix_join.cpp:437-446): tuples (with their payloads) on the
+    wire, every rank's triples concatenated into the caller's buffer: the same multiset
+    of {key, R payload, S payload} as the oracle's restated RHO; too small a buffer is a
+    capacity error that reports the triples needed."""
+    import torch
+
+    for R, S in materialize_cases(sgx):
+        exp = orc.rho_join_triples(R, S, 4)
+        out = np.zeros((len(exp) + 3, 3), dtype=np.uint32)
+        res = multi(sgx, R, S, g, out=out, out_capacity=len(out))
+        assert res.matches == len(exp)
+        assert res.stats["elem_bytes"] == 8  # the payloads travel
+        assert np.array_equal(sorted_triples(out[:len(exp)]), sorted_triples(exp))
+        with pytest.raises(sgx.Mi355Error, match=f"{len(exp)} triples needed"):
+            multi(sgx, R, S, g, out=out, out_capacity=len(exp) - 1)
+    # device output, device-resident inputs
+    R, S = materialize_cases(sgx)[0]
+    exp = orc.rho_join_triples(R, S, 4)
+    dR = torch.from_numpy(R.view(np.int64)).to(gpu)
+    dS = torch.from_numpy(S.view(np.int64)).to(gpu)
+    dout = torch.zeros((len(exp), 3), dtype=torch.int32, device=gpu)
+    assert multi(sgx, dR, S=dS, g=g, out=dout, out_capacity=len(exp)).matches == len(exp)
+    assert np.array_equal(sorted_triples(dout.cpu().numpy().view(np.uint32)), sorted_triples(exp))
+
+
 def test_rccl_single_rank_local_failure_keeps_handle(sgx, orc, gpu):
     """A world of one has no collective to leave: a local failure (injected at the local
     join) returns that error and leaves the communicator usable, so the next sharded
@@ -243,7 +288,7 @@ def test_config4_rehearsal_full_size(sgx, gpu):
         res = sgx.rho_join_multi(R, nR, S, nS, g, transport="rehearsal")
         st = res.stats
         assert res.matches == nS
-        assert st["world"] == g and st["elem_bytes"] == 4 and st["local"]["layout"] in (2, 3)
+        assert st["world"] == g and st["elem_bytes"] == 4 and st["local"]["layout"] in (2, 3, 4)
         assert st["recv_r_max"] == st["recv_r_min"] == nR // g
         assert st["recv_s_max"] == st["recv_s_min"] == nS // g
         sent = _slices_sent(R & 0xFFFFFFFF, g, 4) + _slices_sent(S & 0xFFFFFFFF, g, 4)

@@ -105,3 +105,39 @@ def test_narrow_partitions_match_oracle(sgx, orc, gpu, case):
     rht = sgx.rho_join(R, len(R), S, len(S), radix_bits=BITS, passes=2, algorithm="RHT")
     assert rht.matches == exp and rht.stats["narrow"] == 0
 
+
+NARROW_POOL_CHILD = r"""
+import sys
+import numpy as np
+import sgxamd, oracle
+sys.path.insert(0, sys.argv[1])
+import test_narrow_gpu as T
+for i, case in enumerate(T.CASES):
+    Rk, Sk, narrow = T.case_relations(case, np.random.default_rng(40 + i))
+    R, S = T.rel(Rk), T.rel(Sk)
+    res = sgxamd.rho_join(R, len(R), S, len(S), radix_bits=T.BITS, passes=2)
+    assert res.stats["narrow"] == narrow and res.stats["layout"] == 4, (case, res.stats["narrow"], res.stats["layout"])
+    assert res.matches == oracle.count_join_sort(R, S), case
+print("narrow pool ok")
+"""
+
+
+def test_narrow_pool_matches_oracle():
+    """SGXAMD_NARROW_POOL=1 (opt-in): pass 1 writes the narrow pool (16-bit residuals and
+    their digit bytes), k_place_seg reads it; a relation with a residual past 16 bits
+    (wide_s, wide_r, wide) repeats pass 1 as 4-byte keys behind the guards.  Every case
+    above, in a child process (the switch is read once per process)."""
+    import os
+    import subprocess
+    import sys
+
+    from conftest import PKG, ROOT
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    e = dict(os.environ, SGXAMD_NARROW_POOL="1")
+    e["PYTHONPATH"] = os.pathsep.join([os.path.join(PKG, "python"), os.path.join(ROOT, "oracle"), here,
+                                       e.get("PYTHONPATH", "")])
+    r = subprocess.run([sys.executable, "-c", NARROW_POOL_CHILD, here], env=e, capture_output=True, text=True,
+                       timeout=110)
+    assert r.returncode == 0 and "narrow pool ok" in r.stdout, (r.stdout[-2000:], r.stderr[-2000:])
+

@@ -15,7 +15,8 @@ SGXAMD_NARROW=0 (key partitions stay 4-byte keys where u16 residuals would fit),
 SGXAMD_JOIN_N=0 (narrow relations' build/probe in k_join_x's direct table, one
 workgroup per CU, instead of k_join_n, one task per workgroup), SGXAMD_PLACE=0 (narrow
 relations' pass 2 as k_sort_blk's tile sort instead of k_place_seg's segment
-placement).  The switches are read
+placement), SGXAMD_NARROW_POOL=1 (narrow plans' pass 1 writes the narrow pool of 16-bit
+residuals and their digits instead of 4-byte keys; opt-in).  The switches are read
 once per process, so each setting runs in a child process against the oracle (the
 TPC-H selections ride along: they share the library's workspace)."""
 import os
@@ -83,7 +84,7 @@ print("paths ok")
                                  {"SGXAMD_DIGIT_SIDE": "1", "SGXAMD_BIG_JOIN": "1"},
                                  {"SGXAMD_SMALL_JOIN": "0"},
                                  {"SGXAMD_POOL": "0"}, {"SGXAMD_POOL_SEGS": "3"}, {"SGXAMD_POOL_SEGS": "100000"},
-                                 {"SGXAMD_KEYS": "0"}, {"SGXAMD_SORT2": "0"}, {"SGXAMD_NARROW": "0"}, {"SGXAMD_JOIN_N": "0"}, {"SGXAMD_PLACE": "0"}, {"SGXAMD_CHAIN_HIST": "1"},
+                                 {"SGXAMD_KEYS": "0"}, {"SGXAMD_SORT2": "0"}, {"SGXAMD_NARROW": "0"}, {"SGXAMD_JOIN_N": "0"}, {"SGXAMD_PLACE": "0"}, {"SGXAMD_NARROW_POOL": "1"}, {"SGXAMD_CHAIN_HIST": "1"},
                                  {"SGXAMD_CHAIN_HIST": "1", "SGXAMD_CHAIN_SLOTS": "1"}])
 def test_switch_paths_match_oracle(env):
     e = dict(os.environ, **env)

@@ -116,6 +116,20 @@ def test_inprocess_transport_failure(sgx, orc, dbl):
     assert multi(sgx, R, S, 4).matches == exp
 
 
+@pytest.mark.parametrize("g", [2, 4, 8])
+def test_inprocess_materialize(sgx, orc, dbl, g):
+    """Multi-GPU MATERIALIZE through RcclTransport (tuples with payloads as ncclUint64 on
+    the wire): the ranks' triples equal the oracle's as a multiset."""
+    from test_multi_gpu import materialize_cases, sorted_triples
+
+    for R, S in materialize_cases(sgx):
+        exp = orc.rho_join_triples(R, S, 4)
+        out = np.zeros((len(exp), 3), dtype=np.uint32)
+        res = multi(sgx, R, S, g, out=out, out_capacity=len(out))
+        assert res.matches == len(exp) and res.stats["transport"] == "rccl"
+        assert np.array_equal(sorted_triples(out), sorted_triples(exp))
+
+
 def test_inprocess_config4_full_size(sgx, dbl, gpu):
     """BASELINE config 4 at its size over 8 RCCL ranks (the double on one GPU): pk(2^27)
     join fk(2^30): matches == 2^30, 4-byte keys as ncclUint32 on the wire, exactly 2^24 R
@@ -152,7 +166,7 @@ def test_inprocess_config4_full_size(sgx, dbl, gpu):
 
 
 # ---------------------------------------------------------------- one "process" per GPU
-def sharded(sgx, R, S, g, *, handles=None, algorithm="RHO", timeout=120):
+def sharded(sgx, R, S, g, *, handles=None, algorithm="RHO", timeout=120, outs=None):
     """Rank r's slice of the device tensors R and S (radix_join.cpp:1488-1499 slicing)
     joined by G threads, each standing for one process with its own communicator
     (created here unless `handles` are given).  Returns (results, errors, handles)."""
@@ -172,7 +186,9 @@ def sharded(sgx, R, S, g, *, handles=None, algorithm="RHO", timeout=120):
                 handles[r] = sgx.multi_comm_init(uid, g, r)
             ra, rb = r * (nR // g), (nR if r == g - 1 else (r + 1) * (nR // g))
             sa, sb = r * (nS // g), (nS if r == g - 1 else (r + 1) * (nS // g))
-            res[r] = sgx.rho_join_sharded(handles[r], R[ra:rb], rb - ra, S[sa:sb], sb - sa, algorithm=algorithm)
+            kw = {} if outs is None else {"out": outs[r], "out_capacity": outs[r].shape[0]}
+            res[r] = sgx.rho_join_sharded(handles[r], R[ra:rb], rb - ra, S[sa:sb], sb - sa, algorithm=algorithm,
+                                          **kw)
         except Exception as e:  # noqa: BLE001 - every rank's outcome is checked by the caller
             errs[r] = e
 
@@ -189,6 +205,31 @@ def destroy(sgx, handles):
     for h in handles:
         if h:
             sgx.multi_comm_destroy(h)
+
+
+@pytest.mark.parametrize("g", [2, 4, 8])
+def test_sharded_materialize_chunks(sgx, orc, dbl, gpu, g):
+    """One process per GPU, MATERIALIZE: every rank writes its own output chunk (its
+    local_matches triples, device memory); the chunks together equal the oracle's
+    triples as a multiset and their sizes add up to the global count."""
+    import torch
+
+    from test_multi_gpu import materialize_cases, sorted_triples
+
+    R, S = materialize_cases(sgx)[1]
+    exp = orc.rho_join_triples(R, S, 4)
+    dR = torch.from_numpy(R.view(np.int64)).to(gpu)
+    dS = torch.from_numpy(S.view(np.int64)).to(gpu)
+    outs = [torch.zeros((len(exp), 3), dtype=torch.int32, device=gpu) for _ in range(g)]
+    res, errs, handles = sharded(sgx, dR, dS, g, outs=outs)
+    try:
+        assert errs == [None] * g, errs
+        loc = [r.stats["local_matches"] for r in res]
+        assert all(r.matches == len(exp) for r in res) and sum(loc) == len(exp)
+        got = np.concatenate([o[:n].cpu().numpy().view(np.uint32) for o, n in zip(outs, loc)])
+        assert np.array_equal(sorted_triples(got), sorted_triples(exp))
+    finally:
+        destroy(sgx, handles)
 
 
 @pytest.mark.parametrize("g", [2, 4, 8])
