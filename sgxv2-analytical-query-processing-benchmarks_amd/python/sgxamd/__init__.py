@@ -419,13 +419,18 @@ TRANSPORTS = {"auto": 0, "rccl": 1, "rehearsal": 2}  # MI355_TRANSPORT_*
 
 
 def rho_join_multi(R, nR: int, S, nS: int, ngpus: int, *, transport: str = "auto", algorithm: str = "RHO",
-                   radix_bits: int = 0, passes: int = 0) -> JoinResult:
-    """Multi-GPU count join in one process (mi355_rho_join_multi_ex): ngpus ranks, the
-    radix-shard exchange over RCCL or the one-GPU rehearsal transport."""
-    o = rho_opts(radix_bits, passes, 0, 0, 0, ALGORITHMS[algorithm], None, None, 0)
+                   radix_bits: int = 0, passes: int = 0, out=None, out_capacity: int = 0) -> JoinResult:
+    """Multi-GPU join in one process (mi355_rho_join_multi_ex): ngpus ranks, the
+    radix-shard exchange over RCCL or the one-GPU rehearsal transport.  With `out`
+    (host or device buffer of out_capacity 12-byte triples) the join materialises:
+    every rank's triples, rank 0's first."""
+    o = rho_opts(radix_bits, passes, 0, 1 if out is not None else 0, 0, ALGORITHMS[algorithm], None,
+                 ptr(out) if out is not None else None, out_capacity)
     st = multi_stats()
-    _check(lib.mi355_rho_join_multi_ex(ptr(R), nR, ptr(S), nS, ngpus, TRANSPORTS[transport], C.byref(o),
-                                       C.byref(st)))
+    rc = lib.mi355_rho_join_multi_ex(ptr(R), nR, ptr(S), nS, ngpus, TRANSPORTS[transport], C.byref(o), C.byref(st))
+    if rc == -5:  # MI355_ERR_CAPACITY
+        raise Mi355Error(rc, f"capacity: {int(st.matches)} triples needed")
+    _check(rc)
     return JoinResult(int(st.matches), st)
 
 
@@ -448,9 +453,13 @@ def multi_comm_destroy(handle: int) -> None:
     _check(lib.mi355_multi_comm_destroy(handle))
 
 
-def rho_join_sharded(handle: int, R, nR: int, S, nS: int, *, algorithm: str = "RHO") -> JoinResult:
-    """One rank's part of the multi-GPU count join (collective; device-resident slices)."""
-    o = rho_opts(0, 0, 0, 0, 0, ALGORITHMS[algorithm], None, None, 0)
+def rho_join_sharded(handle: int, R, nR: int, S, nS: int, *, algorithm: str = "RHO", out=None,
+                     out_capacity: int = 0) -> JoinResult:
+    """One rank's part of the multi-GPU join (collective; device-resident slices).  With
+    `out` the join materialises and this rank's own triples (stats["local_matches"] of
+    them) are written to it."""
+    o = rho_opts(0, 0, 0, 1 if out is not None else 0, 0, ALGORITHMS[algorithm], None,
+                 ptr(out) if out is not None else None, out_capacity)
     st = multi_stats()
     _check(lib.mi355_rho_join_sharded(handle, ptr(R), nR, ptr(S), nS, C.byref(o), C.byref(st)))
     return JoinResult(int(st.matches), st)
