@@ -993,15 +993,20 @@ int join_small(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const 
     uint64_t *startR = A.at<uint64_t>(pj.pr.start1), *cntR = A.at<uint64_t>(pj.pr.cnt1);
     uint64_t *startS = A.at<uint64_t>(pj.ps.start1), *cntS = A.at<uint64_t>(pj.ps.cnt1);
     row_t *oR = ctx->t1R.as<row_t>(), *oS = ctx->t1S.as<row_t>();
+    // the digit totals alternate between two sets per call (each call's scatter zeroes
+    // the set the next call's histograms add into)
+    const uint32_t par = ctx->small_parity;
+    ctx->small_parity ^= 1u;
     tm.mark("RS_pass1_hist");
-    RHO_HIP(launch_hist_pair(dR, mR, pj.pr.nseg1, dS, mS, pj.ps.nseg1, pj.key_shift, pol.b1, offsR, offsS, startR, cntR,
-                             startS, cntS, sync, over, pj.over_cap, result + 1, pj.s_chunk, s));
+    RHO_HIP(launch_hist_pair(dR, mR, pj.pr.nseg1, dS, mS, pj.ps.nseg1, pj.key_shift, pol.b1, offsR, offsS,
+                             sync + sync_tot(par, 0), sync + sync_tot(par, 1), sync + kSyncT0, s));
     tm.mark("RS_pass1_scatter");
     // cursors: each segment's offset inside its copy of the digit totals + that copy's
-    // digit start (sync words written by k_hist_pair's last segment of each relation)
-    RHO_HIP(launch_scatter_pair(dR, oR, mR, 2 * pj.pr.nseg1, offsR, sync + kSyncStartR, dS, oS, mS, 2 * pj.ps.nseg1,
-                                offsS, sync + kSyncStartS,
-                                pj.key_shift, pol.b1, s));
+    // digit start (each scatter workgroup scans the totals itself)
+    RHO_HIP(launch_scatter_pair(dR, oR, mR, 2 * pj.pr.nseg1, offsR, sync + sync_tot(par, 0), sync + sync_tot(par ^ 1, 0),
+                                startR, cntR, dS, oS, mS, 2 * pj.ps.nseg1, offsS, sync + sync_tot(par, 1),
+                                sync + sync_tot(par ^ 1, 1), startS, cntS, pj.key_shift, pol.b1, over, pj.over_cap,
+                                result + 1, pj.s_chunk, s));
     tm.mark("join_build_probe");
     const uint64_t P = 1ull << pol.bits;
     const JoinReduce red{result, sync + kSyncTicketJoin};

@@ -52,10 +52,11 @@ hipError_t launch_scan_regions(uint64_t *hist, const uint32_t *seg_base, const u
                                uint32_t nreg, uint32_t bits, uint64_t *part_start, uint64_t *part_count,
                                hipStream_t s);
 
-// Context::sync (u64 words, zero when allocated, left zero by every kernel that uses
-// them): the tickets and digit totals of the in-launch hand-offs of the one-launch
-// histogram (launch_hist_pair) and of the build/probe count reduction.
-constexpr uint32_t kSyncTicketR = 0, kSyncTicketS = 1, kSyncTicket2 = 2, kSyncTicketJoin = 3;
+// Context::sync (u64 words, zero when allocated): the digit totals of the small join's
+// histograms (launch_hist_pair), in two sets that alternate per call (the scatter of a
+// call zeroes the other set), and the ticket of the build/probe count reduction (left
+// zero by the kernel that takes it).
+constexpr uint32_t kSyncTicketJoin = 3;
 // sync[kSyncTicketJoin + 1] holds the device address of the context's mapped host
 // result block (set once, never written by a kernel): the small join's last
 // workgroup stores the six result words there, then the device span of the call
@@ -67,41 +68,44 @@ constexpr uint32_t kHostJoinSpan = 6, kHostJoinDone = 7, kHostJoinWords = 8;
 // Hand-offs spread over kSyncSpread groups of workgroups (segment or workgroup index mod
 // kSyncSpread), so that no device-scope atomic address takes more than 1/kSyncSpread of
 // the grid's updates: the digit totals are kSyncSpread copies [c][kMaxF] (a segment's
-// offset is its place inside its copy; the copies' digit starts [c][kMaxF] add the
-// copies before it), and a ticket of n arrivals is kSyncSpread sub-tickets
-// (sync[ticket + kSyncSub + kNumTickets * c]) whose last arrivers take the ticket itself.
-// Default 1 (no spreading): 8 groups measured no faster, 56.7 vs 55.7 us per 2^20 join
-// (r04l; the small path is latency-bound, not atomic-bound).  SGXAMD_SMALL_SPREAD=8 builds.
+// offset is its place inside its copy; its cursor base adds the copies before it), and a
+// ticket of n arrivals is kSyncSpread sub-tickets (sync[ticket + kSyncSub + kNumTickets *
+// c]) whose last arrivers take the ticket itself.  Default 1 (no spreading): 8 groups
+// measured no faster, 56.7 vs 55.7 us per 2^20 join (r04l; the small path is
+// latency-bound, not atomic-bound).  SGXAMD_SMALL_SPREAD=8 builds.
 #ifndef SGXAMD_SMALL_SPREAD
 #define SGXAMD_SMALL_SPREAD 1
 #endif
 constexpr uint32_t kSyncSpread = SGXAMD_SMALL_SPREAD, kNumTickets = 4;
-constexpr uint32_t kSyncTotR = 8, kSyncTotS = kSyncTotR + kSyncSpread * kMaxF;
-constexpr uint32_t kSyncSub = kSyncTotS + kSyncSpread * kMaxF;  // relative to a ticket's word
-constexpr uint32_t kSyncStartR = kSyncSub + kNumTickets * kSyncSpread, kSyncStartS = kSyncStartR + kSyncSpread * kMaxF;
-constexpr uint32_t kSyncWords = kSyncStartS + kSyncSpread * kMaxF;
+constexpr uint32_t kSyncTot0 = 8, kSyncTotWords = kSyncSpread * kMaxF;
+// totals set `parity` (0 / 1) of relation rel (0 R, 1 S)
+constexpr uint32_t sync_tot(uint32_t parity, uint32_t rel) { return kSyncTot0 + (2 * parity + rel) * kSyncTotWords; }
+constexpr uint32_t kSyncSub = kSyncTot0 + 4 * kSyncTotWords;  // relative to a ticket's word
+constexpr uint32_t kSyncWords = kSyncSub + kNumTickets * (kSyncSpread + 1);
 // Development: small-join workgroup stamps (rho_kernels.hip dbg_stamp), 3 kernels + the
 // build/probe reduction x 3
 // stamps x kStampWgs u64; null turns them off.
 constexpr uint32_t kStampWgs = 1024;
 hipError_t set_debug_stamps(uint64_t *p);
 
-// Small one-pass joins: histograms of R and S, digit starts / counts and the build/probe
-// task list (meta as launch_make_tasks) in one launch.  gridR / gridS workgroups each
-// take two segments of mR / mS (2g, 2g + 1; the scatter's segments).  offs: [d][2 grid]
-// segment offsets
-// inside the segment's copy (g mod kSyncSpread) of digit d's total; the copies' digit
-// starts land in sync[kSyncStartR / kSyncStartS] (the bases of launch_scatter_pair).
+// Small one-pass joins: histograms of R and S in one launch (gridR / gridS workgroups
+// each take two segments of mR / mS, 2g and 2g + 1: the scatter's segments).  offs:
+// [d][2 grid] segment offsets inside the segment's copy (g mod kSyncSpread) of digit d's
+// total in tot (sync_tot of this call's parity, zero at entry).  t0: the call's start
+// (sync[kSyncT0]).
 hipError_t launch_hist_pair(const row_t *R, const SegMap &mR, uint32_t gridR, const row_t *S, const SegMap &mS,
                             uint32_t gridS, uint32_t shift, uint32_t bits, uint64_t *offsR, uint64_t *offsS,
-                            uint64_t *startR, uint64_t *cntR, uint64_t *startS, uint64_t *cntS, uint64_t *sync,
-                            uint64_t *over, uint32_t over_cap, uint64_t *meta, uint64_t s_chunk, hipStream_t s);
-// Both relations' one-pass scatters in one launch (digit-major cursors + the digit starts
-// of each segment's totals copy, cstart [kSyncSpread][kMaxF]).
+                            uint64_t *totR, uint64_t *totS, uint64_t *t0, hipStream_t s);
+// Both relations' one-pass scatters in one launch (cursors: the segment offsets + the
+// digit starts of the segment's totals copy, taken by each workgroup from tot), plus one
+// workgroup that writes the partition table (start / cnt), the task list (over, meta as
+// launch_make_tasks) and zeroes the other totals set (tot_next) for the next call.
 hipError_t launch_scatter_pair(const row_t *R, row_t *outR, const SegMap &mR, uint32_t gridR, const uint64_t *offsR,
-                               const uint64_t *cstartR, const row_t *S, row_t *outS, const SegMap &mS, uint32_t gridS,
-                               const uint64_t *offsS, const uint64_t *cstartS, uint32_t shift, uint32_t bits,
-                               hipStream_t s);
+                               const uint64_t *totR, uint64_t *totR_next, uint64_t *startR, uint64_t *cntR,
+                               const row_t *S, row_t *outS, const SegMap &mS, uint32_t gridS, const uint64_t *offsS,
+                               const uint64_t *totS, uint64_t *totS_next, uint64_t *startS, uint64_t *cntS,
+                               uint32_t shift, uint32_t bits, uint64_t *over, uint32_t over_cap, uint64_t *meta,
+                               uint64_t s_chunk, hipStream_t s);
 
 // Digit side stream of a two-pass partition: the pass-1 scatter also writes, for the
 // tuple it stores at position a of its output, the tuple's pass-2 digit

@@ -244,41 +244,34 @@ __device__ __forceinline__ void st_agent(uint64_t *p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// ----------------------------------------- one-launch histogram + digit layout ---
-// For small one-pass joins: the histograms of R and S, the digit layout and the
-// build/probe task list in ONE launch instead of hist / scan_cols / scan_digits per
-// relation plus make_tasks.  Segment g of a relation adds its digit counts to the
-// relation's digit totals with one device atomic per digit; the value returned is
-// the segment's offset inside the digit (segments take their places in arrival order;
-// the join count does not depend on the order inside a partition).  The relation's
-// last segment turns the totals into digit starts (the scan of radix_join.cpp:901-914);
-// the last of the two relations then builds the task list (k_make_tasks's rule).
+// ----------------------------------------- one-launch histogram (small joins) ---
+// For small one-pass joins: the histograms of R and S in ONE launch.  Segment g of a
+// relation adds its digit counts to the relation's digit totals (this call's set, see
+// launch_scatter_pair) with one device atomic per digit; the value returned is the
+// segment's offset inside the digit (segments take their places in arrival order; the
+// join count does not depend on the order inside a partition).  Nothing else: the digit
+// starts (the scan of radix_join.cpp:901-914) are taken by the scatter's workgroups
+// themselves, each for its own cursors, and the partition table and task list by one
+// extra workgroup of the scatter -- no hand-off at the end of this launch (round 4 ran a
+// relation ticket, the digit scan, a second ticket and the task list serially at its
+// end: 12 of its 20 us, r04v stamps).
 struct HistPairRel {
     const uint32_t *in;   // tuples as u32 words
     SegMap m;
     uint32_t grid;        // segments of the relation
     uint32_t shift;
     uint64_t *offs;       // [d][g] (stride grid): segment g's offset inside its copy of digit d
-    uint64_t *tot;        // [kSyncSpread][kMaxF] digit totals, zero at entry (reset by the last segment)
-    uint64_t *start;      // F digit starts
-    uint64_t *cnt;        // F digit counts
-    uint64_t *ticket;
-    uint64_t *cstart;     // [kSyncSpread][kMaxF]: digit starts of each copy's segments (the scatter's bases)
+    uint64_t *tot;        // [kSyncSpread][kMaxF] digit totals, zero at entry
 };
 
 __global__ __launch_bounds__(kBlock) void k_hist_pair(HistPairRel A, HistPairRel B, uint32_t bits,
-                                                      uint64_t *__restrict__ ticket2, uint64_t *__restrict__ over,
-                                                      uint32_t over_cap, uint64_t *__restrict__ meta,
-                                                      uint64_t s_chunk) {
+                                                      uint64_t *__restrict__ t0) {
     __shared__ uint32_t h[kMaxF], h2[kMaxF];
-    __shared__ uint64_t scratch[kWaves + 1];
-    __shared__ uint32_t flag;
     const bool isB = blockIdx.x >= A.grid;
     const HistPairRel &H = isB ? B : A;
     const uint32_t g = isB ? blockIdx.x - A.grid : blockIdx.x;  // segment g = scatter segments 2g, 2g + 1
     const uint32_t F = 1u << bits;
-    if (blockIdx.x == 0 && threadIdx.x == 0)  // the call's start (small-join device span)
-        ticket2[kSyncT0 - kSyncTicket2] = wall_clock64();
+    if (blockIdx.x == 0 && threadIdx.x == 0) *t0 = wall_clock64();  // the call's start (small-join device span)
     dbg_stamp(0, 0);
     // segment g is two scatter segments (H.m's, halves 2g and 2g + 1: one tile each, so
     // that the scatter's workgroups each load, sort and write one tile): one histogram
@@ -293,66 +286,14 @@ __global__ __launch_bounds__(kBlock) void k_hist_pair(HistPairRel A, HistPairRel
         H.offs[(uint64_t)d * 2 * H.grid + 2 * g + 1] = off + a;
     }
     dbg_stamp(0, 1);
-    if (!arrive_last_spread(H.ticket, H.grid, g, &flag)) return;
-    // the relation's last segment: digit starts and counts, and each copy's bases
-    uint64_t carry = 0;
-    for (uint32_t d0 = 0; d0 < F; d0 += kBlock) {
-        const uint32_t d = d0 + threadIdx.x;
-        uint64_t v = 0, part[kSyncSpread];
-#pragma unroll
-        for (uint32_t c = 0; c < kSyncSpread; ++c) {
-            part[c] = d < F ? ld_agent(&H.tot[(uint64_t)c * kMaxF + d]) : 0ull;
-            v += part[c];
-        }
-        uint64_t tot;
-        const uint64_t ex = block_excl_scan_u64(v, scratch, &tot);
-        if (d < F) {
-            H.start[d] = carry + ex;
-            H.cnt[d] = v;
-            uint64_t b = carry + ex;
-#pragma unroll
-            for (uint32_t c = 0; c < kSyncSpread; ++c) {
-                H.cstart[(uint64_t)c * kMaxF + d] = b;
-                b += part[c];
-                st_agent(&H.tot[(uint64_t)c * kMaxF + d], 0ull);
-            }
-        }
-        carry += tot;
-    }
-    if (!arrive_last(ticket2, 2, &flag)) return;
-    // the last of the two relations: build/probe tasks over P = F partitions (A = R, B = S)
-    uint64_t base = 0, mr = 0, ms = 0;
-    for (uint32_t p0 = 0; p0 < F; p0 += kBlock) {
-        const uint32_t p = p0 + threadIdx.x;
-        const uint64_t nR = p < F ? A.cnt[p] : 0, nS = p < F ? B.cnt[p] : 0;
-        mr = nR > mr ? nR : mr;
-        ms = nS > ms ? nS : ms;
-        const uint64_t k = (nR == 0 || nS <= s_chunk) ? 0 : (nS + s_chunk - 1) / s_chunk - 1;
-        uint64_t tot;
-        const uint64_t ex = base + block_excl_scan_u64(k, scratch, &tot);
-        for (uint64_t j = 0; j < k && ex + j < over_cap; ++j) over[ex + j] = p | ((j + 1) << 32);
-        base += tot;
-    }
-    mr = block_max_u64(mr, scratch);
-    ms = block_max_u64(ms, scratch);
-    if (threadIdx.x == 0) {
-        meta[0] = mr;
-        meta[1] = ms;
-        meta[2] = base;  // n_over (u32, low word; the high word is 0)
-    }
-    dbg_stamp(0, 2);
 }
 
 hipError_t launch_hist_pair(const row_t *R, const SegMap &mR, uint32_t gridR, const row_t *S, const SegMap &mS,
                             uint32_t gridS, uint32_t shift, uint32_t bits, uint64_t *offsR, uint64_t *offsS,
-                            uint64_t *startR, uint64_t *cntR, uint64_t *startS, uint64_t *cntS, uint64_t *sync,
-                            uint64_t *over, uint32_t over_cap, uint64_t *meta, uint64_t s_chunk, hipStream_t s) {
-    const HistPairRel A{reinterpret_cast<const uint32_t *>(R), mR, gridR, shift, offsR, sync + kSyncTotR, startR,
-                        cntR, sync + kSyncTicketR, sync + kSyncStartR};
-    const HistPairRel B{reinterpret_cast<const uint32_t *>(S), mS, gridS, shift, offsS, sync + kSyncTotS, startS,
-                        cntS, sync + kSyncTicketS, sync + kSyncStartS};
-    hipLaunchKernelGGL(k_hist_pair, dim3(gridR + gridS), dim3(kBlock), 0, s, A, B, bits, sync + kSyncTicket2, over,
-                       over_cap, meta, s_chunk);
+                            uint64_t *totR, uint64_t *totS, uint64_t *t0, hipStream_t s) {
+    const HistPairRel A{reinterpret_cast<const uint32_t *>(R), mR, gridR, shift, offsR, totR};
+    const HistPairRel B{reinterpret_cast<const uint32_t *>(S), mS, gridS, shift, offsS, totS};
+    hipLaunchKernelGGL(k_hist_pair, dim3(gridR + gridS), dim3(kBlock), 0, s, A, B, bits, t0);
     return hipGetLastError();
 }
 
@@ -1228,44 +1169,122 @@ __global__ __launch_bounds__(NT, (scatter_waves_per_simd<BITS, ITEMS, NT>())) vo
 }
 
 // Both relations' one-pass scatters in one launch (small joins): workgroups
-// [0, gridR) take R's segments, the rest S's; cursors = the digit-major segment
-// offsets of k_hist_pair plus the digit starts.
+// [0, gridR) take R's segments, [gridR, gridR + gridS) S's, and the last one lays out the
+// partitions.  A scatter workgroup first takes its cursor bases itself -- the digit starts
+// of its segment's totals copy (an exclusive scan over the digits of this call's totals,
+// complete since k_hist_pair's launch ended) -- so no workgroup waits on another.  The
+// layout workgroup writes both relations' partition starts / counts and largest
+// partitions, the build/probe task list (k_make_tasks's rule: the further S chunks of
+// partitions above s_chunk), and zeroes the other set of totals, which the next call's
+// histograms add into (the totals alternate between two sets per call: the scatters
+// still read this call's set).
 struct ScatterPairRel {
     const uint64_t *in;
     uint64_t *out;
     SegMap m;
     uint32_t grid;
     const uint64_t *offs;
-    const uint64_t *cstart;  // [kSyncSpread][kMaxF]: digit starts of each totals copy (k_hist_pair)
+    const uint64_t *tot;  // [kSyncSpread][kMaxF]: this call's digit totals (k_hist_pair)
+    uint64_t *tot_next;   // the other set, zeroed for the next call
+    uint64_t *start, *cnt;  // partition starts / counts (the build/probe's table)
 };
+
+// Digit totals of a relation, start[d] = the exclusive scan (F <= kMaxF, one block).
+// base (optional) += the copies before copy c of each digit.
+template <int NT>
+__device__ __forceinline__ void pair_starts(const uint64_t *__restrict__ tot, uint32_t F, uint32_t c, uint64_t *start,
+                                            uint64_t *count, uint64_t *scratch) {
+    uint64_t carry = 0;
+    for (uint32_t d0 = 0; d0 < F; d0 += NT) {
+        const uint32_t d = d0 + threadIdx.x;
+        uint64_t v = 0, before = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kSyncSpread; ++k) {
+            const uint64_t x = d < F ? tot[(uint64_t)k * kMaxF + d] : 0ull;
+            before += k < c ? x : 0ull;
+            v += x;
+        }
+        uint64_t t;
+        const uint64_t ex = block_excl_scan_u64(v, scratch, &t);
+        if (d < F) {
+            start[d] = carry + ex + before;
+            if (count) count[d] = v;
+        }
+        carry += t;
+    }
+}
 
 template <int BITS, int ITEMS, int NT>
 __global__ __launch_bounds__(NT, (scatter_waves_per_simd<BITS, ITEMS, NT>())) void k_scatter_pair(
-    ScatterPairRel A, ScatterPairRel B, uint32_t shift) {
+    ScatterPairRel A, ScatterPairRel B, uint32_t shift, uint64_t *__restrict__ over, uint32_t over_cap,
+    uint64_t *__restrict__ meta, uint64_t s_chunk) {
     __shared__ ScatterLds<BITS, ITEMS, NT> L;
+    __shared__ uint64_t base[1u << BITS];
+    __shared__ uint64_t scratch[NT / kWave + 1];
+    constexpr uint32_t F = 1u << BITS;
+    if (blockIdx.x == A.grid + B.grid) {  // the layout workgroup
+        uint64_t *cR = reinterpret_cast<uint64_t *>(L.tile), *cS = cR + F;  // (the tile space: no scatter here)
+        pair_starts<NT>(A.tot, F, 0, A.start, cR, scratch);
+        pair_starts<NT>(B.tot, F, 0, B.start, cS, scratch);
+        __syncthreads();
+        uint64_t base_over = 0, mr = 0, ms = 0;
+        for (uint32_t p0 = 0; p0 < F; p0 += NT) {
+            const uint32_t p = p0 + threadIdx.x;
+            const uint64_t nR = p < F ? cR[p] : 0, nS = p < F ? cS[p] : 0;
+            if (p < F) {
+                A.cnt[p] = nR;
+                B.cnt[p] = nS;
+            }
+            mr = nR > mr ? nR : mr;
+            ms = nS > ms ? nS : ms;
+            const uint64_t k = (nR == 0 || nS <= s_chunk) ? 0 : (nS + s_chunk - 1) / s_chunk - 1;
+            uint64_t t;
+            const uint64_t ex = base_over + block_excl_scan_u64(k, scratch, &t);
+            for (uint64_t j = 0; j < k && ex + j < over_cap; ++j) over[ex + j] = p | ((j + 1) << 32);
+            base_over += t;
+        }
+        mr = block_max_u64(mr, scratch);
+        ms = block_max_u64(ms, scratch);
+        if (threadIdx.x == 0) {
+            meta[0] = mr;
+            meta[1] = ms;
+            meta[2] = base_over;  // n_over (u32, low word; the high word is 0)
+        }
+        for (uint32_t i = threadIdx.x; i < kSyncSpread * kMaxF; i += NT) {
+            A.tot_next[i] = 0;
+            B.tot_next[i] = 0;
+        }
+        return;
+    }
     const bool isB = blockIdx.x >= A.grid;
     const ScatterPairRel &P = isB ? B : A;
     const uint32_t g = isB ? blockIdx.x - A.grid : blockIdx.x;
     dbg_stamp(1, 0);
-    scatter_segment<BITS, ITEMS, NT, false>(L, g, P.in, P.out, P.m, shift, P.offs, kDigitMajor, P.grid,
-                                            P.cstart + (uint64_t)(g % kSyncSpread) * kMaxF, nullptr, 0, 0);
+    pair_starts<NT>(P.tot, F, g % kSyncSpread, base, nullptr, scratch);
+    __syncthreads();
+    scatter_segment<BITS, ITEMS, NT, false>(L, g, P.in, P.out, P.m, shift, P.offs, kDigitMajor, P.grid, base, nullptr,
+                                            0, 0);
     dbg_stamp(1, 2);
 }
 
 hipError_t launch_scatter_pair(const row_t *R, row_t *outR, const SegMap &mR, uint32_t gridR, const uint64_t *offsR,
-                               const uint64_t *startR, const row_t *S, row_t *outS, const SegMap &mS, uint32_t gridS,
-                               const uint64_t *offsS, const uint64_t *startS, uint32_t shift, uint32_t bits,
-                               hipStream_t s) {
+                               const uint64_t *totR, uint64_t *totR_next, uint64_t *startR, uint64_t *cntR,
+                               const row_t *S, row_t *outS, const SegMap &mS, uint32_t gridS, const uint64_t *offsS,
+                               const uint64_t *totS, uint64_t *totS_next, uint64_t *startS, uint64_t *cntS,
+                               uint32_t shift, uint32_t bits, uint64_t *over, uint32_t over_cap, uint64_t *meta,
+                               uint64_t s_chunk, hipStream_t s) {
     constexpr int ITEMS = kScatterItems, NT = kScatterThreads;
     const ScatterPairRel A{reinterpret_cast<const uint64_t *>(R), reinterpret_cast<uint64_t *>(outR), mR, gridR,
-                           offsR, startR};
+                           offsR, totR, totR_next, startR, cntR};
     const ScatterPairRel B{reinterpret_cast<const uint64_t *>(S), reinterpret_cast<uint64_t *>(outS), mS, gridS,
-                           offsS, startS};
-    const dim3 grid(gridR + gridS);
+                           offsS, totS, totS_next, startS, cntS};
+    const dim3 grid(gridR + gridS + 1);
 #define PAIR_CASE(BB)                                                                                       \
     case BB:                                                                                                \
-        if constexpr (sizeof(ScatterLds<BB, ITEMS, NT>) <= 160 * 1024 && (1 << BB) <= NT) {                   \
-            hipLaunchKernelGGL((k_scatter_pair<BB, ITEMS, NT>), grid, dim3(NT), 0, s, A, B, shift);           \
+        if constexpr (sizeof(ScatterLds<BB, ITEMS, NT>) + (8u << BB) + 8 * (NT / kWave + 1) <= 160 * 1024 &&  \
+                      (1 << BB) <= NT) {                                                                     \
+            hipLaunchKernelGGL((k_scatter_pair<BB, ITEMS, NT>), grid, dim3(NT), 0, s, A, B, shift, over,       \
+                               over_cap, meta, s_chunk);                                                    \
             break;                                                                                          \
         } else {                                                                                            \
             return hipErrorInvalidValue;                                                                    \

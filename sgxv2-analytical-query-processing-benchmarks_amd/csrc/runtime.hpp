@@ -94,8 +94,9 @@ struct Context {
     // the receive buffers the peers' pieces land in
     DeviceBuffer xsendR, xsendS, xrecvR, xrecvS;
     // in-launch hand-off words (tickets, digit totals) of the small-join path: zeroed
-    // once when allocated, left zero by every kernel that uses them
+    // once when allocated (rho_internal.hpp kSync*)
     DeviceBuffer sync;
+    uint32_t small_parity = 0;  // the small join's digit-totals set for the next call
 };
 
 // Context of the calling thread's current HIP device (created on first use).
