@@ -64,6 +64,11 @@ constexpr uint32_t kSyncTicketJoin = 3;
 // sync[kSyncT0]) and last the done flag (word 7), which the host spins on instead of
 // synchronising the stream.
 constexpr uint32_t kSyncHostResult = kSyncTicketJoin + 1, kSyncT0 = kSyncTicketJoin + 2;
+// the small join's count reduction (rho_kernels.hip join_reduce_last): arrivals << 48 |
+// the summed counts, and the summed build / probe ticks (two 32-bit halves); zero
+// between calls
+constexpr uint32_t kSyncJoinSum = kSyncTicketJoin + 3, kSyncJoinTicks = kSyncTicketJoin + 4;
+static_assert(kSyncJoinTicks < 8, "sync words below the digit totals");
 constexpr uint32_t kHostJoinSpan = 6, kHostJoinDone = 7, kHostJoinWords = 8;
 // Hand-offs spread over kSyncSpread groups of workgroups (segment or workgroup index mod
 // kSyncSpread), so that no device-scope atomic address takes more than 1/kSyncSpread of
@@ -81,7 +86,10 @@ constexpr uint32_t kSyncTot0 = 8, kSyncTotWords = kSyncSpread * kMaxF;
 // totals set `parity` (0 / 1) of relation rel (0 R, 1 S)
 constexpr uint32_t sync_tot(uint32_t parity, uint32_t rel) { return kSyncTot0 + (2 * parity + rel) * kSyncTotWords; }
 constexpr uint32_t kSyncSub = kSyncTot0 + 4 * kSyncTotWords;  // relative to a ticket's word
-constexpr uint32_t kSyncWords = kSyncSub + kNumTickets * (kSyncSpread + 1);
+// the count reduction's group word pairs (join_reduce_last: kJoinGroups of them)
+constexpr uint32_t kJoinGroups = 16;
+constexpr uint32_t kSyncJoinGrp = kSyncSub + kNumTickets * (kSyncSpread + 1);
+constexpr uint32_t kSyncWords = kSyncJoinGrp + 2 * kJoinGroups;
 // Development: small-join workgroup stamps (rho_kernels.hip dbg_stamp), 3 kernels + the
 // build/probe reduction x 3
 // stamps x kStampWgs u64; null turns them off.

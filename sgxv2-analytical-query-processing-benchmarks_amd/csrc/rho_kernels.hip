@@ -2480,71 +2480,82 @@ hipError_t launch_hist_side_blk(const uint8_t *side, const uint64_t *list, const
 //                     (radix_join.cpp:437-446) at task_off[t] + a task-local slot
 //                     taken with one LDS atomic per wave and chain step.
 
-// Count-mode reduction in the join launch itself (replaces k_reduce): the last
-// workgroup to finish sums every workgroup's partial count and build / probe ticks into
-// result[0] / [4] / [5].  red: NW + 2 u64 of LDS (NW = waves per workgroup).
+// Count-mode reduction in the join launch itself (replaces k_reduce), for small joins:
+// every workgroup with a task adds its count into ONE 64-bit device word together with
+// its arrival -- (1 << 48) | count, one atomic -- after adding its build / probe ticks
+// (two 32-bit halves of a second word, waited for first), and the workgroup whose atomic
+// returns n - 1 arrivals is the last: it holds the total (the returned sum + its own
+// count), reads the ticks, resets both words for the next call and writes the result.
+// No per-workgroup count slots, release fences, second ticket or final summation
+// (round 4: a ticket of 256 arrivals, then the last workgroup summing the slots: 3.3 +
+// 2.2 us of the 2^20 join, r05n stamps).  counts / cyc: this workgroup's count and
+// ticks at [blockIdx.x] / [2 blockIdx.x .. + 1] (written by its thread 0).
 __device__ __forceinline__ void join_reduce_last(const uint64_t *__restrict__ counts, const uint64_t *__restrict__ cyc,
                                                  uint64_t *__restrict__ result, uint64_t *__restrict__ ticket,
                                                  uint64_t *red, uint64_t tasks) {
-    const uint32_t nw = blockDim.x / kWave;
-    // workgroups without a task (blockIdx >= tasks; their count slots are 0) do not take
-    // a ticket: every arrival is a device atomic on one address, serialised (≈ 14 ns each)
+    (void)red;
+    // workgroups without a task (blockIdx >= tasks) do not arrive
     const uint64_t n = tasks < gridDim.x ? tasks : gridDim.x;
-    if (blockIdx.x >= n && n > 0) return;
-    if (!arrive_last_spread(ticket, n > 0 ? n : gridDim.x, blockIdx.x, reinterpret_cast<uint32_t *>(red + nw + 1)))
-        return;
+    if ((blockIdx.x >= n && n > 0) || threadIdx.x != 0) return;
+    const uint64_t na = n > 0 ? n : gridDim.x;  // < 2^16 (small-join grids)
+    // two levels: workgroup b arrives at group b mod kJoinGroups (one word pair per group:
+    // arrivals << 48 | counts, and ticks), the last arrival of a group carries the group's
+    // sums to the top pair; at most n / kJoinGroups + kJoinGroups atomics queue on one
+    // address (each ~14 ns: 256 arrivals on one word took 3.6 us)
+    constexpr uint64_t M48 = (1ull << 48) - 1;
+    const uint32_t G = na < kJoinGroups ? (uint32_t)na : kJoinGroups;
+    const uint32_t grp = blockIdx.x % G;
+    const uint64_t members = (na - grp + G - 1) / G;
+    uint64_t *gsum = ticket + (kSyncJoinGrp - kSyncTicketJoin) + 2 * grp, *gtick = gsum + 1;
+    uint64_t *sumw = ticket + (kSyncJoinSum - kSyncTicketJoin);
+    uint64_t *tickw = ticket + (kSyncJoinTicks - kSyncTicketJoin);
+    const uint64_t acc = counts[blockIdx.x];
+    // (per workgroup far below 2^32 ticks: the halves never carry into each other)
+    uint64_t tk = cyc ? ((uint64_t)(uint32_t)cyc[2 * blockIdx.x] << 32) | (uint32_t)cyc[2 * blockIdx.x + 1] : 0ull;
+    if (cyc) {
+        tk += __hip_atomic_fetch_add(gtick, tk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // performed before the arrival below
+    }
     dbg_stamp(3, 0);
-    uint64_t acc = 0, b = 0, p = 0;
-    // only the arrivals' slots (an idle workgroup's slot was never released to this one)
-    const uint32_t na = (uint32_t)(n > 0 ? n : gridDim.x);
-    for (uint32_t i = threadIdx.x; i < na; i += blockDim.x) {
-        acc += counts[i];
-        if (cyc) {
-            b += cyc[2 * i];
-            p += cyc[2 * i + 1];
-        }
+    uint64_t old = __hip_atomic_fetch_add(gsum, (1ull << 48) | acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((old >> 48) != members - 1) return;
+    // the group's last: every member's ticks were added before its arrival
+    const uint64_t gs = (old & M48) + acc;
+    if (cyc) tk = __hip_atomic_fetch_add(gtick, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(gsum, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(gtick, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cyc) {
+        (void)__hip_atomic_fetch_add(tickw, tk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    // the three sums in one block reduction (wave sums, one barrier, thread 0 adds)
-    acc = wave_sum_u64(acc);
-    b = wave_sum_u64(b);
-    p = wave_sum_u64(p);
-    __shared__ uint64_t wsum[3][1024 / kWave];
-    if (__lane_id() == 0) {
-        wsum[0][threadIdx.x / kWave] = acc;
-        wsum[1][threadIdx.x / kWave] = b;
-        wsum[2][threadIdx.x / kWave] = p;
-    }
-    __syncthreads();
-    uint64_t t = 0, tb = 0, tp = 0;
-    if (threadIdx.x == 0)
-        for (uint32_t w = 0; w < nw; ++w) {
-            t += wsum[0][w];
-            tb += wsum[1][w];
-            tp += wsum[2][w];
-        }
+    old = __hip_atomic_fetch_add(sumw, (1ull << 48) | gs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((old >> 48) != G - 1) return;
+    const uint64_t t = (old & M48) + gs;
+    tk = cyc ? __hip_atomic_fetch_add(tickw, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+    __hip_atomic_store(sumw, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(tickw, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t tb = tk >> 32, tp = tk & 0xFFFFFFFFull;
     dbg_stamp(3, 1);
-    if (threadIdx.x == 0) {
-        result[0] = t;
-        if (cyc) {
-            result[4] = tb;
-            result[5] = tp;
-        }
-        // the call's result block in mapped host memory (kSyncHostResult): all six words
-        // (result[1..3] come from the launches before this one), the device span, then
-        // the done flag the host spins on -- the kernel's last memory operation (the
-        // kernel's end releases it; one system fence orders the words before it)
-        volatile uint64_t *h = reinterpret_cast<volatile uint64_t *>(ticket[kSyncHostResult - kSyncTicketJoin]);
-        if (h) {
-            h[0] = t;
-            h[1] = result[1];
-            h[2] = result[2];
-            h[3] = result[3];
-            h[4] = tb;
-            h[5] = tp;
-            h[kHostJoinSpan] = wall_clock64() - ticket[kSyncT0 - kSyncTicketJoin];
-            __threadfence_system();
-            h[kHostJoinDone] = 1;
-        }
+    result[0] = t;
+    if (cyc) {
+        result[4] = tb;
+        result[5] = tp;
+    }
+    // the call's result block in mapped host memory (kSyncHostResult): all six words
+    // (result[1..3] come from the launches before this one), the device span, then the
+    // done flag the host spins on -- the kernel's last memory operation (the kernel's end
+    // releases it; one system fence orders the words before it)
+    volatile uint64_t *h = reinterpret_cast<volatile uint64_t *>(ticket[kSyncHostResult - kSyncTicketJoin]);
+    if (h) {
+        h[0] = t;
+        h[1] = result[1];
+        h[2] = result[2];
+        h[3] = result[3];
+        h[4] = tb;
+        h[5] = tp;
+        h[kHostJoinSpan] = wall_clock64() - ticket[kSyncT0 - kSyncTicketJoin];
+        __threadfence_system();
+        h[kHostJoinDone] = 1;
     }
     dbg_stamp(3, 2);
 }
