@@ -77,6 +77,36 @@ def host_topology() -> dict:
     return info
 
 
+def cpu_mhz(cpus: list[int] | None = None) -> dict:
+    """Current (mean over `cpus`, else all) and maximum core clock in MHz, from cpufreq or
+    /proc/cpuinfo: the CPU baseline varies from box to box, and the clock it ran at is
+    part of reading it."""
+    out: dict = {"cur_mhz": None, "max_mhz": None}
+    cur = []
+    for c in (cpus or range(os.cpu_count() or 0)):
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/cpufreq/scaling_cur_freq") as f:
+                cur.append(int(f.read()) / 1000.0)
+        except (OSError, ValueError):
+            break
+    if not cur:
+        try:
+            with open("/proc/cpuinfo") as f:
+                mhz = [float(ln.split(":", 1)[1]) for ln in f if ln.startswith("cpu MHz")]
+            sel = [mhz[c] for c in cpus if c < len(mhz)] if cpus else mhz
+            cur = sel or mhz
+        except (OSError, ValueError):
+            pass
+    if cur:
+        out["cur_mhz"] = round(sum(cur) / len(cur), 1)
+    try:
+        with open("/sys/devices/system/cpu/cpu0/cpufreq/cpuinfo_max_freq") as f:
+            out["max_mhz"] = round(int(f.read()) / 1000.0, 1)
+    except (OSError, ValueError):
+        pass
+    return out
+
+
 def _cpulist(text: str) -> list[int]:
     out = []
     for part in text.split(","):
@@ -992,6 +1022,11 @@ def main():
                           f"physical cores, median of {lead['joins']} joins")
                if "pinned" in rho_cpu else "config 1 only (no config-2 copy)",
                "rho": rho_cpu, **cpu_info}
+        # the host record as scalars beside the value (the driver's record keeps scalars)
+        clk = cpu_mhz(cpu_info.get("pinned_cpus"))
+        cpu.update({"host_model": topo.get("model"), "host_cur_mhz": clk["cur_mhz"], "host_max_mhz": clk["max_mhz"],
+                    "host_cgroup_cpu_quota": topo.get("cgroup_cpu_quota"),
+                    "host_numa_nodes": len(topo.get("numa_nodes") or {})})
         if scan_col_host is not None:  # config 3 on the host: count / bitvector / index, SIMD512 restated
             scan_cpu = {"rows": len(scan_col_host), "dtype": "i32", "predicate": [0, 26], "threads": threads,
                         "how": "oracle/cpu_baseline.c (SIMD512.cpp AVX-512 formulation, multithreadedscan.cpp "
