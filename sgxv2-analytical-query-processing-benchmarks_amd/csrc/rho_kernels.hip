@@ -688,6 +688,9 @@ __device__ __forceinline__ T lds_pick(bool c, const T *a, const T *b) {
     return *(lds_t *)(uintptr_t)vsel(c, pa, pb);
 }
 
+#ifndef SGXAMD_POOL_GRAN  // pooled keys (4-byte pool): bytes per write granule, 128 or 256
+#define SGXAMD_POOL_GRAN 128
+#endif
 // EXT: 0 = cursor output, contiguous input; 1 = pooled output (PoolOut); 2 = block-list
 // input (the segment's list entries staged in ents).
 // T: the element moved (uint64_t tuple, or uint32_t key of a count-only join).
@@ -698,7 +701,8 @@ struct ScatterLds {
     static constexpr uint32_t F = 1u << BITS;
     static constexpr uint32_t TILE = NT * ITEMS;
     static constexpr uint32_t NW = NT / kWave;
-    static constexpr uint32_t G = 128 / OB;  // elements per 128-B granule
+    // elements per write granule (128 B; the 4-byte key pool SGXAMD_POOL_GRAN)
+    static constexpr uint32_t G = (EXT == 1 && sizeof(T) == 4 && OB == 4 ? SGXAMD_POOL_GRAN : 128) / OB;
     static constexpr uint32_t GPB = kBlk / G;       // granules per pool block
     static constexpr uint32_t MAXDESC = (TILE + (G - 1) * F) / G + F;
     union {
@@ -967,10 +971,10 @@ __device__ __forceinline__ void scatter_tile_write(ScatterLds<BITS, ITEMS, NT, E
                                                       (((x[3] >> shift2) & mask2) << 24);
         }
     } else if constexpr (sizeof(T) == 4) {
-        // keys: 16 lanes per granule, two consecutive keys per lane (one 8-byte store and
+        // keys: G / 2 lanes per granule, two consecutive keys per lane (one 8-byte store and
         // one 2-byte side store), half the rounds and metadata reads of one key per lane
-        constexpr uint32_t NG2 = NT / 16;
-        const uint32_t l2 = 2 * (tid & 15), grp2 = tid / 16;
+        constexpr uint32_t LPG = G / 2, NG2 = NT / LPG;
+        const uint32_t l2 = 2 * (tid & (LPG - 1)), grp2 = tid / LPG;
         // element q of d's run: its carries, then the tile's
         const auto elem = [&](uint32_t d, uint32_t q, uint32_t cd, uint32_t tbx) -> uint32_t {
             return (uint32_t)lds_pick(q < cd, &L.carry[d * CS + q], &L.tile[tbx + q - cd]);
