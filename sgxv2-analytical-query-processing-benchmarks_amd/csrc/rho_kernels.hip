@@ -1828,6 +1828,9 @@ __global__ __launch_bounds__(NT, NT * SGXAMD_SORT_WGS / 256) void k_sort_blk(con
 #ifndef SGXAMD_PLACE_U  // 16-byte loads (4 keys) per thread and tile
 #define SGXAMD_PLACE_U 2
 #endif
+#ifndef SGXAMD_PLACE_XCD  // consecutive segments on one XCD (their shared partial lines meet in one L2)
+#define SGXAMD_PLACE_XCD 1
+#endif
 // Pass 2 of narrow key partitions as one placement per segment (k_place_seg, round 5).
 // radix_cluster (radix_join.cpp:715-761) scatters a region by its pass-2 digit at
 // cursors from a histogram; here the pass-2 histogram (k_hist_side_blk, over the digit
@@ -1880,7 +1883,7 @@ __global__ __launch_bounds__(NT, NT *SGXAMD_PLACE_WGS / 256) void k_place_seg(
     static_assert(kBlk == 4 * kWave && F <= NT, "placement geometry");
     __shared__ LdsT L;
     if (narrow == nullptr || ((*narrow >> (shift + BITS)) >> 16) != 0) return;  // wide: k_sort_blk
-    const uint32_t tid = threadIdx.x, lane = __lane_id(), wave = tid / kWave, g = blockIdx.x;
+    const uint32_t tid = threadIdx.x, lane = __lane_id(), wave = tid / kWave, g = SGXAMD_PLACE_XCD ? xcd_contiguous(blockIdx.x, gridDim.x) : blockIdx.x;
     const uint32_t rshift = shift + BITS;
     uint32_t r;
     uint64_t b, e;
