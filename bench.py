@@ -319,6 +319,8 @@ def algorithmic_bytes(kernel: str, nR: int, nS: int, passes: int = 2, pass2_bits
         if layout == 4 and nar:
             return 5 * n  # read residual + digit byte, write the residual
         return (elem + (2 if nar else elem)) * n  # read + write every element
+    if kernel.endswith("_wire_merge"):  # multi-GPU u16 wire: the senders' pieces gathered (read + write 2 B)
+        return 4 * n
     if kernel == "join_build_probe":  # every partitioned element read once
         return (2 if narrow & 1 else elem) * nR + (2 if narrow & 2 else elem) * nS
     return 0

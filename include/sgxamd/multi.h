@@ -67,14 +67,20 @@ typedef struct mi355_multi_stats {
     uint64_t recv_r_max, recv_r_min;  /* received R tuples per rank (load report) */
     uint64_t recv_s_max, recv_s_min;  /* received S tuples per rank */
     uint64_t max_part_s;       /* largest local S partition over the ranks seen */
-    uint64_t sent_bytes;       /* tuple bytes sent to other ranks (ranks seen) */
+    uint64_t sent_bytes;       /* bytes sent to other ranks (ranks seen): tuples, keys, or on the
+                                  u16 wire residuals and counts rows */
     double ms_total;           /* wall time of the call (max over the ranks seen) */
     double ms_exchange_post;   /* shard partitions + count exchanges + posting the pieces */
     double ms_local;           /* from the last piece posted to the local join's end */
     double ms_allreduce;       /* final match-count all-reduce */
     mi355_rho_stats local;     /* the local join of rank 0 (or of the calling rank) */
-    uint32_t elem_bytes;       /* bytes per exchanged element: 8 (tuples) or 4 (keys only: a
-                                  counting join whose local join reads keys) */
+    uint32_t elem_bytes;       /* bytes per exchanged element: 8 (tuples), 4 (keys only: a
+                                  counting join whose local join reads keys) or 2 (the u16
+                                  wire: every sender runs the receiver's two partition passes
+                                  and sends 2-byte residuals grouped by partition, plus per
+                                  relation and peer one row of P + 1 u64 words: the partition
+                                  counts and its largest key; taken when log2(world) + the
+                                  local radix bits >= 16; SGXAMD_WIRE16=0 turns it off) */
     double ms_tail;            /* device time from S's last piece landing to the local join's
                                   end (max over the ranks seen; the part of the join that no
                                   exchange hides); -1 when no rank measured it (a world of

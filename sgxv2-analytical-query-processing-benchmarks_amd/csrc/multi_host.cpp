@@ -228,7 +228,8 @@ class Transport {
     // collective: after `ready` (the piece's partition on the compute stream), move the
     // piece: the run for destination d starts at send + sum_{d'<d} send_counts[d'];
     // rank q's run lands at recv + sum_{q'<q} recv_counts[q'].  Enqueued on c.
-    // elem: bytes per element (8: row_t tuples; 4: keys of a keys-only exchange).
+    // elem: bytes per element (8: row_t tuples or counts rows; 4: keys of a keys-only
+    // exchange; 2: residuals of the u16 wire).
     virtual int post_exchange(int rank, hipStream_t c, hipEvent_t ready, const void *send,
                               const uint64_t *send_counts, void *recv, const uint64_t *recv_counts, size_t elem) = 0;
     // collective: v[0..n) = element-wise sum / max over the ranks (n <= kMaxReduce)
@@ -351,7 +352,9 @@ class RcclTransport final : public Transport {
         const auto so = prefix(send_counts, world_), ro = prefix(recv_counts, world_);
         const char *send = static_cast<const char *>(send_v);
         char *recv = static_cast<char *>(recv_v);
-        const ncclDataType_t type = elem == 8 ? ncclUint64 : ncclUint32;
+        // (2-byte residuals of the u16 wire travel as bytes)
+        const ncclDataType_t type = elem == 8 ? ncclUint64 : elem == 4 ? ncclUint32 : ncclUint8;
+        const size_t per = elem == 8 || elem == 4 ? 1 : elem;
         MH_HIPC(hipStreamWaitEvent(c, ready, 0));
         if (send_counts[rank])  // this rank's own run: a local copy
             MH_HIPC(hipMemcpyAsync(recv + ro[rank] * elem, send + so[rank] * elem, send_counts[rank] * elem,
@@ -362,10 +365,11 @@ class RcclTransport final : public Transport {
         const char *what = "";
         for (int p = 0; p < world_ && r == ncclSuccess; ++p) {
             if (p == rank) continue;
-            if (send_counts[p] && (r = L.Send(send + so[p] * elem, send_counts[p], type, p, comms_[i], c)) != ncclSuccess)
+            if (send_counts[p] &&
+                (r = L.Send(send + so[p] * elem, send_counts[p] * per, type, p, comms_[i], c)) != ncclSuccess)
                 what = "ncclSend";
             else if (recv_counts[p] &&
-                     (r = L.Recv(recv + ro[p] * elem, recv_counts[p], type, p, comms_[i], c)) != ncclSuccess)
+                     (r = L.Recv(recv + ro[p] * elem, recv_counts[p] * per, type, p, comms_[i], c)) != ncclSuccess)
                 what = "ncclRecv";
         }
         // the group is closed even after a failed call (the thread's group state stays
@@ -529,6 +533,7 @@ int rank_streams(Context *ctx, int nev, RankStreams **out) {
 struct RankOut {
     uint64_t global = 0, local = 0, recv_r = 0, recv_s = 0, sent = 0;
     bool keys = false;       // the exchange moved keys only
+    bool wire16 = false;     // ... as 2-byte residuals of sender-side partitions (the u16 wire)
     bool peer_fail = false;  // the call failed because another rank did
     bool together = false;   // the call failed at a collective every rank left at (the
                              // sequence is intact; nothing to abort)
@@ -643,17 +648,33 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
     // the element format must be the same on every rank (the SGXAMD_KEYS switch and the
     // calling thread's key layout are per process / per thread): keys only when every
     // rank's plan, from the same global sizes, takes the pooled keys layout
+    // and the u16 wire (keys plans whose every residual fits 16 bits): agreed the same way
     mi355_rho_opts kl = lo;
-    uint64_t notkeys = rho::keys_exchange_plan(sum[0] / G, sum[1] / G, cR, cS, &kl) ? 0 : 1;
-    MH_RC(transport_rc(T.allreduce(rank, s, &notkeys, 1, kMax)));
-    o.keys = notkeys == 0;
+    uint64_t agree[2] = {rho::keys_exchange_plan(sum[0] / G, sum[1] / G, cR, cS, &kl) ? 0u : 1u, 1u};
+    if (agree[0] == 0 && rho::wire16_plan(sum[0] / G, sum[1] / G, G, &kl)) agree[1] = 0;
+    MH_RC(transport_rc(T.allreduce(rank, s, agree, 2, kMax)));
+    o.keys = agree[0] == 0;
+    o.wire16 = o.keys && agree[1] == 0;
     if (o.keys) lo = kl;  // the local policy fixed from the global sizes
+    const uint32_t P16 = o.wire16 ? rho::wire16_plan(sum[0] / G, sum[1] / G, G, &lo) : 0;
     const size_t elem = o.keys ? sizeof(uint32_t) : sizeof(row_t);
+    // u16 wire buffers: [residuals (256-B aligned)][G counts rows of P16 + 1 words]; the
+    // receive side of R also holds the gather's scratch (2 G P16 words)
+    const auto res_bytes = [](uint64_t n) { return (std::max<uint64_t>(n, 1) * 2 + 255) & ~uint64_t(255); };
+    const uint64_t rows = (uint64_t)G * (P16 + 1) * sizeof(uint64_t);
     if (fail_rc == MI355_OK) {
         hipError_t e = ctx->xsendR.ensure(std::max<uint64_t>(nR, 1) * elem);
         if (e == hipSuccess) e = ctx->xsendS.ensure(std::max<uint64_t>(nS, 1) * elem);
-        if (e == hipSuccess) e = ctx->xrecvR.ensure(std::max<uint64_t>(cR, 1) * elem);
-        if (e == hipSuccess) e = ctx->xrecvS.ensure(std::max<uint64_t>(cS, 1) * elem);
+        if (!o.wire16) {
+            if (e == hipSuccess) e = ctx->xrecvR.ensure(std::max<uint64_t>(cR, 1) * elem);
+            if (e == hipSuccess) e = ctx->xrecvS.ensure(std::max<uint64_t>(cS, 1) * elem);
+        } else {
+            if (e == hipSuccess) e = ctx->wsendR.ensure(res_bytes(nR) + rows);
+            if (e == hipSuccess) e = ctx->wsendS.ensure(res_bytes(nS) + rows);
+            if (e == hipSuccess)
+                e = ctx->wrecvR.ensure(res_bytes(cR) + rows + 2 * ((uint64_t)G * P16 + G) * sizeof(uint64_t));
+            if (e == hipSuccess) e = ctx->wrecvS.ensure(res_bytes(cS) + rows);
+        }
         if (e != hipSuccess) {
             set_last_error(std::string("exchange buffers (") + std::to_string((2 * (nR + nS) + cR + cS) * elem) +
                            " bytes): " + hipGetErrorString(e));
@@ -691,7 +712,53 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
     // failure from here on is flagged at the final all-reduce
     uint64_t total[2] = {0, 0};
     std::vector<uint64_t> s_piece(K, 0);  // S tuples landing per piece (S's local pass 1 runs per piece)
-    for (int j = 0; j < M; ++j) {
+    std::array<std::vector<uint64_t>, 2> wbase;  // u16 wire: where sender q's run lands
+    if (o.wire16) {
+        // per relation: its pieces' shard scatters, the receiver's two passes over the
+        // keys for each destination (its runs: one per piece), then the counts rows and
+        // the residuals posted; S's scatters and passes run while R is on the wire
+        for (int rel = 0; rel < 2; ++rel) {
+            for (int i = 0; i < K && fail_rc == MI355_OK; ++i)
+                fail(rho::shard_scatter_piece(ctx, s, rel * K + i,
+                                              (rel ? ctx->xsendS : ctx->xsendR).as<char>() + pa[rel * K + i] * elem));
+            DeviceBuffer &ws = rel ? ctx->wsendS : ctx->wsendR, &wr = rel ? ctx->wrecvS : ctx->wrecvR;
+            uint16_t *snd16 = ws.as<uint16_t>();
+            uint64_t *scnt = reinterpret_cast<uint64_t *>(ws.as<char>() + res_bytes(nrel[rel]));
+            uint64_t *rcnt = reinterpret_cast<uint64_t *>(wr.as<char>() + res_bytes(rel ? cS : cR));
+            std::vector<uint64_t> roff((size_t)G * K), rn((size_t)G * K), s16(G, 0), r16(G, 0);
+            for (int q = 0; q < G; ++q)
+                for (int i = 0; i < K; ++i) {
+                    const int j = rel * K + i;
+                    uint64_t off = pa[j];
+                    for (int d = 0; d < q; ++d) off += sc[(size_t)j * G + d];
+                    roff[(size_t)q * K + i] = off;
+                    rn[(size_t)q * K + i] = sc[(size_t)j * G + q];
+                    s16[q] += sc[(size_t)j * G + q];
+                    r16[q] += rc[(size_t)j * G + q];
+                }
+            if (fail_rc == MI355_OK)
+                fail(rho::wire_partition(ctx, s, (rel ? ctx->xsendS : ctx->xsendR).as<uint32_t>(), G, K, roff.data(),
+                                         rn.data(), sum[0] / G, sum[1] / G, &lo, snd16, scnt, rel ? "wireS_" : "wireR_"));
+            // a failed rank still sends (the sizes are agreed): zero counts rows, which
+            // no receiver takes (they do not add up to the announced runs)
+            if (fail_rc != MI355_OK && ws.ptr) (void)hipMemsetAsync(scnt, 0, rows, s);
+            hipEvent_t ready = rs->ev[rel];
+            hip_ok(hipEventRecord(ready, s), "hipEventRecord (residuals ready)");
+            const std::vector<uint64_t> crow(G, (uint64_t)P16 + 1);
+            MH_RC(transport_rc(T.post_exchange(rank, rs->comm, ready, scnt, crow.data(), rcnt, crow.data(),
+                                               sizeof(uint64_t))));
+            MH_RC(transport_rc(T.post_exchange(rank, rs->comm, ready, snd16, s16.data(), wr.ptr, r16.data(),
+                                               sizeof(uint16_t))));
+            wbase[rel].assign(G, 0);
+            for (int q = 0; q < G; ++q) {
+                wbase[rel][q] = total[rel];
+                total[rel] += r16[q];
+                if (q != rank) o.sent += s16[q] * sizeof(uint16_t) + crow[q] * sizeof(uint64_t);
+            }
+            hip_ok(hipEventRecord(rs->ev[2 * K + rel], rs->comm), "hipEventRecord (relation landed)");
+        }
+    }
+    for (int j = 0; j < M && !o.wire16; ++j) {
         const int rel = j / K;
         char *snd = (rel ? ctx->xsendS : ctx->xsendR).as<char>() + pa[j] * elem;
         char *rcv = (rel ? ctx->xrecvS : ctx->xrecvR).as<char>() + total[rel] * elem;
@@ -719,7 +786,22 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
 
     // local join: R's passes once R has landed, S's passes and build/probe once S has.
     // Every failure from here on is this rank's own and is flagged in the final all-reduce.
-    if (fail_rc == MI355_OK) {
+    if (fail_rc == MI355_OK && o.wire16) {
+        if (total[0] && total[1]) {
+            const uint64_t *rcR = reinterpret_cast<const uint64_t *>(ctx->wrecvR.as<char>() + res_bytes(cR));
+            const uint64_t *rcS = reinterpret_cast<const uint64_t *>(ctx->wrecvS.as<char>() + res_bytes(cS));
+            uint64_t *src = const_cast<uint64_t *>(rcR) + (size_t)G * (P16 + 1);
+            const int lrc = injected(rank, kFailLocal)
+                                ? MI355_ERR_OOM
+                                : rho::join_wire16(ctx, s, ctx->wrecvR.as<uint16_t>(), rcR, wbase[0].data(), total[0],
+                                                   ctx->wrecvS.as<uint16_t>(), rcS, wbase[1].data(), total[1], G, &lo,
+                                                   src, rs->ev[2 * K], rs->ev[2 * K + 1], &o.st);
+            fail(lrc);
+            o.local = lrc == MI355_OK ? o.st.matches : 0;
+        } else {
+            hip_ok(hipStreamWaitEvent(s, rs->ev[2 * K + 1], 0), "hipStreamWaitEvent (S landed)");
+        }
+    } else if (fail_rc == MI355_OK) {
         const bool waited = hip_ok(hipStreamWaitEvent(s, rs->ev[2 * K], 0), "hipStreamWaitEvent (R landed)");
         if (waited && total[0] && total[1]) {
             // S's pass 1 runs per piece as it lands (each launch waits for its piece's
@@ -836,7 +918,7 @@ void fill_stats(mi355_multi_stats *st, const std::vector<RankOut> &outs, int G, 
     if (!outs.empty()) {
         st->local_matches = outs[0].local;
         st->local = outs[0].st;
-        st->elem_bytes = outs[0].keys ? 4u : 8u;
+        st->elem_bytes = outs[0].wire16 ? 2u : outs[0].keys ? 4u : 8u;
     }
 }
 

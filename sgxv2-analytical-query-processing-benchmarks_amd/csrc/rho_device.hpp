@@ -51,6 +51,31 @@ int join_pipelined_finish(Context *ctx, const void *dS, uint64_t nS, mi355_rho_s
 // open, and checks that this policy takes the pooled keys layout for any local size up
 // to cap_r / cap_s (the receive capacities).  SGXAMD_KEYS=0 disables it.
 bool keys_exchange_plan(uint64_t nR, uint64_t nS, uint64_t cap_r, uint64_t cap_s, mi355_rho_opts *lo);
+
+// ---- multi-GPU u16 wire (DESIGN.md §5 "Residuals on the wire") ----
+// Whether a keys exchange (lo from keys_exchange_plan, lo->key_shift = log2 G) can send
+// 2-byte residuals instead: the local plan of nR x nS (the mean local sizes) is a
+// two-pass narrow counting RHO plan, and every 32-bit key's residual above the shard and
+// partition bits fits 16 bits (key_shift + bits >= 16).  SGXAMD_WIRE16=0 disables it.
+// Returns the plan's partition count P (0: no).
+uint32_t wire16_plan(uint64_t nR, uint64_t nS, int G, const mi355_rho_opts *lo);
+// Sender: partitions the keys this rank sends each destination (runs of packed u32
+// keys in `keys`: destination q's runs at run_off[q * runs + j], run_n[...]) with the
+// plan of wire16_plan(nR, nS, ...): destination q's residuals go to out16 + the keys of
+// destinations before q, grouped by partition; counts[q * (P + 1) + p] = its partition
+// p's keys, counts[q * (P + 1) + P] = its largest key.  Enqueued on s (no wait).
+int wire_partition(Context *ctx, hipStream_t s, const uint32_t *keys, int G, int runs, const uint64_t *run_off,
+                   const uint64_t *run_n, uint64_t nR, uint64_t nS, const mi355_rho_opts *lo, uint16_t *out16,
+                   uint64_t *counts, const char *tag);
+// Receiver: the counting join of the residuals the G senders sent (r16 / s16: sender
+// q's run at r_base[q] / s_base[q] u16 elements, their counts rows as wire_partition
+// wrote them; nR / nS residuals in all).  R's pieces are gathered after r_landed, S's
+// after s_landed (events on the communication stream), then the build/probe.
+// src_scratch: 2 * (G * P + G) u64.  Synchronises s; st as join_pipelined_finish.
+int join_wire16(Context *ctx, hipStream_t s, const uint16_t *r16, const uint64_t *r_cnt, const uint64_t *r_base,
+                uint64_t nR, const uint16_t *s16, const uint64_t *s_cnt, const uint64_t *s_base, uint64_t nS, int G,
+                const mi355_rho_opts *lo, uint64_t *src_scratch, hipEvent_t r_landed, hipEvent_t s_landed,
+                mi355_rho_stats *st);
 // Tests: enqueue `us` microseconds of waiting on stream s (rho_kernels.hip k_spin).
 hipError_t launch_spin(uint32_t us, hipStream_t s);
 // What mi355_last_join_stats reports for this thread's last join (multi-GPU calls).

@@ -107,6 +107,12 @@ Policy choose_policy(uint64_t nR, uint64_t nS, const mi355_rho_opts *o) {
     } else {
         // odd bit counts: the larger digit in pass 1
         p.b1 = (p.bits + 1) / 2;
+        static const int forced_b1 = [] {  // SGXAMD_PASS1_BITS: development A/B of the split
+            const char *e = std::getenv("SGXAMD_PASS1_BITS");
+            return e ? std::atoi(e) : 0;
+        }();
+        if (forced_b1 > 0 && (uint32_t)forced_b1 < p.bits && p.bits - (uint32_t)forced_b1 <= 8)
+            p.b1 = (uint32_t)forced_b1;
         p.b2 = p.bits - p.b1;
     }
     // chain table large enough that the average partition needs one R chunk
@@ -252,11 +258,12 @@ struct RelPlan {
     } while (0)
 
 // Pooled two-pass partition of one relation (pass 1 when !pass2_now, else pass 2).
+// arena: where rp's scratch lives (null: the context's join scratch)
 int partition_relation_pooled(Context *ctx, hipStream_t s, Timer &tm, const std::string &t, const row_t *in,
                               row_t *t1, row_t *t2, uint8_t *side, RelPlan &rp, const Policy &pol, uint32_t key_shift,
                               const row_t **final_rel, const uint64_t **pstart, const uint64_t **pcnt,
-                              bool pass2_now) {
-    Arena &A = ctx->scratch;
+                              bool pass2_now, Arena *arena = nullptr) {
+    Arena &A = arena ? *arena : ctx->scratch;
     uint64_t *start1 = A.at<uint64_t>(rp.start1);
     uint64_t *cnt1 = A.at<uint64_t>(rp.cnt1);
     uint32_t *segbase2 = A.at<uint32_t>(rp.segbase2);
@@ -583,8 +590,10 @@ PendingJoin &pending_of(const Context *ctx) {
 // may start after S has been produced later in the stream order of s (multi-GPU:
 // R's local passes run while S is still being exchanged).  Caller holds ctx->mu.
 // Policy, workspace and scratch layout of a join of nR x nS tuples (no launches).
+// wire16: the partitions arrive as narrow residuals (the multi-GPU u16 wire, join_wire16):
+// the 16,384-key table and the narrow join, whatever the received sizes.
 int plan_join(Context *ctx, hipStream_t s, uint64_t nR, uint64_t nS, const mi355_rho_opts *opts, PendingJoin &pj,
-              const std::vector<uint64_t> *s_pieces = nullptr) {
+              const std::vector<uint64_t> *s_pieces = nullptr, bool wire16 = false) {
     pj = PendingJoin{};
     pj.s = s;
     pj.nR = nR;
@@ -626,8 +635,8 @@ int plan_join(Context *ctx, hipStream_t s, uint64_t nR, uint64_t nS, const mi355
     // 4: 4096 R and 32,768 S keys per partition read R once per partition instead of once
     // per 8192-key S chunk); enough partitions that one task each fills the chip
     const uint64_t avgR = (nR + P - 1) / P, avgS = (nS + P - 1) / P;
-    if (uses_big_table(opts) && ((pol.rcap == 8192 && avgR > 8192) ||
-                                 (P >= 8192 && avgS > kSChunk && avgR <= kBigRcap && opts_free_bits(opts)))) {
+    if (wire16 || (uses_big_table(opts) && ((pol.rcap == 8192 && avgR > 8192) ||
+                                            (P >= 8192 && avgS > kSChunk && avgR <= kBigRcap && opts_free_bits(opts))))) {
         pj.pol.rcap = kBigRcap;
         // S-heavy plans (BASELINE config 4: 65,536 S keys per partition) probe a
         // partition in one task: 7.24-7.35 vs 7.46-7.52 ms per join with two 32,768-key
@@ -639,12 +648,17 @@ int plan_join(Context *ctx, hipStream_t s, uint64_t nR, uint64_t nS, const mi355
     // 16,384-key table (k_sort_blk writes them, k_join_x reads them)
     const bool narrow = pool == kPoolKeys && counting && pj.algo == kAlgoChaining && pj.pol.rcap == kBigRcap &&
                         pol.passes == 2 && sort2_enabled() && narrow_enabled();
+    if (wire16 && !narrow) {
+        set_last_error("u16 wire: the received partitions need the narrow counting plan");
+        return MI355_ERR_INVALID;
+    }
     pj.pr.narrow = pj.ps.narrow = narrow;
     // ... and pass 1 writes them first as a narrow pool (u16 residuals, read by
     // k_place_seg with their digit side stream); the chain-histogram layout keeps keys,
     // and so do pass-1 digits above 7 bits (the narrow pool's 64-residual granules keep
     // up to 63 carried keys per digit in LDS: 64 KiB at 8 bits, one workgroup per CU)
-    const bool n16 = narrow && pol.b1 <= 7 && uses_digit_side(pol) && place_enabled() && narrow_pool_enabled();
+    const bool n16 = narrow && !wire16 && pol.b1 <= 7 && uses_digit_side(pol) && place_enabled() &&
+                     narrow_pool_enabled();
     pj.pr.narrow16 = n16 && !pj.pr.chain;
     pj.ps.narrow16 = n16 && !pj.ps.chain;
     pj.over_cap = (uint32_t)(nS / pj.s_chunk + 1);
@@ -752,8 +766,15 @@ void fill_join_stats(const Context *ctx, const PendingJoin &pj, const Timer &tm,
 // Second half: S's partition passes, build/probe (and materialisation), then the
 // result read-back.  fork_now: the side stream (overlap on) forks from s here instead
 // of at join_begin, because S only became valid in between.
+// given_s (nullable): S's partitions are already there (fS, part starts, part counts;
+// the u16 wire's gathered residuals): no S passes.
+struct GivenParts {
+    const row_t *f;
+    const uint64_t *ps, *pc;
+};
 int join_finish(Context *ctx, PendingJoin &pj, const row_t *dS, uint64_t nS, mi355_rho_stats *st,
-                output_triple_t *out, uint64_t out_cap, DeviceBuffer *grow, bool fork_now) {
+                output_triple_t *out, uint64_t out_cap, DeviceBuffer *grow, bool fork_now,
+                const GivenParts *given_s = nullptr) {
     if (!pj.active) {
         set_last_error("join_finish without join_begin");
         return MI355_ERR_INVALID;
@@ -779,11 +800,17 @@ int join_finish(Context *ctx, PendingJoin &pj, const row_t *dS, uint64_t nS, mi3
     const row_t *fS = nullptr;
     const uint64_t *psS = nullptr, *pcS = nullptr;
     int rc;
-    for (int pass = 0; pass < (int)pol.passes; ++pass)
-        if ((rc = partition_relation(ctx, sS, tmS, "S_", dS, ctx->t1S.as<row_t>(), ctx->t2S.as<row_t>(),
-                                     ctx->sideS.as<uint8_t>(), pj.ps, pol, pj.key_shift, &fS, &psS, &pcS,
-                                     pass == 1)))
-            return rc;
+    if (given_s) {
+        fS = given_s->f;
+        psS = given_s->ps;
+        pcS = given_s->pc;
+    } else {
+        for (int pass = 0; pass < (int)pol.passes; ++pass)
+            if ((rc = partition_relation(ctx, sS, tmS, "S_", dS, ctx->t1S.as<row_t>(), ctx->t2S.as<row_t>(),
+                                         ctx->sideS.as<uint8_t>(), pj.ps, pol, pj.key_shift, &fS, &psS, &pcS,
+                                         pass == 1)))
+                return rc;
+    }
     if (s2) {
         tm2.end_call();
         RHO_HIP(hipEventRecord(ctx->ev_join, s2));
@@ -1134,6 +1161,142 @@ bool keys_exchange_plan(uint64_t nR, uint64_t nS, uint64_t cap_r, uint64_t cap_s
     }
     const Policy p = choose_policy(nR, nS, lo);
     return pool_fits(cap_r, p) && pool_fits(cap_s, p) && lo->key_shift + p.bits <= 31;
+}
+
+// ---------------------------------------------------------------- multi-GPU u16 wire
+// The exchange's sender runs the receiver's two partition passes (the same plan: both
+// derive it from the global sizes) on the keys it sends each destination, so that the
+// destination's shard bits and partition bits are implied by where a key lands and only
+// its residual above them travels: 2 bytes instead of 4.  The receiver gathers each
+// partition's pieces (one per sender, wire_kernels.hip) and runs the build/probe.
+uint32_t wire16_plan(uint64_t nR, uint64_t nS, int G, const mi355_rho_opts *lo) {
+    static const bool on = [] {
+        const char *e = std::getenv("SGXAMD_WIRE16");
+        return !(e && std::atoi(e) == 0);
+    }();
+    if (!on || !lo || lo->materialize || lo->algorithm == MI355_ALGO_RHT || G < 2 || (uint32_t)G > kWireMaxG)
+        return 0;
+    if (!(keys_enabled() && narrow_enabled() && sort2_enabled())) return 0;
+    const Policy p = choose_policy(nR, nS, lo);
+    // every 32-bit key's residual fits 16 bits: no device-side width check can differ
+    if (p.passes != 2 || !uses_digit_side(p) || lo->key_shift + p.bits < 16 || lo->key_shift + p.bits > 31) return 0;
+    return 1u << p.bits;
+}
+
+int wire_partition(Context *ctx, hipStream_t s, const uint32_t *keys, int G, int runs, const uint64_t *run_off,
+                   const uint64_t *run_n, uint64_t nR, uint64_t nS, const mi355_rho_opts *lo, uint16_t *out16,
+                   uint64_t *counts, const char *tag) {
+    if (pending_of(ctx).active) {
+        set_last_error("wire_partition while a pipelined join is pending on this device");
+        return MI355_ERR_INVALID;
+    }
+    const Policy pol = choose_policy(nR, nS, lo);
+    const uint32_t P = 1u << pol.bits;
+    // a scratch of its own: the shard pieces' plans in ctx->scratch stay valid for the
+    // other relation's scatters, which follow this relation's passes in the stream
+    Arena &A = ctx->wscratch;
+    // every destination's plan first: the arena and the pools sized for the largest, so
+    // that no buffer grows while the loop's launches are queued
+    std::vector<std::vector<uint64_t>> pn((size_t)G);
+    std::vector<uint64_t> nq((size_t)G, 0);
+    size_t arena = 0;
+    uint64_t t1max = 0;
+    RelPlan rp{};
+    for (int q = 0; q < G; ++q) {
+        pn[q].assign(run_n + (size_t)q * runs, run_n + (size_t)(q + 1) * runs);
+        for (uint64_t x : pn[q]) nq[q] += x;
+        if (!nq[q]) continue;
+        if (!pool_fits(nq[q], pol, (uint64_t)runs)) {
+            set_last_error("u16 wire: a destination's keys do not fit the pooled plan");
+            return MI355_ERR_INVALID;
+        }
+        A.reset();
+        plan_relation(A, rp, nq[q], pol, kPoolKeys, &pn[q]);
+        arena = std::max(arena, A.used);
+        t1max = std::max(t1max, rp.t1_tuples);
+    }
+    RHO_HIP(A.buf.ensure(std::max<size_t>(arena, 256)));
+    RHO_HIP(ctx->t1R.ensure(std::max<uint64_t>(t1max, 1) * sizeof(row_t)));
+    RHO_HIP(ctx->sideR.ensure(std::max<uint64_t>(t1max, 16)));
+    Timer &tm = thread_timer();
+    tm.begin_call(s, false);
+    const std::string t = tag;
+    uint64_t doff = 0;
+    for (int q = 0; q < G; ++q) {
+        uint64_t *cq = counts + (size_t)q * (P + 1);
+        if (!nq[q]) {
+            RHO_HIP(hipMemsetAsync(cq, 0, sizeof(uint64_t) * (P + 1), s));
+            continue;
+        }
+        A.reset();
+        plan_relation(A, rp, nq[q], pol, kPoolKeys, &pn[q]);
+        for (int j = 0; j < runs; ++j) rp.piece_off[j] = run_off[(size_t)q * runs + j];
+        rp.narrow = true;  // wire16_plan: every residual fits 16 bits
+        rp.narrow16 = false;
+        rp.in_size = sizeof(uint32_t);
+        const row_t *f = nullptr;
+        const uint64_t *pst = nullptr, *pcn = nullptr;
+        for (int pass = 0; pass < 2; ++pass) {
+            const int rc = partition_relation_pooled(
+                ctx, s, tm, t, reinterpret_cast<const row_t *>(keys), ctx->t1R.as<row_t>(),
+                reinterpret_cast<row_t *>(out16 + doff), ctx->sideR.as<uint8_t>(), rp, pol, lo->key_shift, &f, &pst,
+                &pcn, pass == 1, &A);
+            if (rc) return rc;
+        }
+        RHO_HIP(hipMemcpyAsync(cq, pcn, sizeof(uint64_t) * P, hipMemcpyDeviceToDevice, s));
+        RHO_HIP(hipMemsetAsync(cq + P, 0, sizeof(uint64_t), s));
+        RHO_HIP(hipMemcpyAsync(cq + P, A.at<uint32_t>(rp.kmax) + rp.nseg1, sizeof(uint32_t), hipMemcpyDeviceToDevice,
+                               s));
+        doff += nq[q];
+    }
+    tm.end_call();
+    return MI355_OK;
+}
+
+int join_wire16(Context *ctx, hipStream_t s, const uint16_t *r16, const uint64_t *r_cnt, const uint64_t *r_base,
+                uint64_t nR, const uint16_t *s16, const uint64_t *s_cnt, const uint64_t *s_base, uint64_t nS, int G,
+                const mi355_rho_opts *lo, uint64_t *src_scratch, hipEvent_t r_landed, hipEvent_t s_landed,
+                mi355_rho_stats *st) {
+    PendingJoin &pj = pending_of(ctx);
+    if (pj.active) {
+        set_last_error("a pipelined join is already pending on this context");
+        return MI355_ERR_INVALID;
+    }
+    if (G < 1 || (uint32_t)G > kWireMaxG) {
+        set_last_error("u16 wire: unsupported world size");
+        return MI355_ERR_INVALID;
+    }
+    int rc = plan_join(ctx, s, nR, nS, lo, pj, nullptr, true);
+    if (rc) return rc;
+    const uint32_t P = 1u << pj.pol.bits;
+    Arena &A = ctx->scratch;
+    Timer &tm = thread_timer();
+    const bool per_kernel = thread_timing_enabled() || (lo && lo->timing);
+    tm.begin_call(s, true, !per_kernel);
+    WireBases br{}, bs{};
+    for (int q = 0; q < G; ++q) {
+        br.b[q] = r_base[q];
+        bs.b[q] = s_base[q];
+    }
+    br.b[G] = nR;
+    bs.b[G] = nS;
+    uint16_t *mR = ctx->t2R.as<uint16_t>(), *mS = ctx->t2S.as<uint16_t>();
+    uint64_t *psR = A.at<uint64_t>(pj.pr.pstart), *pcR = A.at<uint64_t>(pj.pr.pcnt);
+    uint64_t *psS = A.at<uint64_t>(pj.ps.pstart), *pcS = A.at<uint64_t>(pj.ps.pcnt);
+    RHO_HIP(hipStreamWaitEvent(s, r_landed, 0));
+    tm.mark("R_wire_merge");
+    RHO_HIP(launch_wire_merge(r16, r_cnt, (uint32_t)G, P, br, src_scratch, psR, pcR,
+                              A.at<uint32_t>(pj.pr.kmax) + pj.pr.nseg1, mR, s));
+    RHO_HIP(hipStreamWaitEvent(s, s_landed, 0));
+    tm.mark("S_wire_merge");
+    RHO_HIP(launch_wire_merge(s16, s_cnt, (uint32_t)G, P, bs, src_scratch + (size_t)G * P + G, psS, pcS,
+                              A.at<uint32_t>(pj.ps.kmax) + pj.ps.nseg1, mS, s));
+    pj.fR = reinterpret_cast<const row_t *>(mR);
+    pj.psR = psR;
+    pj.pcR = pcR;
+    pj.active = true;
+    const GivenParts gs{reinterpret_cast<const row_t *>(mS), psS, pcS};
+    return join_finish(ctx, pj, nullptr, nS, st, nullptr, 0, nullptr, false, &gs);
 }
 
 // Stable partition by destination shard (multi-GPU exchange step).

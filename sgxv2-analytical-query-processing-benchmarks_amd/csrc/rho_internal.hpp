@@ -309,5 +309,18 @@ hipError_t launch_excl_scan(const uint64_t *in, const uint32_t *n_extra, uint64_
 hipError_t launch_reduce(const uint64_t *partials, uint32_t n, uint64_t *result, const uint64_t *cyc, uint32_t ncyc,
                          hipStream_t s);
 
+// Multi-GPU u16 wire (wire_kernels.hip): in = the G senders' runs of u16 residuals, run q
+// at bases.b[q] (b[G] = their total), each grouped by partition; cnt = G rows of P
+// partition counts and the sender's largest key.  Gathers every partition's G pieces
+// into out (contiguous partitions: ps / pc), *narrow = the largest key; a row whose
+// counts do not add up to its run is left out.  src: G * P + G u64 of scratch.
+constexpr uint32_t kWireMaxG = 64;
+struct WireBases {
+    uint64_t b[kWireMaxG + 1];
+};
+hipError_t launch_wire_merge(const uint16_t *in, const uint64_t *cnt, uint32_t G, uint32_t P, const WireBases &bases,
+                             uint64_t *src, uint64_t *ps, uint64_t *pc, uint32_t *narrow, uint16_t *out,
+                             hipStream_t s);
+
 }  // namespace rho
 }  // namespace sgxamd

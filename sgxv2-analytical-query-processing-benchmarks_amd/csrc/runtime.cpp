@@ -169,11 +169,12 @@ void release_workspace(Context *ctx) {
     for (DeviceBuffer *b : {&ctx->inR, &ctx->inS, &ctx->t1R, &ctx->t1S, &ctx->t2R, &ctx->t2S, &ctx->sideR, &ctx->sideS,
                             &ctx->scratch.buf, &ctx->mat, &ctx->tp_mask, &ctx->tp_blk, &ctx->tp_trip, &ctx->scan_in,
                             &ctx->scan_out, &ctx->scan_aux, &ctx->scan_dict, &ctx->xsendR, &ctx->xsendS, &ctx->xrecvR,
-                            &ctx->xrecvS})
+                            &ctx->xrecvS, &ctx->wsendR, &ctx->wsendS, &ctx->wrecvR, &ctx->wrecvS, &ctx->wscratch.buf})
         b->release();
     for (DeviceBuffer &b : ctx->tp_cols) b.release();
     for (DeviceBuffer &b : ctx->tp_rel) b.release();
     ctx->scratch.reset();
+    ctx->wscratch.reset();
 }
 
 hipStream_t thread_stream(Context *ctx, void *explicit_stream) {

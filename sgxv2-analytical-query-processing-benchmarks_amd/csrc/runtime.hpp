@@ -93,6 +93,10 @@ struct Context {
     // multi-GPU exchange workspace (multi_host.cpp): shard-partitioned send buffers and
     // the receive buffers the peers' pieces land in
     DeviceBuffer xsendR, xsendS, xrecvR, xrecvS;
+    // the u16 wire: residuals grouped by destination and partition, then the partition
+    // counts rows (send); the senders' runs, their counts rows and the gather's scratch (receive)
+    DeviceBuffer wsendR, wsendS, wrecvR, wrecvS;
+    Arena wscratch;  // the u16 wire's sender-side passes (rho::wire_partition)
     // in-launch hand-off words (tickets, digit totals) of the small-join path: zeroed
     // once when allocated (rho_internal.hpp kSync*)
     DeviceBuffer sync;

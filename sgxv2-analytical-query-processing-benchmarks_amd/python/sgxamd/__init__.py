@@ -453,12 +453,13 @@ def multi_comm_destroy(handle: int) -> None:
     _check(lib.mi355_multi_comm_destroy(handle))
 
 
-def rho_join_sharded(handle: int, R, nR: int, S, nS: int, *, algorithm: str = "RHO", out=None,
-                     out_capacity: int = 0) -> JoinResult:
+def rho_join_sharded(handle: int, R, nR: int, S, nS: int, *, algorithm: str = "RHO", radix_bits: int = 0,
+                     passes: int = 0, out=None, out_capacity: int = 0) -> JoinResult:
     """One rank's part of the multi-GPU join (collective; device-resident slices).  With
     `out` the join materialises and this rank's own triples (stats["local_matches"] of
-    them) are written to it."""
-    o = rho_opts(0, 0, 0, 1 if out is not None else 0, 0, ALGORITHMS[algorithm], None,
+    them) are written to it.  radix_bits / passes: the local joins' plan (every rank the
+    same; 0 = from the global sizes)."""
+    o = rho_opts(radix_bits, passes, 0, 1 if out is not None else 0, 0, ALGORITHMS[algorithm], None,
                  ptr(out) if out is not None else None, out_capacity)
     st = multi_stats()
     _check(lib.mi355_rho_join_sharded(handle, ptr(R), nR, ptr(S), nS, C.byref(o), C.byref(st)))

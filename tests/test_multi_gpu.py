@@ -78,9 +78,12 @@ def test_keys_only_exchange(sgx, orc, gpu, g, n, kw):
     res = multi(sgx, R, S, g, **kw)
     assert res.matches == exp
     st = res.stats
-    assert st["elem_bytes"] == 4 and st["local"]["layout"] in (2, 3, 4)
-    # every key of a rank except those it keeps goes out once, 4 bytes each
-    assert 4 * (2 * n) * (g - 1) // g * 0.9 < st["sent_bytes"] <= 4 * 2 * n
+    # 2-byte residuals when every key's residual above the shard and partition bits fits
+    # 16 bits (the forced 14-bit plan over 8 ranks), else 4-byte keys
+    wire16 = (g.bit_length() - 1) + st["local"]["radix_bits"] >= 16
+    assert st["elem_bytes"] == (2 if wire16 else 4) and st["local"]["layout"] in (2, 3, 4)
+    # every key of a rank except those it keeps goes out once
+    assert st["sent_bytes"] == _exchange_bytes(st, _keys_out(R, g) + _keys_out(S, g), g)
     # RHT counts over key partitions too (SGXAMD_KEYS=0 in test_paths_gpu keeps tuples)
     rht = multi(sgx, R, S, g, algorithm="RHT", **kw)
     assert rht.matches == exp and rht.stats["elem_bytes"] == 4
@@ -239,21 +242,72 @@ def test_rccl_single_rank_local_failure_keeps_handle(sgx, orc, gpu):
         sgx.multi_comm_destroy(h)
 
 
+@pytest.mark.parametrize("kw", [{}, {"radix_bits": 14, "passes": 2}], ids=["keys", "wire16"])
 @pytest.mark.parametrize("step", [1, 2, 3])
-def test_failure_on_one_rank(sgx, orc, gpu, step):
+def test_failure_on_one_rank(sgx, orc, gpu, step, kw):
     """A rank that fails (exchange buffers, a shard pass of S, its local join) flags it in
     the next collective: every rank leaves the join at the same step, the call returns
     the failed rank's own error (no rank is left waiting in a collective), and the next
-    join on the same transport is exact."""
+    join on the same transport is exact.  Also on the u16 wire (a 14-bit plan over 4
+    ranks), whose sender-side passes and gathers take the local join's place."""
     R, S = sgx.reference_relations(1 << 17, (1 << 17) + 5)
     exp = orc.rho_join(R, S, 4)[0]
     sgx.multi_inject_failure(2, step)
     try:
         with pytest.raises(sgx.Mi355Error, match="rank 2: injected failure"):
-            multi(sgx, R, S, 4)
+            multi(sgx, R, S, 4, **kw)
     finally:
         sgx.multi_inject_failure(-1, 0)
-    assert multi(sgx, R, S, 4).matches == exp
+    res = multi(sgx, R, S, 4, **kw)
+    assert res.matches == exp and (res.stats["elem_bytes"] == 2 or not kw)
+
+
+def _keys_out(rel_, g):
+    """Keys of a host relation that leave their rank's slice (_slices_sent, one per key)."""
+    import torch
+
+    keys = rel_["key"] if rel_.dtype.names else rel_ & 0xFFFFFFFF
+    return _slices_sent(torch.from_numpy(np.asarray(keys, dtype=np.int64)), g, 1)
+
+
+def _exchange_bytes(st, keys_out, g):
+    """sent_bytes of a counting join's keys exchange over all ranks of one process: 4 bytes
+    per key that leaves its rank, or on the u16 wire 2 bytes per key plus, per relation
+    and peer, the sender's counts row (P partition counts and its largest key, 8 bytes
+    each)."""
+    if st["elem_bytes"] == 2:
+        p = 1 << st["local"]["radix_bits"]
+        return 2 * keys_out + 2 * g * (g - 1) * (p + 1) * 8
+    assert st["elem_bytes"] == 4
+    return 4 * keys_out
+
+
+@pytest.mark.parametrize("g", [2, 4, 8])
+def test_wire16_exchange(sgx, orc, gpu, g):
+    """The u16 wire: with log2 g + the local radix bits >= 16, every
+    sender runs the receiver's two passes on the keys it sends each rank, and 2-byte
+    residuals travel with one counts row per relation and peer; each receiver gathers a
+    partition's g pieces (one per sender) and runs the narrow build/probe.  Exact counts
+    against the sort counter on pk / fk, on random keys with duplicates over the whole
+    u32 range (residuals up to 2^16: the windowed direct table), on a hot key, and on
+    sizes that leave some (sender, destination) runs empty; the exact bytes."""
+    bits = 16 - (g.bit_length() - 1)
+    rng = np.random.default_rng(g)
+    cases = [sgx.reference_relations(1 << 20, 1 << 20),
+             (rel(rng.integers(0, 2**32, 300_001, dtype=np.uint64).astype(np.uint32)),
+              rel(rng.integers(0, 2**32, 200_003, dtype=np.uint64).astype(np.uint32))),
+             (rel(rng.integers(0, 5000, 70_000, dtype=np.uint64).astype(np.uint32) * 8),
+              rel(np.full(90_000, 4096 * 8, dtype=np.uint32))),
+             (rel(np.arange(1, 3 * g + 1, dtype=np.uint32)), rel(np.arange(1, 2 * g + 2, dtype=np.uint32)))]
+    for R, S in cases:
+        R = np.concatenate([R, R[: len(R) // 3]])  # duplicate R keys too
+        exp = orc.count_join_sort(R, S)
+        res = multi(sgx, R, S, g, radix_bits=bits, passes=2)
+        st = res.stats
+        assert res.matches == exp, (g, len(R), len(S))
+        assert st["elem_bytes"] == 2 and st["local"]["radix_bits"] == bits
+        assert st["sent_bytes"] == _exchange_bytes(st, _keys_out(R, g) + _keys_out(S, g), g)
+        assert 0 <= st["ms_tail"] <= st["ms_total"]
 
 
 def _slices_sent(keys, g, elem):
@@ -288,12 +342,12 @@ def test_config4_rehearsal_full_size(sgx, gpu):
         res = sgx.rho_join_multi(R, nR, S, nS, g, transport="rehearsal")
         st = res.stats
         assert res.matches == nS
-        assert st["world"] == g and st["elem_bytes"] == 4 and st["local"]["layout"] in (2, 3, 4)
+        assert st["world"] == g and st["elem_bytes"] in (2, 4) and st["local"]["layout"] in (2, 3, 4)
         assert st["recv_r_max"] == st["recv_r_min"] == nR // g
         assert st["recv_s_max"] == st["recv_s_min"] == nS // g
-        sent = _slices_sent(R & 0xFFFFFFFF, g, 4) + _slices_sent(S & 0xFFFFFFFF, g, 4)
-        assert st["sent_bytes"] == sent
-        assert abs(sent - 4 * (nR + nS) * 7 / 8) < 4 * (nR + nS) * 0.001
+        keys_out = _slices_sent(R & 0xFFFFFFFF, g, 1) + _slices_sent(S & 0xFFFFFFFF, g, 1)
+        assert st["sent_bytes"] == _exchange_bytes(st, keys_out, g)
+        assert abs(keys_out - (nR + nS) * 7 / 8) < (nR + nS) * 0.001
         # S's pass 1 ran per landed piece: the device time after S's last piece is a part
         # of the local join (the rehearsal's ranks share one GPU, so only its presence is
         # checked, not its size)
@@ -325,7 +379,7 @@ def test_config5_rehearsal_full_size(sgx, gpu):
         res = sgx.rho_join_multi(R, n, S, n, g, transport="rehearsal")
         st = res.stats
         assert res.matches == n
-        assert st["elem_bytes"] == 4
+        assert st["elem_bytes"] == 2  # 3 shard + 14 partition bits: every residual fits 16 bits
         assert st["recv_r_max"] == st["recv_r_min"] == n // g
         per_rank = torch.bincount((S & (g - 1)).to(torch.int64), minlength=g)
         assert st["recv_s_max"] == int(per_rank.max()) and st["recv_s_min"] == int(per_rank.min())

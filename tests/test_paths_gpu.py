@@ -94,6 +94,40 @@ def test_switch_paths_match_oracle(env):
     assert r.returncode == 0 and "paths ok" in r.stdout, (env, r.stdout[-2000:], r.stderr[-2000:])
 
 
+# The multi-GPU u16 wire under the switches that change the sender's passes or the
+# receiver's build/probe (rehearsal transport, 4 ranks, a 14-bit plan): exact counts;
+# SGXAMD_WIRE16=0 (and SGXAMD_NARROW=0, which it needs) fall back to 4-byte keys.
+WIRE_CHILD = r"""
+import os
+import numpy as np
+import sgxamd, oracle
+dt = np.dtype([("key", "<u4"), ("payload", "<u4")])
+rng = np.random.default_rng(9)
+R = np.zeros(200_003, dtype=dt); R["key"] = rng.integers(0, 2**32, len(R), dtype=np.uint64).astype(np.uint32)
+S = np.zeros(300_007, dtype=dt); S["key"] = rng.integers(0, 2**32, len(S), dtype=np.uint64).astype(np.uint32)
+S[:70_000] = R[:70_000]
+Pk, Fk = sgxamd.reference_relations(1 << 20, 1 << 20, selectivity=50)
+off = os.environ.get("SGXAMD_WIRE16") == "0" or os.environ.get("SGXAMD_NARROW") == "0"
+for A, B in ((R, S), (Pk, Fk)):
+    for g in (4, 8):
+        r = sgxamd.rho_join_multi(A, len(A), B, len(B), g, transport="rehearsal", radix_bits=14, passes=2)
+        assert r.matches == oracle.count_join_sort(A, B), (g, r.matches)
+        assert r.stats["elem_bytes"] == (4 if off else 2), r.stats["elem_bytes"]
+print("wire ok")
+"""
+
+
+@pytest.mark.parametrize("env", [{"SGXAMD_WIRE16": "0"}, {"SGXAMD_NARROW": "0"}, {"SGXAMD_PLACE": "0"},
+                                 {"SGXAMD_JOIN_N": "0"}, {"SGXAMD_CHAIN_HIST": "1"}, {"SGXAMD_PASS1_BITS": "6"},
+                                 {"SGXAMD_POOL_SEGS": "3"}])
+def test_wire16_switches(env):
+    e = dict(os.environ, **env)
+    e["PYTHONPATH"] = os.pathsep.join([os.path.join(PKG, "python"), os.path.join(ROOT, "oracle"),
+                                       e.get("PYTHONPATH", "")])
+    r = subprocess.run([sys.executable, "-c", WIRE_CHILD], env=e, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "wire ok" in r.stdout, (env, r.stdout[-2000:], r.stderr[-2000:])
+
+
 # Chain histograms under skew (rho_kernels.hip launch_chain_fix / k_sort_blk's list path):
 # every S key has the same pass-1 digit, so with 8 pass-1 workgroups each chain holds
 # 2^19 keys (u16 counts wrap: the chain is recounted from its blocks) and a pass-2

@@ -137,7 +137,7 @@ def test_inprocess_config4_full_size(sgx, dbl, gpu):
     name another rank (counted on the device)."""
     import torch
 
-    from test_multi_gpu import _slices_sent
+    from test_multi_gpu import _exchange_bytes, _slices_sent
 
     nR, nS, g = 1 << 27, 1 << 30, 8
     R = torch.empty(nR, dtype=torch.int64, device=gpu)
@@ -149,10 +149,11 @@ def test_inprocess_config4_full_size(sgx, dbl, gpu):
         res = sgx.rho_join_multi(R, nR, S, nS, g, transport="rccl")
         st = res.stats
         assert res.matches == nS
-        assert st["transport"] == "rccl" and st["world"] == g and st["elem_bytes"] == 4
+        assert st["transport"] == "rccl" and st["world"] == g and st["elem_bytes"] in (2, 4)
         assert st["recv_r_max"] == st["recv_r_min"] == nR // g
         assert st["recv_s_max"] == st["recv_s_min"] == nS // g
-        assert st["sent_bytes"] == _slices_sent(R & 0xFFFFFFFF, g, 4) + _slices_sent(S & 0xFFFFFFFF, g, 4)
+        keys_out = _slices_sent(R & 0xFFFFFFFF, g, 1) + _slices_sent(S & 0xFFFFFFFF, g, 1)
+        assert st["sent_bytes"] == _exchange_bytes(st, keys_out, g)
         # the double's transfers are kernels on the communication streams (k_copy), so an
         # exchange starved of CUs by the join's own grids shows up here as time: the tail
         # after S's last piece landed is measured on every rank and stays a part of the step
@@ -166,7 +167,7 @@ def test_inprocess_config4_full_size(sgx, dbl, gpu):
 
 
 # ---------------------------------------------------------------- one "process" per GPU
-def sharded(sgx, R, S, g, *, handles=None, algorithm="RHO", timeout=120, outs=None):
+def sharded(sgx, R, S, g, *, handles=None, algorithm="RHO", timeout=120, outs=None, **kw_plan):
     """Rank r's slice of the device tensors R and S (radix_join.cpp:1488-1499 slicing)
     joined by G threads, each standing for one process with its own communicator
     (created here unless `handles` are given).  Returns (results, errors, handles)."""
@@ -188,7 +189,7 @@ def sharded(sgx, R, S, g, *, handles=None, algorithm="RHO", timeout=120, outs=No
             sa, sb = r * (nS // g), (nS if r == g - 1 else (r + 1) * (nS // g))
             kw = {} if outs is None else {"out": outs[r], "out_capacity": outs[r].shape[0]}
             res[r] = sgx.rho_join_sharded(handles[r], R[ra:rb], rb - ra, S[sa:sb], sb - sa, algorithm=algorithm,
-                                          **kw)
+                                          **kw, **kw_plan)
         except Exception as e:  # noqa: BLE001 - every rank's outcome is checked by the caller
             errs[r] = e
 
@@ -291,19 +292,54 @@ def test_sharded_keys_exchange_exact_bytes(sgx, dbl, gpu):
         assert {r.matches for r in res} == {nS}
         for r, x in enumerate(res):
             st = x.stats
-            assert st["elem_bytes"] == 4
+            assert st["elem_bytes"] in (2, 4)
             kept = 0
             for X in (R, S):
                 n = X.numel()
                 a, b = r * (n // g), (n if r == g - 1 else (r + 1) * (n // g))
                 k = X[a:b] & 0xFFFFFFFF
                 kept += int(((k & (g - 1)) != r).sum().item())
-            assert st["sent_bytes"] == 4 * kept
+            # u16 wire: 2 bytes per key and a counts row (P + 1 words) per relation and peer
+            rows = 2 * (g - 1) * ((1 << st["local"]["radix_bits"]) + 1) * 8
+            assert st["sent_bytes"] == (2 * kept + rows if st["elem_bytes"] == 2 else 4 * kept)
             assert st["recv_r_max"] == nR // g and st["recv_s_max"] == nS // g
     finally:
         destroy(sgx, hs)
         del R, S
         torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("g", [2, 4, 8])
+def test_wire16_rccl(sgx, orc, dbl, gpu, g):
+    """The u16 wire through RcclTransport (residuals as ncclUint8 pairs, counts rows as
+    ncclUint64), in one process and one "process" per rank: exact counts against the sort
+    counter on random keys with duplicates over the whole u32 range and on pk / fk, 2
+    bytes per key on the wire."""
+    import torch
+
+    from test_multi_gpu import _exchange_bytes, _keys_out
+
+    bits = 16 - (g.bit_length() - 1)
+    rng = np.random.default_rng(100 + g)
+    Rh = rel(rng.integers(0, 2**32, 300_001, dtype=np.uint64).astype(np.uint32))
+    Sh = rel(rng.integers(0, 2**32, 200_003, dtype=np.uint64).astype(np.uint32))
+    Sh = np.concatenate([Sh, Rh[:50_000]])  # matches and duplicates
+    exp = orc.count_join_sort(Rh, Sh)
+    res = multi(sgx, Rh, Sh, g, radix_bits=bits, passes=2)
+    st = res.stats
+    assert res.matches == exp and st["transport"] == "rccl" and st["elem_bytes"] == 2
+    assert st["sent_bytes"] == _exchange_bytes(st, _keys_out(Rh, g) + _keys_out(Sh, g), g)
+    Pk, Fk = sgx.reference_relations(1 << 20, 1 << 20)
+    R = torch.from_numpy(Pk.view(np.int64)).to(gpu)
+    S = torch.from_numpy(Fk.view(np.int64)).to(gpu)
+    out, errs, hs = sharded(sgx, R, S, g, radix_bits=bits, passes=2)
+    try:
+        assert errs == [None] * g, errs
+        assert {r.matches for r in out} == {1 << 20}
+        assert all(r.stats["elem_bytes"] == 2 for r in out)
+        assert sum(r.stats["local_matches"] for r in out) == 1 << 20
+    finally:
+        destroy(sgx, hs)
 
 
 @pytest.mark.parametrize("step", [1, 2, 3, 4, 5])
