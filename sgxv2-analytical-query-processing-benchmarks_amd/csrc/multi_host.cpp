@@ -533,7 +533,7 @@ int rank_streams(Context *ctx, int nev, RankStreams **out) {
 struct RankOut {
     uint64_t global = 0, local = 0, recv_r = 0, recv_s = 0, sent = 0;
     bool keys = false;       // the exchange moved keys only
-    bool wire16 = false;     // ... as 2-byte residuals of sender-side partitions (the u16 wire)
+    bool wire16 = false;     // S's keys as 2-byte residuals of sender-side partitions (the u16 wire)
     bool peer_fail = false;  // the call failed because another rank did
     bool together = false;   // the call failed at a collective every rank left at (the
                              // sequence is intact; nothing to abort)
@@ -658,22 +658,20 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
     if (o.keys) lo = kl;  // the local policy fixed from the global sizes
     const uint32_t P16 = o.wire16 ? rho::wire16_plan(sum[0] / G, sum[1] / G, G, &lo) : 0;
     const size_t elem = o.keys ? sizeof(uint32_t) : sizeof(row_t);
-    // u16 wire buffers: [residuals (256-B aligned)][G counts rows of P16 + 1 words]; the
-    // receive side of R also holds the gather's scratch (2 G P16 words)
+    // u16 wire buffers (S): [residuals (256-B aligned)][G counts rows of P16 + 1 words];
+    // the receive side also holds the gather's scratch (rho::wire_scratch_u64)
     const auto res_bytes = [](uint64_t n) { return (std::max<uint64_t>(n, 1) * 2 + 255) & ~uint64_t(255); };
     const uint64_t rows = (uint64_t)G * (P16 + 1) * sizeof(uint64_t);
     if (fail_rc == MI355_OK) {
         hipError_t e = ctx->xsendR.ensure(std::max<uint64_t>(nR, 1) * elem);
         if (e == hipSuccess) e = ctx->xsendS.ensure(std::max<uint64_t>(nS, 1) * elem);
+        if (e == hipSuccess) e = ctx->xrecvR.ensure(std::max<uint64_t>(cR, 1) * elem);
         if (!o.wire16) {
-            if (e == hipSuccess) e = ctx->xrecvR.ensure(std::max<uint64_t>(cR, 1) * elem);
             if (e == hipSuccess) e = ctx->xrecvS.ensure(std::max<uint64_t>(cS, 1) * elem);
         } else {
-            if (e == hipSuccess) e = ctx->wsendR.ensure(res_bytes(nR) + rows);
             if (e == hipSuccess) e = ctx->wsendS.ensure(res_bytes(nS) + rows);
             if (e == hipSuccess)
-                e = ctx->wrecvR.ensure(res_bytes(cR) + rows + 2 * ((uint64_t)G * P16 + G) * sizeof(uint64_t));
-            if (e == hipSuccess) e = ctx->wrecvS.ensure(res_bytes(cS) + rows);
+                e = ctx->wrecvS.ensure(res_bytes(cS) + rows + rho::wire_scratch_u64(G, P16) * sizeof(uint64_t));
         }
         if (e != hipSuccess) {
             set_last_error(std::string("exchange buffers (") + std::to_string((2 * (nR + nS) + cR + cS) * elem) +
@@ -712,53 +710,9 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
     // failure from here on is flagged at the final all-reduce
     uint64_t total[2] = {0, 0};
     std::vector<uint64_t> s_piece(K, 0);  // S tuples landing per piece (S's local pass 1 runs per piece)
-    std::array<std::vector<uint64_t>, 2> wbase;  // u16 wire: where sender q's run lands
-    if (o.wire16) {
-        // per relation: its pieces' shard scatters, the receiver's two passes over the
-        // keys for each destination (its runs: one per piece), then the counts rows and
-        // the residuals posted; S's scatters and passes run while R is on the wire
-        for (int rel = 0; rel < 2; ++rel) {
-            for (int i = 0; i < K && fail_rc == MI355_OK; ++i)
-                fail(rho::shard_scatter_piece(ctx, s, rel * K + i,
-                                              (rel ? ctx->xsendS : ctx->xsendR).as<char>() + pa[rel * K + i] * elem));
-            DeviceBuffer &ws = rel ? ctx->wsendS : ctx->wsendR, &wr = rel ? ctx->wrecvS : ctx->wrecvR;
-            uint16_t *snd16 = ws.as<uint16_t>();
-            uint64_t *scnt = reinterpret_cast<uint64_t *>(ws.as<char>() + res_bytes(nrel[rel]));
-            uint64_t *rcnt = reinterpret_cast<uint64_t *>(wr.as<char>() + res_bytes(rel ? cS : cR));
-            std::vector<uint64_t> roff((size_t)G * K), rn((size_t)G * K), s16(G, 0), r16(G, 0);
-            for (int q = 0; q < G; ++q)
-                for (int i = 0; i < K; ++i) {
-                    const int j = rel * K + i;
-                    uint64_t off = pa[j];
-                    for (int d = 0; d < q; ++d) off += sc[(size_t)j * G + d];
-                    roff[(size_t)q * K + i] = off;
-                    rn[(size_t)q * K + i] = sc[(size_t)j * G + q];
-                    s16[q] += sc[(size_t)j * G + q];
-                    r16[q] += rc[(size_t)j * G + q];
-                }
-            if (fail_rc == MI355_OK)
-                fail(rho::wire_partition(ctx, s, (rel ? ctx->xsendS : ctx->xsendR).as<uint32_t>(), G, K, roff.data(),
-                                         rn.data(), sum[0] / G, sum[1] / G, &lo, snd16, scnt, rel ? "wireS_" : "wireR_"));
-            // a failed rank still sends (the sizes are agreed): zero counts rows, which
-            // no receiver takes (they do not add up to the announced runs)
-            if (fail_rc != MI355_OK && ws.ptr) (void)hipMemsetAsync(scnt, 0, rows, s);
-            hipEvent_t ready = rs->ev[rel];
-            hip_ok(hipEventRecord(ready, s), "hipEventRecord (residuals ready)");
-            const std::vector<uint64_t> crow(G, (uint64_t)P16 + 1);
-            MH_RC(transport_rc(T.post_exchange(rank, rs->comm, ready, scnt, crow.data(), rcnt, crow.data(),
-                                               sizeof(uint64_t))));
-            MH_RC(transport_rc(T.post_exchange(rank, rs->comm, ready, snd16, s16.data(), wr.ptr, r16.data(),
-                                               sizeof(uint16_t))));
-            wbase[rel].assign(G, 0);
-            for (int q = 0; q < G; ++q) {
-                wbase[rel][q] = total[rel];
-                total[rel] += r16[q];
-                if (q != rank) o.sent += s16[q] * sizeof(uint16_t) + crow[q] * sizeof(uint64_t);
-            }
-            hip_ok(hipEventRecord(rs->ev[2 * K + rel], rs->comm), "hipEventRecord (relation landed)");
-        }
-    }
-    for (int j = 0; j < M && !o.wire16; ++j) {
+    std::vector<uint64_t> wbase;  // u16 wire: where sender q's run of S residuals lands
+    // (u16 wire: R's pieces only; S follows below)
+    for (int j = 0; j < (o.wire16 ? K : M); ++j) {
         const int rel = j / K;
         char *snd = (rel ? ctx->xsendS : ctx->xsendR).as<char>() + pa[j] * elem;
         char *rcv = (rel ? ctx->xrecvS : ctx->xrecvR).as<char>() + total[rel] * elem;
@@ -778,6 +732,48 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
         if ((j + 1) % K == 0)
             hip_ok(hipEventRecord(rs->ev[2 * K + rel], rs->comm), "hipEventRecord (relation landed)");
     }
+    if (o.wire16) {
+        // S on the u16 wire: its pieces' shard scatters, then the receiver's two passes
+        // over the keys for each destination (its runs: one per piece), the counts rows
+        // and the residuals posted -- all while R's keys are on the wire; R's local
+        // passes then run while S's residuals are (DESIGN.md §5 "Residuals on the wire")
+        for (int i = 0; i < K && fail_rc == MI355_OK; ++i)
+            fail(rho::shard_scatter_piece(ctx, s, K + i, ctx->xsendS.as<char>() + pa[K + i] * elem));
+        uint16_t *snd16 = ctx->wsendS.as<uint16_t>();
+        uint64_t *scnt = reinterpret_cast<uint64_t *>(ctx->wsendS.as<char>() + res_bytes(nS));
+        uint64_t *rcnt = reinterpret_cast<uint64_t *>(ctx->wrecvS.as<char>() + res_bytes(cS));
+        std::vector<uint64_t> roff((size_t)G * K), rn((size_t)G * K), s16(G, 0), r16(G, 0);
+        for (int q = 0; q < G; ++q)
+            for (int i = 0; i < K; ++i) {
+                const int j = K + i;
+                uint64_t off = pa[j];
+                for (int d = 0; d < q; ++d) off += sc[(size_t)j * G + d];
+                roff[(size_t)q * K + i] = off;
+                rn[(size_t)q * K + i] = sc[(size_t)j * G + q];
+                s16[q] += sc[(size_t)j * G + q];
+                r16[q] += rc[(size_t)j * G + q];
+            }
+        if (fail_rc == MI355_OK)
+            fail(rho::wire_partition(ctx, s, ctx->xsendS.as<uint32_t>(), G, K, roff.data(), rn.data(), sum[0] / G,
+                                     sum[1] / G, &lo, snd16, scnt, "wireS_"));
+        // a failed rank still sends (the sizes are agreed): zero counts rows, which no
+        // receiver takes (they do not add up to the announced runs)
+        if (fail_rc != MI355_OK && ctx->wsendS.ptr) (void)hipMemsetAsync(scnt, 0, rows, s);
+        hipEvent_t ready = rs->ev[K];
+        hip_ok(hipEventRecord(ready, s), "hipEventRecord (residuals ready)");
+        const std::vector<uint64_t> crow(G, (uint64_t)P16 + 1);
+        MH_RC(transport_rc(
+            T.post_exchange(rank, rs->comm, ready, scnt, crow.data(), rcnt, crow.data(), sizeof(uint64_t))));
+        MH_RC(transport_rc(
+            T.post_exchange(rank, rs->comm, ready, snd16, s16.data(), ctx->wrecvS.ptr, r16.data(), sizeof(uint16_t))));
+        wbase.assign(G, 0);
+        for (int q = 0; q < G; ++q) {
+            wbase[q] = total[1];
+            total[1] += r16[q];
+            if (q != rank) o.sent += s16[q] * sizeof(uint16_t) + crow[q] * sizeof(uint64_t);
+        }
+        hip_ok(hipEventRecord(rs->ev[2 * K + 1], rs->comm), "hipEventRecord (S landed)");
+    }
     const bool timed = hipEventRecord(rs->t_land, rs->comm) == hipSuccess;
     o.recv_r = total[0];
     o.recv_s = total[1];
@@ -787,18 +783,21 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
     // local join: R's passes once R has landed, S's passes and build/probe once S has.
     // Every failure from here on is this rank's own and is flagged in the final all-reduce.
     if (fail_rc == MI355_OK && o.wire16) {
-        if (total[0] && total[1]) {
-            const uint64_t *rcR = reinterpret_cast<const uint64_t *>(ctx->wrecvR.as<char>() + res_bytes(cR));
-            const uint64_t *rcS = reinterpret_cast<const uint64_t *>(ctx->wrecvS.as<char>() + res_bytes(cS));
-            uint64_t *src = const_cast<uint64_t *>(rcR) + (size_t)G * (P16 + 1);
-            const int lrc = injected(rank, kFailLocal)
-                                ? MI355_ERR_OOM
-                                : rho::join_wire16(ctx, s, ctx->wrecvR.as<uint16_t>(), rcR, wbase[0].data(), total[0],
-                                                   ctx->wrecvS.as<uint16_t>(), rcS, wbase[1].data(), total[1], G, &lo,
-                                                   src, rs->ev[2 * K], rs->ev[2 * K + 1], &o.st);
+        const bool waited = hip_ok(hipStreamWaitEvent(s, rs->ev[2 * K], 0), "hipStreamWaitEvent (R landed)");
+        if (waited && total[0] && total[1]) {
+            // R's passes (narrow residuals, the plan the senders used for S), then S's
+            // pieces gathered once they have landed, and the build/probe
+            uint64_t *rcS = reinterpret_cast<uint64_t *>(ctx->wrecvS.as<char>() + res_bytes(cS));
+            int lrc = injected(rank, kFailLocal)
+                          ? MI355_ERR_OOM
+                          : rho::join_pipelined_begin(ctx, s, ctx->xrecvR.ptr, total[0], total[1], &lo,
+                                                      (uint32_t)elem, nullptr, 0, true);
+            if (lrc == MI355_OK)
+                lrc = rho::join_pipelined_finish_wire16(ctx, ctx->wrecvS.as<uint16_t>(), rcS, wbase.data(), total[1],
+                                                        G, rcS + (size_t)G * (P16 + 1), rs->ev[2 * K + 1], &o.st);
             fail(lrc);
             o.local = lrc == MI355_OK ? o.st.matches : 0;
-        } else {
+        } else if (waited) {
             hip_ok(hipStreamWaitEvent(s, rs->ev[2 * K + 1], 0), "hipStreamWaitEvent (S landed)");
         }
     } else if (fail_rc == MI355_OK) {

@@ -39,9 +39,10 @@ void forget_context(const Context *ctx);
 // nS); a pooled S pass 1 then runs per piece, each launch after its event in
 // s_landed[i] (finish; null: no waits), so that only the last piece's pass 1, the pool
 // layout, pass 2 and the build/probe follow S's last piece.
+// wire16: S will come as u16-wire residuals (join_pipelined_finish_wire16).
 int join_pipelined_begin(Context *ctx, hipStream_t s, const void *dR, uint64_t nR, uint64_t nS,
                          const mi355_rho_opts *opts, uint32_t in_elem = 8, const uint64_t *s_piece_n = nullptr,
-                         int s_pieces = 0);
+                         int s_pieces = 0, bool wire16 = false);
 // mat (materialising joins, opts->materialize at begin): the triples go to this growable
 // device buffer (st->matches of them).
 int join_pipelined_finish(Context *ctx, const void *dS, uint64_t nS, mi355_rho_stats *st,
@@ -54,7 +55,8 @@ bool keys_exchange_plan(uint64_t nR, uint64_t nS, uint64_t cap_r, uint64_t cap_s
 
 // ---- multi-GPU u16 wire (DESIGN.md §5 "Residuals on the wire") ----
 // Whether a keys exchange (lo from keys_exchange_plan, lo->key_shift = log2 G) can send
-// 2-byte residuals instead: the local plan of nR x nS (the mean local sizes) is a
+// S as 2-byte residuals instead (R's keys still travel as 4 bytes: R's local passes run
+// while S is on the wire, S's sender-side passes while R is): the local plan of nR x nS (the mean local sizes) is a
 // two-pass narrow counting RHO plan, and every 32-bit key's residual above the shard and
 // partition bits fits 16 bits (key_shift + bits >= 16).  SGXAMD_WIRE16=0 disables it.
 // Returns the plan's partition count P (0: no).
@@ -67,15 +69,15 @@ uint32_t wire16_plan(uint64_t nR, uint64_t nS, int G, const mi355_rho_opts *lo);
 int wire_partition(Context *ctx, hipStream_t s, const uint32_t *keys, int G, int runs, const uint64_t *run_off,
                    const uint64_t *run_n, uint64_t nR, uint64_t nS, const mi355_rho_opts *lo, uint16_t *out16,
                    uint64_t *counts, const char *tag);
-// Receiver: the counting join of the residuals the G senders sent (r16 / s16: sender
-// q's run at r_base[q] / s_base[q] u16 elements, their counts rows as wire_partition
-// wrote them; nR / nS residuals in all).  R's pieces are gathered after r_landed, S's
-// after s_landed (events on the communication stream), then the build/probe.
-// src_scratch: 2 * (G * P + G) u64.  Synchronises s; st as join_pipelined_finish.
-int join_wire16(Context *ctx, hipStream_t s, const uint16_t *r16, const uint64_t *r_cnt, const uint64_t *r_base,
-                uint64_t nR, const uint16_t *s16, const uint64_t *s_cnt, const uint64_t *s_base, uint64_t nS, int G,
-                const mi355_rho_opts *lo, uint64_t *src_scratch, hipEvent_t r_landed, hipEvent_t s_landed,
-                mi355_rho_stats *st);
+// Receiver: after join_pipelined_begin(..., wire16 = true) (R's passes, the plan of
+// wire16_plan, R's pass 2 writing residuals), S's residuals as the G senders sent them
+// (sender q's run at s_base[q] u16 elements, its counts row as wire_partition wrote it;
+// nS residuals in all): its pieces are gathered after s_landed (an event on the
+// communication stream), then the build/probe.  scratch: wire_scratch_u64(G, P) u64.
+// Synchronises the stream; st as join_pipelined_finish.
+int join_pipelined_finish_wire16(Context *ctx, const uint16_t *s16, const uint64_t *s_cnt, const uint64_t *s_base,
+                                 uint64_t nS, int G, uint64_t *scratch, hipEvent_t s_landed, mi355_rho_stats *st);
+uint64_t wire_scratch_u64(int G, uint32_t P);
 // Tests: enqueue `us` microseconds of waiting on stream s (rho_kernels.hip k_spin).
 hipError_t launch_spin(uint32_t us, hipStream_t s);
 // What mi355_last_join_stats reports for this thread's last join (multi-GPU calls).

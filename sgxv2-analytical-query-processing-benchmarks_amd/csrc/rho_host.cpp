@@ -590,8 +590,9 @@ PendingJoin &pending_of(const Context *ctx) {
 // may start after S has been produced later in the stream order of s (multi-GPU:
 // R's local passes run while S is still being exchanged).  Caller holds ctx->mu.
 // Policy, workspace and scratch layout of a join of nR x nS tuples (no launches).
-// wire16: the partitions arrive as narrow residuals (the multi-GPU u16 wire, join_wire16):
-// the 16,384-key table and the narrow join, whatever the received sizes.
+// wire16: S's partitions arrive as narrow residuals (the multi-GPU u16 wire,
+// join_pipelined_finish_wire16): the 16,384-key table and the narrow join (R's pass 2
+// writes residuals too), whatever the received sizes.
 int plan_join(Context *ctx, hipStream_t s, uint64_t nR, uint64_t nS, const mi355_rho_opts *opts, PendingJoin &pj,
               const std::vector<uint64_t> *s_pieces = nullptr, bool wire16 = false) {
     pj = PendingJoin{};
@@ -682,8 +683,9 @@ int plan_join(Context *ctx, hipStream_t s, uint64_t nR, uint64_t nS, const mi355
 // may start after S has been produced later in the stream order of s (multi-GPU:
 // R's local passes run while S is still being exchanged).  Caller holds ctx->mu.
 int join_begin(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, uint64_t nS, const mi355_rho_opts *opts,
-               PendingJoin &pj, uint32_t in_elem = sizeof(row_t), const std::vector<uint64_t> *s_pieces = nullptr) {
-    int prc = plan_join(ctx, s, nR, nS, opts, pj, s_pieces);
+               PendingJoin &pj, uint32_t in_elem = sizeof(row_t), const std::vector<uint64_t> *s_pieces = nullptr,
+               bool wire16 = false) {
+    int prc = plan_join(ctx, s, nR, nS, opts, pj, s_pieces, wire16);
     if (prc) return prc;
     if (in_elem != sizeof(row_t)) {  // key input: only the pooled keys layout reads it
         if (!(pj.pr.keys && pj.ps.keys)) {
@@ -1117,7 +1119,8 @@ int join_device(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const
 }
 
 int join_pipelined_begin(Context *ctx, hipStream_t s, const void *dR, uint64_t nR, uint64_t nS,
-                         const mi355_rho_opts *opts, uint32_t in_elem, const uint64_t *s_piece_n, int s_pieces) {
+                         const mi355_rho_opts *opts, uint32_t in_elem, const uint64_t *s_piece_n, int s_pieces,
+                         bool wire16) {
     PendingJoin &pj = pending_of(ctx);
     if (pj.active) {
         set_last_error("a pipelined join is already pending on this context");
@@ -1134,7 +1137,7 @@ int join_pipelined_begin(Context *ctx, hipStream_t s, const void *dR, uint64_t n
         }
     }
     const int rc = join_begin(ctx, s, static_cast<const row_t *>(dR), nR, nS, opts, pj, in_elem,
-                              pieces.empty() ? nullptr : &pieces);
+                              pieces.empty() ? nullptr : &pieces, wire16);
     if (rc) pj.active = false;
     return rc;
 }
@@ -1179,7 +1182,9 @@ uint32_t wire16_plan(uint64_t nR, uint64_t nS, int G, const mi355_rho_opts *lo) 
     if (!(keys_enabled() && narrow_enabled() && sort2_enabled())) return 0;
     const Policy p = choose_policy(nR, nS, lo);
     // every 32-bit key's residual fits 16 bits: no device-side width check can differ
-    if (p.passes != 2 || !uses_digit_side(p) || lo->key_shift + p.bits < 16 || lo->key_shift + p.bits > 31) return 0;
+    if (p.passes != 2 || !uses_digit_side(p) || lo->key_shift + p.bits < 16 || lo->key_shift + p.bits > 31 ||
+        p.bits > 20)
+        return 0;
     return 1u << p.bits;
 }
 
@@ -1253,48 +1258,33 @@ int wire_partition(Context *ctx, hipStream_t s, const uint32_t *keys, int G, int
     return MI355_OK;
 }
 
-int join_wire16(Context *ctx, hipStream_t s, const uint16_t *r16, const uint64_t *r_cnt, const uint64_t *r_base,
-                uint64_t nR, const uint16_t *s16, const uint64_t *s_cnt, const uint64_t *s_base, uint64_t nS, int G,
-                const mi355_rho_opts *lo, uint64_t *src_scratch, hipEvent_t r_landed, hipEvent_t s_landed,
-                mi355_rho_stats *st) {
+uint64_t wire_scratch_u64(int G, uint32_t P) { return wire_scratch_words((uint32_t)G, P); }
+
+int join_pipelined_finish_wire16(Context *ctx, const uint16_t *s16, const uint64_t *s_cnt, const uint64_t *s_base,
+                                 uint64_t nS, int G, uint64_t *scratch, hipEvent_t s_landed, mi355_rho_stats *st) {
     PendingJoin &pj = pending_of(ctx);
-    if (pj.active) {
-        set_last_error("a pipelined join is already pending on this context");
+    if (!pj.active || !pj.ps.narrow) {
+        pj.active = false;
+        set_last_error("join_pipelined_finish_wire16 without a u16-wire join_pipelined_begin");
         return MI355_ERR_INVALID;
     }
     if (G < 1 || (uint32_t)G > kWireMaxG) {
+        pj.active = false;
         set_last_error("u16 wire: unsupported world size");
         return MI355_ERR_INVALID;
     }
-    int rc = plan_join(ctx, s, nR, nS, lo, pj, nullptr, true);
-    if (rc) return rc;
     const uint32_t P = 1u << pj.pol.bits;
     Arena &A = ctx->scratch;
     Timer &tm = thread_timer();
-    const bool per_kernel = thread_timing_enabled() || (lo && lo->timing);
-    tm.begin_call(s, true, !per_kernel);
-    WireBases br{}, bs{};
-    for (int q = 0; q < G; ++q) {
-        br.b[q] = r_base[q];
-        bs.b[q] = s_base[q];
-    }
-    br.b[G] = nR;
+    WireBases bs{};
+    for (int q = 0; q < G; ++q) bs.b[q] = s_base[q];
     bs.b[G] = nS;
-    uint16_t *mR = ctx->t2R.as<uint16_t>(), *mS = ctx->t2S.as<uint16_t>();
-    uint64_t *psR = A.at<uint64_t>(pj.pr.pstart), *pcR = A.at<uint64_t>(pj.pr.pcnt);
+    uint16_t *mS = ctx->t2S.as<uint16_t>();
     uint64_t *psS = A.at<uint64_t>(pj.ps.pstart), *pcS = A.at<uint64_t>(pj.ps.pcnt);
-    RHO_HIP(hipStreamWaitEvent(s, r_landed, 0));
-    tm.mark("R_wire_merge");
-    RHO_HIP(launch_wire_merge(r16, r_cnt, (uint32_t)G, P, br, src_scratch, psR, pcR,
-                              A.at<uint32_t>(pj.pr.kmax) + pj.pr.nseg1, mR, s));
-    RHO_HIP(hipStreamWaitEvent(s, s_landed, 0));
+    RHO_HIP(hipStreamWaitEvent(pj.s, s_landed, 0));
     tm.mark("S_wire_merge");
-    RHO_HIP(launch_wire_merge(s16, s_cnt, (uint32_t)G, P, bs, src_scratch + (size_t)G * P + G, psS, pcS,
-                              A.at<uint32_t>(pj.ps.kmax) + pj.ps.nseg1, mS, s));
-    pj.fR = reinterpret_cast<const row_t *>(mR);
-    pj.psR = psR;
-    pj.pcR = pcR;
-    pj.active = true;
+    RHO_HIP(launch_wire_merge(s16, s_cnt, (uint32_t)G, P, bs, scratch, psS, pcS,
+                              A.at<uint32_t>(pj.ps.kmax) + pj.ps.nseg1, mS, pj.s));
     const GivenParts gs{reinterpret_cast<const row_t *>(mS), psS, pcS};
     return join_finish(ctx, pj, nullptr, nS, st, nullptr, 0, nullptr, false, &gs);
 }

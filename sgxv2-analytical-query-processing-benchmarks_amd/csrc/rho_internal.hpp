@@ -313,13 +313,15 @@ hipError_t launch_reduce(const uint64_t *partials, uint32_t n, uint64_t *result,
 // at bases.b[q] (b[G] = their total), each grouped by partition; cnt = G rows of P
 // partition counts and the sender's largest key.  Gathers every partition's G pieces
 // into out (contiguous partitions: ps / pc), *narrow = the largest key; a row whose
-// counts do not add up to its run is left out.  src: G * P + G u64 of scratch.
+// counts do not add up to its run is left out.  scratch: wire_scratch_words(G, P) u64;
+// P <= 2^20.
 constexpr uint32_t kWireMaxG = 64;
 struct WireBases {
     uint64_t b[kWireMaxG + 1];
 };
+uint64_t wire_scratch_words(uint32_t G, uint32_t P);
 hipError_t launch_wire_merge(const uint16_t *in, const uint64_t *cnt, uint32_t G, uint32_t P, const WireBases &bases,
-                             uint64_t *src, uint64_t *ps, uint64_t *pc, uint32_t *narrow, uint16_t *out,
+                             uint64_t *scratch, uint64_t *ps, uint64_t *pc, uint32_t *narrow, uint16_t *out,
                              hipStream_t s);
 
 }  // namespace rho

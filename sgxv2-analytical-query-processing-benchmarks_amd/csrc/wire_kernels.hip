@@ -15,107 +15,141 @@ namespace rho {
 
 namespace {
 
-constexpr uint32_t kWireBlock = 1024;
+constexpr uint32_t kWireTile = 1024;  // partitions per tile (one thread each)
 constexpr uint32_t kGatherBlock = 256;
 
-// Workgroup q < G: src[q * P + p] = where sender q's piece of partition p starts in the
-// receive buffer (bases.b[q] + the exclusive scan of q's counts).  Workgroup G: pc[p] =
-// the partition's keys over all senders, ps = their exclusive scan, *narrow = the
-// largest key of any sender (the word the build/probe sizes its direct count table by).
-// cnt: G rows of P counts + the sender's largest key.  A row is used only when its
-// counts add up to the run the count exchange announced (bases.b[q + 1] - bases.b[q]):
-// a sender that failed after the count exchange sent zeros or stale counts, and its
-// pieces are left out (the final all-reduce reports the failure) instead of steering
-// the gather and the build/probe outside the buffers.  valid[q]: the verdict (both
-// workgroups reach it from the same sums).  Thread t takes partitions [t C, (t + 1) C).
-__global__ __launch_bounds__(kWireBlock) void k_wire_scan(const uint64_t *__restrict__ cnt, uint32_t G, uint32_t P,
-                                                          WireBases bases, uint64_t *__restrict__ src,
-                                                          uint32_t *__restrict__ valid, uint64_t *__restrict__ ps,
-                                                          uint64_t *__restrict__ pc, uint32_t *__restrict__ narrow) {
-    __shared__ uint64_t scratch[kWireBlock / kWave + 1];
+// Scratch (u64 words from `w`): src [G][P] (a piece's offset inside its tile of its
+// sender's run), dst [G][P] (where the piece lands), tsum [G][T] (the row's tile
+// totals), tbase [G][T] (where a tile's pieces start in the receive buffer), pbase [T]
+// (where a tile's partitions start in the output), valid [G] (u32).
+struct WireScratch {
+    uint64_t *src, *dst, *tsum, *tbase, *pbase;
+    uint32_t *valid;
+    __device__ WireScratch(uint64_t *w, uint32_t G, uint32_t P, uint32_t T)
+        : src(w), dst(w + (uint64_t)G * P), tsum(dst + (uint64_t)G * P), tbase(tsum + (uint64_t)G * T),
+          pbase(tbase + (uint64_t)G * T), valid(reinterpret_cast<uint32_t *>(pbase + T)) {}
+};
+
+// Grid (T, G): row q's counts in tile t, one per thread (coalesced), their exclusive
+// scan (the pieces' offsets inside the tile) and the tile's total.
+__global__ __launch_bounds__(kWireTile) void k_wire_rows(const uint64_t *__restrict__ cnt, uint32_t P, uint32_t T,
+                                                         uint64_t *__restrict__ src, uint64_t *__restrict__ tsum) {
+    __shared__ uint64_t scratch[kWireTile / kWave + 1];
+    const uint32_t t = blockIdx.x, q = blockIdx.y, p = t * kWireTile + threadIdx.x;
+    const uint64_t v = p < P ? cnt[(uint64_t)q * (P + 1) + p] : 0;
+    uint64_t total;
+    const uint64_t ex = block_excl_scan_u64(v, scratch, &total);
+    if (p < P) src[(uint64_t)q * P + p] = ex;
+    if (threadIdx.x == 0) tsum[(uint64_t)q * T + t] = total;
+}
+
+// One workgroup: a row is used only when its counts add up to the run the count
+// exchange announced (bases.b[q + 1] - bases.b[q]) -- a sender that failed after the
+// count exchange sent zeroed or stale rows, and its pieces are left out (the final
+// all-reduce reports the failure) instead of steering the gather and the build/probe
+// outside the buffers.  Then the tiles' bases in the receive buffer per row, the
+// partitions' tile totals over the valid rows and their exclusive scan, and *narrow =
+// the largest key of the valid rows (the word the build/probe sizes its table by).
+// T <= kWireTile (P <= 2^20).
+__global__ __launch_bounds__(kWireTile) void k_wire_bases(const uint64_t *__restrict__ cnt, uint32_t G, uint32_t P,
+                                                          uint32_t T, WireBases bases, uint64_t *__restrict__ w,
+                                                          uint32_t *__restrict__ narrow) {
+    __shared__ uint64_t scratch[kWireTile / kWave + 1];
     __shared__ uint32_t ok[kWireMaxG];
-    const uint32_t q = blockIdx.x, t = threadIdx.x;
-    const uint32_t C = (P + kWireBlock - 1) / kWireBlock;
-    const uint32_t p0 = min(P, t * C), p1 = min(P, p0 + C);
-    const uint64_t stride = (uint64_t)P + 1;
-    uint64_t local = 0, total = 0;
-    if (q < G) {
-        const uint64_t *c = cnt + q * stride;
-        for (uint32_t p = p0; p < p1; ++p) local += c[p];
-        uint64_t run = bases.b[q] + block_excl_scan_u64(local, scratch, &total);
-        for (uint32_t p = p0; p < p1; ++p) {
-            src[(uint64_t)q * P + p] = run;
-            run += c[p];
+    const WireScratch sc(w, G, P, T);
+    const uint32_t i = threadIdx.x;
+    if (i < G) {
+        uint64_t run = bases.b[i];
+        for (uint32_t t = 0; t < T; ++t) {
+            sc.tbase[(uint64_t)i * T + t] = run;
+            run += sc.tsum[(uint64_t)i * T + t];
         }
-        if (t == 0) valid[q] = total == bases.b[q + 1] - bases.b[q] ? 1u : 0u;
-        return;
-    }
-    for (uint32_t r = 0; r < G; ++r) {
-        local = 0;
-        for (uint32_t p = p0; p < p1; ++p) local += cnt[r * stride + p];
-        (void)block_excl_scan_u64(local, scratch, &total);
-        if (t == 0) ok[r] = total == bases.b[r + 1] - bases.b[r] ? 1u : 0u;
+        ok[i] = run == bases.b[i + 1] ? 1u : 0u;
+        sc.valid[i] = ok[i];
     }
     __syncthreads();
-    local = 0;
-    for (uint32_t p = p0; p < p1; ++p) {
-        uint64_t s = 0;
-        for (uint32_t r = 0; r < G; ++r)
-            if (ok[r]) s += cnt[r * stride + p];
-        pc[p] = s;
-        local += s;
-    }
-    uint64_t run = block_excl_scan_u64(local, scratch, &total);
-    for (uint32_t p = p0; p < p1; ++p) {
-        ps[p] = run;
-        run += pc[p];
-    }
-    if (t == 0) {
+    // (T <= kWireTile: one tile total per thread)
+    uint64_t v = 0;
+    if (i < T)
+        for (uint32_t q = 0; q < G; ++q)
+            if (ok[q]) v += sc.tsum[(uint64_t)q * T + i];
+    uint64_t total;
+    const uint64_t ex = block_excl_scan_u64(v, scratch, &total);
+    if (i < T) sc.pbase[i] = ex;
+    if (i == 0) {
         uint64_t m = 0;
-        for (uint32_t r = 0; r < G; ++r)
-            if (ok[r]) m = max(m, cnt[r * stride + P]);
+        for (uint32_t q = 0; q < G; ++q)
+            if (ok[q]) m = max(m, cnt[(uint64_t)q * (P + 1) + P]);
         *narrow = (uint32_t)min<uint64_t>(m, 0xFFFFFFFFull);
     }
 }
 
+// Grid T: partition p's keys over the valid rows (pc), its start (ps: the tile's base +
+// the exclusive scan inside the tile), and where each valid sender's piece lands (dst).
+__global__ __launch_bounds__(kWireTile) void k_wire_parts(const uint64_t *__restrict__ cnt, uint32_t G, uint32_t P,
+                                                          uint32_t T, uint64_t *__restrict__ w,
+                                                          uint64_t *__restrict__ ps, uint64_t *__restrict__ pc) {
+    __shared__ uint64_t scratch[kWireTile / kWave + 1];
+    const WireScratch sc(w, G, P, T);
+    const uint32_t t = blockIdx.x, p = t * kWireTile + threadIdx.x;
+    const uint64_t stride = (uint64_t)P + 1;
+    uint64_t v = 0;
+    if (p < P)
+        for (uint32_t q = 0; q < G; ++q)
+            if (sc.valid[q]) v += cnt[q * stride + p];
+    uint64_t total;
+    const uint64_t start = sc.pbase[t] + block_excl_scan_u64(v, scratch, &total);
+    if (p >= P) return;
+    ps[p] = start;
+    pc[p] = v;
+    uint64_t d = start;
+    for (uint32_t q = 0; q < G; ++q)
+        if (sc.valid[q]) {
+            sc.dst[(uint64_t)q * P + p] = d;
+            d += cnt[q * stride + p];
+        }
+}
+
 // One wave per piece (partition p, sender q), the pieces of one partition on
-// consecutive waves (their destinations are consecutive): the piece lands at ps[p] +
-// the pieces of the (valid) senders before q.  Lanes copy consecutive residuals (128 B
-// per wave and step).
+// consecutive waves (their destinations are consecutive).  Lanes copy consecutive
+// residuals (128 B per wave and step).
 __global__ __launch_bounds__(kGatherBlock) void k_wire_gather(const uint16_t *__restrict__ in,
                                                               const uint64_t *__restrict__ cnt, uint32_t G, uint32_t P,
-                                                              const uint64_t *__restrict__ src,
-                                                              const uint32_t *__restrict__ valid,
-                                                              const uint64_t *__restrict__ ps,
+                                                              uint32_t T, const uint64_t *__restrict__ w,
                                                               uint16_t *__restrict__ out) {
-    const uint64_t w = (uint64_t)blockIdx.x * (kGatherBlock / kWave) + threadIdx.x / kWave;
-    if (w >= (uint64_t)G * P) return;
-    const uint32_t lane = __lane_id(), p = (uint32_t)(w / G), q = (uint32_t)(w % G);
-    const uint64_t stride = (uint64_t)P + 1;
-    const uint64_t n = cnt[q * stride + p];
-    if (n == 0 || !valid[q]) return;
-    uint64_t d = ps[p];
-    for (uint32_t r = 0; r < q; ++r)
-        if (valid[r]) d += cnt[r * stride + p];
-    const uint16_t *s = in + src[(uint64_t)q * P + p];
-    uint16_t *o = out + d;
+    const uint64_t wv = (uint64_t)blockIdx.x * (kGatherBlock / kWave) + threadIdx.x / kWave;
+    if (wv >= (uint64_t)G * P) return;
+    const WireScratch sc(const_cast<uint64_t *>(w), G, P, T);
+    const uint32_t lane = __lane_id(), p = (uint32_t)(wv / G), q = (uint32_t)(wv % G);
+    const uint64_t n = cnt[(uint64_t)q * (P + 1) + p];
+    if (n == 0 || !sc.valid[q]) return;
+    const uint64_t qp = (uint64_t)q * P + p;
+    const uint16_t *s = in + sc.tbase[(uint64_t)q * T + p / kWireTile] + sc.src[qp];
+    uint16_t *o = out + sc.dst[qp];
     for (uint64_t i = lane; i < n; i += kWave) o[i] = s[i];
 }
 
 }  // namespace
 
+uint64_t wire_scratch_words(uint32_t G, uint32_t P) {
+    const uint64_t T = (P + kWireTile - 1) / kWireTile;
+    return 2ull * G * P + 2ull * G * T + T + (G + 1) / 2 + 1;
+}
+
 hipError_t launch_wire_merge(const uint16_t *in, const uint64_t *cnt, uint32_t G, uint32_t P, const WireBases &bases,
-                             uint64_t *src, uint64_t *ps, uint64_t *pc, uint32_t *narrow, uint16_t *out,
+                             uint64_t *scratch, uint64_t *ps, uint64_t *pc, uint32_t *narrow, uint16_t *out,
                              hipStream_t s) {
     if (G == 0 || G > kWireMaxG || P == 0) return hipErrorInvalidValue;
-    uint32_t *valid = reinterpret_cast<uint32_t *>(src + (uint64_t)G * P);
-    hipLaunchKernelGGL(k_wire_scan, dim3(G + 1), dim3(kWireBlock), 0, s, cnt, G, P, bases, src, valid, ps, pc,
-                       narrow);
+    const uint32_t T = (P + kWireTile - 1) / kWireTile;
+    if (T > kWireTile) return hipErrorInvalidValue;  // P <= 2^20
+    hipLaunchKernelGGL(k_wire_rows, dim3(T, G), dim3(kWireTile), 0, s, cnt, P, T, scratch,
+                       scratch + 2ull * G * P);
+    hipLaunchKernelGGL(k_wire_bases, dim3(1), dim3(kWireTile), 0, s, cnt, G, P, T, bases, scratch, narrow);
+    hipLaunchKernelGGL(k_wire_parts, dim3(T), dim3(kWireTile), 0, s, cnt, G, P, T, scratch, ps, pc);
     const uint64_t waves = (uint64_t)G * P, per = kGatherBlock / kWave;
     const uint64_t grid = (waves + per - 1) / per;
     if (grid > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_wire_gather, dim3((uint32_t)grid), dim3(kGatherBlock), 0, s, in, cnt, G, P, src, valid, ps,
-                       out);
+    hipLaunchKernelGGL(k_wire_gather, dim3((uint32_t)grid), dim3(kGatherBlock), 0, s, in, cnt, G, P, T, scratch, out);
     return hipGetLastError();
 }
 

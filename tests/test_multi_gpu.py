@@ -83,7 +83,7 @@ def test_keys_only_exchange(sgx, orc, gpu, g, n, kw):
     wire16 = (g.bit_length() - 1) + st["local"]["radix_bits"] >= 16
     assert st["elem_bytes"] == (2 if wire16 else 4) and st["local"]["layout"] in (2, 3, 4)
     # every key of a rank except those it keeps goes out once
-    assert st["sent_bytes"] == _exchange_bytes(st, _keys_out(R, g) + _keys_out(S, g), g)
+    assert st["sent_bytes"] == _exchange_bytes(st, _keys_out(R, g), _keys_out(S, g), g)
     # RHT counts over key partitions too (SGXAMD_KEYS=0 in test_paths_gpu keeps tuples)
     rht = multi(sgx, R, S, g, algorithm="RHT", **kw)
     assert rht.matches == exp and rht.stats["elem_bytes"] == 4
@@ -270,24 +270,25 @@ def _keys_out(rel_, g):
     return _slices_sent(torch.from_numpy(np.asarray(keys, dtype=np.int64)), g, 1)
 
 
-def _exchange_bytes(st, keys_out, g):
+def _exchange_bytes(st, out_r, out_s, g):
     """sent_bytes of a counting join's keys exchange over all ranks of one process: 4 bytes
-    per key that leaves its rank, or on the u16 wire 2 bytes per key plus, per relation
-    and peer, the sender's counts row (P partition counts and its largest key, 8 bytes
-    each)."""
+    per key that leaves its rank, except that on the u16 wire S's keys go as 2-byte
+    residuals plus, per peer, the sender's counts row (P partition counts and its
+    largest key, 8 bytes each)."""
     if st["elem_bytes"] == 2:
         p = 1 << st["local"]["radix_bits"]
-        return 2 * keys_out + 2 * g * (g - 1) * (p + 1) * 8
+        return 4 * out_r + 2 * out_s + g * (g - 1) * (p + 1) * 8
     assert st["elem_bytes"] == 4
-    return 4 * keys_out
+    return 4 * (out_r + out_s)
 
 
 @pytest.mark.parametrize("g", [2, 4, 8])
 def test_wire16_exchange(sgx, orc, gpu, g):
     """The u16 wire: with log2 g + the local radix bits >= 16, every
-    sender runs the receiver's two passes on the keys it sends each rank, and 2-byte
-    residuals travel with one counts row per relation and peer; each receiver gathers a
-    partition's g pieces (one per sender) and runs the narrow build/probe.  Exact counts
+    sender runs the receiver's two passes on the S keys it sends each rank, and 2-byte
+    residuals travel with one counts row per peer (R's keys as 4 bytes, partitioned by
+    the receiver while S is on the wire); each receiver gathers a partition's g pieces
+    (one per sender) and runs the narrow build/probe.  Exact counts
     against the sort counter on pk / fk, on random keys with duplicates over the whole
     u32 range (residuals up to 2^16: the windowed direct table), on a hot key, and on
     sizes that leave some (sender, destination) runs empty; the exact bytes."""
@@ -306,7 +307,7 @@ def test_wire16_exchange(sgx, orc, gpu, g):
         st = res.stats
         assert res.matches == exp, (g, len(R), len(S))
         assert st["elem_bytes"] == 2 and st["local"]["radix_bits"] == bits
-        assert st["sent_bytes"] == _exchange_bytes(st, _keys_out(R, g) + _keys_out(S, g), g)
+        assert st["sent_bytes"] == _exchange_bytes(st, _keys_out(R, g), _keys_out(S, g), g)
         assert 0 <= st["ms_tail"] <= st["ms_total"]
 
 
@@ -345,9 +346,9 @@ def test_config4_rehearsal_full_size(sgx, gpu):
         assert st["world"] == g and st["elem_bytes"] in (2, 4) and st["local"]["layout"] in (2, 3, 4)
         assert st["recv_r_max"] == st["recv_r_min"] == nR // g
         assert st["recv_s_max"] == st["recv_s_min"] == nS // g
-        keys_out = _slices_sent(R & 0xFFFFFFFF, g, 1) + _slices_sent(S & 0xFFFFFFFF, g, 1)
-        assert st["sent_bytes"] == _exchange_bytes(st, keys_out, g)
-        assert abs(keys_out - (nR + nS) * 7 / 8) < (nR + nS) * 0.001
+        out_r, out_s = _slices_sent(R & 0xFFFFFFFF, g, 1), _slices_sent(S & 0xFFFFFFFF, g, 1)
+        assert st["sent_bytes"] == _exchange_bytes(st, out_r, out_s, g)
+        assert abs(out_r + out_s - (nR + nS) * 7 / 8) < (nR + nS) * 0.001
         # S's pass 1 ran per landed piece: the device time after S's last piece is a part
         # of the local join (the rehearsal's ranks share one GPU, so only its presence is
         # checked, not its size)

@@ -152,8 +152,8 @@ def test_inprocess_config4_full_size(sgx, dbl, gpu):
         assert st["transport"] == "rccl" and st["world"] == g and st["elem_bytes"] in (2, 4)
         assert st["recv_r_max"] == st["recv_r_min"] == nR // g
         assert st["recv_s_max"] == st["recv_s_min"] == nS // g
-        keys_out = _slices_sent(R & 0xFFFFFFFF, g, 1) + _slices_sent(S & 0xFFFFFFFF, g, 1)
-        assert st["sent_bytes"] == _exchange_bytes(st, keys_out, g)
+        out_r, out_s = _slices_sent(R & 0xFFFFFFFF, g, 1), _slices_sent(S & 0xFFFFFFFF, g, 1)
+        assert st["sent_bytes"] == _exchange_bytes(st, out_r, out_s, g)
         # the double's transfers are kernels on the communication streams (k_copy), so an
         # exchange starved of CUs by the join's own grids shows up here as time: the tail
         # after S's last piece landed is measured on every rank and stays a part of the step
@@ -293,15 +293,16 @@ def test_sharded_keys_exchange_exact_bytes(sgx, dbl, gpu):
         for r, x in enumerate(res):
             st = x.stats
             assert st["elem_bytes"] in (2, 4)
-            kept = 0
+            out = []
             for X in (R, S):
                 n = X.numel()
                 a, b = r * (n // g), (n if r == g - 1 else (r + 1) * (n // g))
                 k = X[a:b] & 0xFFFFFFFF
-                kept += int(((k & (g - 1)) != r).sum().item())
-            # u16 wire: 2 bytes per key and a counts row (P + 1 words) per relation and peer
-            rows = 2 * (g - 1) * ((1 << st["local"]["radix_bits"]) + 1) * 8
-            assert st["sent_bytes"] == (2 * kept + rows if st["elem_bytes"] == 2 else 4 * kept)
+                out.append(int(((k & (g - 1)) != r).sum().item()))
+            # u16 wire: S as 2 bytes per key and a counts row (P + 1 words) per peer
+            rows = (g - 1) * ((1 << st["local"]["radix_bits"]) + 1) * 8
+            assert st["sent_bytes"] == (4 * out[0] + 2 * out[1] + rows if st["elem_bytes"] == 2
+                                        else 4 * (out[0] + out[1]))
             assert st["recv_r_max"] == nR // g and st["recv_s_max"] == nS // g
     finally:
         destroy(sgx, hs)
@@ -311,8 +312,8 @@ def test_sharded_keys_exchange_exact_bytes(sgx, dbl, gpu):
 
 @pytest.mark.parametrize("g", [2, 4, 8])
 def test_wire16_rccl(sgx, orc, dbl, gpu, g):
-    """The u16 wire through RcclTransport (residuals as ncclUint8 pairs, counts rows as
-    ncclUint64), in one process and one "process" per rank: exact counts against the sort
+    """The u16 wire through RcclTransport (S's residuals as ncclUint8 pairs, its counts
+    rows as ncclUint64, R's keys as ncclUint32), in one process and one "process" per rank: exact counts against the sort
     counter on random keys with duplicates over the whole u32 range and on pk / fk, 2
     bytes per key on the wire."""
     import torch
@@ -328,7 +329,7 @@ def test_wire16_rccl(sgx, orc, dbl, gpu, g):
     res = multi(sgx, Rh, Sh, g, radix_bits=bits, passes=2)
     st = res.stats
     assert res.matches == exp and st["transport"] == "rccl" and st["elem_bytes"] == 2
-    assert st["sent_bytes"] == _exchange_bytes(st, _keys_out(Rh, g) + _keys_out(Sh, g), g)
+    assert st["sent_bytes"] == _exchange_bytes(st, _keys_out(Rh, g), _keys_out(Sh, g), g)
     Pk, Fk = sgx.reference_relations(1 << 20, 1 << 20)
     R = torch.from_numpy(Pk.view(np.int64)).to(gpu)
     S = torch.from_numpy(Fk.view(np.int64)).to(gpu)
