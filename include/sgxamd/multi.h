@@ -118,6 +118,14 @@ int mi355_last_multi_stats(mi355_multi_stats *out);
 /* Pieces each relation is exchanged in (default 4; 1..64); applies to later calls. */
 void mi355_multi_set_pieces(int pieces);
 
+/* S's keys on the wire as 2-byte residuals of sender-side partitions (the u16 wire,
+ * DESIGN.md §5): 0 never (4-byte keys), 1 (default; SGXAMD_WIRE16 sets the initial mode)
+ * when the local join takes the narrow 16,384-key-table plan anyway and every residual
+ * fits 16 bits (log2 G + the local radix bits >= 16), 2 whenever the residuals fit
+ * (forcing the narrow plan; tests).  Every rank of a join must use the same mode (the
+ * ranks agree on the lowest). */
+void mi355_multi_set_wire(int mode);
+
 /* Frees the workspaces (exchange and join buffers) of the rehearsal transport's
  * logical ranks, which are otherwise kept for the process: call it between large
  * rehearsal joins that do not reuse them.  The calling thread's device must be the

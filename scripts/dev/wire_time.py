@@ -2,7 +2,7 @@
 (one GPU), u16 wire on or off (SGXAMD_WIRE16), to profile the sender-side passes and the
 gather kernels (run under rocprofv3 --kernel-trace --stats).  The rehearsal's "wire" is
 device memory, so the totals say nothing about xGMI; the kernel times do.
-usage: python scripts/dev/wire_time.py [c4|c2] [reps]"""
+usage: python scripts/dev/wire_time.py [c4|c2] [reps] [G]   (c2: 2^28 R and S keys per rank)"""
 import os
 import sys
 import time
@@ -15,8 +15,8 @@ import sgxamd  # noqa: E402
 
 work = sys.argv[1] if len(sys.argv) > 1 else "c4"
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
-g = 8
-nR, nS = ((1 << 27), (1 << 30)) if work == "c4" else ((1 << 28), (1 << 28))
+g = int(sys.argv[3]) if len(sys.argv) > 3 else 8
+nR, nS = ((1 << 27), (1 << 30)) if work == "c4" else ((g << 28), (g << 28))
 R = torch.empty(nR, dtype=torch.int64, device="cuda")
 S = torch.empty(nS, dtype=torch.int64, device="cuda")
 sgxamd.gen_pk_dev(R, nR, 0, nR, 11111)

@@ -1172,6 +1172,8 @@ int mi355_rho_join_multi(const table_t *relR, const table_t *relS, const joincon
 
 void mi355_multi_set_pieces(int pieces) { multi::g_pieces = std::max(1, std::min(64, pieces)); }
 
+void mi355_multi_set_wire(int mode) { rho::set_wire_mode(mode); }
+
 int mi355_multi_release(void) {
     std::lock_guard<std::mutex> lk(multi::g_reh_mu);
     int cur = 0;

@@ -61,6 +61,10 @@ bool keys_exchange_plan(uint64_t nR, uint64_t nS, uint64_t cap_r, uint64_t cap_s
 // partition bits fits 16 bits (key_shift + bits >= 16).  SGXAMD_WIRE16=0 disables it.
 // Returns the plan's partition count P (0: no).
 uint32_t wire16_plan(uint64_t nR, uint64_t nS, int G, const mi355_rho_opts *lo);
+// mi355_multi_set_wire: 0 off, 1 where the local plan is narrow anyway, 2 whenever the
+// residuals fit (tests).
+void set_wire_mode(int mode);
+int wire_mode();
 // Sender: partitions the keys this rank sends each destination (runs of packed u32
 // keys in `keys`: destination q's runs at run_off[q * runs + j], run_n[...]) with the
 // plan of wire16_plan(nR, nS, ...): destination q's residuals go to out16 + the keys of

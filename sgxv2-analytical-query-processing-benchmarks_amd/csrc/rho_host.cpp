@@ -590,6 +590,15 @@ PendingJoin &pending_of(const Context *ctx) {
 // may start after S has been produced later in the stream order of s (multi-GPU:
 // R's local passes run while S is still being exchanged).  Caller holds ctx->mu.
 // Policy, workspace and scratch layout of a join of nR x nS tuples (no launches).
+// The 16,384-key counting table with 32,768-key S chunks: partitions above 8192 R keys,
+// and plans sized for those S chunks (plan_join).
+bool takes_big_table(const Policy &pol, uint64_t nR, uint64_t nS, const mi355_rho_opts *opts) {
+    const uint64_t P = 1ull << pol.bits;
+    const uint64_t avgR = (nR + P - 1) / P, avgS = (nS + P - 1) / P;
+    return uses_big_table(opts) && ((pol.rcap == 8192 && avgR > 8192) ||
+                                    (P >= 8192 && avgS > kSChunk && avgR <= kBigRcap && opts_free_bits(opts)));
+}
+
 // wire16: S's partitions arrive as narrow residuals (the multi-GPU u16 wire,
 // join_pipelined_finish_wire16): the 16,384-key table and the narrow join (R's pass 2
 // writes residuals too), whatever the received sizes.
@@ -635,9 +644,8 @@ int plan_join(Context *ctx, hipStream_t s, uint64_t nR, uint64_t nS, const mi355
     // keys, and plans sized for those S chunks (S much larger than R, e.g. BASELINE config
     // 4: 4096 R and 32,768 S keys per partition read R once per partition instead of once
     // per 8192-key S chunk); enough partitions that one task each fills the chip
-    const uint64_t avgR = (nR + P - 1) / P, avgS = (nS + P - 1) / P;
-    if (wire16 || (uses_big_table(opts) && ((pol.rcap == 8192 && avgR > 8192) ||
-                                            (P >= 8192 && avgS > kSChunk && avgR <= kBigRcap && opts_free_bits(opts))))) {
+    const uint64_t avgS = (nS + P - 1) / P;
+    if (wire16 || takes_big_table(pol, nR, nS, opts)) {
         pj.pol.rcap = kBigRcap;
         // S-heavy plans (BASELINE config 4: 65,536 S keys per partition) probe a
         // partition in one task: 7.24-7.35 vs 7.46-7.52 ms per join with two 32,768-key
@@ -1172,15 +1180,27 @@ bool keys_exchange_plan(uint64_t nR, uint64_t nS, uint64_t cap_r, uint64_t cap_s
 // destination's shard bits and partition bits are implied by where a key lands and only
 // its residual above them travels: 2 bytes instead of 4.  The receiver gathers each
 // partition's pieces (one per sender, wire_kernels.hip) and runs the build/probe.
+namespace {
+std::atomic<int> g_wire_mode{-1};  // -1: not set (SGXAMD_WIRE16, default 1)
+}
+void set_wire_mode(int mode) { g_wire_mode = mode < 0 ? 0 : (mode > 2 ? 2 : mode); }
+int wire_mode() {
+    const int m = g_wire_mode.load();
+    if (m >= 0) return m;
+    const char *e = std::getenv("SGXAMD_WIRE16");
+    return e ? std::max(0, std::min(2, std::atoi(e))) : 1;
+}
+
 uint32_t wire16_plan(uint64_t nR, uint64_t nS, int G, const mi355_rho_opts *lo) {
-    static const bool on = [] {
-        const char *e = std::getenv("SGXAMD_WIRE16");
-        return !(e && std::atoi(e) == 0);
-    }();
-    if (!on || !lo || lo->materialize || lo->algorithm == MI355_ALGO_RHT || G < 2 || (uint32_t)G > kWireMaxG)
+    const int mode = wire_mode();
+    if (!mode || !lo || lo->materialize || lo->algorithm == MI355_ALGO_RHT || G < 2 || (uint32_t)G > kWireMaxG)
         return 0;
     if (!(keys_enabled() && narrow_enabled() && sort2_enabled())) return 0;
     const Policy p = choose_policy(nR, nS, lo);
+    // mode 1: only where the local join takes the narrow plan anyway (the 16,384-key
+    // table): elsewhere (BASELINE config 4 at G = 8: 1,024 R keys per partition) forcing
+    // it costs more compute than the halved S bytes save (r05x5)
+    if (mode == 1 && !takes_big_table(p, nR, nS, lo)) return 0;
     // every 32-bit key's residual fits 16 bits: no device-side width check can differ
     if (p.passes != 2 || !uses_digit_side(p) || lo->key_shift + p.bits < 16 || lo->key_shift + p.bits > 31 ||
         p.bits > 20)

@@ -229,6 +229,7 @@ SIGNATURES = {
                                          C.POINTER(multi_stats)]),
     "mi355_last_multi_stats": (C.c_int, [C.POINTER(multi_stats)]),
     "mi355_multi_set_pieces": (None, [C.c_int]),
+    "mi355_multi_set_wire": (None, [C.c_int]),
     "mi355_multi_inject_failure": (None, [C.c_int, C.c_int]),
     "mi355_multi_set_rccl_library": (C.c_int, [C.c_char_p]),
     "mi355_multi_release": (C.c_int, []),
@@ -468,6 +469,11 @@ def rho_join_sharded(handle: int, R, nR: int, S, nS: int, *, algorithm: str = "R
 
 def multi_set_pieces(pieces: int) -> None:
     lib.mi355_multi_set_pieces(pieces)
+
+
+def multi_set_wire(mode: int) -> None:
+    """The u16 wire: 0 off, 1 auto (default), 2 whenever the residuals fit (mi355_multi_set_wire)."""
+    lib.mi355_multi_set_wire(mode)
 
 
 def release_workspace() -> None:

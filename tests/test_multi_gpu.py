@@ -31,6 +31,16 @@ def multi(sgx, R, S, g, **kw):
     return sgx.rho_join_multi(R, len(R), S, len(S), g, transport="rehearsal", **kw)
 
 
+@pytest.fixture
+def wire16(sgx):
+    """The u16 wire whenever the residuals fit (mode 2), not only where the local plan
+    is the narrow 16,384-key-table plan anyway (the default, mode 1: relations of
+    2^27+ keys per rank)."""
+    sgx.multi_set_wire(2)
+    yield
+    sgx.multi_set_wire(1)
+
+
 @pytest.mark.parametrize("g", [2, 4, 8])
 def test_reference_pk_fk(sgx, orc, gpu, g):
     n = 1 << 18
@@ -68,7 +78,7 @@ def test_zipf_and_sel(sgx, orc, gpu):
 
 @pytest.mark.parametrize("g,n,kw", [(2, 1 << 23, {}), (4, 1 << 23, {}), (8, 1 << 21, {"radix_bits": 14, "passes": 2}),
                                     (4, 1 << 20, {"radix_bits": 10, "passes": 2})])
-def test_keys_only_exchange(sgx, orc, gpu, g, n, kw):
+def test_keys_only_exchange(sgx, orc, gpu, wire16, g, n, kw):
     """Counting joins whose local plan takes the pooled keys layout exchange 4-byte keys:
     the default policy from the mean local sizes (2^23 over 2 / 4 ranks: 10 / 9 bits, two
     passes) or a forced two-pass plan.  Exact counts, half the bytes of the tuple
@@ -244,7 +254,7 @@ def test_rccl_single_rank_local_failure_keeps_handle(sgx, orc, gpu):
 
 @pytest.mark.parametrize("kw", [{}, {"radix_bits": 14, "passes": 2}], ids=["keys", "wire16"])
 @pytest.mark.parametrize("step", [1, 2, 3])
-def test_failure_on_one_rank(sgx, orc, gpu, step, kw):
+def test_failure_on_one_rank(sgx, orc, gpu, wire16, step, kw):
     """A rank that fails (exchange buffers, a shard pass of S, its local join) flags it in
     the next collective: every rank leaves the join at the same step, the call returns
     the failed rank's own error (no rank is left waiting in a collective), and the next
@@ -283,7 +293,7 @@ def _exchange_bytes(st, out_r, out_s, g):
 
 
 @pytest.mark.parametrize("g", [2, 4, 8])
-def test_wire16_exchange(sgx, orc, gpu, g):
+def test_wire16_exchange(sgx, orc, gpu, wire16, g):
     """The u16 wire: with log2 g + the local radix bits >= 16, every
     sender runs the receiver's two passes on the S keys it sends each rank, and 2-byte
     residuals travel with one counts row per peer (R's keys as 4 bytes, partitioned by
@@ -380,7 +390,7 @@ def test_config5_rehearsal_full_size(sgx, gpu):
         res = sgx.rho_join_multi(R, n, S, n, g, transport="rehearsal")
         st = res.stats
         assert res.matches == n
-        assert st["elem_bytes"] == 2  # 3 shard + 14 partition bits: every residual fits 16 bits
+        assert st["elem_bytes"] == 4  # 2^25 keys per rank: not the narrow local plan (mode 1)
         assert st["recv_r_max"] == st["recv_r_min"] == n // g
         per_rank = torch.bincount((S & (g - 1)).to(torch.int64), minlength=g)
         assert st["recv_s_max"] == int(per_rank.max()) and st["recv_s_min"] == int(per_rank.min())

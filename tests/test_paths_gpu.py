@@ -108,6 +108,8 @@ S = np.zeros(300_007, dtype=dt); S["key"] = rng.integers(0, 2**32, len(S), dtype
 S[:70_000] = R[:70_000]
 Pk, Fk = sgxamd.reference_relations(1 << 20, 1 << 20, selectivity=50)
 off = os.environ.get("SGXAMD_WIRE16") == "0" or os.environ.get("SGXAMD_NARROW") == "0"
+if os.environ.get("SGXAMD_WIRE16") != "0":
+    sgxamd.multi_set_wire(2)  # whenever the residuals fit (these relations are small)
 for A, B in ((R, S), (Pk, Fk)):
     for g in (4, 8):
         r = sgxamd.rho_join_multi(A, len(A), B, len(B), g, transport="rehearsal", radix_bits=14, passes=2)

@@ -312,10 +312,18 @@ def test_sharded_keys_exchange_exact_bytes(sgx, dbl, gpu):
 
 @pytest.mark.parametrize("g", [2, 4, 8])
 def test_wire16_rccl(sgx, orc, dbl, gpu, g):
-    """The u16 wire through RcclTransport (S's residuals as ncclUint8 pairs, its counts
-    rows as ncclUint64, R's keys as ncclUint32), in one process and one "process" per rank: exact counts against the sort
-    counter on random keys with duplicates over the whole u32 range and on pk / fk, 2
-    bytes per key on the wire."""
+    """The u16 wire (forced: mode 2) through RcclTransport (S's residuals as ncclUint8
+    pairs, its counts rows as ncclUint64, R's keys as ncclUint32), in one process and one
+    "process" per rank: exact counts against the sort counter on random keys with
+    duplicates over the whole u32 range and on pk / fk, the exact bytes."""
+    sgx.multi_set_wire(2)
+    try:
+        _wire16_rccl(sgx, orc, gpu, g)
+    finally:
+        sgx.multi_set_wire(1)
+
+
+def _wire16_rccl(sgx, orc, gpu, g):
     import torch
 
     from test_multi_gpu import _exchange_bytes, _keys_out
