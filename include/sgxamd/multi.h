@@ -76,11 +76,11 @@ typedef struct mi355_multi_stats {
     mi355_rho_stats local;     /* the local join of rank 0 (or of the calling rank) */
     uint32_t elem_bytes;       /* bytes per exchanged element: 8 (tuples), 4 (keys only: a
                                   counting join whose local join reads keys) or 2 (the u16
-                                  wire: every sender runs the receiver's two partition passes
+                                  wire, mi355_multi_set_wire: R's keys travel as 4 bytes, and
+                                  for S every sender runs the receiver's two partition passes
                                   and sends 2-byte residuals grouped by partition, plus per
-                                  relation and peer one row of P + 1 u64 words: the partition
-                                  counts and its largest key; taken when log2(world) + the
-                                  local radix bits >= 16; SGXAMD_WIRE16=0 turns it off) */
+                                  peer one row of P + 1 u64 words: the partition counts and
+                                  its largest key) */
     double ms_tail;            /* device time from S's last piece landing to the local join's
                                   end (max over the ranks seen; the part of the join that no
                                   exchange hides); -1 when no rank measured it (a world of
