@@ -651,16 +651,19 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
     // and the u16 wire (keys plans whose every residual fits 16 bits): agreed the same way
     mi355_rho_opts kl = lo;
     uint64_t agree[2] = {rho::keys_exchange_plan(sum[0] / G, sum[1] / G, cR, cS, &kl) ? 0u : 1u, 1u};
-    if (agree[0] == 0 && rho::wire16_plan(sum[0] / G, sum[1] / G, G, &kl)) agree[1] = 0;
+    bool need_kmax = false;
+    if (agree[0] == 0 && rho::wire16_plan(sum[0] / G, sum[1] / G, G, &kl, &need_kmax)) agree[1] = 0;
     MH_RC(transport_rc(T.allreduce(rank, s, agree, 2, kMax)));
     o.keys = agree[0] == 0;
     o.wire16 = o.keys && agree[1] == 0;
     if (o.keys) lo = kl;  // the local policy fixed from the global sizes
-    const uint32_t P16 = o.wire16 ? rho::wire16_plan(sum[0] / G, sum[1] / G, G, &lo) : 0;
+    const uint32_t P16 = o.wire16 ? rho::wire16_plan(sum[0] / G, sum[1] / G, G, &lo, &need_kmax) : 0;
     const size_t elem = o.keys ? sizeof(uint32_t) : sizeof(row_t);
     // u16 wire buffers (S): [residuals (256-B aligned)][G counts rows of P16 + 1 words];
     // the receive side also holds the gather's scratch (rho::wire_scratch_u64)
     const auto res_bytes = [](uint64_t n) { return (std::max<uint64_t>(n, 1) * 2 + 255) & ~uint64_t(255); };
+    // (the send side: 4 bytes per key, rho::wire_partition writes a wide destination as keys)
+    const auto snd_bytes = [](uint64_t n) { return (std::max<uint64_t>(n, 1) * 4 + 255) & ~uint64_t(255); };
     const uint64_t rows = (uint64_t)G * (P16 + 1) * sizeof(uint64_t);
     if (fail_rc == MI355_OK) {
         hipError_t e = ctx->xsendR.ensure(std::max<uint64_t>(nR, 1) * elem);
@@ -669,7 +672,8 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
         if (!o.wire16) {
             if (e == hipSuccess) e = ctx->xrecvS.ensure(std::max<uint64_t>(cS, 1) * elem);
         } else {
-            if (e == hipSuccess) e = ctx->wsendS.ensure(res_bytes(nS) + rows);
+            if (e == hipSuccess) e = ctx->wsendS.ensure(snd_bytes(nS) + rows);
+            if (e == hipSuccess && need_kmax) e = ctx->xrecvS.ensure(std::max<uint64_t>(cS, 1) * elem);  // fallback
             if (e == hipSuccess)
                 e = ctx->wrecvS.ensure(res_bytes(cS) + rows + rho::wire_scratch_u64(G, P16) * sizeof(uint64_t));
         }
@@ -712,37 +716,43 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
     std::vector<uint64_t> s_piece(K, 0);  // S tuples landing per piece (S's local pass 1 runs per piece)
     std::vector<uint64_t> wbase;  // u16 wire: where sender q's run of S residuals lands
     // (u16 wire: R's pieces only; S follows below)
-    for (int j = 0; j < (o.wire16 ? K : M); ++j) {
-        const int rel = j / K;
-        char *snd = (rel ? ctx->xsendS : ctx->xsendR).as<char>() + pa[j] * elem;
-        char *rcv = (rel ? ctx->xrecvS : ctx->xrecvR).as<char>() + total[rel] * elem;
-        if (fail_rc == MI355_OK) fail(rho::shard_scatter_piece(ctx, s, j, snd));
-        hipEvent_t ready = rs->ev[j];
-        hip_ok(hipEventRecord(ready, s), "hipEventRecord (piece ready)");
-        if (const uint32_t us = exchange_delay_us())  // tests: every piece lands late
-            hip_ok(rho::launch_spin(us, rs->comm), "launch_spin (exchange delay)");
-        const uint64_t *scj = sc.data() + (size_t)j * G, *rcj = rc.data() + (size_t)j * G;
-        MH_RC(transport_rc(T.post_exchange(rank, rs->comm, ready, snd, scj, rcv, rcj, elem)));
-        for (int q = 0; q < G; ++q) {
-            total[rel] += rcj[q];
-            if (rel) s_piece[j - K] += rcj[q];
-            if (q != rank) o.sent += scj[q] * elem;
+    bool s_scattered = false;
+    const auto post_pieces = [&](int j0, int j1) -> int {
+        for (int j = j0; j < j1; ++j) {
+            const int rel = j / K;
+            char *snd = (rel ? ctx->xsendS : ctx->xsendR).as<char>() + pa[j] * elem;
+            char *rcv = (rel ? ctx->xrecvS : ctx->xrecvR).as<char>() + total[rel] * elem;
+            if (fail_rc == MI355_OK && !(rel && s_scattered)) fail(rho::shard_scatter_piece(ctx, s, j, snd));
+            hipEvent_t ready = rs->ev[j];
+            hip_ok(hipEventRecord(ready, s), "hipEventRecord (piece ready)");
+            if (const uint32_t us = exchange_delay_us())  // tests: every piece lands late
+                hip_ok(rho::launch_spin(us, rs->comm), "launch_spin (exchange delay)");
+            const uint64_t *scj = sc.data() + (size_t)j * G, *rcj = rc.data() + (size_t)j * G;
+            MH_RC(transport_rc(T.post_exchange(rank, rs->comm, ready, snd, scj, rcv, rcj, elem)));
+            for (int q = 0; q < G; ++q) {
+                total[rel] += rcj[q];
+                if (rel) s_piece[j - K] += rcj[q];
+                if (q != rank) o.sent += scj[q] * elem;
+            }
+            if (rel) hip_ok(hipEventRecord(rs->ev[2 * K + 2 + (j - K)], rs->comm), "hipEventRecord (S piece landed)");
+            if ((j + 1) % K == 0)
+                hip_ok(hipEventRecord(rs->ev[2 * K + rel], rs->comm), "hipEventRecord (relation landed)");
         }
-        if (rel) hip_ok(hipEventRecord(rs->ev[2 * K + 2 + (j - K)], rs->comm), "hipEventRecord (S piece landed)");
-        if ((j + 1) % K == 0)
-            hip_ok(hipEventRecord(rs->ev[2 * K + rel], rs->comm), "hipEventRecord (relation landed)");
-    }
+        return MI355_OK;
+    };
+    MH_RC(post_pieces(0, o.wire16 ? K : M));
+    // S on the u16 wire: its pieces' shard scatters, then the receiver's two passes over
+    // the keys for each destination (its runs: one per piece), the counts rows and the
+    // residuals posted -- all while R's keys are on the wire; R's local passes then run
+    // while S's residuals are (DESIGN.md §5 "Residuals on the wire")
+    uint16_t *snd16 = o.wire16 ? ctx->wsendS.as<uint16_t>() : nullptr;
+    uint64_t *scnt = o.wire16 ? reinterpret_cast<uint64_t *>(ctx->wsendS.as<char>() + snd_bytes(nS)) : nullptr;
+    uint64_t *rcnt = o.wire16 ? reinterpret_cast<uint64_t *>(ctx->wrecvS.as<char>() + res_bytes(cS)) : nullptr;
+    std::vector<uint64_t> s16(G, 0), r16(G, 0);
     if (o.wire16) {
-        // S on the u16 wire: its pieces' shard scatters, then the receiver's two passes
-        // over the keys for each destination (its runs: one per piece), the counts rows
-        // and the residuals posted -- all while R's keys are on the wire; R's local
-        // passes then run while S's residuals are (DESIGN.md §5 "Residuals on the wire")
         for (int i = 0; i < K && fail_rc == MI355_OK; ++i)
             fail(rho::shard_scatter_piece(ctx, s, K + i, ctx->xsendS.as<char>() + pa[K + i] * elem));
-        uint16_t *snd16 = ctx->wsendS.as<uint16_t>();
-        uint64_t *scnt = reinterpret_cast<uint64_t *>(ctx->wsendS.as<char>() + res_bytes(nS));
-        uint64_t *rcnt = reinterpret_cast<uint64_t *>(ctx->wrecvS.as<char>() + res_bytes(cS));
-        std::vector<uint64_t> roff((size_t)G * K), rn((size_t)G * K), s16(G, 0), r16(G, 0);
+        std::vector<uint64_t> roff((size_t)G * K), rn((size_t)G * K);
         for (int q = 0; q < G; ++q)
             for (int i = 0; i < K; ++i) {
                 const int j = K + i;
@@ -753,9 +763,30 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
                 s16[q] += sc[(size_t)j * G + q];
                 r16[q] += rc[(size_t)j * G + q];
             }
+        s_scattered = true;
         if (fail_rc == MI355_OK)
             fail(rho::wire_partition(ctx, s, ctx->xsendS.as<uint32_t>(), G, K, roff.data(), rn.data(), sum[0] / G,
                                      sum[1] / G, &lo, snd16, scnt, "wireS_"));
+        if (need_kmax) {
+            // the plan does not guarantee 16-bit residuals (log2 G + bits < 16): S's
+            // largest key over all ranks decides; otherwise S goes as keys (its shard
+            // scatter is in xsendS already) and the local join takes the 4-byte plan
+            std::vector<uint64_t> km(G, 0);
+            if (fail_rc == MI355_OK) {
+                for (int q = 0; q < G; ++q)
+                    hip_ok(hipMemcpyAsync(&km[q], scnt + (size_t)q * (P16 + 1) + P16, sizeof(uint64_t),
+                                          hipMemcpyDeviceToHost, s),
+                           "hipMemcpyAsync (largest key)");
+                hip_ok(hipStreamSynchronize(s), "hipStreamSynchronize (largest key)");
+            }
+            uint64_t kmax = fail_rc == MI355_OK ? *std::max_element(km.begin(), km.end()) : 0;
+            MH_RC(transport_rc(T.allreduce(rank, s, &kmax, 1, kMax)));
+            if (((kmax >> (dest_bits + (uint32_t)__builtin_ctz(P16))) >> 16) != 0) o.wire16 = false;
+        }
+    }
+    if (!o.wire16 && s_scattered) {  // the residuals do not fit: S's pieces as keys
+        MH_RC(post_pieces(K, M));
+    } else if (o.wire16) {
         // a failed rank still sends (the sizes are agreed): zero counts rows, which no
         // receiver takes (they do not add up to the announced runs)
         if (fail_rc != MI355_OK && ctx->wsendS.ptr) (void)hipMemsetAsync(scnt, 0, rows, s);

@@ -56,16 +56,21 @@ bool keys_exchange_plan(uint64_t nR, uint64_t nS, uint64_t cap_r, uint64_t cap_s
 // ---- multi-GPU u16 wire (DESIGN.md §5 "Residuals on the wire") ----
 // Whether a keys exchange (lo from keys_exchange_plan, lo->key_shift = log2 G) can send
 // S as 2-byte residuals instead (R's keys still travel as 4 bytes: R's local passes run
-// while S is on the wire, S's sender-side passes while R is): the local plan of nR x nS (the mean local sizes) is a
-// two-pass narrow counting RHO plan, and every 32-bit key's residual above the shard and
-// partition bits fits 16 bits (key_shift + bits >= 16).  SGXAMD_WIRE16=0 disables it.
-// Returns the plan's partition count P (0: no).
-uint32_t wire16_plan(uint64_t nR, uint64_t nS, int G, const mi355_rho_opts *lo);
+// while S is on the wire, S's sender-side passes while R is): the local plan of nR x nS
+// (the mean local sizes) is a two-pass narrow counting RHO plan, and every 32-bit key's
+// residual above the shard and partition bits fits 16 bits (key_shift + bits >= 16) --
+// or, with need_kmax, may: then *need_kmax is set and the caller must check S's largest
+// key over all ranks (2-byte residuals only when (kmax >> (key_shift + bits)) < 2^16).
+// mi355_multi_set_wire / SGXAMD_WIRE16 select the mode.  Returns the plan's partition
+// count P (0: no).
+uint32_t wire16_plan(uint64_t nR, uint64_t nS, int G, const mi355_rho_opts *lo, bool *need_kmax = nullptr);
 // mi355_multi_set_wire: 0 off, 1 where the local plan is narrow anyway, 2 whenever the
 // residuals fit (tests).
 void set_wire_mode(int mode);
 int wire_mode();
-// Sender: partitions the keys this rank sends each destination (runs of packed u32
+// Sender (out16: 4 bytes per key -- a destination whose residuals do not fit 16 bits,
+// possible only with need_kmax, is written as keys and the caller sends S as keys):
+// partitions the keys this rank sends each destination (runs of packed u32
 // keys in `keys`: destination q's runs at run_off[q * runs + j], run_n[...]) with the
 // plan of wire16_plan(nR, nS, ...): destination q's residuals go to out16 + the keys of
 // destinations before q, grouped by partition; counts[q * (P + 1) + p] = its partition

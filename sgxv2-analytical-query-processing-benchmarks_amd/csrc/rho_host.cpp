@@ -1191,7 +1191,8 @@ int wire_mode() {
     return e ? std::max(0, std::min(2, std::atoi(e))) : 1;
 }
 
-uint32_t wire16_plan(uint64_t nR, uint64_t nS, int G, const mi355_rho_opts *lo) {
+uint32_t wire16_plan(uint64_t nR, uint64_t nS, int G, const mi355_rho_opts *lo, bool *need_kmax) {
+    if (need_kmax) *need_kmax = false;
     const int mode = wire_mode();
     if (!mode || !lo || lo->materialize || lo->algorithm == MI355_ALGO_RHT || G < 2 || (uint32_t)G > kWireMaxG)
         return 0;
@@ -1201,10 +1202,13 @@ uint32_t wire16_plan(uint64_t nR, uint64_t nS, int G, const mi355_rho_opts *lo) 
     // table): elsewhere (BASELINE config 4 at G = 8: 1,024 R keys per partition) forcing
     // it costs more compute than the halved S bytes save (r05x5)
     if (mode == 1 && !takes_big_table(p, nR, nS, lo)) return 0;
-    // every 32-bit key's residual fits 16 bits: no device-side width check can differ
-    if (p.passes != 2 || !uses_digit_side(p) || lo->key_shift + p.bits < 16 || lo->key_shift + p.bits > 31 ||
-        p.bits > 20)
-        return 0;
+    if (p.passes != 2 || !uses_digit_side(p) || lo->key_shift + p.bits > 31 || p.bits > 20) return 0;
+    // every 32-bit key's residual fits 16 bits, or (need_kmax) the caller checks S's
+    // largest key over all ranks before the residuals are posted
+    if (lo->key_shift + p.bits < 16) {
+        if (!need_kmax) return 0;
+        *need_kmax = true;
+    }
     return 1u << p.bits;
 }
 

@@ -88,9 +88,9 @@ def test_keys_only_exchange(sgx, orc, gpu, wire16, g, n, kw):
     res = multi(sgx, R, S, g, **kw)
     assert res.matches == exp
     st = res.stats
-    # 2-byte residuals when every key's residual above the shard and partition bits fits
-    # 16 bits (the forced 14-bit plan over 8 ranks), else 4-byte keys
-    wire16 = (g.bit_length() - 1) + st["local"]["radix_bits"] >= 16
+    # S as 2-byte residuals when its keys' residuals above the shard and partition bits
+    # fit 16 bits (u16 wire forced: mode 2), else 4-byte keys
+    wire16 = (int(S["key"].max()) >> ((g.bit_length() - 1) + st["local"]["radix_bits"])) < 2**16
     assert st["elem_bytes"] == (2 if wire16 else 4) and st["local"]["layout"] in (2, 3, 4)
     # every key of a rank except those it keeps goes out once
     assert st["sent_bytes"] == _exchange_bytes(st, _keys_out(R, g), _keys_out(S, g), g)
@@ -319,6 +319,25 @@ def test_wire16_exchange(sgx, orc, gpu, wire16, g):
         assert st["elem_bytes"] == 2 and st["local"]["radix_bits"] == bits
         assert st["sent_bytes"] == _exchange_bytes(st, _keys_out(R, g), _keys_out(S, g), g)
         assert 0 <= st["ms_tail"] <= st["ms_total"]
+
+
+def test_wire16_largest_key_check(sgx, orc, gpu, wire16):
+    """2 ranks and a 14-bit plan: log2 G + bits = 15 < 16, so the residuals fit 16 bits
+    only when S's keys allow.  The senders run their passes, then S's largest key over
+    the ranks decides: 2-byte residuals for keys below 2^31 (pk / fk), else S goes as
+    4-byte keys (its shard scatter reused) and the local join takes the 4-byte plan --
+    exact either way, and the bytes say which."""
+    R, S = sgx.reference_relations(1 << 20, 1 << 20)
+    res = multi(sgx, R, S, 2, radix_bits=14, passes=2)
+    assert res.matches == orc.count_join_sort(R, S) and res.stats["elem_bytes"] == 2
+    assert res.stats["sent_bytes"] == _exchange_bytes(res.stats, _keys_out(R, 2), _keys_out(S, 2), 2)
+    rng = np.random.default_rng(77)
+    R2 = rel(rng.integers(0, 2**32, 200_001, dtype=np.uint64).astype(np.uint32))
+    S2 = rel(np.concatenate([rng.integers(0, 2**32, 150_000, dtype=np.uint64).astype(np.uint32),
+                             R2["key"][:60_000], np.array([2**32 - 1], dtype=np.uint32)]))
+    res = multi(sgx, R2, S2, 2, radix_bits=14, passes=2)
+    assert res.matches == orc.count_join_sort(R2, S2) and res.stats["elem_bytes"] == 4
+    assert res.stats["sent_bytes"] == 4 * (_keys_out(R2, 2) + _keys_out(S2, 2))
 
 
 def _slices_sent(keys, g, elem):

@@ -338,6 +338,9 @@ def _wire16_rccl(sgx, orc, gpu, g):
     st = res.stats
     assert res.matches == exp and st["transport"] == "rccl" and st["elem_bytes"] == 2
     assert st["sent_bytes"] == _exchange_bytes(st, _keys_out(Rh, g), _keys_out(Sh, g), g)
+    if g == 2:  # log2 G + 14 bits < 16: S's largest key decides (here: too large, keys)
+        res = multi(sgx, Rh, Sh, g, radix_bits=14, passes=2)
+        assert res.matches == exp and res.stats["elem_bytes"] == 4
     Pk, Fk = sgx.reference_relations(1 << 20, 1 << 20)
     R = torch.from_numpy(Pk.view(np.int64)).to(gpu)
     S = torch.from_numpy(Fk.view(np.int64)).to(gpu)
