@@ -2348,6 +2348,9 @@ hipError_t launch_block_list(const PoolOut &po, const uint64_t *lbase, uint64_t 
 // step's digit bytes in flight another 18-20 % (0.087 -> 0.071): the kernel was bound
 // by its two dependent loads per step more than by the LDS.
 constexpr uint32_t kLaneHistF = 128;
+#ifndef SGXAMD_HSIDE_U
+#define SGXAMD_HSIDE_U 4
+#endif
 __device__ __forceinline__ void hist_side_lanes(const uint8_t *__restrict__ side, const uint64_t *__restrict__ list,
                                                 uint64_t b, uint64_t e, uint32_t F, uint64_t *__restrict__ out) {
     static_assert(kPass2Ents <= 4096, "u16 lane counters");
@@ -2360,7 +2363,7 @@ __device__ __forceinline__ void hist_side_lanes(const uint8_t *__restrict__ side
     for (uint32_t i = tid; i < ne; i += kBlock) ents[i] = list[b + i];
     __syncthreads();
     const uint32_t grp = tid / 16, l = tid % 16;
-    constexpr int U = 4;  // blocks per 16-lane group and step
+    constexpr int U = SGXAMD_HSIDE_U;  // blocks per 16-lane group and step
     constexpr uint32_t SPAN = 16 * U;
     // one step: the 16-B digit pieces of U blocks per group (entries past ne load nothing)
     const auto load_step = [&](uint32_t i0, uint4 (&q)[U], uint32_t (&nv)[U]) {
