@@ -968,6 +968,16 @@ bool small_join_enabled() {
     return on;
 }
 
+// SGXAMD_SMALL_DIRECT=0 (development A/B, read once): the small joins' build/probe keeps
+// the chain table where the direct count table would fit.
+bool small_direct_enabled() {
+    static const bool on = [] {
+        const char *e = std::getenv("SGXAMD_SMALL_DIRECT");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return on;
+}
+
 int join_small(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const row_t *dS, uint64_t nS,
                const mi355_rho_opts *opts, mi355_rho_stats *st) {
     PendingJoin &pj = pending_of(ctx);
@@ -1035,21 +1045,25 @@ int join_small(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const 
     const uint32_t par = ctx->small_parity;
     ctx->small_parity ^= 1u;
     tm.mark("RS_pass1_hist");
+    // R's largest key (the direct count table of the build/probe), per parity set
+    uint64_t *kmax = small_direct_enabled() ? sync + kSyncKmax : nullptr;
     RHO_HIP(launch_hist_pair(dR, mR, pj.pr.nseg1, dS, mS, pj.ps.nseg1, pj.key_shift, pol.b1, offsR, offsS,
-                             sync + sync_tot(par, 0), sync + sync_tot(par, 1), sync + kSyncT0, s));
+                             sync + sync_tot(par, 0), sync + sync_tot(par, 1), sync + kSyncT0, s,
+                             kmax ? kmax + par : nullptr));
     tm.mark("RS_pass1_scatter");
     // cursors: each segment's offset inside its copy of the digit totals + that copy's
     // digit start (each scatter workgroup scans the totals itself)
     RHO_HIP(launch_scatter_pair(dR, oR, mR, 2 * pj.pr.nseg1, offsR, sync + sync_tot(par, 0), sync + sync_tot(par ^ 1, 0),
                                 startR, cntR, dS, oS, mS, 2 * pj.ps.nseg1, offsS, sync + sync_tot(par, 1),
                                 sync + sync_tot(par ^ 1, 1), startS, cntS, pj.key_shift, pol.b1, over, pj.over_cap,
-                                result + 1, pj.s_chunk, s));
+                                result + 1, pj.s_chunk, s, kmax ? kmax + (par ^ 1) : nullptr));
     tm.mark("join_build_probe");
     const uint64_t P = 1ull << pol.bits;
     const JoinReduce red{result, sync + kSyncTicketJoin};
     RHO_HIP(launch_join(oR, oS, startR, cntR, startS, cntS, P, over, reinterpret_cast<uint32_t *>(result + 3),
                         pj.key_shift + pol.bits, pol.rcap, pj.s_chunk, pj.join_grid, kJoinCount, pj.algo,
-                        A.at<uint64_t>(pj.off_counts), nullptr, nullptr, A.at<uint64_t>(pj.off_cyc), s, &red));
+                        A.at<uint64_t>(pj.off_counts), nullptr, nullptr, A.at<uint64_t>(pj.off_cyc), s, &red, 2,
+                        nullptr, nullptr, nullptr, 0, kmax ? kmax + par : nullptr));
     tm.end_call();
     // the join's last workgroup wrote the result words into host_join: no copy back, and
     // without per-kernel events no stream synchronisation either (a launch + synchronise

@@ -89,7 +89,10 @@ constexpr uint32_t kSyncSub = kSyncTot0 + 4 * kSyncTotWords;  // relative to a t
 // the count reduction's group word pairs (join_reduce_last: kJoinGroups of them)
 constexpr uint32_t kJoinGroups = 16;
 constexpr uint32_t kSyncJoinGrp = kSyncSub + kNumTickets * (kSyncSpread + 1);
-constexpr uint32_t kSyncWords = kSyncJoinGrp + 2 * kJoinGroups;
+// R's largest key (k_hist_pair; the direct table of k_join), one word per parity set: the
+// scatter's layout workgroup zeroes the next call's
+constexpr uint32_t kSyncKmax = kSyncJoinGrp + 2 * kJoinGroups;
+constexpr uint32_t kSyncWords = kSyncKmax + 2;
 // Development: small-join workgroup stamps (rho_kernels.hip dbg_stamp), 3 kernels + the
 // build/probe reduction x 3
 // stamps x kStampWgs u64; null turns them off.
@@ -101,9 +104,10 @@ hipError_t set_debug_stamps(uint64_t *p);
 // [d][2 grid] segment offsets inside the segment's copy (g mod kSyncSpread) of digit d's
 // total in tot (sync_tot of this call's parity, zero at entry).  t0: the call's start
 // (sync[kSyncT0]).
+// kmaxR (nullable, zero at entry): R's largest key, max-ed in.
 hipError_t launch_hist_pair(const row_t *R, const SegMap &mR, uint32_t gridR, const row_t *S, const SegMap &mS,
                             uint32_t gridS, uint32_t shift, uint32_t bits, uint64_t *offsR, uint64_t *offsS,
-                            uint64_t *totR, uint64_t *totS, uint64_t *t0, hipStream_t s);
+                            uint64_t *totR, uint64_t *totS, uint64_t *t0, hipStream_t s, uint64_t *kmaxR = nullptr);
 // Both relations' one-pass scatters in one launch (cursors: the segment offsets + the
 // digit starts of the segment's totals copy, taken by each workgroup from tot), plus one
 // workgroup that writes the partition table (start / cnt), the task list (over, meta as
@@ -113,7 +117,7 @@ hipError_t launch_scatter_pair(const row_t *R, row_t *outR, const SegMap &mR, ui
                                const row_t *S, row_t *outS, const SegMap &mS, uint32_t gridS, const uint64_t *offsS,
                                const uint64_t *totS, uint64_t *totS_next, uint64_t *startS, uint64_t *cntS,
                                uint32_t shift, uint32_t bits, uint64_t *over, uint32_t over_cap, uint64_t *meta,
-                               uint64_t s_chunk, hipStream_t s);
+                               uint64_t s_chunk, hipStream_t s, uint64_t *kmax_next = nullptr);
 
 // Digit side stream of a two-pass partition: the pass-1 scatter also writes, for the
 // tuple it stores at position a of its output, the tuple's pass-2 digit
@@ -287,7 +291,10 @@ hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, 
                        int mode, int algo, uint64_t *counts, const uint64_t *task_off, output_triple_t *out,
                        uint64_t *cyc, hipStream_t s, const JoinReduce *reduce = nullptr, int key_stride = 2,
                        uint32_t *tickets = nullptr, const uint32_t *narrow_r = nullptr,
-                       const uint32_t *narrow_s = nullptr, uint32_t tasks_max = 0);
+                       const uint32_t *narrow_s = nullptr, uint32_t tasks_max = 0,
+                       const uint64_t *small_kmax = nullptr);
+// small_kmax (nullable; tuples, counting, the small joins' 1,024-thread chaining table):
+// R's largest key -- chunks whose residuals fit count in a direct table.
 // key_stride 2: R / S are row_t partitions; 1: packed u32 keys (counting RHO only —
 // the partitions of a counting join carry keys only after the input read).
 // tickets (nullable; a u32 that is zero at the launch, e.g. meta[5] of launch_make_tasks):

@@ -122,9 +122,11 @@ __device__ __forceinline__ bool hist_segment(const uint32_t *__restrict__ in_wor
 
 // Histograms of two consecutive segments of a single-region map (2g and 2g + 1, even
 // starts) into h / h2 with both segments' 16-B loads in flight together (one memory round
-// trip per step instead of one per segment).  false: both empty.
+// trip per step instead of one per segment).  false: both empty.  kmax: this thread's
+// largest key seen (max-ed in).
 __device__ __forceinline__ bool hist_two_segments(const uint32_t *__restrict__ in_words, const SegMap &m, uint32_t g,
-                                                  uint32_t shift, uint32_t bits, uint32_t *h, uint32_t *h2) {
+                                                  uint32_t shift, uint32_t bits, uint32_t *h, uint32_t *h2,
+                                                  uint32_t &kmax) {
     const uint64_t n = m.single_n, seg = m.seg_size;
     const uint64_t bA = min<uint64_t>(2ull * g * seg, n), eA = min<uint64_t>(bA + seg, n), eB = min<uint64_t>(eA + seg, n);
     if (bA >= eB) return false;
@@ -149,16 +151,26 @@ __device__ __forceinline__ bool hist_two_segments(const uint32_t *__restrict__ i
             if (k < npa) {
                 atomicAdd(&h[(qa[u].x >> shift) & mask], 1u);
                 atomicAdd(&h[(qa[u].z >> shift) & mask], 1u);
+                kmax = max(kmax, max(qa[u].x, qa[u].z));
             }
             if (k < npb) {
                 atomicAdd(&h2[(qb[u].x >> shift) & mask], 1u);
                 atomicAdd(&h2[(qb[u].z >> shift) & mask], 1u);
+                kmax = max(kmax, max(qb[u].x, qb[u].z));
             }
         }
     }
     if (threadIdx.x == 0) {  // odd trailing tuples (segments start at even offsets)
-        if ((eA - bA) & 1) atomicAdd(&h[(in_words[2 * (eA - 1)] >> shift) & mask], 1u);
-        if ((eB - eA) & 1) atomicAdd(&h2[(in_words[2 * (eB - 1)] >> shift) & mask], 1u);
+        if ((eA - bA) & 1) {
+            const uint32_t k = in_words[2 * (eA - 1)];
+            atomicAdd(&h[(k >> shift) & mask], 1u);
+            kmax = max(kmax, k);
+        }
+        if ((eB - eA) & 1) {
+            const uint32_t k = in_words[2 * (eB - 1)];
+            atomicAdd(&h2[(k >> shift) & mask], 1u);
+            kmax = max(kmax, k);
+        }
     }
     __syncthreads();
     return true;
@@ -262,6 +274,7 @@ struct HistPairRel {
     uint32_t shift;
     uint64_t *offs;       // [d][g] (stride grid): segment g's offset inside its copy of digit d
     uint64_t *tot;        // [kSyncSpread][kMaxF] digit totals, zero at entry
+    uint64_t *kmax;       // (nullable) the relation's largest key, max-ed in (zero at entry)
 };
 
 __global__ __launch_bounds__(kBlock) void k_hist_pair(HistPairRel A, HistPairRel B, uint32_t bits,
@@ -276,7 +289,19 @@ __global__ __launch_bounds__(kBlock) void k_hist_pair(HistPairRel A, HistPairRel
     // segment g is two scatter segments (H.m's, halves 2g and 2g + 1: one tile each, so
     // that the scatter's workgroups each load, sort and write one tile): one histogram
     // each, their sum to the totals, the second half's offset after the first half's
-    const bool any = hist_two_segments(H.in, H.m, g, H.shift, bits, h, h2);
+    uint32_t km = 0;
+    const bool any = hist_two_segments(H.in, H.m, g, H.shift, bits, h, h2, km);
+    if (H.kmax) {  // one device atomic per workgroup (h2's words are free after the counts)
+        km = wave_max_u32(km);
+        __shared__ uint32_t wm[kBlock / kWave];
+        if (__lane_id() == 0) wm[threadIdx.x / kWave] = km;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t m = 0;
+            for (uint32_t w = 0; w < kBlock / kWave; ++w) m = max(m, wm[w]);
+            if (m) __hip_atomic_fetch_max(H.kmax, (uint64_t)m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
     uint64_t *tot_c = H.tot + (uint64_t)(g % kSyncSpread) * kMaxF;  // this segment's copy of the totals
     for (uint32_t d = threadIdx.x; d < F; d += kBlock) {
         const uint32_t a = any ? h[d] : 0u, v = a + (any ? h2[d] : 0u);
@@ -290,9 +315,9 @@ __global__ __launch_bounds__(kBlock) void k_hist_pair(HistPairRel A, HistPairRel
 
 hipError_t launch_hist_pair(const row_t *R, const SegMap &mR, uint32_t gridR, const row_t *S, const SegMap &mS,
                             uint32_t gridS, uint32_t shift, uint32_t bits, uint64_t *offsR, uint64_t *offsS,
-                            uint64_t *totR, uint64_t *totS, uint64_t *t0, hipStream_t s) {
-    const HistPairRel A{reinterpret_cast<const uint32_t *>(R), mR, gridR, shift, offsR, totR};
-    const HistPairRel B{reinterpret_cast<const uint32_t *>(S), mS, gridS, shift, offsS, totS};
+                            uint64_t *totR, uint64_t *totS, uint64_t *t0, hipStream_t s, uint64_t *kmaxR) {
+    const HistPairRel A{reinterpret_cast<const uint32_t *>(R), mR, gridR, shift, offsR, totR, kmaxR};
+    const HistPairRel B{reinterpret_cast<const uint32_t *>(S), mS, gridS, shift, offsS, totS, nullptr};
     hipLaunchKernelGGL(k_hist_pair, dim3(gridR + gridS), dim3(kBlock), 0, s, A, B, bits, t0);
     return hipGetLastError();
 }
@@ -1221,7 +1246,7 @@ __device__ __forceinline__ void pair_starts(const uint64_t *__restrict__ tot, ui
 template <int BITS, int ITEMS, int NT>
 __global__ __launch_bounds__(NT, (scatter_waves_per_simd<BITS, ITEMS, NT>())) void k_scatter_pair(
     ScatterPairRel A, ScatterPairRel B, uint32_t shift, uint64_t *__restrict__ over, uint32_t over_cap,
-    uint64_t *__restrict__ meta, uint64_t s_chunk) {
+    uint64_t *__restrict__ meta, uint64_t s_chunk, uint64_t *__restrict__ kmax_next) {
     __shared__ ScatterLds<BITS, ITEMS, NT> L;
     __shared__ uint64_t base[1u << BITS];
     __shared__ uint64_t scratch[NT / kWave + 1];
@@ -1258,6 +1283,7 @@ __global__ __launch_bounds__(NT, (scatter_waves_per_simd<BITS, ITEMS, NT>())) vo
             A.tot_next[i] = 0;
             B.tot_next[i] = 0;
         }
+        if (kmax_next && threadIdx.x == 0) *kmax_next = 0;  // the next call's largest R key
         return;
     }
     const bool isB = blockIdx.x >= A.grid;
@@ -1276,7 +1302,7 @@ hipError_t launch_scatter_pair(const row_t *R, row_t *outR, const SegMap &mR, ui
                                const row_t *S, row_t *outS, const SegMap &mS, uint32_t gridS, const uint64_t *offsS,
                                const uint64_t *totS, uint64_t *totS_next, uint64_t *startS, uint64_t *cntS,
                                uint32_t shift, uint32_t bits, uint64_t *over, uint32_t over_cap, uint64_t *meta,
-                               uint64_t s_chunk, hipStream_t s) {
+                               uint64_t s_chunk, hipStream_t s, uint64_t *kmax_next) {
     constexpr int ITEMS = kScatterItems, NT = kScatterThreads;
     const ScatterPairRel A{reinterpret_cast<const uint64_t *>(R), reinterpret_cast<uint64_t *>(outR), mR, gridR,
                            offsR, totR, totR_next, startR, cntR};
@@ -1288,7 +1314,7 @@ hipError_t launch_scatter_pair(const row_t *R, row_t *outR, const SegMap &mR, ui
         if constexpr (sizeof(ScatterLds<BB, ITEMS, NT>) + (8u << BB) + 8 * (NT / kWave + 1) <= 160 * 1024 &&  \
                       (1 << BB) <= NT) {                                                                     \
             hipLaunchKernelGGL((k_scatter_pair<BB, ITEMS, NT>), grid, dim3(NT), 0, s, A, B, shift, over,       \
-                               over_cap, meta, s_chunk);                                                    \
+                               over_cap, meta, s_chunk, kmax_next);                                         \
             break;                                                                                          \
         } else {                                                                                            \
             return hipErrorInvalidValue;                                                                    \
@@ -2609,7 +2635,14 @@ struct JoinLds<RCAP, kJoinWrite, NW> {
 };
 
 // KS: u32 words per partitioned element (2: row_t tuples; 1: packed keys, counting only).
-template <int RCAP, int MODE, int BLOCK = kBlock, int KS = 2>
+// DIRECT (counting; small joins): task_off holds R's largest key (one u64; the unused
+// output offsets of a counting launch).  When every R residual (key >> hash_shift) is
+// below 2 RCAP, a chunk is counted in a direct table instead of the chain table: one u16
+// counter per residual (two per head word), R's keys add 1, S's keys read their
+// residual's counter (residuals identify keys inside a partition: the low hash_shift
+// bits are the partition's).  One LDS atomic per R key and one read per S key instead of
+// the chain's exchange, two stores, and the walk.
+template <int RCAP, int MODE, int BLOCK = kBlock, int KS = 2, bool DIRECT = false>
 __global__ __launch_bounds__(BLOCK) void k_join(const uint64_t *__restrict__ R, const uint64_t *__restrict__ S,
                                                  const uint64_t *__restrict__ r_start,
                                                  const uint64_t *__restrict__ r_count,
@@ -2630,6 +2663,10 @@ __global__ __launch_bounds__(BLOCK) void k_join(const uint64_t *__restrict__ R, 
     const uint64_t T = P + *n_over;
     uint64_t matches = 0;
     uint64_t bcyc = 0, pcyc = 0;  // build / probe wall-clock ticks of this workgroup
+    static_assert(!DIRECT || MODE == kJoinCount, "the direct table counts");
+    // residuals in use (u16 counters): 0 = the chain table
+    const uint32_t tlim = DIRECT && (task_off[0] >> hash_shift) < 2ull * RCAP
+                              ? (uint32_t)(task_off[0] >> hash_shift) + 1u : 0u;
     for (uint64_t t = blockIdx.x; t < T; t += gridDim.x) {
         uint64_t p, chunk;
         decode_task(t, P, over, p, chunk);
@@ -2657,6 +2694,41 @@ __global__ __launch_bounds__(BLOCK) void k_join(const uint64_t *__restrict__ R, 
                         kr[u] = i < nrc ? __builtin_nontemporal_load(Rk + r_start[p] + rc + i) : 0u;
                     else
                         kr[u] = i < nrc ? ld_nt(rp + rc + i) : 0ull;
+                }
+                if (DIRECT && tlim) {
+                    for (uint32_t i = tid; i < (tlim + 1) / 2; i += BLOCK) L.head[i] = 0;
+                    __syncthreads();
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const uint32_t i = tid + u * BLOCK;
+                        if (i < nrc) {
+                            const uint32_t r = (uint32_t)kr[u] >> hash_shift;
+                            atomicAdd(&L.head[r >> 1], 1u << ((r & 1u) * 16u));
+                        }
+                    }
+                    __syncthreads();
+                    const uint64_t c_probe = wall_clock64();
+                    bcyc += c_probe - c_build;
+                    for (uint64_t s0 = 0; s0 < nS; s0 += RCAP) {
+                        uint32_t ks[U];
+#pragma unroll
+                        for (int u = 0; u < U; ++u) {
+                            const uint64_t i = s0 + tid + u * BLOCK;
+                            if constexpr (KS == 1)
+                                ks[u] = i < nS ? __builtin_nontemporal_load(Sk + s_start[p] + s_lo + i) : 0u;
+                            else
+                                ks[u] = i < nS ? __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(sp + i)) : 0u;
+                        }
+#pragma unroll
+                        for (int u = 0; u < U; ++u) {
+                            const uint64_t i = s0 + tid + u * BLOCK;
+                            const uint32_t r = ks[u] >> hash_shift;
+                            if (i < nS && r < tlim) tmatch += (L.head[r >> 1] >> ((r & 1u) * 16u)) & 0xFFFFu;
+                        }
+                    }
+                    __syncthreads();
+                    pcyc += wall_clock64() - c_probe;
+                    continue;
                 }
                 for (uint32_t i = tid; i < (N + 3) / 4; i += BLOCK)
                     reinterpret_cast<uint4 *>(L.head)[i] = make_uint4(0, 0, 0, 0);
@@ -3966,7 +4038,8 @@ hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, 
                        const uint32_t *n_over, uint32_t hash_shift, uint32_t rcap, uint64_t s_chunk, uint32_t grid,
                        int mode, int algo, uint64_t *counts, const uint64_t *task_off, output_triple_t *out,
                        uint64_t *cyc, hipStream_t s, const JoinReduce *reduce, int key_stride, uint32_t *tickets,
-                       const uint32_t *narrow_r, const uint32_t *narrow_s, uint32_t tasks_max) {
+                       const uint32_t *narrow_r, const uint32_t *narrow_s, uint32_t tasks_max,
+                       const uint64_t *small_kmax) {
     if (key_stride == 1)
         return launch_join_keys(R, S, r_start, r_count, s_start, s_count, P, over, n_over, hash_shift, rcap, s_chunk,
                                 grid, mode, algo, counts, cyc, s, reduce, tickets, narrow_r, narrow_s, tasks_max);
@@ -4009,9 +4082,14 @@ hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, 
         // instead of 256, so that a CU holds 16 waves to hide the load latencies
 #define JOIN_WIDE(RC)                                                                                        \
     case RC:                                                                                                 \
-        hipLaunchKernelGGL((k_join<RC, kJoinCount, 1024>), dim3(grid), dim3(1024), 0, s, R64, S64, r_start,   \
-                           r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts, task_off, out, \
-                           cyc, rres, rtick);                                                                \
+        if (small_kmax) /* the direct table where R's residuals allow (task_off: R's largest key) */       \
+            hipLaunchKernelGGL((k_join<RC, kJoinCount, 1024, 2, true>), dim3(grid), dim3(1024), 0, s, R64,    \
+                               S64, r_start, r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk, \
+                               counts, small_kmax, out, cyc, rres, rtick);                                    \
+        else                                                                                                 \
+            hipLaunchKernelGGL((k_join<RC, kJoinCount, 1024>), dim3(grid), dim3(1024), 0, s, R64, S64,        \
+                               r_start, r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk,      \
+                               counts, task_off, out, cyc, rres, rtick);                                      \
         break;
         switch (rcap) {
             JOIN_WIDE(2048)

@@ -4,7 +4,8 @@ stream), SGXAMD_BIG_JOIN=0 (R partitions above 8192 tuples in 8192-tuple chain t
 instead of the 16,384-tuple counting table; the 5-bit plan below has 32,768-tuple
 partitions), SGXAMD_SMALL_JOIN=0
 (small one-pass joins on the regular launch sequence instead of the three-launch path:
-the (5, 1) plan and the full-range cases below take it), SGXAMD_POOL=0 (two-pass plans
+the (5, 1) plan and the full-range cases below take it), SGXAMD_SMALL_DIRECT=0 (their
+build/probe keeps the chain table where the direct count table fits), SGXAMD_POOL=0 (two-pass plans
 with a pass-1 histogram and cursors instead of the pooled pass 1 and block-list pass 2;
 SGXAMD_POOL_SEGS sets the pooled pass-1 workgroups: 3 gives large pools, 100000 one
 tile per segment), SGXAMD_KEYS=0 (counting joins move whole tuples instead of keys),
@@ -82,7 +83,7 @@ print("paths ok")
 
 @pytest.mark.parametrize("env", [{"SGXAMD_DIGIT_SIDE": "0", "SGXAMD_BIG_JOIN": "0"},
                                  {"SGXAMD_DIGIT_SIDE": "1", "SGXAMD_BIG_JOIN": "1"},
-                                 {"SGXAMD_SMALL_JOIN": "0"},
+                                 {"SGXAMD_SMALL_JOIN": "0"}, {"SGXAMD_SMALL_DIRECT": "0"},
                                  {"SGXAMD_POOL": "0"}, {"SGXAMD_POOL_SEGS": "3"}, {"SGXAMD_POOL_SEGS": "100000"},
                                  {"SGXAMD_KEYS": "0"}, {"SGXAMD_SORT2": "0"}, {"SGXAMD_NARROW": "0"}, {"SGXAMD_JOIN_N": "0"}, {"SGXAMD_PLACE": "0"}, {"SGXAMD_NARROW_POOL": "1"}, {"SGXAMD_CHAIN_HIST": "1"},
                                  {"SGXAMD_CHAIN_HIST": "1", "SGXAMD_CHAIN_SLOTS": "1"}])

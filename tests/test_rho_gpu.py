@@ -75,6 +75,36 @@ def test_random_with_duplicates(sgx, orc, gpu, seed, nR, nS, kmax):
         assert gpu_join(sgx, R, S, radix_bits=bits, passes=passes).matches == exp
 
 
+@pytest.mark.parametrize("case", ["edge_fit", "edge_over", "dups_multichunk", "s_above_r"])
+def test_small_join_direct_table(sgx, orc, gpu, case):
+    """Small one-pass joins count a chunk in a direct table of u16 counters when R's
+    largest residual (key >> radix bits) is below 2 x the chain table's capacity (8192 at
+    4096 R keys per partition, 8 bits over 2^20 R keys): at the edge (residuals up to
+    8191), one past it (8192: the chain table), R duplicates with partitions above the
+    table (several R chunks per partition), and S keys above R's range (no counter)."""
+    rng = np.random.default_rng(31)
+    n = 1 << 20
+    if case == "edge_fit":
+        rk = rng.integers(0, 8192 << 8, n)
+        rk[0] = (8192 << 8) - 1
+        sk = rng.integers(0, 8192 << 8, n)
+    elif case == "edge_over":
+        rk = rng.integers(0, 8192 << 8, n)
+        rk[0] = 8192 << 8
+        sk = rng.integers(0, (8192 << 8) + 1, n)
+    elif case == "dups_multichunk":
+        rk = np.concatenate([rng.integers(0, 1000 << 8, n - 20000), np.full(20000, 77 << 8)])
+        sk = rng.integers(0, 1000 << 8, n)
+    else:
+        rk = rng.integers(0, 4000 << 8, n)
+        sk = rng.integers(0, 2**32, n)
+        sk[: n // 2] = rng.integers(0, 4000 << 8, n // 2)
+    R, S = rel(rk.astype(np.uint32)), rel(sk.astype(np.uint32))
+    exp = orc.count_join_sort(R, S)
+    res = gpu_join(sgx, R, S, radix_bits=8, passes=1)
+    assert res.matches == exp, (case, res.matches, exp)
+
+
 @pytest.mark.parametrize("bits,kmax", [(6, 1 << 22), (5, 2**32 - 1), (4, 1 << 19), (1, 1 << 12)])
 def test_big_table_partitions(sgx, orc, gpu, bits, kmax):
     """Partitions above 8192 R tuples take the 16,384-tuple counting tables (RHO's chain
