@@ -950,6 +950,18 @@ __device__ __forceinline__ uint32_t scatter_tile_sort(ScatterLds<BITS, ITEMS, NT
 }
 
 // Phases D-E of the tile sorted by scatter_tile_sort (gtot = its granule count).
+// The digit side stream's byte stores (non-temporal with SGXAMD_SIDE_NT).
+#ifndef SGXAMD_SIDE_NT
+#define SGXAMD_SIDE_NT 1
+#endif
+__device__ __forceinline__ void st_side(uint8_t *p, uint8_t v) {
+#if SGXAMD_SIDE_NT
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+
 // SIDE: every stored tuple's next-pass digit also goes to side[a] (a 16-lane group
 // writes 16 consecutive bytes next to its 128-B granule).
 // OB 2 (narrow pool): the elements written are the keys' residuals key >> rshift, u16.
@@ -1046,7 +1058,7 @@ __device__ __forceinline__ void scatter_tile_write(ScatterLds<BITS, ITEMS, NT, E
             } else if (w.v0 || w.v1) {
                 const uint32_t o = w.v0 ? 0u : 1u, x = w.v0 ? w.x0 : w.x1;
                 st_nt(reinterpret_cast<uint32_t *>(out + w.a + o), x);
-                if (SIDE) side[w.a + o] = (uint8_t)((x >> shift2) & mask2);
+                if (SIDE) st_side(side + w.a + o, (uint8_t)((x >> shift2) & mask2));
             }
         };
         // pooled pass 1: two granules per group and round, so that their LDS read
@@ -1072,7 +1084,7 @@ __device__ __forceinline__ void scatter_tile_write(ScatterLds<BITS, ITEMS, NT, E
             const uint32_t q = jj * G + lane;
             const T x = lds_pick(q < cd, &L.carry[d * CS + q], &L.tile[(m.x & TB) + q - cd]);
             st_nt(out + a, x);
-            if (SIDE) side[a] = (uint8_t)(((uint32_t)x >> shift2) & mask2);
+            if (SIDE) st_side(side + a, (uint8_t)(((uint32_t)x >> shift2) & mask2));
         }
     } else
     for (uint32_t j = grp; j < gtot; j += NG) {
@@ -1095,7 +1107,7 @@ __device__ __forceinline__ void scatter_tile_write(ScatterLds<BITS, ITEMS, NT, E
         // next-pass digit beside the tuple: the 16 lanes of a granule write 16
         // consecutive bytes (measured faster than gathering them into one 16-B store
         // per granule with DPP)
-        if (SIDE && valid) side[a] = (uint8_t)(((uint32_t)x >> shift2) & mask2);
+        if (SIDE && valid) st_side(side + a, (uint8_t)(((uint32_t)x >> shift2) & mask2));
     }
     __syncthreads();
     // E. new carries (the next tile's phase A touches only cnt; C/D come after barriers)
@@ -1854,6 +1866,9 @@ __global__ __launch_bounds__(NT, NT * SGXAMD_SORT_WGS / 256) void k_sort_blk(con
 #ifndef SGXAMD_PLACE_U  // 16-byte loads (4 keys) per thread and tile
 #define SGXAMD_PLACE_U 2
 #endif
+#ifndef SGXAMD_PLACE_NT_STORE  // non-temporal 16-byte stores of the runs
+#define SGXAMD_PLACE_NT_STORE 1
+#endif
 #ifndef SGXAMD_PLACE_XCD  // consecutive segments on one XCD (their shared partial lines meet in one L2)
 #define SGXAMD_PLACE_XCD 1
 #endif
@@ -2029,8 +2044,14 @@ __global__ __launch_bounds__(NT, NT *SGXAMD_PLACE_WGS / 256) void k_place_seg(
         const uint32_t a8 = min((a + 7) & ~7u, z), z8 = max(z & ~7u, a8);
         if (lane < a8 - a) o[a + lane] = L.res[a + lane];
         if (lane < z - z8) o[z8 + lane] = L.res[z8 + lane];
-        for (uint32_t q = a8 + 8 * lane; q < z8; q += 8 * kWave)
+        for (uint32_t q = a8 + 8 * lane; q < z8; q += 8 * kWave) {
+#if SGXAMD_PLACE_NT_STORE
+            __builtin_nontemporal_store(*reinterpret_cast<const u32x4_t *>(&L.res[q]),
+                                        reinterpret_cast<u32x4_t *>(o + q));
+#else
             *reinterpret_cast<uint4 *>(o + q) = *reinterpret_cast<const uint4 *>(&L.res[q]);
+#endif
+        }
     }
 }
 
