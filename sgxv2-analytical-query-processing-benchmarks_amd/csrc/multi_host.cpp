@@ -661,9 +661,13 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
     const size_t elem = o.keys ? sizeof(uint32_t) : sizeof(row_t);
     // u16 wire buffers (S): [residuals (256-B aligned)][G counts rows of P16 + 1 words];
     // the receive side also holds the gather's scratch (rho::wire_scratch_u64)
-    const auto res_bytes = [](uint64_t n) { return (std::max<uint64_t>(n, 1) * 2 + 255) & ~uint64_t(255); };
-    // (the send side: 4 bytes per key, rho::wire_partition writes a wide destination as keys)
-    const auto snd_bytes = [](uint64_t n) { return (std::max<uint64_t>(n, 1) * 4 + 255) & ~uint64_t(255); };
+    // (every sender's run padded to 8 residuals: rho::wire_pad)
+    const auto res_bytes = [G](uint64_t n) {
+        return ((std::max<uint64_t>(n, 1) + 8ull * G) * 2 + 255) & ~uint64_t(255);
+    };
+    // (the send side: 4 bytes per key, rho::wire_partition writes a wide destination as keys
+    // -- at most 2 (n + 7 G) u16 slots with the runs padded to 8 residuals)
+    const auto snd_bytes = [G](uint64_t n) { return (std::max<uint64_t>(n, 1) * 4 + 32ull * G + 255) & ~uint64_t(255); };
     const uint64_t rows = (uint64_t)G * (P16 + 1) * sizeof(uint64_t);
     if (fail_rc == MI355_OK) {
         hipError_t e = ctx->xsendR.ensure(std::max<uint64_t>(nR, 1) * elem);
@@ -714,7 +718,7 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
     // failure from here on is flagged at the final all-reduce
     uint64_t total[2] = {0, 0};
     std::vector<uint64_t> s_piece(K, 0);  // S tuples landing per piece (S's local pass 1 runs per piece)
-    std::vector<uint64_t> wbase;  // u16 wire: where sender q's run of S residuals lands
+    std::vector<uint64_t> wbase, wcount;  // u16 wire: where sender q's run of S residuals lands, its residuals
     // (u16 wire: R's pieces only; S follows below)
     bool s_scattered = false;
     const auto post_pieces = [&](int j0, int j1) -> int {
@@ -795,14 +799,25 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
         const std::vector<uint64_t> crow(G, (uint64_t)P16 + 1);
         MH_RC(transport_rc(
             T.post_exchange(rank, rs->comm, ready, scnt, crow.data(), rcnt, crow.data(), sizeof(uint64_t))));
-        MH_RC(transport_rc(
-            T.post_exchange(rank, rs->comm, ready, snd16, s16.data(), ctx->wrecvS.ptr, r16.data(), sizeof(uint16_t))));
-        wbase.assign(G, 0);
+        // every run padded to 8 residuals on both sides (rho::wire_pad): each sender's run
+        // starts on 16 bytes in the send and the receive buffer; the padding is never read
+        std::vector<uint64_t> s16p(G), r16p(G);
         for (int q = 0; q < G; ++q) {
-            wbase[q] = total[1];
+            s16p[q] = rho::wire_pad(s16[q]);
+            r16p[q] = rho::wire_pad(r16[q]);
+        }
+        MH_RC(transport_rc(
+            T.post_exchange(rank, rs->comm, ready, snd16, s16p.data(), ctx->wrecvS.ptr, r16p.data(), sizeof(uint16_t))));
+        wbase.assign(G, 0);
+        uint64_t at = 0;
+        for (int q = 0; q < G; ++q) {
+            wbase[q] = at;
+            at += r16p[q];
             total[1] += r16[q];
+            // (the residuals; the padding, at most 14 bytes per peer, is not counted)
             if (q != rank) o.sent += s16[q] * sizeof(uint16_t) + crow[q] * sizeof(uint64_t);
         }
+        wcount = r16;
         hip_ok(hipEventRecord(rs->ev[2 * K + 1], rs->comm), "hipEventRecord (S landed)");
     }
     const bool timed = hipEventRecord(rs->t_land, rs->comm) == hipSuccess;
@@ -824,7 +839,7 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
                           : rho::join_pipelined_begin(ctx, s, ctx->xrecvR.ptr, total[0], total[1], &lo,
                                                       (uint32_t)elem, nullptr, 0, true);
             if (lrc == MI355_OK)
-                lrc = rho::join_pipelined_finish_wire16(ctx, ctx->wrecvS.as<uint16_t>(), rcS, wbase.data(), total[1],
+                lrc = rho::join_pipelined_finish_wire16(ctx, ctx->wrecvS.as<uint16_t>(), rcS, wbase.data(), wcount.data(), total[1],
                                                         G, rcS + (size_t)G * (P16 + 1), rs->ev[2 * K + 1], &o.st);
             fail(lrc);
             o.local = lrc == MI355_OK ? o.st.matches : 0;
@@ -1243,6 +1258,19 @@ int mi355_multi_comm_init(const void *id128, int nranks, int rank, void **comm) 
         set_last_error("mi355_multi_comm_init: bad arguments (nranks a power of two)");
         return MI355_ERR_INVALID;
     }
+    // counted before the library is even looked up (under g_all_mu, the lock
+    // mi355_multi_set_rccl_library checks it under), so it cannot be swapped between here
+    // and the communicator's end; rolled back on every early return
+    {
+        std::lock_guard<std::mutex> lk(multi::g_all_mu);
+        ++multi::g_live_handles;
+    }
+    struct Counted {
+        bool keep = false;
+        ~Counted() {
+            if (!keep) --multi::g_live_handles;
+        }
+    } counted;
     MH_RC(multi::require_rccl());
     const multi::Rccl &lib = multi::rccl();
     if (!lib.CommSplit) {
@@ -1255,22 +1283,13 @@ int mi355_multi_comm_init(const void *id128, int nranks, int rank, void **comm) 
     MH_HIP(hipGetDevice(&h->device));
     ncclUniqueId id;
     std::memcpy(&id, id128, sizeof(id));
-    // counted before the communicator exists (under g_all_mu, the lock
-    // mi355_multi_set_rccl_library checks it under), so the library cannot be swapped
-    // while this init runs; rolled back if the init fails
-    {
-        std::lock_guard<std::mutex> lk(multi::g_all_mu);
-        ++multi::g_live_handles;
-    }
     const ncclResult_t ir = lib.CommInitRank(&h->comm, nranks, id, rank);
     if (ir != ncclSuccess) {
-        --multi::g_live_handles;
         set_last_error(std::string("ncclCommInitRank: ") + lib.ErrorString(ir));
         return MI355_ERR_COMM;
     }
     const ncclResult_t sr = lib.CommSplit(h->comm, 0, rank, &h->ccomm, nullptr);
     if (sr != ncclSuccess) {
-        --multi::g_live_handles;
         set_last_error(std::string("ncclCommSplit (count communicator): ") + lib.ErrorString(sr));
         h->abort_comms();
         return MI355_ERR_COMM;
@@ -1292,6 +1311,7 @@ int mi355_multi_comm_init(const void *id128, int nranks, int rank, void **comm) 
     // without a context the rank still takes part in the joins' collectives, flagged as
     // failed (mi355_rho_join_sharded), so the communicator is kept
     *comm = h.release();
+    counted.keep = true;  // released by mi355_multi_comm_destroy
     return MI355_OK;
 }
 

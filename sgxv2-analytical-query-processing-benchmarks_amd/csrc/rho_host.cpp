@@ -111,7 +111,11 @@ Policy choose_policy(uint64_t nR, uint64_t nS, const mi355_rho_opts *o) {
             const char *e = std::getenv("SGXAMD_PASS1_BITS");
             return e ? std::atoi(e) : 0;
         }();
-        if (forced_b1 > 0 && (uint32_t)forced_b1 < p.bits && p.bits - (uint32_t)forced_b1 <= 8)
+        // (single-GPU joins only: it is a per-process setting, and the ranks of a multi-GPU
+        // join -- key_shift > 0 -- must agree on the split, which numbers the u16 wire's
+        // partitions; a pass-1 digit is at most kMaxF = 2^9 bins)
+        if (forced_b1 > 0 && forced_b1 <= 9 && (uint32_t)forced_b1 < p.bits && p.bits - (uint32_t)forced_b1 <= 8 &&
+            !(o && o->key_shift > 0))
             p.b1 = (uint32_t)forced_b1;
         p.b2 = p.bits - p.b1;
     }
@@ -680,7 +684,7 @@ int plan_join(Context *ctx, hipStream_t s, uint64_t nR, uint64_t nS, const mi355
     // result[0] = matches, [1] / [2] = largest R / S partition, [3] = extra S-chunk tasks
     // (u32), [4] / [5] = build / probe ticks: one read-back for all six; [6] = the
     // build/probe's task tickets (zeroed by launch_make_tasks with [1..5])
-    pj.off_result = A.reserve(sizeof(uint64_t) * 7);
+    pj.off_result = A.reserve(sizeof(uint64_t) * 8);  // (launch_make_tasks zeroes all 8 words, [7] the reduction ticket)
     pj.off_cyc = A.reserve(sizeof(uint64_t) * 2 * pj.join_grid);
     RHO_HIP(A.buf.ensure(A.used));
     return MI355_OK;
@@ -845,14 +849,19 @@ int join_finish(Context *ctx, PendingJoin &pj, const row_t *dS, uint64_t nS, mi3
                               join_grid));
     if (!pj.materialize) {
         tm.mark("join_build_probe");
+        // the 16,384-key table's k_join_x sums the count slots itself (k_reduce folded in)
+        const bool fold = algo == kAlgoChaining && pol.rcap == kBigRcap;
         RHO_HIP(launch_join(fR, fS, psR, pcR, psS, pcS, P, over, n_over, hash_shift, pol.rcap, pj.s_chunk, join_grid,
                             kJoinCount, algo, counts, nullptr, nullptr, cyc, s, nullptr, pj.pr.keys ? 1 : 2,
                             reinterpret_cast<uint32_t *>(result + 6),
                             pj.pr.narrow ? A.at<uint32_t>(pj.pr.kmax) + pj.pr.nseg1 : nullptr,
                             pj.ps.narrow ? A.at<uint32_t>(pj.ps.kmax) + pj.ps.nseg1 : nullptr,
-                            (uint32_t)std::min<uint64_t>(P + pj.over_cap - 1, 0xFFFFFFFFull)));
-        tm.mark("join_reduce");
-        RHO_HIP(launch_reduce(counts, join_grid, result, cyc, join_grid, s));
+                            (uint32_t)std::min<uint64_t>(P + pj.over_cap - 1, 0xFFFFFFFFull), nullptr,
+                            fold ? result : nullptr));
+        if (!fold) {
+            tm.mark("join_reduce");
+            RHO_HIP(launch_reduce(counts, join_grid, result, cyc, join_grid, s));
+        }
     } else {
         tm.mark("join_build_probe");
         RHO_HIP(launch_join(fR, fS, psR, pcR, psS, pcS, P, over, n_over, hash_shift, pol.rcap, pj.s_chunk, join_grid,
@@ -984,7 +993,10 @@ int join_small(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const 
     int rc = plan_join(ctx, s, nR, nS, opts, pj);
     if (rc) return rc;
     const Policy &pol = pj.pol;
-    if (!ctx->sync.ptr) {  // hand-off words: zero once, every kernel leaves them zero
+    // hand-off words: zero once, every kernel leaves them zero -- and zeroed again after a
+    // call that failed between the parity flip and its result (a launch error, a flag
+    // timeout): its totals, kmax words or tickets may be left behind
+    if (!ctx->sync.ptr || ctx->sync_dirty) {
         RHO_HIP(ctx->sync.ensure(kSyncWords * sizeof(uint64_t)));
         RHO_HIP(hipMemsetAsync(ctx->sync.ptr, 0, kSyncWords * sizeof(uint64_t), s));
         // the mapped host result block and its device address in sync[kSyncHostResult]
@@ -997,6 +1009,8 @@ int join_small(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const 
         RHO_HIP(hipMemcpyAsync(ctx->sync.as<uint64_t>() + kSyncHostResult, ctx->host_result + 8, sizeof(uint64_t),
                                hipMemcpyHostToDevice, s));
         RHO_HIP(hipStreamSynchronize(s));
+        ctx->small_parity = 0;
+        ctx->sync_dirty = false;
     }
     Timer &tm = thread_timer();
     const bool per_kernel = thread_timing_enabled() || (opts && opts->timing);
@@ -1044,6 +1058,7 @@ int join_small(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const 
     // the set the next call's histograms add into)
     const uint32_t par = ctx->small_parity;
     ctx->small_parity ^= 1u;
+    ctx->sync_dirty = true;  // until the result is in (every error return below leaves it set)
     tm.mark("RS_pass1_hist");
     // R's largest key (the direct count table of the build/probe), per parity set
     uint64_t *kmax = small_direct_enabled() ? sync + kSyncKmax : nullptr;
@@ -1078,6 +1093,7 @@ int join_small(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, const 
     }
     for (int i = 0; i < 6; ++i) ctx->host_result[i] = hj[i];
     ctx->host_result[6] = 0;  // (no narrow partitions in a small join)
+    ctx->sync_dirty = false;
     tm.collect();
     fill_join_stats(ctx, pj, tm, span, st);
     if (want_stamps) {
@@ -1290,7 +1306,7 @@ int wire_partition(Context *ctx, hipStream_t s, const uint32_t *keys, int G, int
         RHO_HIP(hipMemsetAsync(cq + P, 0, sizeof(uint64_t), s));
         RHO_HIP(hipMemcpyAsync(cq + P, A.at<uint32_t>(rp.kmax) + rp.nseg1, sizeof(uint32_t), hipMemcpyDeviceToDevice,
                                s));
-        doff += nq[q];
+        doff += wire_pad(nq[q]);  // every destination's run starts on 16 bytes (k_place_seg's copies)
     }
     tm.end_call();
     return MI355_OK;
@@ -1299,7 +1315,8 @@ int wire_partition(Context *ctx, hipStream_t s, const uint32_t *keys, int G, int
 uint64_t wire_scratch_u64(int G, uint32_t P) { return wire_scratch_words((uint32_t)G, P); }
 
 int join_pipelined_finish_wire16(Context *ctx, const uint16_t *s16, const uint64_t *s_cnt, const uint64_t *s_base,
-                                 uint64_t nS, int G, uint64_t *scratch, hipEvent_t s_landed, mi355_rho_stats *st) {
+                                 const uint64_t *s_n, uint64_t nS, int G, uint64_t *scratch, hipEvent_t s_landed,
+                                 mi355_rho_stats *st) {
     PendingJoin &pj = pending_of(ctx);
     if (!pj.active || !pj.ps.narrow) {
         pj.active = false;
@@ -1315,8 +1332,10 @@ int join_pipelined_finish_wire16(Context *ctx, const uint16_t *s16, const uint64
     Arena &A = ctx->scratch;
     Timer &tm = thread_timer();
     WireBases bs{};
-    for (int q = 0; q < G; ++q) bs.b[q] = s_base[q];
-    bs.b[G] = nS;
+    for (int q = 0; q < G; ++q) {
+        bs.b[q] = s_base[q];
+        bs.n[q] = s_n[q];
+    }
     uint16_t *mS = ctx->t2S.as<uint16_t>();
     uint64_t *psS = A.at<uint64_t>(pj.ps.pstart), *pcS = A.at<uint64_t>(pj.ps.pcnt);
     RHO_HIP(hipStreamWaitEvent(pj.s, s_landed, 0));

@@ -292,7 +292,12 @@ hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, 
                        uint64_t *cyc, hipStream_t s, const JoinReduce *reduce = nullptr, int key_stride = 2,
                        uint32_t *tickets = nullptr, const uint32_t *narrow_r = nullptr,
                        const uint32_t *narrow_s = nullptr, uint32_t tasks_max = 0,
-                       const uint64_t *small_kmax = nullptr);
+                       const uint64_t *small_kmax = nullptr, uint64_t *fold = nullptr);
+// fold (nullable; counting joins on the 16,384-key table, k_join_x): the join's 8-word
+// result block -- k_join_x's last workgroup sums the count and tick slots into
+// fold[0] / [4] / [5] (k_reduce's job; fold[7], zeroed by launch_make_tasks, is the
+// arrival ticket), whether k_join_x joined or k_join_n did.  Returns
+// hipErrorNotSupported (nothing launched) when the plan takes another kernel.
 // small_kmax (nullable; tuples, counting, the small joins' 1,024-thread chaining table):
 // R's largest key -- chunks whose residuals fit count in a direct table.
 // key_stride 2: R / S are row_t partitions; 1: packed u32 keys (counting RHO only —
@@ -317,14 +322,15 @@ hipError_t launch_reduce(const uint64_t *partials, uint32_t n, uint64_t *result,
                          hipStream_t s);
 
 // Multi-GPU u16 wire (wire_kernels.hip): in = the G senders' runs of u16 residuals, run q
-// at bases.b[q] (b[G] = their total), each grouped by partition; cnt = G rows of P
+// at bases.b[q] (bases.n[q] residuals), each grouped by partition; cnt = G rows of P
 // partition counts and the sender's largest key.  Gathers every partition's G pieces
 // into out (contiguous partitions: ps / pc), *narrow = the largest key; a row whose
 // counts do not add up to its run is left out.  scratch: wire_scratch_words(G, P) u64;
 // P <= 2^20.
 constexpr uint32_t kWireMaxG = 64;
 struct WireBases {
-    uint64_t b[kWireMaxG + 1];
+    uint64_t b[kWireMaxG];  // where sender q's run starts (a multiple of 8 residuals)
+    uint64_t n[kWireMaxG];  // its residuals (the count exchange's announcement)
 };
 uint64_t wire_scratch_words(uint32_t G, uint32_t P);
 hipError_t launch_wire_merge(const uint16_t *in, const uint64_t *cnt, uint32_t G, uint32_t P, const WireBases &bases,

@@ -1912,6 +1912,16 @@ struct PlaceLds {
 
 // I16: the input is a narrow pool (k_scatter_pool OB 2): u16 residuals, the digits in the
 // side stream beside them; else 4-byte keys.
+// A wide relation (a residual past 16 bits: known on the device only) takes the tile
+// sort itself (sort_blk_body over the 4-byte keys, NT x 16384 / NT keys per tile, 4-byte
+// keys written to out as u32), so that no k_sort_blk launch waits beside it (round 6:
+// one launch less per relation; k_sort_blk's own geometry, 512 x 32 with two workgroups
+// per CU, measured 0.487 against 0.53-0.55 ms for this one, r03v-x / r05c).
+template <int BITS, int NT>
+union PlaceOrSortLds {
+    PlaceLds<BITS, NT> p;
+    SortBlkLds<BITS, NT, 16384 / NT> w;
+};
 template <int BITS, int NT, int U, bool I16>
 __global__ __launch_bounds__(NT, NT *SGXAMD_PLACE_WGS / 256) void k_place_seg(
     const uint32_t *__restrict__ in, const uint8_t *__restrict__ side, const uint64_t *__restrict__ list,
@@ -1922,8 +1932,14 @@ __global__ __launch_bounds__(NT, NT *SGXAMD_PLACE_WGS / 256) void k_place_seg(
     constexpr uint32_t F = LdsT::F, mask = F - 1, NW = NT / kWave;
     constexpr uint32_t BPT = NW * U;  // blocks per tile: U per wave, one 16-byte load per lane each
     static_assert(kBlk == 4 * kWave && F <= NT, "placement geometry");
-    __shared__ LdsT L;
-    if (narrow == nullptr || ((*narrow >> (shift + BITS)) >> 16) != 0) return;  // wide: k_sort_blk
+    __shared__ PlaceOrSortLds<BITS, NT> LU;
+    LdsT &L = LU.p;
+    if (narrow == nullptr) return;
+    if (((*narrow >> (shift + BITS)) >> 16) != 0) {  // wide: the 4-byte keys' tile sort
+        sort_blk_body<BITS, NT, 16384 / NT, false>(LU.w, in, list, reinterpret_cast<uint32_t *>(out), m, shift,
+                                                   cursors);
+        return;
+    }
     const uint32_t tid = threadIdx.x, lane = __lane_id(), wave = tid / kWave, g = SGXAMD_PLACE_XCD ? xcd_contiguous(blockIdx.x, gridDim.x) : blockIdx.x;
     const uint32_t rshift = shift + BITS;
     uint32_t r;
@@ -2055,6 +2071,251 @@ __global__ __launch_bounds__(NT, NT *SGXAMD_PLACE_WGS / 256) void k_place_seg(
     }
 }
 
+// The same placement with one workgroup per CU walking a run of segments (round 6,
+// VERDICT r05 item 5).  k_place_seg's workgroup starts every segment cold: the segment
+// table, the list entries and the cursors are dependent loads, and no key of the segment
+// is read while the previous workgroup's runs are copied out (one workgroup per CU: the
+// segment fills the LDS).  Here the next segment's list entries and cursors are read
+// while the current segment is placed, and its first PF tiles are loaded into registers
+// before the current segment's runs are copied out (loads issued before the copy-out's
+// stores: gfx950 retires both through one in-order vmcnt), so its reads overlap the
+// copy-out's writes; its other tiles stream as in k_place_seg.  The run layout of a
+// segment (counts from the cursors, the slot ranges' scan) is computed by wave 0 alone,
+// F / 64 digits per lane.
+template <int BITS>
+struct PlaceRunLds {
+    static constexpr uint32_t F = 1u << BITS;
+    static constexpr uint32_t CAP = kPass2Ents * kBlk + 14 * F;
+    alignas(16) uint16_t res[CAP];
+    uint64_t ents[2][kPass2Ents];  // list entries of the current and the next segment
+    uint64_t dst[F];
+    uint32_t pos[F], st[F], pb[F + 1], cnt[F];
+    uint32_t sbase[kMaxF + 1];     // segments per region (prefix)
+};
+
+#ifndef SGXAMD_PLACE_PF  // k_place_run: tiles of the next segment loaded during a copy-out
+#define SGXAMD_PLACE_PF 2
+#endif
+template <int BITS, int NT, bool I16>
+__global__ __launch_bounds__(NT, NT / 256) void k_place_run(
+    const uint32_t *__restrict__ in, const uint8_t *__restrict__ side, const uint64_t *__restrict__ list,
+    uint16_t *__restrict__ out, SegMap m, uint32_t shift, const uint64_t *__restrict__ cursors,
+    const uint64_t *__restrict__ part_start, const uint64_t *__restrict__ part_count,
+    const uint32_t *__restrict__ narrow) {
+    using LdsT = PlaceRunLds<BITS>;
+    constexpr uint32_t F = LdsT::F, mask = F - 1, NW = NT / kWave, U = 2;
+    constexpr uint32_t BPT = NW * U;               // blocks per tile
+    constexpr uint32_t NTL = kPass2Ents / BPT;     // tiles per (full) segment
+    constexpr uint32_t PF = SGXAMD_PLACE_PF;
+    constexpr uint32_t DPL = F > kWave ? F / kWave : 1u;  // digits per lane of wave 0
+    static_assert(kBlk == 4 * kWave && F <= NT && kPass2Ents % BPT == 0 && PF < NTL, "placement geometry");
+    __shared__ LdsT L;
+    if (narrow == nullptr || ((*narrow >> (shift + BITS)) >> 16) != 0) return;  // wide: k_sort_blk
+    const uint32_t tid = threadIdx.x, lane = __lane_id(), wave = tid / kWave;
+    const uint32_t rshift = shift + BITS;
+    for (uint32_t i = tid; i <= m.nreg; i += NT) L.sbase[i] = m.seg_base[i];
+    __syncthreads();
+    const uint32_t nseg = L.sbase[m.nreg];
+    // XCD x (workgroups b with b mod 8 = x) takes the x-th contiguous eighth of the
+    // segments, its workgroups in lock step over consecutive segments (workgroup i of the
+    // XCD: segments i, i + WX, ...), so that at any time an XCD places neighbouring
+    // segments -- their shared partial lines meet in its L2, as in k_place_seg's
+    // dispatch order.  (grid: a multiple of 8)
+    const uint32_t WX = gridDim.x / 8, x = blockIdx.x % 8, wi = blockIdx.x / 8;
+    const uint32_t perx = (nseg + 7) / 8;
+    const uint32_t xb = min(nseg, x * perx), xe = min(nseg, xb + perx);
+    const uint32_t g0 = xb + wi, g1 = xe;
+    if (g0 >= g1) return;
+    // segment g: its region, list range and whether it is its region's last
+    struct Seg {
+        uint32_t r, nent, last;
+        uint64_t b;
+    };
+    const auto seg_of = [&](uint32_t g) -> Seg {
+        uint32_t lo = 0, hi = m.nreg;  // largest lo with sbase[lo] <= g
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (L.sbase[mid] <= g) lo = mid; else hi = mid;
+        }
+        Seg s;
+        s.r = lo;
+        const uint64_t rs = m.reg_start[lo], rc = m.reg_count[lo];
+        s.b = rs + (uint64_t)(g - L.sbase[lo]) * m.seg_size;
+        const uint64_t e = min(s.b + m.seg_size, rs + rc);
+        s.nent = e > s.b ? (uint32_t)(e - s.b) : 0u;
+        s.last = g + 1 == L.sbase[lo + 1] ? 1u : 0u;
+        return s;
+    };
+    // wave 0, lane l: digits l + 64 i (i < DPL) -- their cursors and the next ones
+    uint64_t cur[DPL], nxt[DPL];
+    const auto fetch_cursors = [&](uint32_t g, const Seg &s) {
+#pragma unroll
+        for (uint32_t i = 0; i < DPL; ++i) {
+            const uint32_t d = lane + kWave * i;
+            cur[i] = nxt[i] = 0;
+            if (d < F) {
+                cur[i] = cursors[(uint64_t)g * F + d];
+                nxt[i] = s.last ? part_start[(uint64_t)s.r * F + d] + part_count[(uint64_t)s.r * F + d]
+                                : cursors[(uint64_t)(g + 1) * F + d];
+            }
+        }
+    };
+    const auto fetch_ents = [&](const Seg &s, uint32_t slot) {
+        for (uint32_t i = tid; i < kPass2Ents; i += NT) L.ents[slot][i] = i < s.nent ? list[s.b + i] : 0ull;
+    };
+    // tile t of the segment in ents[slot]: item u of wave w = block t * BPT + u * NW + w,
+    // lane l its keys 4l..4l+3 (I16: .x/.y the four residuals, .z their four digits);
+    // entries past the segment are 0 (no block: every key masked out)
+    const auto load_tile = [&](uint32_t slot, uint32_t t, uint4(&k)[U]) -> uint32_t {
+        uint32_t vm = 0;
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            const uint32_t idx = t * BPT + u * NW + wave;
+            const uint64_t en = idx < kPass2Ents ? L.ents[slot][idx] : 0ull;  // one address per wave
+            const uint32_t phys = __builtin_amdgcn_readfirstlane((uint32_t)en);
+            const uint32_t fill = __builtin_amdgcn_readfirstlane((uint32_t)(en >> 32));
+            if constexpr (I16) {
+                const uint16_t *b16 = reinterpret_cast<const uint16_t *>(in) + (uint64_t)phys * kBlk;
+                const uint64_t r = buf_ld_nt_u64(make_rsrc(b16, (fill * 2u + 3u) & ~3u), lane * 8u, 0);
+                const uint32_t dg = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(
+                    make_rsrc(side + (uint64_t)phys * kBlk, (fill + 3u) & ~3u), (int)(lane * 4u), 0, 2);
+                k[u] = make_uint4((uint32_t)r, (uint32_t)(r >> 32), dg, 0u);
+            } else {
+                k[u] = buf_ld_nt_u128(make_rsrc(in + (uint64_t)phys * kBlk, fill * 4u), lane * 16u, 0);
+            }
+            const uint32_t f = fill > 4 * lane ? min(fill - 4 * lane, 4u) : 0u;
+            vm |= ((1u << f) - 1u) << (4 * u);
+        }
+        return vm;
+    };
+    const auto place_tile = [&](const uint4(&k)[U], uint32_t vm) {
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            if constexpr (I16) {
+                const uint32_t rr[2] = {k[u].x, k[u].y};
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if ((vm >> (4 * u + j)) & 1u)
+                        L.res[atomicAdd(&L.pos[(k[u].z >> (8 * j)) & mask], 1u)] =
+                            (uint16_t)(rr[j >> 1] >> (16 * (j & 1)));
+            } else {
+                const uint32_t x[4] = {k[u].x, k[u].y, k[u].z, k[u].w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if ((vm >> (4 * u + j)) & 1u)
+                        L.res[atomicAdd(&L.pos[(x[j] >> shift) & mask], 1u)] = (uint16_t)(x[j] >> rshift);
+            }
+        }
+    };
+    // the first PF tiles of the next segment load while the current one is copied out
+    uint4 pf[PF][U];
+    uint32_t pm[PF];
+    const auto load_head = [&](uint32_t slot) {
+#pragma unroll
+        for (uint32_t t = 0; t < PF; ++t) pm[t] = load_tile(slot, t, pf[t]);
+    };
+    // the segment's tiles: the head from pf, the rest streamed with one tile in flight
+    // while one is placed (two register sets, loads unconditional)
+    const auto place_segment = [&](uint32_t slot, uint32_t nt) {
+        uint4 ka[U], kb[U];
+        uint32_t ma = load_tile(slot, PF, ka);
+#pragma unroll
+        for (uint32_t t = 0; t < PF; ++t) {
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u)
+                asm volatile("" ::"v"(pf[t][u].x), "v"(pf[t][u].y), "v"(pf[t][u].z), "v"(pf[t][u].w));
+            place_tile(pf[t], pm[t]);
+        }
+        for (uint32_t t = PF; t < nt; t += 2) {
+            const uint32_t mb = load_tile(slot, t + 1, kb);
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) asm volatile("" ::"v"(ka[u].x), "v"(ka[u].y), "v"(ka[u].z), "v"(ka[u].w));
+            place_tile(ka, ma);
+            if (t + 1 >= nt) break;
+            ma = load_tile(slot, t + 2, ka);
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) asm volatile("" ::"v"(kb[u].x), "v"(kb[u].y), "v"(kb[u].z), "v"(kb[u].w));
+            place_tile(kb, mb);
+        }
+    };
+    // the run layout of the segment whose cursors are in cur / nxt (wave 0): counts,
+    // slot ranges of round_up8(count + 7) from a multiple of 8, run starts at dst mod 8
+    const auto layout = [&]() {
+        if (wave != 0) return;
+        uint32_t c[DPL], sl[DPL], tot = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < DPL; ++i) {
+            c[i] = (uint32_t)(nxt[i] - cur[i]);
+            sl[i] = c[i] ? (c[i] + 7 + 7) & ~7u : 0u;
+        }
+        uint32_t base = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < DPL; ++i) {
+            const uint32_t d = lane + kWave * i;
+            const uint32_t incl = wave_incl_scan_u32(sl[i]);
+            const uint32_t p = base + incl - sl[i];
+            if (d < F) {
+                L.pb[d] = p;
+                L.st[d] = L.pos[d] = p + (uint32_t)(cur[i] & 7);
+                L.dst[d] = cur[i];
+                L.cnt[d] = c[i];
+            }
+            base += __shfl(incl, kWave - 1, kWave);
+        }
+        (void)tot;
+        if (lane == 0) L.pb[F] = base;
+    };
+    // the runs out (k_place_seg's copy-out)
+    const auto copy_out = [&]() {
+        const uint32_t total = L.pb[F];
+        const uint32_t C = ((total + NW - 1) / NW + 7) & ~7u;
+        const uint32_t q0 = wave * C, q1 = min(total, q0 + C);
+        if (q0 >= q1) return;
+        uint32_t lo = 0, hi = F;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (L.pb[mid] <= q0) lo = mid; else hi = mid;
+        }
+        for (uint32_t d = __builtin_amdgcn_readfirstlane(lo); d < F; ++d) {
+            if (__builtin_amdgcn_readfirstlane(L.pb[d]) >= q1) break;
+            const uint32_t rs = __builtin_amdgcn_readfirstlane(L.st[d]);
+            const uint32_t re = rs + __builtin_amdgcn_readfirstlane(L.cnt[d]);
+            const uint32_t a = max(rs, q0), z = min(re, q1);
+            if (a >= z) continue;
+            uint16_t *o = out + uni_u64(L.dst[d]);
+            o -= rs;
+            const uint32_t a8 = min((a + 7) & ~7u, z), z8 = max(z & ~7u, a8);
+            if (lane < a8 - a) o[a + lane] = L.res[a + lane];
+            if (lane < z - z8) o[z8 + lane] = L.res[z8 + lane];
+            for (uint32_t q = a8 + 8 * lane; q < z8; q += 8 * kWave)
+                __builtin_nontemporal_store(*reinterpret_cast<const u32x4_t *>(&L.res[q]),
+                                            reinterpret_cast<u32x4_t *>(o + q));
+        }
+    };
+    // prologue: the first segment's entries, cursors and head tiles
+    Seg sc = seg_of(g0);
+    fetch_ents(sc, 0);
+    if (wave == 0) fetch_cursors(g0, sc);
+    __syncthreads();
+    load_head(0);
+    for (uint32_t g = g0, it = 0; g < g1; g += WX, ++it) {
+        const uint32_t slot = it & 1u;
+        layout();  // (cur / nxt of g)
+        __syncthreads();  // pos / st / pb / dst / cnt set; the previous copy-out is done
+        place_segment(slot, (sc.nent + BPT - 1) / BPT);
+        const bool more = g + WX < g1;
+        if (more) {
+            sc = seg_of(g + WX);
+            fetch_ents(sc, slot ^ 1u);
+            if (wave == 0) fetch_cursors(g + WX, sc);
+        }
+        __syncthreads();  // the segment is placed; the next entries are in LDS
+        if (more) load_head(slot ^ 1u);
+        copy_out();
+        __syncthreads();  // the runs are out (res, the layout and ents[slot] are free)
+    }
+}
+
 // Elements per thread per tile: 8 tuples (32 KiB tiles); keys: 12 in the pooled pass 1
 // (24 KiB tiles; 16 spill 17-19 VGPRs at the 128-register cap), 16 in the block-list
 // pass 2 (larger tiles amortise the per-tile work: 0.75 -> 0.69 ms per 2^28 keys).
@@ -2176,6 +2437,20 @@ bool place_enabled() {
     }();
     return on;
 }
+uint32_t cu_count();
+// SGXAMD_PLACE_RUN=1 (development A/B switch, read once): the placement as k_place_run
+// (one workgroup per CU over a run of segments, the next segment's first tiles loaded
+// while the current one's runs are copied out) instead of k_place_seg.  Measured and
+// not the default (round 6, profiles/r06_place_run_ab.log): 0.33 / 0.32 ms per 2^28
+// keys with 2 tiles ahead against k_place_seg's 0.33 / 0.32, 4 ahead 0.34 / 0.33, 6
+// ahead 0.37, the whole next segment in registers 0.39.
+bool place_run_enabled() {
+    static const bool on = [] {
+        const char *e = std::getenv("SGXAMD_PLACE_RUN");
+        return e && std::atoi(e) == 1;
+    }();
+    return on;
+}
 template <typename T>
 hipError_t launch_scatter_blk_t(const void *in, const uint64_t *list, void *out, const SegMap &m, uint32_t grid,
                                 uint32_t shift, uint32_t bits, const uint64_t *cursors, hipStream_t s,
@@ -2190,10 +2465,23 @@ hipError_t launch_scatter_blk_t(const void *in, const uint64_t *list, void *out,
             // device only)
             const bool place = narrow && part_start && part_count && m.seg_lb == nullptr && place_enabled();
             if (side16 && !place) return hipErrorInvalidValue;  // a narrow pool is read by k_place_seg only
+            // the placements' 16-byte run copies assume that residual 8k of `out` sits on a
+            // 16-byte boundary (each u16-wire destination's pass 2 starts on one)
+            if (place && (reinterpret_cast<uintptr_t>(out) & 15u) != 0) return hipErrorInvalidValue;
             const uint32_t skip = place ? 1u : 0u;
+            const bool run = place && place_run_enabled();
+            const uint32_t grid_run = std::max<uint32_t>(8, std::min<uint32_t>(grid, cu_count()) & ~7u);
 #define SORT_CASE(B)                                                                                              \
     case B:                                                                                                       \
-        if (place && side16)                                                                                      \
+        if (run && side16)                                                                                        \
+            hipLaunchKernelGGL((k_place_run<B, 1024, true>), dim3(grid_run), dim3(1024), 0, s, ik, side16, list,  \
+                               reinterpret_cast<uint16_t *>(out), m, shift, cursors, part_start, part_count,       \
+                               narrow);                                                                           \
+        else if (run)                                                                                             \
+            hipLaunchKernelGGL((k_place_run<B, 1024, false>), dim3(grid_run), dim3(1024), 0, s, ik, nullptr, list, \
+                               reinterpret_cast<uint16_t *>(out), m, shift, cursors, part_start, part_count,       \
+                               narrow);                                                                           \
+        else if (place && side16)                                                                                 \
             hipLaunchKernelGGL((k_place_seg<B, SGXAMD_PLACE_NT, SGXAMD_PLACE_U, true>), dim3(grid),             \
                                dim3(SGXAMD_PLACE_NT), 0, s, ik, side16, list, reinterpret_cast<uint16_t *>(out), m, \
                                shift, cursors, part_start, part_count, narrow);                                   \
@@ -2201,8 +2489,9 @@ hipError_t launch_scatter_blk_t(const void *in, const uint64_t *list, void *out,
             hipLaunchKernelGGL((k_place_seg<B, SGXAMD_PLACE_NT, SGXAMD_PLACE_U, false>), dim3(grid),            \
                                dim3(SGXAMD_PLACE_NT), 0, s, ik, nullptr, list, reinterpret_cast<uint16_t *>(out), \
                                m, shift, cursors, part_start, part_count, narrow);                                \
-        hipLaunchKernelGGL((k_sort_blk<B, SGXAMD_SORT_NT, SGXAMD_SORT_ITEMS>), dim3(grid), dim3(SGXAMD_SORT_NT), 0, s, \
-                           ik, list, ok, m, shift, cursors, narrow, skip);                                        \
+        if (!place || run) /* (k_place_seg sorts a wide relation itself) */                                      \
+            hipLaunchKernelGGL((k_sort_blk<B, SGXAMD_SORT_NT, SGXAMD_SORT_ITEMS>), dim3(grid), dim3(SGXAMD_SORT_NT), 0, \
+                               s, ik, list, ok, m, shift, cursors, narrow, skip);                                 \
         break;
             switch (bits) {
                 SORT_CASE(1)
@@ -3286,6 +3575,50 @@ __device__ __forceinline__ void join_x_body(
     if (red_ticket) join_reduce_last(counts, cyc, red_result, red_ticket, L.red, tk.T);
 }
 
+// k_reduce folded into k_join_x (its workgroups are few -- one per CU -- and, on narrow
+// relations, idle): every workgroup arrives on res[7] after its slots are written; the
+// last sums the ncounts count slots and tick pairs (k_join_n's or k_join_x's) into
+// res[0] / [4] / [5].  Called by every thread of the workgroup.
+template <int BLOCK>
+__device__ __forceinline__ void x_fold_reduce(const uint64_t *__restrict__ counts, const uint64_t *__restrict__ cyc,
+                                              uint32_t ncounts, uint64_t *__restrict__ res, uint64_t *red) {
+    constexpr uint32_t NW = BLOCK / kWave;
+    __shared__ uint32_t last;
+    __syncthreads();  // this workgroup's slot writes are issued
+    if (threadIdx.x == 0) {
+        __threadfence();
+        last = atomicAdd(reinterpret_cast<unsigned long long *>(&res[7]), 1ull) == gridDim.x - 1 ? 1u : 0u;
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    uint64_t c = 0, b = 0, p = 0;
+    for (uint32_t i = threadIdx.x; i < ncounts; i += BLOCK) {
+        c += __hip_atomic_load(&counts[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cyc) {
+            b += __hip_atomic_load(&cyc[2 * i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            p += __hip_atomic_load(&cyc[2 * i + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    c = wave_sum_u64(c);
+    b = wave_sum_u64(b);
+    p = wave_sum_u64(p);
+    const uint32_t w = threadIdx.x / kWave;
+    __syncthreads();  // (red: the join body's last use is done)
+    if (__lane_id() == 0) {
+        red[w] = c;
+        red[NW + w] = b;
+        red[2 * NW + w] = p;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        uint64_t t = 0;
+        for (uint32_t k = 0; k < NW; ++k) t += red[threadIdx.x * NW + k];
+        if (threadIdx.x == 0) res[0] = t;
+        else if (cyc) res[3 + threadIdx.x] = t;
+    }
+}
+
 template <int RCAP, int BLOCK, int UP, int KS = 1>
 __global__ __launch_bounds__(BLOCK, 1) void k_join_x(
     const uint64_t *__restrict__ R, const uint64_t *__restrict__ S, const uint64_t *__restrict__ r_start,
@@ -3293,12 +3626,16 @@ __global__ __launch_bounds__(BLOCK, 1) void k_join_x(
     uint64_t P, const uint64_t *__restrict__ over, const uint32_t *__restrict__ n_over, uint32_t hash_shift,
     uint64_t s_chunk, uint64_t *__restrict__ counts, uint64_t *__restrict__ cyc, uint64_t *__restrict__ red_result,
     uint64_t *__restrict__ red_ticket, uint32_t ncounts, uint32_t *__restrict__ tickets,
-    const uint32_t *__restrict__ narrow_r, const uint32_t *__restrict__ narrow_s, uint32_t skip_narrow) {
+    const uint32_t *__restrict__ narrow_r, const uint32_t *__restrict__ narrow_s, uint32_t skip_narrow,
+    uint64_t *__restrict__ fold) {
     __shared__ JoinLdsX<RCAP, BLOCK / kWave> L;
     // (the same test as k_sort_blk's, which wrote the partitions)
     const bool nr = narrow_r != nullptr && ((*narrow_r >> hash_shift) >> 16) == 0;
     const bool ns = narrow_s != nullptr && ((*narrow_s >> hash_shift) >> 16) == 0;
-    if (skip_narrow && (nr || ns)) return;  // k_join_n, launched beside it, joins them
+    if (skip_narrow && (nr || ns)) {  // k_join_n, launched beside it, joined them
+        if (fold) x_fold_reduce<BLOCK>(counts, cyc, ncounts, fold, reinterpret_cast<uint64_t *>(L.head));
+        return;
+    }
     // the direct table's counters: residuals below 2^(the fewest residual bits of a narrow
     // relation; 16 for a wide one) — BASELINE config 2's keys 1..2^28 over 14 bits: 2^14
     const auto res_bits = [&](bool n, const uint32_t *kmax) -> uint32_t {
@@ -3327,6 +3664,7 @@ __global__ __launch_bounds__(BLOCK, 1) void k_join_x(
     }
 #undef JOIN_X_BODY
 #undef JOIN_X_BODY_U
+    if (fold) x_fold_reduce<BLOCK>(counts, cyc, ncounts, fold, reinterpret_cast<uint64_t *>(L.head));
 }
 
 // ------------------------------------------- narrow build/probe (round 5) ---
@@ -3992,8 +4330,9 @@ hipError_t launch_join_keys(const void *R, const void *S, const uint64_t *r_star
                             const uint32_t *n_over, uint32_t hash_shift, uint32_t rcap, uint64_t s_chunk,
                             uint32_t grid, int mode, int algo, uint64_t *counts, uint64_t *cyc, hipStream_t s,
                             const JoinReduce *reduce, uint32_t *tickets, const uint32_t *narrow_r,
-                            const uint32_t *narrow_s, uint32_t tasks_max) {
+                            const uint32_t *narrow_s, uint32_t tasks_max, uint64_t *fold) {
     if (mode != kJoinCount) return hipErrorInvalidValue;
+    if (fold && (reduce || algo != kAlgoChaining || rcap != kBigRcap)) return hipErrorNotSupported;
     // narrow partitions are read by the 16,384-key chaining table only
     if ((narrow_r || narrow_s) && !(algo == kAlgoChaining && rcap == kBigRcap)) return hipErrorInvalidValue;
     const uint64_t *R64 = static_cast<const uint64_t *>(R);
@@ -4039,7 +4378,7 @@ hipError_t launch_join_keys(const void *R, const void *S, const uint64_t *r_star
         }
         hipLaunchKernelGGL((k_join_x<kBigRcap, 1024, 8, 1>), dim3(std::min<uint32_t>(grid, cu_count())), dim3(1024), 0,
                            s, R64, S64, r_start, r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts,
-                           cyc, rres, rtick, grid, tickets, narrow_r, narrow_s, nar ? 1u : 0u);
+                           cyc, rres, rtick, grid, tickets, narrow_r, narrow_s, nar ? 1u : 0u, fold);
         return hipGetLastError();
     }
 #define KEYS_CASE(RC)                                                                                                   case RC:                                                                                                                hipLaunchKernelGGL((k_join<RC, kJoinCount, kBlock, 1>), dim3(grid), dim3(kBlock), 0, s, R64, S64, r_start,                            r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts, nullptr, nullptr,                             cyc, rres, rtick);                                                                               break;
@@ -4060,10 +4399,12 @@ hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, 
                        int mode, int algo, uint64_t *counts, const uint64_t *task_off, output_triple_t *out,
                        uint64_t *cyc, hipStream_t s, const JoinReduce *reduce, int key_stride, uint32_t *tickets,
                        const uint32_t *narrow_r, const uint32_t *narrow_s, uint32_t tasks_max,
-                       const uint64_t *small_kmax) {
+                       const uint64_t *small_kmax, uint64_t *fold) {
     if (key_stride == 1)
         return launch_join_keys(R, S, r_start, r_count, s_start, s_count, P, over, n_over, hash_shift, rcap, s_chunk,
-                                grid, mode, algo, counts, cyc, s, reduce, tickets, narrow_r, narrow_s, tasks_max);
+                                grid, mode, algo, counts, cyc, s, reduce, tickets, narrow_r, narrow_s, tasks_max, fold);
+    if (fold && (mode != kJoinCount || reduce || algo == kAlgoHistogram || rcap != kBigRcap))
+        return hipErrorNotSupported;
     if (narrow_r || narrow_s) return hipErrorInvalidValue;
     const uint64_t *R64 = reinterpret_cast<const uint64_t *>(R);
     const uint64_t *S64 = reinterpret_cast<const uint64_t *>(S);
@@ -4097,7 +4438,7 @@ hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, 
         if (mode != kJoinCount) return hipErrorInvalidValue;
         hipLaunchKernelGGL((k_join_x<kBigRcap, 1024, 8, 2>), dim3(std::min<uint32_t>(grid, cu_count())), dim3(1024), 0,
                            s, R64, S64, r_start, r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts,
-                           cyc, rres, rtick, grid, tickets, nullptr, nullptr, 0u);
+                           cyc, rres, rtick, grid, tickets, nullptr, nullptr, 0u, fold);
     } else if (mode == kJoinCount && grid <= 512 && rcap <= 4096) {
         // few tasks (small joins: one workgroup per CU at most): 1,024 threads per table
         // instead of 256, so that a CU holds 16 waves to hide the load latencies
@@ -4179,7 +4520,10 @@ __global__ __launch_bounds__(kBlock) void k_make_tasks(const uint64_t *__restric
 hipError_t launch_make_tasks(const uint64_t *r_count, const uint64_t *s_count, uint64_t P, uint64_t *over,
                              uint32_t over_cap, uint64_t *meta, uint64_t s_chunk, hipStream_t s, uint64_t *zero,
                              uint64_t *zero2, uint32_t nzero) {
-    hipError_t e = hipMemsetAsync(meta, 0, 6 * sizeof(uint64_t), s);
+    // meta = result + 1 of the join's 8-word, 256-byte aligned result block: the whole
+    // block in one aligned fill (meta's 48 bytes alone, 8-byte aligned, took three fill
+    // kernels: head, body and tail -- 13.7 us per join in the r05g trace)
+    hipError_t e = hipMemsetAsync(meta - 1, 0, 8 * sizeof(uint64_t), s);
     if (e != hipSuccess) return e;
     uint32_t *n_over = reinterpret_cast<uint32_t *>(meta + 2);
     uint64_t blocks = (P + kBlock - 1) / kBlock;

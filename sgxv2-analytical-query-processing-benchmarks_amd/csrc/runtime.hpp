@@ -101,6 +101,7 @@ struct Context {
     // once when allocated (rho_internal.hpp kSync*)
     DeviceBuffer sync;
     uint32_t small_parity = 0;  // the small join's digit-totals set for the next call
+    bool sync_dirty = false;    // a small join failed after its parity flip: re-zero sync first
 };
 
 // Context of the calling thread's current HIP device (created on first use).

@@ -44,7 +44,7 @@ __global__ __launch_bounds__(kWireTile) void k_wire_rows(const uint64_t *__restr
 }
 
 // One workgroup: a row is used only when its counts add up to the run the count
-// exchange announced (bases.b[q + 1] - bases.b[q]) -- a sender that failed after the
+// exchange announced (bases.n[q]) -- a sender that failed after the
 // count exchange sent zeroed or stale rows, and its pieces are left out (the final
 // all-reduce reports the failure) instead of steering the gather and the build/probe
 // outside the buffers.  Then the tiles' bases in the receive buffer per row, the
@@ -64,7 +64,7 @@ __global__ __launch_bounds__(kWireTile) void k_wire_bases(const uint64_t *__rest
             sc.tbase[(uint64_t)i * T + t] = run;
             run += sc.tsum[(uint64_t)i * T + t];
         }
-        ok[i] = run == bases.b[i + 1] ? 1u : 0u;
+        ok[i] = run == bases.b[i] + bases.n[i] ? 1u : 0u;
         sc.valid[i] = ok[i];
     }
     __syncthreads();
