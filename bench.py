@@ -644,6 +644,7 @@ def main():
     # BASELINE configs 4 and 5 in the same run (strong totals over the N GPUs), each
     # with its load report; the headline value stays config 2
     configs_info = {}
+    cpu_cfg_rel = {}  # host copies of the c4 / c5 relations for their CPU legs (rank 0, N = 1)
     if args.workload == "c2" and not args.no_configs and args.dist_backend == "gloo" and world > 1:
         configs_info["skipped"] = ("configs 4 / 5 are not run in the gloo rehearsal (tuples staged through host "
                                    "memory; not a scaling number)")
@@ -671,6 +672,10 @@ def main():
             }
             if world > 1:
                 configs_info[wl]["multi"] = gather_multi(res_w[-1])
+            if rank == 0 and world == 1 and not args.no_cpu_baseline:
+                # the CPU baseline joins these same relations later (one device-to-host copy,
+                # outside every timed region)
+                cpu_cfg_rel[wl] = (Rw.cpu().numpy().view(ROW_DT), Sw.cpu().numpy().view(ROW_DT))
             del Rw, Sw
             torch.cuda.empty_cache()
         # config 2 on the reference's own relations (native.cpp:62-101: glibc rand() Knuth
@@ -730,23 +735,59 @@ def main():
                   "path": "three-launch small-join path (one-pass plan)"}
         del R1, S1, R1h, S1h
 
-    # measured stream-copy ceiling of this GPU: device-to-device copy of
-    # 2 GiB, read + write bytes over the event time of the copy kernel, best of 5
-    src = torch.empty(1 << 28, dtype=torch.int64, device=dev)
+    # measured stream ceilings of this GPU, from the library's own probe
+    # kernels (mi355_stream_probe: grid-stride 16-byte accesses over 2 GiB buffers) timed
+    # with HIP events on the stream they run on, best of 5 per shape; the copy ceiling is
+    # the best copy shape (read + write bytes), each big kernel is priced against it too
+    nb = 1 << 31
+    src = torch.empty(nb // 8, dtype=torch.int64, device=dev)
     dst = torch.empty_like(src)
-    dst.copy_(src)
+    src.fill_(1)
+    cur = torch.cuda.Stream()  # a stream of its own (not the null stream: the library maps that to its own)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    best = float("inf")
-    for _ in range(5):
-        ev0.record()
-        dst.copy_(src)
-        ev1.record()
-        ev1.synchronize()
-        best = min(best, ev0.elapsed_time(ev1))
+    cur.wait_stream(torch.cuda.current_stream())
+
+    def probe_best(kind, **kw):
+        sgxamd.stream_probe(kind, src, dst, nb, stream=cur.cuda_stream, **kw)
+        best = float("inf")
+        for _ in range(5):
+            ev0.record(cur)
+            sgxamd.stream_probe(kind, src, dst, nb, stream=cur.cuda_stream, **kw)
+            ev1.record(cur)
+            ev1.synchronize()
+            best = min(best, ev0.elapsed_time(ev1))
+        return (2 if kind == "copy" else 1) * nb / (best * 1e-3) / 1e9
+
+    shapes = {}
+    for ntl, nts in ((True, True), (True, False), (False, False)):
+        for u in (4, 8):
+            for grid in (2048, 8192, 32768):
+                name = f"copy U{u} grid{grid}{' ntl' if ntl else ''}{' nts' if nts else ''}"
+                shapes[name] = probe_best("copy", nt_load=ntl, nt_store=nts, loads_in_flight=u, grid=grid)
+    read_ceiling = max(probe_best("read", nt_load=True, loads_in_flight=u, grid=g) for u in (4, 8) for g in (2048, 8192))
+    write_ceiling = max(probe_best("write", nt_store=nts, loads_in_flight=4, grid=g) for nts in (True, False)
+                        for g in (2048, 8192))
+    best_shape = max(shapes, key=shapes.get)
+    copy_ceiling = shapes[best_shape]
     # scalars: the driver's parser keeps the roofline's scalar fields only
-    roofline["measured_copy_ceiling_GB_per_s"] = round(2 * src.numel() * 8 / (best * 1e-3) / 1e9, 1)
-    roofline["measured_copy_ceiling_how"] = ("torch copy_ of 2 GiB device to device, read + write bytes, best of 5 "
-                                             "(HIP events)")
+    roofline["measured_copy_ceiling_GB_per_s"] = round(copy_ceiling, 1)
+    roofline["measured_copy_ceiling_how"] = (
+        f"in-tree streaming copy kernel (mi355_stream_probe, {best_shape}: 16-byte loads / stores, 2 GiB, read + "
+        f"write bytes, HIP events on its stream, best of 5; best of {len(shapes)} shapes)")
+    roofline["measured_read_ceiling_GB_per_s"] = round(read_ceiling, 1)
+    roofline["measured_write_ceiling_GB_per_s"] = round(write_ceiling, 1)
+    roofline["frac_of_copy_ceiling"] = round(roofline["achieved"] / copy_ceiling, 4)
+    roofline["probe_frac_of_copy_ceiling"] = round(probe_gbs / copy_ceiling, 4)
+    roofline["step_frac_of_copy_ceiling"] = round(step_bytes / (ms_per_step * 1e-3) / 1e9 / copy_ceiling, 4)
+    rho_info["ceilings"] = {"copy_shapes_GB_per_s": {k: round(v, 1) for k, v in shapes.items()},
+                            "read_GB_per_s": round(read_ceiling, 1), "write_GB_per_s": round(write_ceiling, 1)}
+    # every big kernel of the step at its algorithmic bytes: GB/s, fraction of 8 TB/s and
+    # of the measured copy ceiling
+    rho_info["kernel_rooflines"] = {
+        k: {"ms": round(v, 4), "GB_per_s": round(algorithmic_bytes(k, nR, nS, *plan) / (v * 1e-3) / 1e9, 1),
+            "frac_of_peak": round(algorithmic_bytes(k, nR, nS, *plan) / (v * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "frac_of_copy_ceiling": round(algorithmic_bytes(k, nR, nS, *plan) / (v * 1e-3) / 1e9 / copy_ceiling, 4)}
+        for k, v in sorted(avg.items()) if algorithmic_bytes(k, nR, nS, *plan) > 0 and v > 0.02}
     del src, dst
     torch.cuda.empty_cache()
 
@@ -1017,6 +1058,24 @@ def main():
         if configs_info is not None:
             configs_info["c1"] = {"workload": "RHO join |R|=|S|=2^20, reference generators (BASELINE config 1)",
                                   "cpu": rho_cpu["config1"], "gpu": c1_gpu}
+        # BASELINE configs 4 and 5 on the host: the oracle RHO on the relations the GPU joined
+        # (c4 pk 2^27 x fk 2^30, c5 pk 2^28 x the Zipf stream), the same pinned cores
+        for wl, (Rh, Sh) in list(cpu_cfg_rel.items()):
+            medw, repsw, tw = timed_rho(Rh, Sh, threads, pinned, args.cpu_seconds)
+            cw = {"R": len(Rh), "S": len(Sh), "threads": threads, "kind": "port",
+                  "M_probed_tuples_per_s": round(len(Sh) / medw / 1e6, 1),
+                  "M_rec_per_s_reference_formula": round((len(Rh) + len(Sh)) / medw / 1e6, 1),
+                  "ms": round(medw * 1e3, 2), "joins": repsw, "radix_bits": tw["radix_bits"], "passes": tw["passes"],
+                  "sample": f"oracle RHO on the {wl} relations the GPU joined, {threads} threads pinned, median of "
+                            f"{repsw} joins"}
+            rho_cpu[wl] = cw
+            if wl in configs_info:
+                configs_info[wl]["cpu"] = cw
+                gpu_v = configs_info[wl].get("M_probed_tuples_per_s")
+                if gpu_v:
+                    configs_info[wl]["gpu_over_cpu"] = round(gpu_v / cw["M_probed_tuples_per_s"], 1)
+            del Rh, Sh
+            cpu_cfg_rel.pop(wl)
         lead = rho_cpu.get("pinned") or rho_cpu["config1"]
         cpu = {"value": lead["M_probed_tuples_per_s"], "unit": "M probed tuples/s", "cores": threads, "kind": "port",
                "sample": (f"oracle RHO (radix_join.cpp restated, pthreads) on the 2^28 x 2^28 config-2 relations "

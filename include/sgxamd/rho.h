@@ -191,6 +191,16 @@ void mi355_set_stream(void *stream);
  * process.  MI355_ERR_INVALID while a pipelined join is pending. */
 int mi355_release_workspace(void);
 
+/* HBM ceiling probe (measurement: bench.py's roofline ceilings).  One grid-stride
+ * streaming kernel of 256-thread workgroups over device buffers, enqueued on `stream`
+ * (null: the library stream): kind 0 copies `bytes` from src to dst, 1 reads src (dst:
+ * one 16-byte word, written only if an impossible xor appears), 2 writes dst.  nt_load /
+ * nt_store: non-temporal accesses; loads_in_flight: 16-byte accesses per thread and
+ * step (1, 2, 4 or 8); grid: workgroups (0: 4096).  16-byte aligned buffers, bytes a
+ * multiple of 16 (MI355_ERR_INVALID otherwise). */
+int mi355_stream_probe(int kind, const void *src, void *dst, uint64_t bytes, int nt_load, int nt_store,
+                       int loads_in_flight, uint32_t grid, void *stream);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

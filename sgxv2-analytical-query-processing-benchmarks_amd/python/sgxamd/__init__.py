@@ -217,6 +217,7 @@ SIGNATURES = {
     "mi355_set_key_layout": (None, [C.c_int]),
     "mi355_timing_get": (C.c_int, [C.POINTER(C.c_char_p), C.POINTER(C.c_double), C.c_int]),
     "mi355_set_stream": (None, [_P]),
+    "mi355_stream_probe": (C.c_int, [C.c_int, _P, _P, C.c_uint64, C.c_int, C.c_int, C.c_int, C.c_uint32, _P]),
     # multi.h
     "mi355_rho_join_multi_ex": (C.c_int, [_P, C.c_uint64, _P, C.c_uint64, C.c_int, C.c_int, C.POINTER(rho_opts),
                                           C.POINTER(multi_stats)]),
@@ -670,6 +671,15 @@ def gen_zipf_dev(out, count: int, first: int, alphabet: int, theta: float, seed:
                  stream: int | None = None) -> None:
     """Rows [first, first+count) of a device Zipf(theta) relation over keys 1..alphabet."""
     _check(lib.mi355_gen_zipf_dev(ptr(out), count, first, alphabet, theta, seed, stream or None))
+
+
+def stream_probe(kind: str, src, dst, nbytes: int, *, nt_load: bool = True, nt_store: bool = True,
+                 loads_in_flight: int = 4, grid: int = 0, stream: int | None = None) -> None:
+    """Enqueue one HBM ceiling probe (mi355_stream_probe): kind "copy" (src -> dst),
+    "read" (src; dst a 16-byte word) or "write" (dst), 16-byte accesses."""
+    k = {"copy": 0, "read": 1, "write": 2}[kind]
+    _check(lib.mi355_stream_probe(k, ptr(src) if src is not None else None, ptr(dst), nbytes, int(nt_load),
+                                  int(nt_store), loads_in_flight, grid, stream or None))
 
 
 def gen_scan_dev(out, n: int, mode: int, seed: int, dtype: str = "i32", stream: int | None = None) -> None:
