@@ -661,14 +661,16 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
     const size_t elem = o.keys ? sizeof(uint32_t) : sizeof(row_t);
     // u16 wire buffers (S): [residuals (256-B aligned)][G counts rows of P16 + 1 words];
     // the receive side also holds the gather's scratch (rho::wire_scratch_u64)
-    // (every sender's run padded to 8 residuals: rho::wire_pad)
-    const auto res_bytes = [G](uint64_t n) {
-        return ((std::max<uint64_t>(n, 1) + 8ull * G) * 2 + 255) & ~uint64_t(255);
-    };
+    // (every sender's run in a slot of rho::wire_slot residuals: its partitions padded to 8)
+    const uint64_t slack = (uint64_t)G * (8ull * P16 + 16);  // (rho::wire_slot's padding, per run)
+    const auto res_bytes = [slack](uint64_t n) { return ((std::max<uint64_t>(n, 1) + slack) * 2 + 255) & ~uint64_t(255); };
     // (the send side: 4 bytes per key, rho::wire_partition writes a wide destination as keys
-    // -- at most 2 (n + 7 G) u16 slots with the runs padded to 8 residuals)
-    const auto snd_bytes = [G](uint64_t n) { return (std::max<uint64_t>(n, 1) * 4 + 32ull * G + 255) & ~uint64_t(255); };
-    const uint64_t rows = (uint64_t)G * (P16 + 1) * sizeof(uint64_t);
+    // -- at most 2 n u16 slots past the last destination's start)
+    const auto snd_bytes = [slack](uint64_t n) {
+        return (std::max<uint64_t>(n, 1) * 4 + slack * 2 + 255) & ~uint64_t(255);
+    };
+    const uint64_t RW = rho::wire_row_words(P16);
+    const uint64_t rows = (uint64_t)G * RW * sizeof(uint64_t);
     if (fail_rc == MI355_OK) {
         hipError_t e = ctx->xsendR.ensure(std::max<uint64_t>(nR, 1) * elem);
         if (e == hipSuccess) e = ctx->xsendS.ensure(std::max<uint64_t>(nS, 1) * elem);
@@ -718,7 +720,7 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
     // failure from here on is flagged at the final all-reduce
     uint64_t total[2] = {0, 0};
     std::vector<uint64_t> s_piece(K, 0);  // S tuples landing per piece (S's local pass 1 runs per piece)
-    std::vector<uint64_t> wbase, wcount;  // u16 wire: where sender q's run of S residuals lands, its residuals
+    std::vector<uint64_t> wbase, wcount, wspan;  // u16 wire: sender q's run of S residuals: start, keys, slot
     // (u16 wire: R's pieces only; S follows below)
     bool s_scattered = false;
     const auto post_pieces = [&](int j0, int j1) -> int {
@@ -778,7 +780,7 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
             std::vector<uint64_t> km(G, 0);
             if (fail_rc == MI355_OK) {
                 for (int q = 0; q < G; ++q)
-                    hip_ok(hipMemcpyAsync(&km[q], scnt + (size_t)q * (P16 + 1) + P16, sizeof(uint64_t),
+                    hip_ok(hipMemcpyAsync(&km[q], scnt + (size_t)q * RW + 2 * P16, sizeof(uint64_t),
                                           hipMemcpyDeviceToHost, s),
                            "hipMemcpyAsync (largest key)");
                 hip_ok(hipStreamSynchronize(s), "hipStreamSynchronize (largest key)");
@@ -796,15 +798,16 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
         if (fail_rc != MI355_OK && ctx->wsendS.ptr) (void)hipMemsetAsync(scnt, 0, rows, s);
         hipEvent_t ready = rs->ev[K];
         hip_ok(hipEventRecord(ready, s), "hipEventRecord (residuals ready)");
-        const std::vector<uint64_t> crow(G, (uint64_t)P16 + 1);
+        const std::vector<uint64_t> crow(G, RW);
         MH_RC(transport_rc(
             T.post_exchange(rank, rs->comm, ready, scnt, crow.data(), rcnt, crow.data(), sizeof(uint64_t))));
-        // every run padded to 8 residuals on both sides (rho::wire_pad): each sender's run
-        // starts on 16 bytes in the send and the receive buffer; the padding is never read
+        // every run in a slot of rho::wire_slot residuals on both sides: each sender's run
+        // starts on 16 bytes in the send and the receive buffer, its partitions padded to 8
+        // residuals (the build/probe reads them in place); the padding is never read
         std::vector<uint64_t> s16p(G), r16p(G);
         for (int q = 0; q < G; ++q) {
-            s16p[q] = rho::wire_pad(s16[q]);
-            r16p[q] = rho::wire_pad(r16[q]);
+            s16p[q] = rho::wire_slot(s16[q], P16);
+            r16p[q] = rho::wire_slot(r16[q], P16);
         }
         MH_RC(transport_rc(
             T.post_exchange(rank, rs->comm, ready, snd16, s16p.data(), ctx->wrecvS.ptr, r16p.data(), sizeof(uint16_t))));
@@ -814,10 +817,12 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
             wbase[q] = at;
             at += r16p[q];
             total[1] += r16[q];
-            // (the residuals; the padding, at most 14 bytes per peer, is not counted)
+            // (the residuals; the slot's padding, at most (8 P + 15) x 2 bytes per peer, is not
+            // counted)
             if (q != rank) o.sent += s16[q] * sizeof(uint16_t) + crow[q] * sizeof(uint64_t);
         }
         wcount = r16;
+        wspan = r16p;
         hip_ok(hipEventRecord(rs->ev[2 * K + 1], rs->comm), "hipEventRecord (S landed)");
     }
     const bool timed = hipEventRecord(rs->t_land, rs->comm) == hipSuccess;
@@ -839,8 +844,9 @@ int rank_join(Transport &T, int rank, Context *ctx, hipStream_t s, const row_t *
                           : rho::join_pipelined_begin(ctx, s, ctx->xrecvR.ptr, total[0], total[1], &lo,
                                                       (uint32_t)elem, nullptr, 0, true);
             if (lrc == MI355_OK)
-                lrc = rho::join_pipelined_finish_wire16(ctx, ctx->wrecvS.as<uint16_t>(), rcS, wbase.data(), wcount.data(), total[1],
-                                                        G, rcS + (size_t)G * (P16 + 1), rs->ev[2 * K + 1], &o.st);
+                lrc = rho::join_pipelined_finish_wire16(ctx, ctx->wrecvS.as<uint16_t>(), rcS, wbase.data(),
+                                                        wcount.data(), wspan.data(), total[1], G, rcS + (size_t)G * RW,
+                                                        rs->ev[2 * K + 1], &o.st);
             fail(lrc);
             o.local = lrc == MI355_OK ? o.st.matches : 0;
         } else if (waited) {

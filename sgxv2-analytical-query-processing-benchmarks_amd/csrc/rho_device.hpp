@@ -73,23 +73,33 @@ int wire_mode();
 // partitions the keys this rank sends each destination (runs of packed u32
 // keys in `keys`: destination q's runs at run_off[q * runs + j], run_n[...]) with the
 // plan of wire16_plan(nR, nS, ...): destination q's residuals go to out16 +
-// sum_{q' < q} wire_pad(keys of q') (a 16-byte boundary: k_place_seg's whole-line
-// copies), grouped by partition; counts[q * (P + 1) + p] = its partition
-// p's keys, counts[q * (P + 1) + P] = its largest key.  Enqueued on s (no wait).
+// sum_{q' < q} wire_slot(keys of q', P) (a 16-byte boundary: k_place_seg's whole-line
+// copies), grouped by partition, every partition on a multiple of 8 residuals;
+// counts[q * (2 P + 1) + p] = its partition p's keys, [+ P + p] its start in the run,
+// [+ 2 P] its largest key.  Enqueued on s (no wait).
 int wire_partition(Context *ctx, hipStream_t s, const uint32_t *keys, int G, int runs, const uint64_t *run_off,
                    const uint64_t *run_n, uint64_t nR, uint64_t nS, const mi355_rho_opts *lo, uint16_t *out16,
                    uint64_t *counts, const char *tag);
 // Receiver: after join_pipelined_begin(..., wire16 = true) (R's passes, the plan of
 // wire16_plan, R's pass 2 writing residuals), S's residuals as the G senders sent them
-// (sender q's run of s_n[q] residuals at s_base[q] u16 elements, its counts row as
-// wire_partition wrote it; nS residuals in all): its pieces are gathered after s_landed
-// (an event on the communication stream), then the build/probe.  scratch:
-// wire_scratch_u64(G, P) u64.  Synchronises the stream; st as join_pipelined_finish.
+// (sender q's run of s_n[q] keys at s_base[q] u16 elements in a slot of s_span[q], its
+// counts row as wire_partition wrote it; nS keys in all): after s_landed (an event on the
+// communication stream) the build/probe reads S's partitions in place as their G pieces
+// (G <= 8; more, or SGXAMD_WIRE_GATHER=1: the pieces are gathered into contiguous
+// partitions first).  scratch: wire_scratch_u64(G, P) u64.  Synchronises the stream; st
+// as join_pipelined_finish.
 int join_pipelined_finish_wire16(Context *ctx, const uint16_t *s16, const uint64_t *s_cnt, const uint64_t *s_base,
-                                 const uint64_t *s_n, uint64_t nS, int G, uint64_t *scratch, hipEvent_t s_landed,
-                                 mi355_rho_stats *st);
+                                 const uint64_t *s_n, const uint64_t *s_span, uint64_t nS, int G, uint64_t *scratch,
+                                 hipEvent_t s_landed, mi355_rho_stats *st);
 // A destination's (sender's) run of u16 residuals on the wire, padded to 8 (16 bytes).
 inline uint64_t wire_pad(uint64_t n) { return (n + 7) & ~uint64_t(7); }
+// The slot of a run of n keys on the wire: its P partitions each start on a multiple of 8
+// (at most 8 P + 8 residuals of padding, rho_internal.hpp wire_pad_slack), so the
+// receiver reads them in place.  A multiple of 8; none for an empty run (wire_partition
+// writes nothing for it).
+inline uint64_t wire_slot(uint64_t n, uint32_t P) { return n ? wire_pad(n) + 8ull * P + 8 : 0; }
+// Words of one counts row: P partition counts, P partition starts, the largest key.
+inline uint64_t wire_row_words(uint32_t P) { return 2ull * P + 1; }
 uint64_t wire_scratch_u64(int G, uint32_t P);
 // Tests: enqueue `us` microseconds of waiting on stream s (rho_kernels.hip k_spin).
 hipError_t launch_spin(uint32_t us, hipStream_t s);

@@ -244,6 +244,7 @@ struct RelPlan {
     size_t kmax;   // pooled keys: the segments' largest keys, then the relation's ([nseg1])
     bool narrow;   // pass 2 writes u16 residuals when the largest key allows (plan_join)
     bool narrow16; // pass 1 writes a narrow pool first (u16 residuals, the 4-byte pool repeated if a residual does not fit)
+    bool pad_parts = false;  // pass 2's partitions start on multiples of 8 elements (the u16 wire's senders)
     // pooled pass 1 per input piece (the multi-GPU exchange's received pieces): piece i is
     // elements [piece_off[i], + piece_n[i]), its segments start at piece_g0[i]; its launch
     // waits for piece_ev[i] (null: no wait)
@@ -368,7 +369,7 @@ int partition_relation_pooled(Context *ctx, hipStream_t s, Timer &tm, const std:
     tm.mark((t + "pass2_hist").c_str());
     RHO_HIP(launch_hist_side_blk(side, list, m2, rp.grid2, pol.b2, hist2, s));
     tm.mark((t + "pass2_scan").c_str());
-    RHO_HIP(launch_scan_regions(hist2, segbase2, start1, F1, pol.b2, ps, pc, s));
+    RHO_HIP(launch_scan_regions(hist2, segbase2, start1, F1, pol.b2, ps, pc, s, rp.pad_parts));
     tm.mark((t + "pass2_scatter").c_str());
     RHO_HIP(launch_scatter_blk(t1, list, t2, rp.keys ? 4u : 8u, m2, rp.grid2, key_shift + pol.b1, pol.b2, hist2, s,
                                narrow, ps, pc, rp.narrow16 ? side : nullptr));
@@ -488,6 +489,7 @@ void plan_relation(Arena &A, RelPlan &rp, uint64_t n, const Policy &pol, int poo
     rp.chain = false;
     rp.narrow = false;
     rp.narrow16 = false;
+    rp.pad_parts = false;
     rp.kmax = 0;
     rp.in_size = sizeof(row_t);
     rp.piece_off.clear();
@@ -674,7 +676,9 @@ int plan_join(Context *ctx, hipStream_t s, uint64_t nR, uint64_t nS, const mi355
                      narrow_pool_enabled();
     pj.pr.narrow16 = n16 && !pj.pr.chain;
     pj.ps.narrow16 = n16 && !pj.ps.chain;
-    pj.over_cap = (uint32_t)(nS / pj.s_chunk + 1);
+    // (wire16: S may come as pieces, each partition's task list over 8 x its units: up to
+    // 7 more per piece, kPieceMaxG pieces)
+    pj.over_cap = (uint32_t)((nS + (wire16 ? 7ull * kPieceMaxG * P : 0ull)) / pj.s_chunk + 1);
     // one workgroup per task up to 2048 (few partitions with a large S — a tiny build
     // side — still spread their S chunks over the chip)
     pj.join_grid = (uint32_t)std::min<uint64_t>(P + pj.over_cap - 1, 2048);
@@ -785,6 +789,11 @@ void fill_join_stats(const Context *ctx, const PendingJoin &pj, const Timer &tm,
 struct GivenParts {
     const row_t *f;
     const uint64_t *ps, *pc;
+    // the u16 wire's S read in place (join_pipelined_finish_wire16): f = the receive
+    // buffer of residuals (bytes), its pieces; ps unused
+    bool pieces = false;
+    uint64_t bytes = 0;
+    WirePieces w{};
 };
 int join_finish(Context *ctx, PendingJoin &pj, const row_t *dS, uint64_t nS, mi355_rho_stats *st,
                 output_triple_t *out, uint64_t out_cap, DeviceBuffer *grow, bool fork_now,
@@ -845,9 +854,22 @@ int join_finish(Context *ctx, PendingJoin &pj, const row_t *dS, uint64_t nS, mi3
     tm.mark("join_tasks");
     // narrow plans: k_join_n adds into the count and tick slots, zeroed here
     const bool nar = !pj.materialize && (pj.pr.narrow || pj.ps.narrow) && narrow_join_enabled();
-    RHO_HIP(launch_make_tasks(pcR, pcS, P, over, pj.over_cap, result + 1, pj.s_chunk, s, nar ? counts : nullptr, cyc,
-                              join_grid));
-    if (!pj.materialize) {
+    const bool pieces = given_s && given_s->pieces;
+    // (S in pieces: the task list splits each partition's units, 8 per unit)
+    RHO_HIP(launch_make_tasks(pcR, pieces ? given_s->w.units8 : pcS, P, over, pj.over_cap, result + 1, pj.s_chunk, s,
+                              nar || pieces ? counts : nullptr, cyc, join_grid));
+    if (pieces) {
+        if (pj.materialize || pj.algo != kAlgoChaining || pol.rcap != kBigRcap || !pj.pr.narrow || !pj.ps.narrow) {
+            set_last_error("u16 wire pieces: the plan is not the narrow counting table");
+            return MI355_ERR_INVALID;
+        }
+        tm.mark("join_build_probe");
+        RHO_HIP(launch_join_pieces(fR, psR, pcR, reinterpret_cast<const uint16_t *>(fS), given_s->bytes, given_s->w,
+                                   P, over, n_over, hash_shift, pj.s_chunk, join_grid,
+                                   (uint32_t)std::min<uint64_t>(P + pj.over_cap - 1, 0xFFFFFFFFull), counts, cyc,
+                                   reinterpret_cast<uint32_t *>(result + 6), A.at<uint32_t>(pj.pr.kmax) + pj.pr.nseg1,
+                                   A.at<uint32_t>(pj.ps.kmax) + pj.ps.nseg1, result, s));
+    } else if (!pj.materialize) {
         tm.mark("join_build_probe");
         // the 16,384-key table's k_join_x sums the count slots itself (k_reduce folded in)
         const bool fold = algo == kAlgoChaining && pol.rcap == kBigRcap;
@@ -1281,10 +1303,11 @@ int wire_partition(Context *ctx, hipStream_t s, const uint32_t *keys, int G, int
     tm.begin_call(s, false);
     const std::string t = tag;
     uint64_t doff = 0;
+    const uint64_t RW = 2ull * P + 1;  // a row: counts, starts, the largest key
     for (int q = 0; q < G; ++q) {
-        uint64_t *cq = counts + (size_t)q * (P + 1);
+        uint64_t *cq = counts + (size_t)q * RW;
         if (!nq[q]) {
-            RHO_HIP(hipMemsetAsync(cq, 0, sizeof(uint64_t) * (P + 1), s));
+            RHO_HIP(hipMemsetAsync(cq, 0, sizeof(uint64_t) * RW, s));
             continue;
         }
         A.reset();
@@ -1292,6 +1315,8 @@ int wire_partition(Context *ctx, hipStream_t s, const uint32_t *keys, int G, int
         for (int j = 0; j < runs; ++j) rp.piece_off[j] = run_off[(size_t)q * runs + j];
         rp.narrow = true;  // wire16_plan: every residual fits 16 bits
         rp.narrow16 = false;
+        rp.pad_parts = true;  // every partition on 16 bytes: the receiver reads them in place
+        rp.chain = false;     // (the padded partition starts come from k_scan_regions: the side stream's plan)
         rp.in_size = sizeof(uint32_t);
         const row_t *f = nullptr;
         const uint64_t *pst = nullptr, *pcn = nullptr;
@@ -1303,10 +1328,13 @@ int wire_partition(Context *ctx, hipStream_t s, const uint32_t *keys, int G, int
             if (rc) return rc;
         }
         RHO_HIP(hipMemcpyAsync(cq, pcn, sizeof(uint64_t) * P, hipMemcpyDeviceToDevice, s));
-        RHO_HIP(hipMemsetAsync(cq + P, 0, sizeof(uint64_t), s));
-        RHO_HIP(hipMemcpyAsync(cq + P, A.at<uint32_t>(rp.kmax) + rp.nseg1, sizeof(uint32_t), hipMemcpyDeviceToDevice,
-                               s));
-        doff += wire_pad(nq[q]);  // every destination's run starts on 16 bytes (k_place_seg's copies)
+        RHO_HIP(hipMemcpyAsync(cq + P, pst, sizeof(uint64_t) * P, hipMemcpyDeviceToDevice, s));
+        RHO_HIP(hipMemsetAsync(cq + 2 * P, 0, sizeof(uint64_t), s));
+        RHO_HIP(hipMemcpyAsync(cq + 2 * P, A.at<uint32_t>(rp.kmax) + rp.nseg1, sizeof(uint32_t),
+                               hipMemcpyDeviceToDevice, s));
+        // every destination's run starts on 16 bytes (k_place_seg's copies) and spans its
+        // padded partitions
+        doff += wire_slot(nq[q], P);
     }
     tm.end_call();
     return MI355_OK;
@@ -1314,9 +1342,20 @@ int wire_partition(Context *ctx, hipStream_t s, const uint32_t *keys, int G, int
 
 uint64_t wire_scratch_u64(int G, uint32_t P) { return wire_scratch_words((uint32_t)G, P); }
 
+// SGXAMD_WIRE_GATHER=1 (development A/B switch, read once): the u16 wire's receiver
+// gathers S's pieces into contiguous partitions before the build/probe (round 5's path)
+// instead of reading them in place.
+inline bool wire_gather_forced() {
+    static const bool on = [] {
+        const char *e = std::getenv("SGXAMD_WIRE_GATHER");
+        return e && std::atoi(e) == 1;
+    }();
+    return on;
+}
+
 int join_pipelined_finish_wire16(Context *ctx, const uint16_t *s16, const uint64_t *s_cnt, const uint64_t *s_base,
-                                 const uint64_t *s_n, uint64_t nS, int G, uint64_t *scratch, hipEvent_t s_landed,
-                                 mi355_rho_stats *st) {
+                                 const uint64_t *s_n, const uint64_t *s_span, uint64_t nS, int G, uint64_t *scratch,
+                                 hipEvent_t s_landed, mi355_rho_stats *st) {
     PendingJoin &pj = pending_of(ctx);
     if (!pj.active || !pj.ps.narrow) {
         pj.active = false;
@@ -1332,16 +1371,27 @@ int join_pipelined_finish_wire16(Context *ctx, const uint16_t *s16, const uint64
     Arena &A = ctx->scratch;
     Timer &tm = thread_timer();
     WireBases bs{};
+    uint64_t end = 0;
     for (int q = 0; q < G; ++q) {
         bs.b[q] = s_base[q];
         bs.n[q] = s_n[q];
+        bs.span[q] = s_span[q];
+        end = std::max(end, s_base[q] + s_span[q]);
+    }
+    uint64_t *psS = A.at<uint64_t>(pj.ps.pstart), *pcS = A.at<uint64_t>(pj.ps.pcnt);
+    uint32_t *narrowS = A.at<uint32_t>(pj.ps.kmax) + pj.ps.nseg1;
+    RHO_HIP(hipStreamWaitEvent(pj.s, s_landed, 0));
+    if ((uint32_t)G <= kPieceMaxG && !wire_gather_forced() && end * 2 <= 0xFFFFFFF0ull) {
+        // S's partitions read in place: only the piece table is built
+        tm.mark("S_wire_pieces");
+        RHO_HIP(launch_wire_pieces(s_cnt, (uint32_t)G, P, bs, scratch, pcS, narrowS, pj.s));
+        const GivenParts gs{reinterpret_cast<const row_t *>(s16), psS, pcS, true, end * 2,
+                            wire_pieces_of(scratch, (uint32_t)G, P)};
+        return join_finish(ctx, pj, nullptr, nS, st, nullptr, 0, nullptr, false, &gs);
     }
     uint16_t *mS = ctx->t2S.as<uint16_t>();
-    uint64_t *psS = A.at<uint64_t>(pj.ps.pstart), *pcS = A.at<uint64_t>(pj.ps.pcnt);
-    RHO_HIP(hipStreamWaitEvent(pj.s, s_landed, 0));
     tm.mark("S_wire_merge");
-    RHO_HIP(launch_wire_merge(s16, s_cnt, (uint32_t)G, P, bs, scratch, psS, pcS,
-                              A.at<uint32_t>(pj.ps.kmax) + pj.ps.nseg1, mS, pj.s));
+    RHO_HIP(launch_wire_merge(s16, s_cnt, (uint32_t)G, P, bs, scratch, psS, pcS, narrowS, mS, pj.s));
     const GivenParts gs{reinterpret_cast<const row_t *>(mS), psS, pcS};
     return join_finish(ctx, pj, nullptr, nS, st, nullptr, 0, nullptr, false, &gs);
 }

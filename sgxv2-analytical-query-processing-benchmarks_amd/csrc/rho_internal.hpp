@@ -47,10 +47,13 @@ hipError_t launch_scan_single(uint64_t *hist, uint32_t nseg, uint32_t bits, uint
                               uint32_t *next_seg_base, uint64_t next_seg_size, hipStream_t s);
 
 // Multi-region scan: hist [g][F] -> absolute write cursors (in place) and the
-// (region, digit) partition table part_start/part_count [nreg * F].
+// (region, digit) partition table part_start/part_count [nreg * F].  pad: every
+// partition starts on a multiple of 8 elements (the u16 wire's senders), the layout
+// then spans at most wire_pad_slack(nreg * F) elements more.
 hipError_t launch_scan_regions(uint64_t *hist, const uint32_t *seg_base, const uint64_t *reg_start,
                                uint32_t nreg, uint32_t bits, uint64_t *part_start, uint64_t *part_count,
-                               hipStream_t s);
+                               hipStream_t s, bool pad = false);
+inline uint64_t wire_pad_slack(uint64_t partitions) { return 8 * partitions + 8; }
 
 // Context::sync (u64 words, zero when allocated): the digit totals of the small join's
 // histograms (launch_hist_pair), in two sets that alternate per call (the scatter of a
@@ -321,21 +324,45 @@ hipError_t launch_excl_scan(const uint64_t *in, const uint32_t *n_extra, uint64_
 hipError_t launch_reduce(const uint64_t *partials, uint32_t n, uint64_t *result, const uint64_t *cyc, uint32_t ncyc,
                          hipStream_t s);
 
-// Multi-GPU u16 wire (wire_kernels.hip): in = the G senders' runs of u16 residuals, run q
-// at bases.b[q] (bases.n[q] residuals), each grouped by partition; cnt = G rows of P
-// partition counts and the sender's largest key.  Gathers every partition's G pieces
-// into out (contiguous partitions: ps / pc), *narrow = the largest key; a row whose
-// counts do not add up to its run is left out.  scratch: wire_scratch_words(G, P) u64;
-// P <= 2^20.
+// Multi-GPU u16 wire (wire_kernels.hip): the G senders' runs of u16 residuals, run q at
+// bases.b[q] residuals of the receive buffer (a multiple of 8) with bases.n[q] keys in a
+// slot of bases.span[q] residuals, each grouped by partition, every partition starting
+// on a multiple of 8; rows = G rows of 2 P + 1 words: P partition counts, P partition
+// starts (relative to the run) and the sender's largest key.  A row whose counts do not
+// add up to n[q], or whose pieces pass its slot, is left out; *narrow = the largest key
+// of the rows kept.  scratch: wire_scratch_words(G, P) u64; P <= 2^20.
 constexpr uint32_t kWireMaxG = 64;
 struct WireBases {
-    uint64_t b[kWireMaxG];  // where sender q's run starts (a multiple of 8 residuals)
-    uint64_t n[kWireMaxG];  // its residuals (the count exchange's announcement)
+    uint64_t b[kWireMaxG];     // where sender q's run starts (a multiple of 8 residuals)
+    uint64_t n[kWireMaxG];     // its keys (the count exchange's announcement)
+    uint64_t span[kWireMaxG];  // its slot (residuals)
+};
+// The piece table in the scratch: ub / nk [p][q] (u32: piece (p, q)'s first unit of 8
+// residuals in the receive buffer, its keys), units8[p] = 8 x partition p's units.
+struct WirePieces {
+    uint32_t *ub, *nk;
+    uint64_t *units8;
+    uint32_t G, P;
 };
 uint64_t wire_scratch_words(uint32_t G, uint32_t P);
-hipError_t launch_wire_merge(const uint16_t *in, const uint64_t *cnt, uint32_t G, uint32_t P, const WireBases &bases,
-                             uint64_t *scratch, uint64_t *ps, uint64_t *pc, uint32_t *narrow, uint16_t *out,
-                             hipStream_t s);
+WirePieces wire_pieces_of(uint64_t *scratch, uint32_t G, uint32_t P);
+// The piece table (k_join_np reads S in place) and pc[p] = partition p's keys.
+hipError_t launch_wire_pieces(const uint64_t *rows, uint32_t G, uint32_t P, const WireBases &bases, uint64_t *scratch,
+                              uint64_t *pc, uint32_t *narrow, hipStream_t s);
+// The piece table, then every partition's pieces gathered into out (contiguous
+// partitions ps / pc): the path for G > kPieceMax.
+hipError_t launch_wire_merge(const uint16_t *in, const uint64_t *rows, uint32_t G, uint32_t P,
+                             const WireBases &bases, uint64_t *scratch, uint64_t *ps, uint64_t *pc, uint32_t *narrow,
+                             uint16_t *out, hipStream_t s);
+// k_join_np (the build/probe over R's contiguous narrow partitions and S's pieces,
+// kPieceMax = 8 senders at most), then k_join_x with the count reduction folded in
+// (fold: the join's result block).
+constexpr uint32_t kPieceMaxG = 8;
+hipError_t launch_join_pieces(const void *R, const uint64_t *r_start, const uint64_t *r_count, const uint16_t *s16,
+                              uint64_t s_bytes, const WirePieces &w, uint64_t P, const uint64_t *over,
+                              const uint32_t *n_over, uint32_t hash_shift, uint64_t s_chunk, uint32_t grid,
+                              uint32_t tasks_max, uint64_t *counts, uint64_t *cyc, uint32_t *tickets,
+                              const uint32_t *narrow_r, const uint32_t *narrow_s, uint64_t *fold, hipStream_t s);
 
 }  // namespace rho
 }  // namespace sgxamd

@@ -441,11 +441,14 @@ hipError_t launch_scan_single(uint64_t *hist, uint32_t nseg, uint32_t bits, uint
 // One block per region.  Cursors for [g][d] and the partition table.  The region's
 // segments are split among S = 512 / F threads per digit (tid = j * F + d), so the
 // reads of one digit's column run in parallel instead of as one dependent chain.
+// pad (the u16 wire's senders): every partition starts on a multiple of 8 elements --
+// region r's partitions from round_up8(reg_start[r] + 8 F r), each taking round_up8(its
+// count): at most 8 F P / F + 8 elements past the unpadded layout (wire_pad_slack).
 __global__ __launch_bounds__(kMaxF) void k_scan_regions(uint64_t *__restrict__ hist,
                                                         const uint32_t *__restrict__ seg_base,
                                                         const uint64_t *__restrict__ reg_start, uint32_t F,
                                                         uint64_t *__restrict__ part_start,
-                                                        uint64_t *__restrict__ part_count) {
+                                                        uint64_t *__restrict__ part_count, uint32_t pad) {
     __shared__ uint64_t scratch[kMaxF / kWave + 1];
     __shared__ uint64_t part[kMaxF];   // [j][d]: sum of thread j's chunk, then its prefix inside d
     __shared__ uint64_t startd[kMaxF];
@@ -467,9 +470,10 @@ __global__ __launch_bounds__(kMaxF) void k_scan_regions(uint64_t *__restrict__ h
         }
     }
     uint64_t tot;
-    const uint64_t ex = block_excl_scan_u64(j == 0 ? total : 0, scratch, &tot);  // digits are tids 0..F-1
+    const uint64_t ex = block_excl_scan_u64(j == 0 ? (pad ? (total + 7) & ~7ull : total) : 0, scratch,
+                                            &tot);  // digits are tids 0..F-1
     if (j == 0) {
-        const uint64_t start = reg_start[r] + ex;
+        const uint64_t start = (pad ? (reg_start[r] + 8ull * F * r + 7) & ~7ull : reg_start[r]) + ex;
         startd[d] = start;
         part_start[(uint64_t)r * F + d] = start;
         part_count[(uint64_t)r * F + d] = total;
@@ -484,10 +488,10 @@ __global__ __launch_bounds__(kMaxF) void k_scan_regions(uint64_t *__restrict__ h
 }
 
 hipError_t launch_scan_regions(uint64_t *hist, const uint32_t *seg_base, const uint64_t *reg_start, uint32_t nreg,
-                               uint32_t bits, uint64_t *part_start, uint64_t *part_count, hipStream_t s) {
+                               uint32_t bits, uint64_t *part_start, uint64_t *part_count, hipStream_t s, bool pad) {
     const uint32_t F = 1u << bits;
     hipLaunchKernelGGL(k_scan_regions, dim3(nreg), dim3(kMaxF), 0, s, hist, seg_base, reg_start, F, part_start,
-                       part_count);
+                       part_count, pad ? 1u : 0u);
     return hipGetLastError();
 }
 
@@ -790,13 +794,17 @@ struct PoolState {
 // Waves per SIMD that the LDS footprint allows (__launch_bounds__ second argument:
 // k workgroups per CU of NT threads <=> k * NT / 256 waves per SIMD), so the
 // register allocation never becomes the tighter occupancy limit.
+#ifndef SGXAMD_POOL_MAXW  // pooled pass 1: waves per SIMD the register budget is cut for
+#define SGXAMD_POOL_MAXW 4
+#endif
 template <int BITS, int ITEMS, int NT, int EXT = 0, typename T = uint64_t, int OB = (int)sizeof(T)>
 constexpr int scatter_waves_per_simd() {
     constexpr int k = (160 * 1024) / (int)sizeof(ScatterLds<BITS, ITEMS, NT, EXT, T, OB>);
     constexpr int w = (k < 1 ? 1 : k) * NT / 256;
     // at most 4 waves/SIMD (128 VGPRs): fewer registers spill, and a scratch reload is
     // a vector-memory op whose wait would also wait for every store in flight
-    return w < 1 ? 1 : (w > 4 ? 4 : w);
+    constexpr int cap = EXT == 1 ? SGXAMD_POOL_MAXW : 4;
+    return w < 1 ? 1 : (w > cap ? cap : w);
 }
 
 // One tile of the segment behind rsrc (byte offset soff of the tile); lanes past the
@@ -2322,6 +2330,9 @@ __global__ __launch_bounds__(NT, NT / 256) void k_place_run(
 #ifndef SGXAMD_KEY_ITEMS
 #define SGXAMD_KEY_ITEMS 12
 #endif
+#ifndef SGXAMD_POOL_NT  // pooled pass 1: threads per workgroup
+#define SGXAMD_POOL_NT kScatterThreads
+#endif
 #ifndef SGXAMD_KEY_ITEMS_BLK
 #define SGXAMD_KEY_ITEMS_BLK 16
 #endif
@@ -2334,7 +2345,7 @@ template <typename T, int IS>
 hipError_t launch_scatter_pool_t(const void *in, void *out, const SegMap &m, uint32_t grid, uint32_t shift,
                                  uint32_t bits, const PoolOut &po, const DigitSide &ds, hipStream_t s,
                                  uint32_t *chain) {
-    constexpr int ITEMS = items_of<T, 1>(), NT = kScatterThreads;
+    constexpr int ITEMS = items_of<T, 1>(), NT = SGXAMD_POOL_NT;
     const char *ib = static_cast<const char *>(in);
     T *o = static_cast<T *>(out);
     const uint32_t mask2 = (1u << ds.bits2) - 1u;
@@ -3761,20 +3772,25 @@ __device__ __forceinline__ uint32_t n_get(const uint32_t *cnt, uint32_t k) {
 // One strip of a relation: build (BUILD: adds) or probe (returns the matches).
 // NAR: u16 residuals; else u32 keys (residual = key >> hash_shift).  GEN: the general
 // body's window mapping (wb: the window's first residual, wl: its counters in use).
-template <int BLOCK, int L, bool C16, bool NAR, bool BUILD, bool GEN>
+// PC (pieces, the u16 wire's S side): load j of this lane holds nv[j] valid residuals
+// (its first ones), whatever r says.
+template <int BLOCK, int L, bool C16, bool NAR, bool BUILD, bool GEN, bool PC = false>
 __device__ __forceinline__ uint32_t n_strip(uint32_t *cnt, const NRange &r, uint32_t k, uint4 (&v)[L],
-                                            uint32_t hash_shift, uint32_t wb, uint32_t wl) {
+                                            uint32_t hash_shift, uint32_t wb, uint32_t wl,
+                                            const uint32_t *nv = nullptr) {
     constexpr uint32_t KPL = NAR ? 8 : 4;
     constexpr uint32_t D = BUILD ? JoinLdsN<BLOCK, C16>::DR : JoinLdsN<BLOCK, C16>::DS;
+    static_assert(!PC || (NAR && !BUILD), "pieces: the S side's u16 residuals");
     // the strip's first and last units may straddle the range's ends (uniform test)
     const uint32_t u0 = k * (uint32_t)(BLOCK * L);
     const bool edge = (k == 0 && r.h != 0) || (u0 + BLOCK * L) * KPL > r.h + r.n;
     uint32_t m = 0;
 #pragma unroll
     for (int j = 0; j < L; ++j) {
-        const uint32_t q0 = (u0 + threadIdx.x + (uint32_t)j * BLOCK) * KPL;
+        const uint32_t q0 = PC ? 0u : (u0 + threadIdx.x + (uint32_t)j * BLOCK) * KPL;
+        const uint32_t h = PC ? 0u : r.h, n = PC ? nv[j] : r.n;
         if constexpr (!GEN) {  // (both narrow, every residual inside the table)
-            if (edge && (q0 < r.h || q0 + KPL > r.h + r.n)) n_fix16(v[j], q0, r.h, r.n, D);
+            if (PC ? n < KPL : (edge && (q0 < r.h || q0 + KPL > r.h + r.n))) n_fix16(v[j], q0, h, n, D);
             const uint32_t c[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -3792,7 +3808,7 @@ __device__ __forceinline__ uint32_t n_strip(uint32_t *cnt, const NRange &r, uint
             for (int i = 0; i < (int)KPL; ++i) {
                 const uint32_t key = NAR ? ((c[i / 2] >> ((i & 1) * 16)) & 0xFFFFu) : (c[i] >> hash_shift);
                 const uint32_t x = key - wb;
-                const uint32_t e = (q0 + (uint32_t)i - r.h < r.n && x < wl) ? x : D;
+                const uint32_t e = (q0 + (uint32_t)i - h < n && x < wl) ? x : D;
                 if constexpr (BUILD) n_add<C16>(cnt, e);
                 else m += n_get<C16>(cnt, e);
             }
@@ -3801,32 +3817,81 @@ __device__ __forceinline__ uint32_t n_strip(uint32_t *cnt, const NRange &r, uint
     return m;
 }
 
+// The u16 wire's S side read in place (round 6): partition p of S is
+// G pieces, one per sender, each starting on a 16-byte unit of the receive buffer (the
+// senders pad every partition to 8 residuals, multi_host.cpp); a task's S chunk is a range
+// of units in the partition's unit space (its pieces' units back to back).  Lane unit u
+// finds its piece by comparing u with the pieces' first units (G <= kPieceMax, unrolled:
+// the arrays stay in SGPRs) and loads its 16 bytes; its valid residuals are the piece's
+// keys left (at most 8).  Replaces the gather into contiguous partitions (k_wire_gather).
+constexpr uint32_t kPieceMax = 8;
+struct SPieces {
+    __amdgpu_buffer_rsrc_t rs;  // the receive buffer of residuals
+    uint32_t u0, nu, G;         // the chunk's first unit (partition unit space), its units, pieces
+    uint32_t up[kPieceMax];     // first unit of piece q in the partition's unit space
+    uint32_t ub[kPieceMax];     // piece q's first unit in the receive buffer
+    uint32_t nk[kPieceMax];     // its keys
+};
+
+template <int BLOCK, int L>
+__device__ __forceinline__ void n_load_pieces(const SPieces &sp, uint32_t k, uint4 (&v)[L], uint32_t (&nv)[L]) {
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+        const uint32_t i = k * (uint32_t)(BLOCK * L) + threadIdx.x + (uint32_t)j * BLOCK;  // unit of the chunk
+        const uint32_t u = sp.u0 + i;
+        uint32_t up = sp.up[0], ub = sp.ub[0], nk = sp.nk[0];
+#pragma unroll
+        for (uint32_t q = 1; q < kPieceMax; ++q) {
+            const bool in = q < sp.G && u >= sp.up[q];
+            up = in ? sp.up[q] : up;
+            ub = in ? sp.ub[q] : ub;
+            nk = in ? sp.nk[q] : nk;
+        }
+        const uint32_t r = u - up, left = nk > 8 * r ? nk - 8 * r : 0u;
+        const bool ok = i < sp.nu;
+        nv[j] = ok ? min(left, 8u) : 0u;
+        // (a unit past the chunk reads 0 through the buffer bounds)
+        v[j] = buf_ld_nt_u128(sp.rs, ok ? (ub + r) * 16u : 0xFFFFFFF0u, 0);
+    }
+}
+
 // One task (a partition's S chunk): per R chunk of kBigRcap keys and per window, clear,
 // build from R's strips, probe S's strips; the strips of one (chunk, window) pass are
 // one sequence with the next strip's loads in flight while one is processed.
-template <int BLOCK, int L, bool C16, bool NR, bool NS, bool GEN>
+// PC: S is the u16 wire's pieces (sp), not the contiguous range [s_base, + nS).
+template <int BLOCK, int L, bool C16, bool NR, bool NS, bool GEN, bool PC = false>
 __device__ __forceinline__ uint64_t join_n_task(JoinLdsN<BLOCK, C16> &Ls, const void *rk, const void *sk,
                                                 uint64_t r_base, uint64_t nR, uint64_t s_base, uint32_t nS,
-                                                uint32_t hash_shift, uint32_t lim, uint64_t &bt, uint64_t &pt) {
+                                                uint32_t hash_shift, uint32_t lim, uint64_t &bt, uint64_t &pt,
+                                                const SPieces *sp = nullptr) {
     constexpr uint32_t SB = BLOCK * L * 16u;
     constexpr int ER = NR ? 2 : 4, ES = NS ? 2 : 4;
+    static_assert(!PC || NS, "pieces hold u16 residuals");
     const uint32_t nwin = GEN ? (lim + kNarrowCap - 1) / kNarrowCap : 1u;
-    const NRange sr = n_range<ES, SB>(sk, s_base, nS);
+    const NRange sr = PC ? NRange{nullptr, 0u, 0u, 0u, 0u} : n_range<ES, SB>(sk, s_base, nS);
+    const uint32_t s_strips = PC ? (sp->nu + BLOCK * L - 1) / (BLOCK * L) : sr.strips;
     uint64_t m = 0;
     bool first = true;
     for (uint64_t rc = 0; rc < nR; rc += kBigRcap) {
         const NRange rr = n_range<ER, SB>(rk, r_base + rc, (uint32_t)min(nR - rc, (uint64_t)kBigRcap));
-        const uint32_t nsr = rr.strips, ns = nsr + sr.strips;
+        const uint32_t nsr = rr.strips, ns = nsr + s_strips;
         for (uint32_t w = 0; w < nwin; ++w) {
             const uint32_t wb = w * kNarrowCap, wl = GEN ? min(kNarrowCap, lim - wb) : kNarrowCap;
             const uint64_t t0 = wall_clock64();
             uint4 va[L], vb[L];
-            const auto load = [&](uint32_t i, uint4(&v)[L]) {
+            uint32_t nva[L], nvb[L];
+            const auto load = [&](uint32_t i, uint4(&v)[L], uint32_t(&nv)[L]) {
                 const bool isr = i < nsr;
+                if constexpr (PC) {
+                    if (!isr) {  // (uniform)
+                        n_load_pieces<BLOCK, L>(*sp, i < ns ? i - nsr : 0xFFFFu, v, nv);
+                        return;
+                    }
+                }
                 n_load<BLOCK, L>(isr ? rr.p : sr.p, isr ? rr.bytes : (i < ns ? sr.bytes : 0u), isr ? i : i - nsr, v);
             };
             uint64_t tb = t0;
-            const auto step = [&](uint32_t i, uint4(&v)[L]) {
+            const auto step = [&](uint32_t i, uint4(&v)[L], const uint32_t(&nv)[L]) {
                 if (i < nsr) {
                     n_strip<BLOCK, L, C16, NR, true, GEN>(Ls.cnt, rr, i, v, hash_shift, wb, wl);
                     if (i + 1 == nsr) {
@@ -3834,10 +3899,10 @@ __device__ __forceinline__ uint64_t join_n_task(JoinLdsN<BLOCK, C16> &Ls, const 
                         tb = wall_clock64();
                     }
                 } else {
-                    m += n_strip<BLOCK, L, C16, NS, false, GEN>(Ls.cnt, sr, i - nsr, v, hash_shift, wb, wl);
+                    m += n_strip<BLOCK, L, C16, NS, false, GEN, PC>(Ls.cnt, sr, i - nsr, v, hash_shift, wb, wl, nv);
                 }
             };
-            load(0, va);
+            load(0, va, nva);
             if (!first) __syncthreads();  // the previous pass's probe is done with the table
             first = false;
             for (uint32_t i = threadIdx.x; i < JoinLdsN<BLOCK, C16>::WORDS / 4; i += BLOCK)
@@ -3845,15 +3910,15 @@ __device__ __forceinline__ uint64_t join_n_task(JoinLdsN<BLOCK, C16> &Ls, const 
             __syncthreads();
             // two register sets, the loop unrolled by two (no copy of a set in flight)
             for (uint32_t i = 0;; i += 2) {
-                load(i + 1, vb);
+                load(i + 1, vb, nvb);
 #pragma unroll
                 for (int j = 0; j < L; ++j) asm volatile("" ::"v"(va[j].x), "v"(va[j].y), "v"(va[j].z), "v"(va[j].w));
-                step(i, va);
+                step(i, va, nva);
                 if (i + 1 >= ns) break;
-                load(i + 2, va);
+                load(i + 2, va, nva);
 #pragma unroll
                 for (int j = 0; j < L; ++j) asm volatile("" ::"v"(vb[j].x), "v"(vb[j].y), "v"(vb[j].z), "v"(vb[j].w));
-                step(i + 1, vb);
+                step(i + 1, vb, nvb);
                 if (i + 2 >= ns) break;
             }
             bt += tb - t0;
@@ -3919,6 +3984,69 @@ __global__ __launch_bounds__(BLOCK, BLOCK *SGXAMD_JN_WPC / 256) void k_join_n(
         m = join_n_task<BLOCK, L, C16, true, false, true>(Ls, R, S, rb, nR, sb, nS, hash_shift, lim, bt, pt);
     else
         m = join_n_task<BLOCK, L, C16, false, true, true>(Ls, R, S, rb, nR, sb, nS, hash_shift, lim, bt, pt);
+    m = wave_sum_u64(m);
+    if (__lane_id() == 0) Ls.red[threadIdx.x / kWave] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t acc = 0;
+        for (int w = 0; w < BLOCK / kWave; ++w) acc += Ls.red[w];
+        const uint32_t slot = (uint32_t)(t % nslots);
+        if (acc) atomicAdd((unsigned long long *)&counts[slot], (unsigned long long)acc);
+        if (cyc) {
+            atomicAdd((unsigned long long *)&cyc[2 * slot], (unsigned long long)bt);
+            atomicAdd((unsigned long long *)&cyc[2 * slot + 1], (unsigned long long)pt);
+        }
+    }
+}
+
+// k_join_n over the u16 wire's S pieces (join_n_task PC): task t = (partition p, S chunk
+// of s_chunk / 8 units of p's unit space).  piece_ub / piece_nk [p * G + q]: piece (p,
+// q)'s first unit in the receive buffer s16 and its keys; s_units8[p] = 8 x p's units
+// (the task list's S sizes, launch_make_tasks).  Both relations are narrow here (the
+// u16 wire's plan).
+template <int BLOCK, int L, bool C16>
+__global__ __launch_bounds__(BLOCK, BLOCK *SGXAMD_JN_WPC / 256) void k_join_np(
+    const void *__restrict__ R, const uint16_t *__restrict__ s16, uint32_t s_bytes,
+    const uint64_t *__restrict__ r_start, const uint64_t *__restrict__ r_count, const uint32_t *__restrict__ piece_ub,
+    const uint32_t *__restrict__ piece_nk, uint32_t G, const uint64_t *__restrict__ s_units8, uint64_t P,
+    const uint64_t *__restrict__ over, const uint32_t *__restrict__ n_over, uint32_t hash_shift, uint64_t s_chunk,
+    uint64_t *__restrict__ counts, uint64_t *__restrict__ cyc, uint32_t nslots, uint32_t *__restrict__ tickets,
+    const uint32_t *__restrict__ narrow_r, const uint32_t *__restrict__ narrow_s) {
+    __shared__ JoinLdsN<BLOCK, C16> Ls;
+    const uint32_t xr = *narrow_r >> hash_shift, xs = *narrow_s >> hash_shift;
+    if (xr >= 0x10000u || xs >= 0x10000u) return;  // (the plan guarantees both)
+    if (tickets && blockIdx.x == 0 && threadIdx.x == 0) tickets[1] = 1u | 2u | 4u;
+    const uint64_t t = blockIdx.x;
+    if (t >= P + *n_over) return;
+    uint64_t p, chunk;
+    decode_task(t, P, over, p, chunk);
+    const uint64_t nR = r_count[p];
+    const uint32_t units = (uint32_t)(s_units8[p] / 8), cu = (uint32_t)(s_chunk / 8);
+    const uint32_t u0 = (uint32_t)chunk * cu;
+    const uint32_t nu = u0 < units ? min(cu, units - u0) : 0u;
+    if (nR == 0 || nu == 0) return;
+    SPieces sp;
+    sp.rs = make_rsrc(s16, s_bytes);
+    sp.u0 = u0;
+    sp.nu = nu;
+    sp.G = G;
+    uint32_t at = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < kPieceMax; ++q) {
+        const uint32_t nk = q < G ? piece_nk[p * G + q] : 0u;
+        sp.up[q] = at;
+        sp.ub[q] = q < G ? piece_ub[p * G + q] : 0u;
+        sp.nk[q] = nk;
+        at += (nk + 7) / 8;
+    }
+    const uint32_t lim = min(xr, xs) + 1;
+    uint64_t bt = 0, pt = 0, m;
+    if (xr < kNarrowCap && xs < kNarrowCap)
+        m = join_n_task<BLOCK, L, C16, true, true, false, true>(Ls, R, nullptr, r_start[p], nR, 0, 0, hash_shift, lim,
+                                                                bt, pt, &sp);
+    else
+        m = join_n_task<BLOCK, L, C16, true, true, true, true>(Ls, R, nullptr, r_start[p], nR, 0, 0, hash_shift, lim,
+                                                               bt, pt, &sp);
     m = wave_sum_u64(m);
     if (__lane_id() == 0) Ls.red[threadIdx.x / kWave] = m;
     __syncthreads();
@@ -4390,6 +4518,29 @@ hipError_t launch_join_keys(const void *R, const void *S, const uint64_t *r_star
             return hipErrorInvalidValue;
     }
 #undef KEYS_CASE
+    return hipGetLastError();
+}
+
+hipError_t launch_join_pieces(const void *R, const uint64_t *r_start, const uint64_t *r_count, const uint16_t *s16,
+                              uint64_t s_bytes, const WirePieces &w, uint64_t P, const uint64_t *over,
+                              const uint32_t *n_over, uint32_t hash_shift, uint64_t s_chunk, uint32_t grid,
+                              uint32_t tasks_max, uint64_t *counts, uint64_t *cyc, uint32_t *tickets,
+                              const uint32_t *narrow_r, const uint32_t *narrow_s, uint64_t *fold, hipStream_t s) {
+    static_assert(kPieceMaxG == kPieceMax, "one bound");
+    if (w.G == 0 || w.G > kPieceMax || s_bytes > 0xFFFFFFF0ull || (s_chunk & 7) || !narrow_r || !narrow_s)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL((k_join_np<SGXAMD_JN_BLOCK, SGXAMD_JN_L, SGXAMD_JN_C16 != 0>), dim3(std::max<uint32_t>(tasks_max, 1)),
+                       dim3(SGXAMD_JN_BLOCK), 0, s, R, s16, (uint32_t)s_bytes, r_start, r_count, w.ub, w.nk, w.G,
+                       w.units8, P, over, n_over, hash_shift, s_chunk, counts, cyc, grid, tickets, narrow_r, narrow_s);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    // the count reduction (k_join_x returns at once on narrow relations; its workgroups sum
+    // the slots)
+    const uint64_t *R64 = static_cast<const uint64_t *>(R);
+    hipLaunchKernelGGL((k_join_x<kBigRcap, 1024, 8, 1>), dim3(std::min<uint32_t>(grid, cu_count())), dim3(1024), 0, s,
+                       R64, reinterpret_cast<const uint64_t *>(s16), r_start, r_count, r_start, r_count, P, over,
+                       n_over, hash_shift, s_chunk, counts, cyc, nullptr, nullptr, grid, tickets, narrow_r, narrow_s,
+                       1u, fold);
     return hipGetLastError();
 }
 

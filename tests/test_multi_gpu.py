@@ -283,11 +283,12 @@ def _keys_out(rel_, g):
 def _exchange_bytes(st, out_r, out_s, g):
     """sent_bytes of a counting join's keys exchange over all ranks of one process: 4 bytes
     per key that leaves its rank, except that on the u16 wire S's keys go as 2-byte
-    residuals plus, per peer, the sender's counts row (P partition counts and its
-    largest key, 8 bytes each)."""
+    residuals plus, per peer, the sender's counts row (P partition counts, P partition
+    starts and its largest key, 8 bytes each); the padding of each run's slot (its
+    partitions on 16-byte boundaries, read in place) is not counted."""
     if st["elem_bytes"] == 2:
         p = 1 << st["local"]["radix_bits"]
-        return 4 * out_r + 2 * out_s + g * (g - 1) * (p + 1) * 8
+        return 4 * out_r + 2 * out_s + g * (g - 1) * (2 * p + 1) * 8
     assert st["elem_bytes"] == 4
     return 4 * (out_r + out_s)
 

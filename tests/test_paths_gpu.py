@@ -122,6 +122,7 @@ print("wire ok")
 
 
 @pytest.mark.parametrize("env", [{"SGXAMD_WIRE16": "0"}, {"SGXAMD_NARROW": "0"}, {"SGXAMD_PLACE": "0"}, {"SGXAMD_PLACE_RUN": "1"},
+                                 {"SGXAMD_WIRE_GATHER": "1"},
                                  {"SGXAMD_JOIN_N": "0"}, {"SGXAMD_CHAIN_HIST": "1"}, {"SGXAMD_PASS1_BITS": "6"},
                                  {"SGXAMD_POOL_SEGS": "3"}])
 def test_wire16_switches(env):

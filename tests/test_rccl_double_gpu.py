@@ -299,8 +299,8 @@ def test_sharded_keys_exchange_exact_bytes(sgx, dbl, gpu):
                 a, b = r * (n // g), (n if r == g - 1 else (r + 1) * (n // g))
                 k = X[a:b] & 0xFFFFFFFF
                 out.append(int(((k & (g - 1)) != r).sum().item()))
-            # u16 wire: S as 2 bytes per key and a counts row (P + 1 words) per peer
-            rows = (g - 1) * ((1 << st["local"]["radix_bits"]) + 1) * 8
+            # u16 wire: S as 2 bytes per key and a counts row (2 P + 1 words) per peer
+            rows = (g - 1) * (2 * (1 << st["local"]["radix_bits"]) + 1) * 8  # counts, starts, largest key
             assert st["sent_bytes"] == (4 * out[0] + 2 * out[1] + rows if st["elem_bytes"] == 2
                                         else 4 * (out[0] + out[1]))
             assert st["recv_r_max"] == nR // g and st["recv_s_max"] == nS // g
