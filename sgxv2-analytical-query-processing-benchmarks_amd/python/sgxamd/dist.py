@@ -251,6 +251,10 @@ def _cxx_comm(group) -> int:
     the join's first collective)."""
     key = id(group)
     if key not in _comms:
+        if os.environ.get("SGXAMD_RCCL_LIBRARY"):  # tests: the RCCL test double (tests/rccl_double)
+            from . import multi_set_rccl_library
+
+            multi_set_rccl_library(os.environ["SGXAMD_RCCL_LIBRARY"])
         rank = dist.get_rank(group)
         obj = [None]
         if rank == 0:
@@ -277,8 +281,12 @@ def _cxx_comm(group) -> int:
 
 
 def _use_cxx(R: torch.Tensor, group, partition_fn, local_join_fn) -> bool:
+    """The C++ RCCL path: a torch nccl (RCCL) group, or any torch backend with
+    SGXAMD_DIST_IMPL=cxx-any -- the test rehearsal of rank processes sharing one GPU on
+    the RCCL test double (gloo carries only the unique id's broadcast there)."""
+    impl = os.environ.get("SGXAMD_DIST_IMPL", "cxx")
     return (R.is_cuda and partition_fn is None and local_join_fn is None
-            and dist.get_backend(group) == "nccl" and os.environ.get("SGXAMD_DIST_IMPL", "cxx") == "cxx")
+            and ((impl == "cxx" and dist.get_backend(group) == "nccl") or impl == "cxx-any"))
 
 
 def _sharded_cxx(R: torch.Tensor, S: torch.Tensor, group, algorithm: str, chunks: int) -> ShardedJoinResult:
@@ -307,6 +315,11 @@ def sharded_rho_join(R: torch.Tensor, S: torch.Tensor, *, group=None, partition_
     Collective: every rank of `group` must call it (with the same `chunks`).  Returns
     the global match count on every rank.
     """
+    # (decided before partition_fn takes its default: an injected partition or local join
+    # selects the torch.distributed path; round 6 found this test after the default, so the
+    # C++ RCCL path was never taken -- tests/test_rccl_double_gpu.py::
+    # test_bench_rank_processes_on_double runs bench.py's ranks through it now)
+    cxx = _use_cxx(R, group, partition_fn, local_join_fn) if dist.is_initialized() else False
     partition_fn = partition_fn or _default_partition
     local = _InjectedLocalJoin(local_join_fn) if local_join_fn is not None else _LibraryLocalJoin(algorithm)
     world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -321,7 +334,7 @@ def sharded_rho_join(R: torch.Tensor, S: torch.Tensor, *, group=None, partition_
         ms["local_join"] = (time.perf_counter() - t0) * 1e3
         return ShardedJoinResult(int(m), int(m), R.numel(), S.numel(), ms, st)
 
-    if _use_cxx(R, group, partition_fn, local_join_fn):
+    if cxx:
         # RCCL through the C++ library; torch's stream is synchronised first (the library
         # runs on its own streams unless mi355_set_stream named torch's).  A failure
         # raises: the library fails every rank at the same collective step, so no rank

@@ -33,9 +33,24 @@
 // rank that never posts its part cannot hang a test.  ncclCommAbort releases every
 // waiter of the communicator's world at once.
 //
+// Ranks as PROCESSES (RCCL_DOUBLE_XPROC=1; round 6): the one-process-per-GPU path of a
+// torchrun job -- mi355_multi_comm_init with rank 0's unique id broadcast by the caller,
+// the split count communicator, mi355_rho_join_sharded -- run by rank processes that
+// share this box's one GPU.  A communicator is a POSIX shared-memory block named after
+// the unique id (created by the first rank to arrive, unlinked once every rank mapped
+// it): a barrier, per (src, dst) channel a ring of posted sends and their acks, and a
+// host slot per rank for the collectives.  ncclSend publishes the IPC handle of its
+// buffer's allocation (hipIpcGetMemHandle) and offset once the send's data is ready on
+// its stream (the host waits for it); the receiver maps the allocation
+// (hipIpcOpenMemHandle, cached), copies with k_copy on its stream, waits for the copy and
+// acks; the sender returns from ncclGroupEnd once every send is acked.  All-gather and
+// all-reduce go through the host slots.  Every wait is bounded (rccl_double_set_timeout_ms).
+//
 // Test infrastructure only: the product loads librccl.so.1; nothing here is on the path.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <fcntl.h>
+#include <sys/mman.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -50,6 +65,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace {
@@ -151,9 +167,49 @@ bool World::barrier(std::unique_lock<std::mutex> &lk) {
 
 }  // namespace
 
+// ---------------------------------------------------------------- ranks as processes
+namespace {
+
+constexpr int kXMax = 16;          // ranks
+constexpr int kXRing = 64;         // posted sends in flight per channel
+constexpr size_t kXSlot = 1 << 16; // host bytes per rank for a collective
+
+struct XPost {
+    std::atomic<uint64_t> seq;  // the post's sequence number once published (0: empty)
+    std::atomic<uint64_t> ack;  // the receiver's ack of that sequence number
+    hipIpcMemHandle_t mem;
+    uint64_t off, bytes;
+    int failed;
+};
+
+struct XShm {
+    std::atomic<int> joined, n, aborted;
+    std::atomic<uint64_t> bar_count, bar_gen;
+    XPost chan[kXMax][kXMax][kXRing];  // [src][dst]
+    int color[kXMax], key[kXMax];
+    uint64_t slot_bytes[kXMax];
+    uint8_t slot[kXMax][kXSlot];
+};
+
+bool xproc() {
+    static const bool on = [] {
+        const char *e = std::getenv("RCCL_DOUBLE_XPROC");
+        return e && std::atoi(e) == 1;
+    }();
+    return on;
+}
+
+}  // namespace
+
 struct ncclComm {
     std::shared_ptr<World> w;
     int rank = 0, dev = 0;
+    // ranks as processes
+    XShm *x = nullptr;
+    int n = 0;
+    std::string name;
+    uint64_t sseq[kXMax] = {}, rseq[kXMax] = {};  // last send / receive sequence per peer
+    int splits = 0;
 };
 
 namespace {
@@ -200,7 +256,10 @@ size_t type_size(ncclDataType_t t) {
     }
 }
 
+ncclResult_t xrun_group(std::vector<Op> &ops);
+
 ncclResult_t run_group(std::vector<Op> &ops) {
+    if (!ops.empty() && ops[0].comm->x) return xrun_group(ops);
     // phase 1: publish every send
     std::vector<std::shared_ptr<SendPost>> mine;
     for (const Op &o : ops) {
@@ -264,7 +323,7 @@ ncclResult_t run_group(std::vector<Op> &ops) {
 
 ncclResult_t enqueue(bool send, void *buf, size_t count, ncclDataType_t t, int peer, ncclComm_t comm,
                      hipStream_t s) {
-    if (!comm || peer < 0 || peer >= comm->w->n || !type_size(t)) return ncclInvalidArgument;
+    if (!comm || peer < 0 || peer >= (comm->x ? comm->n : comm->w->n) || !type_size(t)) return ncclInvalidArgument;
     if (fail_now(comm->rank)) return ncclSystemError;
     t_ops.push_back(Op{send, comm, peer, buf, count * type_size(t), s});
     if (t_group > 0) return ncclSuccess;
@@ -282,6 +341,171 @@ void reduce_into(std::vector<uint64_t> &acc, const std::vector<uint64_t> &x, siz
         else if (op == ncclMax) a[i] = std::max(a[i], b[i]);
         else a[i] = std::min(a[i], b[i]);
     }
+}
+
+// ---- ranks as processes (XShm communicators)
+
+template <typename Pred>
+bool xwait(XShm *x, Pred p) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0;; ++i) {
+        if (p()) return true;
+        if (x->aborted.load()) return false;
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(g_timeout_ms.load())) {
+            x->aborted.store(1);  // a peer never came: the communicator is unusable
+            return false;
+        }
+        if (i > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+}
+
+bool xbarrier(ncclComm *c) {
+    XShm *x = c->x;
+    const uint64_t g = x->bar_gen.load();
+    if (x->bar_count.fetch_add(1) + 1 == (uint64_t)c->n) {
+        x->bar_count.store(0);
+        x->bar_gen.fetch_add(1);
+        return true;
+    }
+    return xwait(x, [&] { return x->bar_gen.load() != g; });
+}
+
+// map (creating if first) the block `name`, join it as `rank` of n, wait for every rank;
+// rank 0 unlinks the name once all have mapped it
+ncclResult_t xjoin(const std::string &name, int n, int rank, ncclComm *c) {
+    if (n > kXMax) return ncclInvalidArgument;
+    const int fd = shm_open(name.c_str(), O_CREAT | O_RDWR, 0600);
+    if (fd < 0) return ncclSystemError;
+    if (ftruncate(fd, sizeof(XShm)) != 0) {
+        close(fd);
+        return ncclSystemError;
+    }
+    void *m = mmap(nullptr, sizeof(XShm), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (m == MAP_FAILED) return ncclSystemError;
+    XShm *x = static_cast<XShm *>(m);
+    int expect = 0;
+    if (!x->n.compare_exchange_strong(expect, n) && expect != n) {
+        munmap(m, sizeof(XShm));
+        return ncclInvalidArgument;
+    }
+    c->x = x;
+    c->n = n;
+    c->rank = rank;
+    c->name = name;
+    x->joined.fetch_add(1);
+    const bool ok = xwait(x, [&] { return x->joined.load() >= n; }) && xbarrier(c);
+    if (rank == 0) shm_unlink(name.c_str());
+    if (!ok) {
+        munmap(m, sizeof(XShm));
+        c->x = nullptr;
+        return ncclSystemError;
+    }
+    return ncclSuccess;
+}
+
+std::string xname(const ncclUniqueId &id) {
+    static const char *hex = "0123456789abcdef";
+    std::string s = "/rccld_";
+    for (int i = 0; i < 24; ++i) {
+        const uint8_t b = static_cast<uint8_t>(id.internal[i]);
+        s += hex[b >> 4];
+        s += hex[b & 15];
+    }
+    return s;
+}
+
+// a peer's allocation mapped into this process (never unmapped: test double)
+std::mutex g_ipc_mu;
+std::map<std::string, char *> g_ipc;
+char *xopen(const hipIpcMemHandle_t &h) {
+    const std::string k(reinterpret_cast<const char *>(&h), sizeof(h));
+    std::lock_guard<std::mutex> lk(g_ipc_mu);
+    auto it = g_ipc.find(k);
+    if (it != g_ipc.end()) return it->second;
+    void *p = nullptr;
+    if (hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) return nullptr;
+    g_ipc[k] = static_cast<char *>(p);
+    return static_cast<char *>(p);
+}
+
+ncclResult_t xrun_group(std::vector<Op> &ops) {
+    ncclResult_t rc = ncclSuccess;
+    struct Mine {
+        XShm *x;
+        XPost *p;
+        uint64_t seq;
+    };
+    std::vector<Mine> mine;
+    // phase 1: every send published once its data is ready on its stream
+    for (const Op &o : ops) {
+        if (!o.send) continue;
+        ncclComm *c = o.comm;
+        XShm *x = c->x;
+        hipIpcMemHandle_t h{};
+        uint64_t off = 0;
+        if (o.bytes) {
+            hipEvent_t e = nullptr;
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess || hipEventRecord(e, o.stream) != hipSuccess ||
+                hipEventSynchronize(e) != hipSuccess)
+                return ncclUnhandledCudaError;
+            (void)hipEventDestroy(e);
+            void *base = nullptr;
+            size_t sz = 0;
+            if (hipMemGetAddressRange(&base, &sz, o.buf) != hipSuccess || hipIpcGetMemHandle(&h, base) != hipSuccess)
+                return ncclUnhandledCudaError;
+            off = static_cast<uint64_t>(static_cast<char *>(o.buf) - static_cast<char *>(base));
+        }
+        const uint64_t seq = ++c->sseq[o.peer];
+        XPost &p = x->chan[c->rank][o.peer][seq % kXRing];
+        if (seq > (uint64_t)kXRing && !xwait(x, [&] { return p.ack.load() >= seq - kXRing; })) return ncclSystemError;
+        p.mem = h;
+        p.off = off;
+        p.bytes = o.bytes;
+        p.failed = 0;
+        p.seq.store(seq, std::memory_order_release);
+        mine.push_back({x, &p, seq});
+    }
+    // phase 2: every receive takes the peer's next post on the channel, copies, acks
+    for (const Op &o : ops) {
+        if (o.send) continue;
+        ncclComm *c = o.comm;
+        XShm *x = c->x;
+        const uint64_t seq = ++c->rseq[o.peer];
+        XPost &p = x->chan[o.peer][c->rank][seq % kXRing];
+        if (!xwait(x, [&] { return p.seq.load(std::memory_order_acquire) == seq; })) return ncclSystemError;
+        const bool ok = p.bytes == o.bytes;
+        if (!ok) rc = ncclInvalidUsage;
+        if (ok && o.bytes) {
+            char *src = xopen(p.mem);
+            if (!src || copy_d2d(o.buf, src + p.off, o.bytes, o.stream) != hipSuccess ||
+                hipStreamSynchronize(o.stream) != hipSuccess)
+                return ncclUnhandledCudaError;
+        }
+        p.failed = ok ? 0 : 1;
+        p.ack.store(seq, std::memory_order_release);
+    }
+    // phase 3: the sender returns once every send was copied (its buffer is free again)
+    for (const Mine &m : mine) {
+        if (!xwait(m.x, [&] { return m.p->ack.load(std::memory_order_acquire) >= m.seq; })) return ncclSystemError;
+        if (m.p->failed) rc = ncclInvalidUsage;
+    }
+    return rc;
+}
+
+// one rank's bytes into its host slot, a barrier, then f(slots), a barrier
+template <typename F>
+ncclResult_t xcollective(ncclComm *c, const void *send, size_t bytes, hipStream_t s, F f) {
+    XShm *x = c->x;
+    if (bytes > kXSlot) return ncclInvalidArgument;
+    if (hipMemcpyAsync(x->slot[c->rank], send, bytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return ncclUnhandledCudaError;
+    x->slot_bytes[c->rank] = bytes;
+    if (!xbarrier(c)) return ncclSystemError;
+    const ncclResult_t r = f();
+    if (!xbarrier(c)) return ncclSystemError;
+    return r;
 }
 
 }  // namespace
@@ -318,6 +542,17 @@ ncclResult_t ncclGetUniqueId(ncclUniqueId *id) {
 
 ncclResult_t ncclCommInitRank(ncclComm_t *comm, int nranks, ncclUniqueId id, int rank) {
     if (!comm || nranks < 1 || rank < 0 || rank >= nranks) return ncclInvalidArgument;
+    if (xproc()) {
+        auto *c = new ncclComm;
+        const ncclResult_t r = xjoin(xname(id), nranks, rank, c);
+        if (r != ncclSuccess) {
+            delete c;
+            return r;
+        }
+        (void)hipGetDevice(&c->dev);
+        *comm = c;
+        return ncclSuccess;
+    }
     const std::string key(id.internal, sizeof(id.internal));
     std::shared_ptr<World> w;
     {
@@ -358,6 +593,33 @@ ncclResult_t ncclCommInitAll(ncclComm_t *comms, int ndev, const int *devlist) {
 ncclResult_t ncclCommSplit(ncclComm_t comm, int color, int key, ncclComm_t *newcomm, ncclConfig_t *) {
     if (!comm || !newcomm) return ncclInvalidArgument;
     if (fail_now(comm->rank)) return ncclSystemError;
+    if (comm->x) {
+        XShm *x = comm->x;
+        x->color[comm->rank] = color;
+        x->key[comm->rank] = key;
+        if (!xbarrier(comm)) return ncclSystemError;
+        std::vector<std::pair<int, int>> members;
+        for (int r = 0; r < comm->n; ++r)
+            if (x->color[r] == color) members.push_back({x->key[r], r});
+        std::sort(members.begin(), members.end());
+        int newrank = 0;
+        while (members[newrank].second != comm->rank) ++newrank;
+        const std::string name = comm->name + "_s" + std::to_string(comm->splits++) + "c" + std::to_string(color);
+        if (!xbarrier(comm)) return ncclSystemError;  // (colors read before any rank's next split)
+        if (color == NCCL_SPLIT_NOCOLOR) {
+            *newcomm = nullptr;
+            return ncclSuccess;
+        }
+        auto *c = new ncclComm;
+        const ncclResult_t r = xjoin(name, (int)members.size(), newrank, c);
+        if (r != ncclSuccess) {
+            delete c;
+            return r;
+        }
+        c->dev = comm->dev;
+        *newcomm = c;
+        return ncclSuccess;
+    }
     World &w = *comm->w;
     std::unique_lock<std::mutex> lk(w.mu);
     w.slots[comm->rank].color = color;
@@ -387,6 +649,7 @@ ncclResult_t ncclCommSplit(ncclComm_t comm, int color, int key, ncclComm_t *newc
 }
 
 ncclResult_t ncclCommDestroy(ncclComm_t comm) {
+    if (comm && comm->x) munmap(comm->x, sizeof(XShm));
     delete comm;
     return ncclSuccess;
 }
@@ -395,6 +658,10 @@ ncclResult_t ncclCommDestroy(ncclComm_t comm) {
 // waiters this abort releases); a few bytes per aborted communicator are leaked.
 ncclResult_t ncclCommAbort(ncclComm_t comm) {
     if (!comm) return ncclSuccess;
+    if (comm->x) {
+        comm->x->aborted.store(1);
+        return ncclSuccess;
+    }
     std::lock_guard<std::mutex> lk(comm->w->mu);
     comm->w->aborted = true;
     comm->w->cv.notify_all();
@@ -427,6 +694,15 @@ ncclResult_t ncclAllGather(const void *send, void *recv, size_t count, ncclDataT
     const size_t bytes = count * type_size(t);
     if (!comm || !bytes) return ncclInvalidArgument;
     if (fail_now(comm->rank)) return ncclSystemError;
+    if (comm->x) {
+        return xcollective(comm, send, bytes, s, [&]() -> ncclResult_t {
+            for (int q = 0; q < comm->n; ++q)
+                if (hipMemcpyAsync(static_cast<char *>(recv) + q * bytes, comm->x->slot[q], bytes,
+                                   hipMemcpyHostToDevice, s) != hipSuccess)
+                    return ncclUnhandledCudaError;
+            return hipStreamSynchronize(s) == hipSuccess ? ncclSuccess : ncclUnhandledCudaError;
+        });
+    }
     World &w = *comm->w;
     const int r = comm->rank;
     hipEvent_t ready = nullptr, done = nullptr;
@@ -459,6 +735,27 @@ ncclResult_t ncclAllReduce(const void *send, void *recv, size_t count, ncclDataT
         (op != ncclSum && op != ncclMax && op != ncclMin))
         return ncclInvalidArgument;
     if (fail_now(comm->rank)) return ncclSystemError;
+    if (comm->x) {
+        return xcollective(comm, send, count * es, s, [&]() -> ncclResult_t {
+            const size_t words = (count * es + 7) / 8;
+            std::vector<uint64_t> acc(words), x(words);
+            std::memcpy(acc.data(), comm->x->slot[0], count * es);
+            for (int q = 1; q < comm->n; ++q) {
+                std::memcpy(x.data(), comm->x->slot[q], count * es);
+                switch (t) {
+                    case ncclInt32: reduce_into<int32_t>(acc, x, count, op); break;
+                    case ncclUint32: reduce_into<uint32_t>(acc, x, count, op); break;
+                    case ncclInt64: reduce_into<int64_t>(acc, x, count, op); break;
+                    case ncclUint64: reduce_into<uint64_t>(acc, x, count, op); break;
+                    default: reduce_into<double>(acc, x, count, op); break;
+                }
+            }
+            if (hipMemcpyAsync(recv, acc.data(), count * es, hipMemcpyHostToDevice, s) != hipSuccess ||
+                hipStreamSynchronize(s) != hipSuccess)
+                return ncclUnhandledCudaError;
+            return ncclSuccess;
+        });
+    }
     World &w = *comm->w;
     const int r = comm->rank;
     std::vector<uint64_t> mine((count * es + 7) / 8);
