@@ -45,10 +45,25 @@ void DeviceBuffer::release() {
     bytes = 0;
 }
 
+// The per-kernel timing events skip the system-scope release fence an event performs by
+// default (hipEventDisableSystemFence): they only time kernels of one stream, whose
+// results the next kernel sees through the kernel boundary's own device-scope release.
+// With the fence, every event between two kernels wrote the L2's dirty lines back to
+// memory first: 5.5-6.3 us between the kernels of a join step at each of its 12 events
+// (r06l kernel trace), about 70 us of a 2.6-ms step.  SGXAMD_TIMER_FENCE=1 keeps the
+// fence (development A/B switch, read once).
+static unsigned timer_event_flags() {
+    static const unsigned f = [] {
+        const char *e = std::getenv("SGXAMD_TIMER_FENCE");
+        return (e && std::atoi(e) == 1) ? (unsigned)hipEventDefault : (unsigned)hipEventDisableSystemFence;
+    }();
+    return f;
+}
+
 hipEvent_t Timer::get_event() {
     if (used_ == pool_.size()) {
         hipEvent_t ev = nullptr;
-        if (hipEventCreate(&ev) != hipSuccess) return nullptr;
+        if (hipEventCreateWithFlags(&ev, timer_event_flags()) != hipSuccess) return nullptr;
         pool_.push_back(ev);
     }
     return pool_[used_++];
