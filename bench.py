@@ -190,7 +190,8 @@ LAYOUTS = {
     2: "pooled pass 1; a counting join moves 4-byte keys after reading the 8-byte input tuples "
        "(the payloads are never read by the count; SGXAMD_KEYS=0 moves whole tuples)",
     3: "pooled pass 1 of 4-byte keys with per-chain pass-2 digit histograms counted in LDS (no digit side "
-       "stream; chain-aligned pass-2 segments; SGXAMD_CHAIN_HIST=0 keeps the side stream)",
+       "stream; the pass-2 histogram sums whole chains' histograms and counts the cut chains' keys; "
+       "SGXAMD_CHAIN_HIST=0 keeps the side stream)",
     4: "pooled pass 1 of a narrow plan writing the keys' 16-bit residuals and their pass-2 digit bytes (a narrow "
        "pool, 11 B per tuple; repeated as 4-byte keys when a residual does not fit); pass 2 places each segment "
        "in LDS (opt-in: SGXAMD_NARROW_POOL=1; measured equal to layout 2, r05j)",
@@ -291,7 +292,9 @@ def algorithmic_bytes(kernel: str, nR: int, nS: int, passes: int = 2, pass2_bits
     """Bytes a kernel must move per launch (DESIGN.md 'Kernels and their rooflines').
 
     Two-pass plans: the pass-1 scatter also writes one pass-2 digit byte per tuple (the
-    digit side stream) and the pass-2 histogram reads those bytes, not the tuples.
+    digit side stream) and the pass-2 histogram reads those bytes, not the tuples; with
+    chain histograms (layout 3, the default for 7 + 6/7-bit key plans) pass 1 writes a
+    histogram per chain instead and the pass-2 histogram reads those.
     elem: bytes per partitioned element after the input read — 8 (row_t tuples) or 4
     (counting joins move keys only: the pass-1 scatter reads 8-byte tuples and
     writes 4-byte keys, pass 2 and the build/probe read and write keys).
@@ -307,6 +310,14 @@ def algorithmic_bytes(kernel: str, nR: int, nS: int, passes: int = 2, pass2_bits
     side = (passes == 2 and pass2_bits <= 8 and os.environ.get("SGXAMD_DIGIT_SIDE", "1") != "0" and layout != 3)
     if kernel.endswith("pass2_hist") and side:
         return n              # one digit byte per tuple
+    if layout == 3 and (kernel.endswith("pass2_hist") or kernel.endswith("pass1_scatter")):
+        # chain histograms: u32 [2^7 pass-1 digits][pass-1 segments][2^pass2_bits], written by
+        # pass 1 and read by the pass-2 histogram (the cut chains' keys it also reads are
+        # not counted: the side stream's plan has no such reads)
+        segs = int(os.environ.get("SGXAMD_POOL_SEGS", "512"))
+        seg = max(-(-(-(-n // segs)) // 4096) * 4096, 4096)
+        chist = 4 * 128 * (-(-n // seg)) * (1 << pass2_bits)
+        return chist if kernel.endswith("pass2_hist") else (8 + elem) * n + chist
     if kernel.endswith("_hist"):
         return 8 * n          # read every tuple once (key only used, AoS line read)
     if kernel.endswith("pass1_scatter"):

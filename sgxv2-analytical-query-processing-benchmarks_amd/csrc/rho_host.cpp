@@ -163,11 +163,13 @@ inline bool keys_enabled() {
 }
 // Pooled key plans with a 7-bit pass 1 and a 6- or 7-bit pass 2 count every chain's
 // pass-2 digits in the pass-1 scatter (chain histograms, rho_internal.hpp
-// launch_scatter_pool): no digit side stream is written or read, and the pass-2
-// histogram pass becomes one scan over the chain histograms (launch_chain_scan).
-// Off by default: the chain-aligned pass-2 segments made k_sort_blk 0.05 ms slower per
-// relation than the histogram pass they replace saves (r04k).
-// SGXAMD_CHAIN_HIST=1 takes them (development A/B switch; results identical).
+// launch_scatter_pool): no digit side stream is written, and the pass-2 histogram sums
+// the chain histograms of a segment's whole chains and counts only its cut chains' keys
+// (launch_hist_chain).  Round 6: 2.50-2.51 ms per step vs 2.60-2.62 with the side stream
+// (pass 1 0.72 vs 0.745 ms, the pass-2 histogram 0.035 vs 0.071 ms per relation;
+// profiles/r06n_chain_hist_ab.log).  SGXAMD_CHAIN_HIST=0 keeps the side stream
+// (development A/B switch; results identical); the narrow pool (SGXAMD_NARROW_POOL=1)
+// writes the side stream and takes no chain histograms.
 // Narrow key partitions (counting RHO with the 16,384-key table over key partitions):
 // pass 1 takes the largest key, and when the residuals above the radix bits fit 16 bits, pass 2
 // writes them as u16 and the build/probe reads 2 instead of 4 bytes per key
@@ -194,19 +196,9 @@ inline bool narrow_pool_enabled() {
 inline bool chain_enabled() {
     static const bool on = [] {
         const char *e = std::getenv("SGXAMD_CHAIN_HIST");
-        return e && std::atoi(e) == 1;
+        return !(e && std::atoi(e) == 0);
     }();
-    return on;
-}
-// Slot targets of the chain-aligned pass-2 segments (launch_chain_scan): 1 = kPass2Ents
-// less two mean chains, 2 = less the region's longest chain.  SGXAMD_CHAIN_SLOTS (A/B).
-inline uint32_t chain_slot_mode() {
-    static const uint32_t m = [] {
-        const char *e = std::getenv("SGXAMD_CHAIN_SLOTS");
-        const int v = e ? std::atoi(e) : 2;
-        return (uint32_t)(v == 1 ? 1 : 2);
-    }();
-    return m;
+    return on && !narrow_pool_enabled();
 }
 constexpr uint32_t kPoolSegs = 512;  // two 512-thread workgroups per CU: one wave of workgroups
 inline uint32_t pool_segs() {
@@ -240,7 +232,7 @@ struct RelPlan {
     // scratch offsets (pooled: hist1 holds the chain records, tot1 their column totals)
     size_t hist1, tot1, start1, cnt1, segbase2, hist2, pstart, pcnt;
     size_t binfo, used, lbase, lcount, list;
-    size_t chist, seglb, segle, segc0;  // chain histograms [F1][nseg1][F2], pass-2 segment ranges
+    size_t chist;  // chain histograms [F1][nseg1][F2]
     size_t kmax;   // pooled keys: the segments' largest keys, then the relation's ([nseg1])
     bool narrow;   // pass 2 writes u16 residuals when the largest key allows (plan_join)
     bool narrow16; // pass 1 writes a narrow pool first (u16 residuals, the 4-byte pool repeated if a residual does not fit)
@@ -305,7 +297,7 @@ int partition_relation_pooled(Context *ctx, hipStream_t s, Timer &tm, const std:
         };
         const auto layout = [&](const PoolOut &p) -> int {
             RHO_HIP(launch_pool_layout(p.cnt, rp.nseg1, pol.b1, A.at<uint64_t>(rp.tot1), start1, cnt1, lbase, lcount,
-                                       segbase2, s, rp.chain ? chain_slot_mode() : 0u, p.kmax, p.guard,
+                                       segbase2, s, p.kmax, p.guard,
                                        p.guard_shift));
             RHO_HIP(launch_block_list(p, lbase, list, pol.b1, s));
             return MI355_OK;
@@ -344,30 +336,13 @@ int partition_relation_pooled(Context *ctx, hipStream_t s, Timer &tm, const std:
     uint64_t *pc = A.at<uint64_t>(rp.pcnt);
     const SegMap m2{lbase, lcount, segbase2, F1, kPass2Ents, rp.n};
     const uint32_t *narrow = rp.narrow ? A.at<uint32_t>(rp.kmax) + rp.nseg1 : nullptr;
-    if (rp.chain) {
-        // the chain histograms (recounted where a count may have wrapped) give the
-        // chain-aligned pass-2 segments, their cursors and the partition table
-        uint32_t *seglb = A.at<uint32_t>(rp.seglb), *segle = A.at<uint32_t>(rp.segle);
-        tm.mark((t + "pass2_chain").c_str());
-        RHO_HIP(launch_chain_fix(A.at<uint64_t>(rp.hist1), A.at<uint64_t>(rp.tot1), rp.nseg1, pol.b1, pol.b2, lbase,
-                                 list, reinterpret_cast<const uint32_t *>(t1), key_shift + pol.b1,
-                                 A.at<uint32_t>(rp.chist), s));
-        RHO_HIP(launch_chain_scan(A.at<uint64_t>(rp.hist1), rp.nseg1, chain_slot_mode(), A.at<uint32_t>(rp.chist),
-                                  pol.b1, pol.b2,
-                                  start1, lbase, lcount, segbase2, hist2, seglb, segle, A.at<uint32_t>(rp.segc0), ps,
-                                  pc, s));
-        SegMap mc = m2;
-        mc.seg_lb = seglb;
-        mc.seg_le = segle;
-        tm.mark((t + "pass2_scatter").c_str());
-        RHO_HIP(launch_scatter_blk(t1, list, t2, 4u, mc, rp.grid2, key_shift + pol.b1, pol.b2, hist2, s, narrow));
-        *final_rel = t2;
-        *pstart = ps;
-        *pcnt = pc;
-        return MI355_OK;
-    }
     tm.mark((t + "pass2_hist").c_str());
-    RHO_HIP(launch_hist_side_blk(side, list, m2, rp.grid2, pol.b2, hist2, s));
+    if (rp.chain)  // from the chain histograms pass 1 stored (and the cut chains' keys)
+        RHO_HIP(launch_hist_chain(A.at<uint64_t>(rp.hist1), A.at<uint64_t>(rp.tot1), rp.nseg1,
+                                  A.at<uint32_t>(rp.chist), list, reinterpret_cast<const uint32_t *>(t1), m2,
+                                  rp.grid2, key_shift + pol.b1, pol.b2, hist2, s));
+    else
+        RHO_HIP(launch_hist_side_blk(side, list, m2, rp.grid2, pol.b2, hist2, s));
     tm.mark((t + "pass2_scan").c_str());
     RHO_HIP(launch_scan_regions(hist2, segbase2, start1, F1, pol.b2, ps, pc, s, rp.pad_parts));
     tm.mark((t + "pass2_scatter").c_str());
@@ -524,14 +499,13 @@ void plan_relation(Arena &A, RelPlan &rp, uint64_t n, const Policy &pol, int poo
         rp.keys = pool == kPoolKeys;
         // chain histograms: 32-bit list positions and a u32 segment slot table
         rp.chain = rp.keys && chain_enabled() && sort2_enabled() && chain_hist_supported(pol.b1, pol.b2) &&
-                   max_blocks < (1ull << 31);
+                   nseg <= kHistChainMaxSegs;
         rp.seg1 = seg;
         rp.nseg1 = nseg;
         rp.pool_blocks = (uint32_t)pb;
         rp.t1_tuples = (uint64_t)nseg * pb * kBlk;
-        // pass-2 segments: kPass2Ents blocks, or chain-aligned slots of at least kPass2Ents / 2
-        // blocks (chain_slot_target), at most one partial slot per region either way
-        rp.grid2 = (uint32_t)(max_blocks / (rp.chain ? kPass2Ents / 2 : kPass2Ents)) + F1 + 1;
+        // pass-2 segments: kPass2Ents blocks, at most one partial segment per region
+        rp.grid2 = (uint32_t)(max_blocks / kPass2Ents) + F1 + 1;
     }
     // (+ 1: a small join's histogram workgroups write two offsets per 2-tile segment)
     rp.hist1 = A.reserve(sizeof(uint64_t) * (size_t)F1 * (std::max<uint32_t>(rp.nseg1, 1) + 1));
@@ -554,9 +528,6 @@ void plan_relation(Arena &A, RelPlan &rp, uint64_t n, const Policy &pol, int poo
     }
     if (rp.chain) {
         rp.chist = A.reserve(sizeof(uint32_t) * (size_t)F1 * rp.nseg1 * F2);
-        rp.seglb = A.reserve(sizeof(uint32_t) * (size_t)rp.grid2);
-        rp.segle = A.reserve(sizeof(uint32_t) * (size_t)rp.grid2);
-        rp.segc0 = A.reserve(sizeof(uint32_t) * (size_t)rp.grid2);
     }
 }
 
@@ -1316,7 +1287,6 @@ int wire_partition(Context *ctx, hipStream_t s, const uint32_t *keys, int G, int
         rp.narrow = true;  // wire16_plan: every residual fits 16 bits
         rp.narrow16 = false;
         rp.pad_parts = true;  // every partition on 16 bytes: the receiver reads them in place
-        rp.chain = false;     // (the padded partition starts come from k_scan_regions: the side stream's plan)
         rp.in_size = sizeof(uint32_t);
         const row_t *f = nullptr;
         const uint64_t *pst = nullptr, *pcn = nullptr;

@@ -20,8 +20,6 @@ constexpr int kTile = kScatterThreads * kScatterItems;  // tuples per scatter ti
 // Which contiguous slice of the input a partition workgroup owns.  Regions are
 // the bins of the previous pass (or the whole relation); each region is cut into
 // segments of seg_size tuples, one workgroup per segment.
-// seg_lb / seg_le (chain-aligned block-list segments, launch_chain_scan): segment g is
-// [seg_lb[g], seg_le[g]) of the list, for g < seg_base[nreg]; empty segments are holes.
 struct SegMap {
     const uint64_t *reg_start;  // nullptr => one region [0, single_n)
     const uint64_t *reg_count;
@@ -29,8 +27,6 @@ struct SegMap {
     uint32_t nreg;
     uint64_t seg_size;
     uint64_t single_n;
-    const uint32_t *seg_lb = nullptr;
-    const uint32_t *seg_le = nullptr;
 };
 
 // Histogram layout selector: digit-major [d][g] (single region: column scans)
@@ -181,30 +177,9 @@ hipError_t launch_scatter_pool(const void *in, uint32_t in_size, void *out, uint
 bool chain_hist_supported(uint32_t bits1, uint32_t bits2);
 // Whether pass 2 of key partitions is the LDS sort k_sort_blk (SGXAMD_SORT2).
 bool sort2_enabled();
-// Recount the chain histograms of chains with more than 65,535 elements (their u16 counts
-// may have wrapped) from their blocks: cnt / tot the column-scanned chain records and
-// their totals, keys the pass-1 output, shift2 the pass-2 digit's shift.
-hipError_t launch_chain_fix(const uint64_t *cnt, const uint64_t *tot, uint32_t nseg, uint32_t bits1, uint32_t bits2,
-                            const uint64_t *lbase, const uint64_t *list, const uint32_t *keys, uint32_t shift2,
-                            uint32_t *chain, hipStream_t s);
-// Chain-histogram plans: one workgroup per region from the column-scanned chain records
-// (po.cnt) and the chain histograms: the pass-2 segments, cut at chain boundaries (slot k
-// of region d holds the chains whose first block lies in [T*k, T*(k+1)) of d's list, T a
-// little below kPass2Ents (mode 1: less two mean chains, rho_kernels.hip
-// chain_slot_target; mode 2: less the region's longest chain), so a segment is T blocks
-// + the rest of one chain; empty slots are holes), as list
-// ranges seg_lb / seg_le; the pass-2 cursors [slot][F2] (the histogram + scan of
-// launch_hist_side_blk + launch_scan_regions, without reading the elements) and the
-// partition table part_start / part_count [d][F2].  seg_c0: scratch, one u32 per slot.
-hipError_t launch_chain_scan(const uint64_t *cnt, uint32_t nseg, uint32_t mode, const uint32_t *chain, uint32_t bits1,
-                             uint32_t bits2, const uint64_t *region_start, const uint64_t *lbase,
-                             const uint64_t *lcount, const uint32_t *seg_base, uint64_t *cursors, uint32_t *seg_lb,
-                             uint32_t *seg_le, uint32_t *seg_c0, uint64_t *part_start, uint64_t *part_count,
-                             hipStream_t s);
 // After launch_scan_single-style column scans of po.cnt (k_scan_cols, in place): region
 // tuple starts / counts (the pass-2 output layout), region block-list bases / lengths
 // and the pass-2 segment table (kPass2Ents blocks per segment).
-// chain_mode 1 / 2: the slots of chain-aligned segments (launch_chain_scan) instead.
 // kmax (nullable): the segments' largest keys (PoolOut::kmax), folded into kmax[nseg] —
 // the relation's largest key, which tells pass 2 and the build/probe whether the key
 // residuals above the radix bits fit 16 bits (narrow partitions, launch_scatter_blk).
@@ -212,7 +187,7 @@ hipError_t launch_chain_scan(const uint64_t *cnt, uint32_t nseg, uint32_t mode, 
 // bits (the 4-byte pool repeated after a narrow pool that stood, PoolOut::guard).
 hipError_t launch_pool_layout(uint64_t *cnt, uint32_t nseg, uint32_t bits, uint64_t *totals, uint64_t *start,
                               uint64_t *count, uint64_t *lbase, uint64_t *lcount, uint32_t *seg_base, hipStream_t s,
-                              uint32_t chain_mode = 0, uint32_t *kmax = nullptr, const uint32_t *guard = nullptr,
+                              uint32_t *kmax = nullptr, const uint32_t *guard = nullptr,
                               uint32_t gshift = 0);
 // The block list: region d's blocks at [lbase[d], lbase[d] + lcount[d]) as
 // physical block | fill << 32.
@@ -221,6 +196,15 @@ hipError_t launch_block_list(const PoolOut &po, const uint64_t *lbase, uint64_t 
 // reg_count = lcount, seg_size = kPass2Ents).
 hipError_t launch_hist_side_blk(const uint8_t *side, const uint64_t *list, const SegMap &m, uint32_t grid,
                                 uint32_t bits, uint64_t *hist, hipStream_t s);
+// The same histogram from the chain histograms (chain plans: no side stream): cnt / tot
+// the column-scanned chain records and their totals (launch_pool_layout), chain the chain
+// histograms u32 [d][g][F2] (launch_scatter_pool), keys the pass-1 output; the cut and
+// possibly wrapped chains' parts are counted from their keys (digit (key >> shift2) &
+// (F2 - 1)).  nseg <= kHistChainMaxSegs pass-1 segments.
+constexpr uint32_t kHistChainMaxSegs = 16384;
+hipError_t launch_hist_chain(const uint64_t *cnt, const uint64_t *tot, uint32_t nseg, const uint32_t *chain,
+                             const uint64_t *list, const uint32_t *keys, const SegMap &m, uint32_t grid,
+                             uint32_t shift2, uint32_t bits2, uint64_t *hist, hipStream_t s);
 // narrow (nullable; key partitions through k_sort_blk only): the relation's largest key
 // (launch_pool_layout).  When every key's residual above the radix bits (key >>
 // (shift + bits)) fits 16 bits, the partitions are written as those u16 residuals —

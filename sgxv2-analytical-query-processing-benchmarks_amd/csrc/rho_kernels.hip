@@ -44,13 +44,6 @@ __device__ __forceinline__ uint64_t uni_u64(uint64_t v) {
 // __syncthreads() (every thread of the block must call it).
 __device__ __forceinline__ bool seg_lookup(const SegMap &m, uint32_t g, uint32_t *lds_base, uint32_t &r,
                                            uint64_t &b, uint64_t &e) {
-    if (m.seg_lb != nullptr) {  // chain-aligned segments (launch_chain_scan): explicit ranges, holes empty
-        r = 0;
-        if (g >= m.seg_base[m.nreg]) return false;
-        b = m.seg_lb[g];
-        e = m.seg_le[g];
-        return b < e;
-    }
     if (m.reg_start == nullptr) {
         r = 0;
         b = (uint64_t)g * m.seg_size;
@@ -495,197 +488,6 @@ hipError_t launch_scan_regions(uint64_t *hist, const uint32_t *seg_base, const u
     return hipGetLastError();
 }
 
-// Chain-aligned pass-2 segments (chain histograms): slot k of a region holds the chains
-// whose first block lies in [T*k, T*(k+1)) of its list, so a segment is T blocks plus the
-// part of its last chain past the boundary, less the part of its first chain before it:
-// shorter than T + L for chains of at most L blocks.  Slot mode 1: T = kPass2Ents less
-// two mean chains of the region (at least half of kPass2Ents); mode 2: T = kPass2Ents
-// less the region's longest chain (k_chain_scan), so that no segment passes kPass2Ents
-// blocks (k_sort_blk's four 64-block tiles; T = kPass2Ents made 4.25 per segment, a
-// fifth nearly empty tile).  The layout reserves slots for T = kPass2Ents / 2 in mode 2.
-__host__ __device__ __forceinline__ uint32_t chain_slot_target(uint64_t blocks, uint32_t nseg) {
-#ifdef SGXAMD_CHAIN_T_FIXED
-    (void)blocks, (void)nseg;
-    return kPass2Ents;
-#else
-    const uint64_t mean = nseg ? (blocks + nseg - 1) / nseg : 0;
-    return kPass2Ents - (uint32_t)min<uint64_t>(kPass2Ents / 2, 2 * mean);
-#endif
-}
-
-// Chain-histogram plans (launch_chain_scan): one workgroup of 1,024 threads per region r
-// (pass-1 digit).  cnt: the chain records [r][g] after the column scan (exclusive
-// prefixes blocks << 40 | elements of the chains before g); chain: u32 [r][g][F2].
-constexpr uint32_t kChainLds = 4096;  // chain starts / slot chains staged in LDS (more: read in place)
-__global__ __launch_bounds__(1024) void k_chain_scan(const uint64_t *__restrict__ cnt, uint32_t nseg, uint32_t mode,
-                                                     const uint32_t *__restrict__ chain, uint32_t F2,
-                                                     const uint64_t *__restrict__ region_start,
-                                                     const uint64_t *__restrict__ lbase,
-                                                     const uint64_t *__restrict__ lcount,
-                                                     const uint32_t *__restrict__ seg_base,
-                                                     uint64_t *__restrict__ cursors, uint32_t *__restrict__ seg_lb,
-                                                     uint32_t *__restrict__ seg_le, uint32_t *__restrict__ seg_c0,
-                                                     uint64_t *__restrict__ part_start,
-                                                     uint64_t *__restrict__ part_count) {
-    __shared__ uint64_t scratch[1024 / kWave + 1];
-    __shared__ uint64_t part[1024];  // [j][d]: group j's column sums, then their exclusive prefix inside d
-    __shared__ uint64_t pst[1024];   // partition starts of the region (d < F2)
-    __shared__ uint32_t cst[kChainLds];  // chain g's first block inside the region's list
-    __shared__ uint32_t sc0[kChainLds];  // slot k's first chain
-    const uint32_t r = blockIdx.x, tid = threadIdx.x;
-    const uint64_t *rec = cnt + (uint64_t)r * nseg;
-    const uint32_t *ch = chain + (uint64_t)r * nseg * F2;
-    const uint32_t s0 = seg_base[r], ns = seg_base[r + 1] - s0;
-    const uint64_t B = lcount[r], lb0 = lbase[r];
-    const bool lds_c = nseg <= kChainLds, lds_s = ns <= kChainLds;  // workgroup-uniform
-    uint64_t lmax = 0;  // the region's longest chain (blocks)
-    for (uint32_t g = tid; g < nseg; g += 1024) {
-        const uint32_t a = (uint32_t)(rec[g] >> 40);
-        const uint64_t b = g + 1 < nseg ? (rec[g + 1] >> 40) : B;
-        lmax = max(lmax, b - a);
-        if (lds_c) cst[g] = a;
-    }
-    uint32_t T = chain_slot_target(B, nseg);
-    if (mode == 2) {
-        lmax = block_max_u64(lmax, scratch);
-        T = (uint32_t)max<uint64_t>(kPass2Ents / 2, lmax < kPass2Ents ? kPass2Ents - lmax : 0);
-    }
-    __syncthreads();
-    const auto start_of = [&](uint32_t g) -> uint32_t { return lds_c ? cst[g] : (uint32_t)(rec[g] >> 40); };
-    const auto first_at = [&](uint64_t x) -> uint32_t {  // first chain whose blocks start at or after x
-        uint32_t lo = 0, hi = nseg;
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (start_of(mid) < x) lo = mid + 1; else hi = mid;
-        }
-        return lo;
-    };
-    for (uint32_t k = tid; k < ns; k += 1024) {
-        const uint32_t c0 = first_at((uint64_t)T * k), c1 = first_at((uint64_t)T * (k + 1));
-        seg_lb[s0 + k] = (uint32_t)(lb0 + (c0 < nseg ? start_of(c0) : B));
-        seg_le[s0 + k] = (uint32_t)(lb0 + (c1 < nseg ? start_of(c1) : B));
-        if (lds_s) sc0[k] = c0; else seg_c0[s0 + k] = c0;
-    }
-    // column sums of the chain histograms, nseg split among S = 1024 / F2 threads per digit
-    const uint32_t S = 1024 / F2, d = tid % F2, j = tid / F2;
-    const uint32_t per = (nseg + S - 1) / S, ga = min(nseg, j * per), gb = min(nseg, ga + per);
-    uint64_t sum = 0;
-#pragma unroll 8
-    for (uint32_t g = ga; g < gb; ++g) sum += ch[(uint64_t)g * F2 + d];
-    part[tid] = sum;
-    __syncthreads();
-    uint64_t total = 0;
-    if (j == 0)
-        for (uint32_t jj = 0; jj < S; ++jj) {
-            const uint64_t t = part[jj * F2 + d];
-            part[jj * F2 + d] = total;
-            total += t;
-        }
-    uint64_t tot;
-    const uint64_t ex = block_excl_scan_u64(j == 0 ? total : 0, scratch, &tot);  // digits are tids 0..F2-1
-    if (j == 0) {
-        const uint64_t st = region_start[r] + ex;
-        pst[d] = st;
-        part_start[(uint64_t)r * F2 + d] = st;
-        part_count[(uint64_t)r * F2 + d] = total;
-    }
-    __syncthreads();  // pst, part and the slot chains
-    // cursors: slot k starts at chain c0(k), so its cursor of digit d is the partition's
-    // start plus the counts of d in every chain before c0(k)
-    const auto c0_of = [&](uint32_t k) -> uint32_t { return lds_s ? sc0[k] : seg_c0[s0 + k]; };
-    uint64_t run = pst[d] + part[tid];
-    uint32_t lo = 0, hi = ns;  // first slot with c0 >= ga
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (c0_of(mid) < ga) lo = mid + 1; else hi = mid;
-    }
-    uint32_t k = lo;
-    for (uint32_t g = ga; g < gb; ++g) {
-        for (; k < ns && c0_of(k) == g; ++k) cursors[(uint64_t)(s0 + k) * F2 + d] = run;
-        run += ch[(uint64_t)g * F2 + d];
-    }
-}
-
-hipError_t launch_chain_scan(const uint64_t *cnt, uint32_t nseg, uint32_t mode, const uint32_t *chain, uint32_t bits1,
-                             uint32_t bits2, const uint64_t *region_start, const uint64_t *lbase,
-                             const uint64_t *lcount, const uint32_t *seg_base, uint64_t *cursors, uint32_t *seg_lb,
-                             uint32_t *seg_le, uint32_t *seg_c0, uint64_t *part_start, uint64_t *part_count,
-                             hipStream_t s) {
-    const uint32_t F2 = 1u << bits2;
-    if (F2 < 2 || F2 > 1024 || 1024 % F2) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_chain_scan, dim3(1u << bits1), dim3(1024), 0, s, cnt, nseg, mode, chain, F2, region_start, lbase,
-                       lcount, seg_base, cursors, seg_lb, seg_le, seg_c0, part_start, part_count);
-    return hipGetLastError();
-}
-
-// Chains whose u16 chain-histogram counts may have wrapped (more than 65,535 elements;
-// the chain records say so): recounted from their blocks.  One workgroup per pass-1
-// segment g, its chains in turn (a uniform test per chain; nothing to do for any chain
-// of fewer elements, i.e. every chain of unskewed data).  Four waves, four blocks per
-// wave and step, a 16-byte piece of a block per lane.
-__global__ __launch_bounds__(256) void k_chain_fix(const uint64_t *__restrict__ cnt, const uint64_t *__restrict__ tot,
-                                                   uint32_t nseg, uint32_t F1, uint32_t F2,
-                                                   const uint64_t *__restrict__ lbase,
-                                                   const uint64_t *__restrict__ list, const uint32_t *__restrict__ keys,
-                                                   uint32_t shift2, uint32_t *__restrict__ chain) {
-    __shared__ uint32_t h[kMaxF];
-    __shared__ uint64_t rng[kMaxF][2];  // chain d's records: its own and the next (its end)
-    __shared__ uint32_t big[kMaxF / 32];
-    constexpr uint64_t M40 = (1ull << 40) - 1;
-    constexpr int U = 4;
-    const uint32_t g = blockIdx.x, tid = threadIdx.x, lane = __lane_id(), wave = tid / kWave;
-    // which chains of segment g need a recount: every record read at once
-    for (uint32_t d = tid; d < kMaxF / 32; d += 256) big[d] = 0;
-    __syncthreads();
-    for (uint32_t d = tid; d < F1; d += 256) {
-        const uint64_t e0 = cnt[(uint64_t)d * nseg + g];
-        const uint64_t e1 = g + 1 < nseg ? cnt[(uint64_t)d * nseg + g + 1] : tot[d];
-        rng[d][0] = e0;
-        rng[d][1] = e1;
-        if ((e1 & M40) - (e0 & M40) > 65535) atomicOr(&big[d / 32], 1u << (d % 32));
-    }
-    __syncthreads();
-    for (uint32_t d = 0; d < F1; ++d) {
-        if (!((big[d / 32] >> (d % 32)) & 1u)) continue;  // workgroup-uniform
-        const uint64_t e0 = rng[d][0], e1 = rng[d][1];
-        for (uint32_t i = tid; i < F2; i += 256) h[i] = 0;
-        __syncthreads();
-        const uint64_t k0 = lbase[d] + (e0 >> 40), k1 = lbase[d] + (e1 >> 40);
-        for (uint64_t k = k0 + wave; k < k1; k += 4 * U) {
-            uint4 q[U];
-            uint32_t fill[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint64_t kk = k + 4 * u;
-                const uint64_t en = kk < k1 ? list[kk] : 0ull;
-                fill[u] = (uint32_t)(en >> 32);
-                q[u] = lane * 4 < fill[u] ? *reinterpret_cast<const uint4 *>(keys + (uint64_t)(uint32_t)en * kBlk + lane * 4)
-                                          : make_uint4(0, 0, 0, 0);
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint32_t w[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    if (lane * 4 + j < fill[u]) atomicAdd(&h[(w[j] >> shift2) & (F2 - 1)], 1u);
-            }
-        }
-        __syncthreads();
-        for (uint32_t i = tid; i < F2; i += 256) chain[((uint64_t)d * nseg + g) * F2 + i] = h[i];
-        __syncthreads();
-    }
-}
-
-hipError_t launch_chain_fix(const uint64_t *cnt, const uint64_t *tot, uint32_t nseg, uint32_t bits1, uint32_t bits2,
-                            const uint64_t *lbase, const uint64_t *list, const uint32_t *keys, uint32_t shift2,
-                            uint32_t *chain, hipStream_t s) {
-    if (nseg == 0) return hipSuccess;
-    if (bits2 > 9) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_chain_fix, dim3(nseg), dim3(256), 0, s, cnt, tot, nseg, 1u << bits1, 1u << bits2, lbase, list,
-                       keys, shift2, chain);
-    return hipGetLastError();
-}
-
 // --------------------------------------------------------------- scatter ---
 // Partition copy of one segment per workgroup (partition_copy, radix_join.cpp:659-697),
 // organised like the reference's software write-combining variant
@@ -757,9 +559,9 @@ struct ScatterLds {
 // digits, two u16 counts per LDS word, counted in phase C while the tile is in
 // registers (replacing the digit side stream and the pass-2 histogram pass over it),
 // stored as u32 [d][g][F2] at the segment's end.  A count wraps only in a chain of more
-// than 65,535 elements (a heavily skewed digit); launch_chain_fix recounts those chains
-// from their blocks (checking the chain records), so no flush sits in the scatter's
-// loop, which has no register to spare.
+// than 65,535 elements (a heavily skewed digit); the pass-2 histogram (k_hist_chain)
+// counts those chains from their keys (checking the chain records), so no flush sits in
+// the scatter's loop, which has no register to spare.
 struct ChainState {
     uint32_t *h2;   // LDS [F][F2 / 2]
     uint32_t *out;  // global [F][nseg][F2] (u32)
@@ -1659,9 +1461,8 @@ __global__ __launch_bounds__(NT, (scatter_waves_per_simd<BITS, ITEMS, NT, 2, T>(
 // same workgroup moments later (in its XCD's L2); only the runs' ends at segment
 // boundaries are written as partial lines by two workgroups.  The next tile's keys
 // load while a tile is sorted and written (two register sets).
-// List entries staged in LDS: a fixed-size segment (kPass2Ents) or a chain-aligned one
-// (launch_chain_scan: up to kPass2Ents blocks + one chain); longer segments (one chain
-// of a heavily skewed digit) read their entries from the list itself.
+// List entries staged in LDS: a segment of up to kSortEnts blocks (kPass2Ents); longer
+// segments read their entries from the list itself.
 constexpr uint32_t kSortEnts = 1024;
 template <int BITS, int NT, int ITEMS>
 struct SortBlkLds {
@@ -2474,7 +2275,7 @@ hipError_t launch_scatter_blk_t(const void *in, const uint64_t *list, void *out,
             // narrow relations: k_place_seg (fixed-size segments with their partition
             // ends); k_sort_blk then returns at once for them (the width is known on the
             // device only)
-            const bool place = narrow && part_start && part_count && m.seg_lb == nullptr && place_enabled();
+            const bool place = narrow && part_start && part_count && place_enabled();
             if (side16 && !place) return hipErrorInvalidValue;  // a narrow pool is read by k_place_seg only
             // the placements' 16-byte run copies assume that residual 8k of `out` sits on a
             // 16-byte boundary (each u16-wire destination's pass 2 starts on one)
@@ -2593,8 +2394,8 @@ hipError_t launch_scatter_blk(const void *in, const uint64_t *list, void *out, u
 __global__ __launch_bounds__(1024) void k_pool_layout(const uint64_t *__restrict__ totals, uint32_t F,
                                                       uint64_t *__restrict__ start, uint64_t *__restrict__ count,
                                                       uint64_t *__restrict__ lbase, uint64_t *__restrict__ lcount,
-                                                      uint32_t *__restrict__ seg_base, uint32_t chain_nseg,
-                                                      uint32_t chain_mode, uint32_t *__restrict__ kmax,
+                                                      uint32_t *__restrict__ seg_base, uint32_t nseg,
+                                                      uint32_t *__restrict__ kmax,
                                                       const uint32_t *__restrict__ guard, uint32_t gshift) {
     __shared__ uint64_t scratch[1024 / kWave + 1];
     __shared__ uint32_t kmax_all;
@@ -2606,10 +2407,7 @@ __global__ __launch_bounds__(1024) void k_pool_layout(const uint64_t *__restrict
     uint64_t tot;
     const uint64_t ex_t = block_excl_scan_u64(tup, scratch, &tot);
     const uint64_t ex_b = block_excl_scan_u64(blk, scratch, &tot);
-    // chain-aligned slots (chain_mode > 0: launch_chain_scan; mode 2 reserves slots for
-    // its smallest target) or kPass2Ents-block segments
-    const uint32_t T = chain_mode == 2 ? kPass2Ents / 2 : chain_mode ? chain_slot_target(blk, chain_nseg) : kPass2Ents;
-    const uint64_t ns = (blk + T - 1) / T;
+    const uint64_t ns = (blk + kPass2Ents - 1) / kPass2Ents;  // kPass2Ents-block segments
     const uint64_t ex_s = block_excl_scan_u64(ns, scratch, &tot);
     if (d < F) {
         start[d] = ex_t;
@@ -2619,25 +2417,25 @@ __global__ __launch_bounds__(1024) void k_pool_layout(const uint64_t *__restrict
         seg_base[d] = (uint32_t)ex_s;
     }
     if (d == 0) seg_base[F] = (uint32_t)tot;
-    if (kmax) {  // (chain_nseg: the pass-1 segments) the relation's largest key into kmax[nseg]
+    if (kmax) {  // the relation's largest key into kmax[nseg]
         uint32_t x = 0;
-        for (uint32_t i = d; i < chain_nseg; i += blockDim.x) x = max(x, kmax[i]);
+        for (uint32_t i = d; i < nseg; i += blockDim.x) x = max(x, kmax[i]);
         if (x) atomicMax(&kmax_all, x);
         __syncthreads();
-        if (d == 0) kmax[chain_nseg] = kmax_all;
+        if (d == 0) kmax[nseg] = kmax_all;
     }
 }
 
 hipError_t launch_pool_layout(uint64_t *cnt, uint32_t nseg, uint32_t bits, uint64_t *totals, uint64_t *start,
                               uint64_t *count, uint64_t *lbase, uint64_t *lcount, uint32_t *seg_base, hipStream_t s,
-                              uint32_t chain_mode, uint32_t *kmax, const uint32_t *guard, uint32_t gshift) {
+                              uint32_t *kmax, const uint32_t *guard, uint32_t gshift) {
     const uint32_t F = 1u << bits;
     hipLaunchKernelGGL(k_scan_cols, dim3(F), dim3(kBlock), 0, s, cnt, nseg, totals, guard, gshift);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const uint32_t threads = F < 64 ? 64 : F;
     hipLaunchKernelGGL(k_pool_layout, dim3(1), dim3(threads), 0, s, totals, F, start, count, lbase, lcount, seg_base,
-                       nseg, chain_mode, kmax, guard, gshift);
+                       nseg, kmax, guard, gshift);
     return hipGetLastError();
 }
 
@@ -2809,6 +2607,132 @@ hipError_t launch_hist_side_blk(const uint8_t *side, const uint64_t *list, const
                                 uint32_t bits, uint64_t *hist, hipStream_t s) {
     if (grid == 0) return hipSuccess;
     hipLaunchKernelGGL(k_hist_side_blk, dim3(grid), dim3(kBlock), 0, s, side, list, m, bits, hist);
+    return hipGetLastError();
+}
+
+// Pass-2 histogram of a block-list segment from the chain histograms (no side stream).
+// Region r's list holds its chains one after another (chain j = pass-1 segment j's
+// blocks of digit r, k_block_list), so a segment of kPass2Ents blocks is whole chains
+// plus at most a cut chain at either end.  The whole chains' digit counts are summed
+// from the chain histograms pass 1 stored; the cut parts -- and a whole chain of more
+// than 65,535 elements, whose u16 counts may have wrapped (possible only when
+// kPass2Ents > 256) -- are counted from their keys.  Uniform 2^28-key relations: about
+// 16 whole chains (8 KiB of histograms) and 16 blocks of keys (16 KiB) per segment
+// instead of its 64 KiB of side-stream bytes, and 4,096 LDS atomics instead of 65,536.
+constexpr uint32_t kHistChainRanges = 8;  // cut / wrapped chain parts per segment (<= 2 + kPass2Ents / 256)
+static_assert(kPass2Ents <= 1024, "k_hist_chain's range table");
+__global__ __launch_bounds__(kBlock) void k_hist_chain(const uint64_t *__restrict__ rec,
+                                                       const uint64_t *__restrict__ tot, uint32_t nseg,
+                                                       const uint32_t *__restrict__ chain,
+                                                       const uint64_t *__restrict__ list,
+                                                       const uint32_t *__restrict__ keys, SegMap m, uint32_t shift2,
+                                                       uint32_t bits2, uint64_t *__restrict__ hist) {
+    constexpr uint64_t M40 = (1ull << 40) - 1;
+    __shared__ uint32_t sbase[kMaxF + 1];
+    __shared__ uint32_t h[kMaxF];
+    __shared__ uint32_t good[kHistChainMaxSegs / 32];  // whole chains read from their histograms
+    __shared__ uint32_t rg[kHistChainRanges][2];         // [p0, p1) region-local list ranges counted from keys
+    __shared__ uint32_t jlo, jhi, nrg;
+    const uint32_t g = blockIdx.x, tid = threadIdx.x, lane = __lane_id(), wave = tid / kWave;
+    uint32_t r;
+    uint64_t b, e;
+    if (!seg_lookup(m, g, sbase, r, b, e)) return;
+    const uint32_t F2 = 1u << bits2;
+    const uint64_t lb0 = m.reg_start[r];
+    const uint64_t lb = b - lb0, le = e - lb0;
+    const uint64_t *rc = rec + (uint64_t)r * nseg;
+    for (uint32_t i = tid; i < F2; i += kBlock) h[i] = 0;
+    for (uint32_t i = tid; i < (nseg + 31) / 32; i += kBlock) good[i] = 0;
+    if (tid == 0) {
+        jlo = 0xFFFFFFFFu;
+        jhi = 0;
+        nrg = 0;
+    }
+    __syncthreads();
+    // classify the region's chains against [lb, le)
+    for (uint32_t j = tid; j < nseg; j += kBlock) {
+        const uint64_t v0 = rc[j], v1 = j + 1 < nseg ? rc[j + 1] : tot[r];
+        const uint64_t a0 = v0 >> 40, a1 = v1 >> 40;
+        const uint64_t p0 = max(a0, lb), p1 = min(a1, le);
+        if (p0 >= p1) continue;  // outside the segment (or empty)
+        if (a0 >= lb && a1 <= le && (v1 & M40) - (v0 & M40) <= 65535) {
+            atomicOr(&good[j / 32], 1u << (j % 32));
+            atomicMin(&jlo, j);
+            atomicMax(&jhi, j);
+        } else {
+            const uint32_t k = atomicAdd(&nrg, 1u);
+            if (k < kHistChainRanges) {
+                rg[k][0] = (uint32_t)p0;
+                rg[k][1] = (uint32_t)p1;
+            }
+        }
+    }
+    __syncthreads();
+    // whole chains: F2 digits x Q chain groups, the sums folded into h
+    {
+        const uint32_t Q = kBlock / F2, d = tid % F2, q = tid / F2;
+        const uint32_t *ch = chain + (uint64_t)r * nseg * F2 + d;
+        uint32_t sum = 0;
+        if (jlo <= jhi) {
+            constexpr int U = 4;
+            for (uint32_t j0 = jlo + q; j0 <= jhi; j0 += U * Q) {
+                uint32_t c[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t j = j0 + u * Q;
+                    c[u] = j <= jhi && ((good[j / 32] >> (j % 32)) & 1u) ? ch[(uint64_t)j * F2] : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) sum += c[u];
+            }
+        }
+        if (sum) atomicAdd(&h[d], sum);
+    }
+    // cut / wrapped parts from their keys: each wave U blocks per step, a lane 4 keys of one
+    const uint32_t nr = min(nrg, kHistChainRanges);
+    uint32_t nb = 0;
+    for (uint32_t k = 0; k < nr; ++k) nb += rg[k][1] - rg[k][0];
+    const uint32_t mask2 = F2 - 1;
+    constexpr int U = 4;
+    constexpr uint32_t NW = kBlock / kWave;
+    for (uint32_t i0 = wave; i0 < nb; i0 += U * NW) {
+        uint4 q[U];
+        uint32_t fill[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            uint32_t i = i0 + u * NW, p = 0xFFFFFFFFu;
+            for (uint32_t k = 0; k < nr && p == 0xFFFFFFFFu; ++k) {  // block i of the ranges
+                const uint32_t w = rg[k][1] - rg[k][0];
+                if (i < w) p = rg[k][0] + i; else i -= w;
+            }
+            fill[u] = 0;
+            q[u] = make_uint4(0, 0, 0, 0);
+            if (p != 0xFFFFFFFFu) {
+                const uint64_t en = list[lb0 + p];
+                fill[u] = (uint32_t)(en >> 32);
+                if (lane * 4 < fill[u])
+                    q[u] = ld_nt(reinterpret_cast<const uint4 *>(keys + (uint64_t)(uint32_t)en * kBlk) + lane);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t w[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (lane * 4 + j < fill[u]) atomicAdd(&h[(w[j] >> shift2) & mask2], 1u);
+        }
+    }
+    __syncthreads();
+    for (uint32_t d = tid; d < F2; d += kBlock) hist[(uint64_t)g * F2 + d] = h[d];
+}
+
+hipError_t launch_hist_chain(const uint64_t *cnt, const uint64_t *tot, uint32_t nseg, const uint32_t *chain,
+                             const uint64_t *list, const uint32_t *keys, const SegMap &m, uint32_t grid,
+                             uint32_t shift2, uint32_t bits2, uint64_t *hist, hipStream_t s) {
+    if (grid == 0) return hipSuccess;
+    if (nseg > kHistChainMaxSegs || bits2 > 9) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_hist_chain, dim3(grid), dim3(kBlock), 0, s, cnt, tot, nseg, chain, list, keys, m, shift2,
+                       bits2, hist);
     return hipGetLastError();
 }
 

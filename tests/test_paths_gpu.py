@@ -10,8 +10,8 @@ with a pass-1 histogram and cursors instead of the pooled pass 1 and block-list 
 SGXAMD_POOL_SEGS sets the pooled pass-1 workgroups: 3 gives large pools, 100000 one
 tile per segment), SGXAMD_KEYS=0 (counting joins move whole tuples instead of keys),
 SGXAMD_SORT2=0 (pass 2 of key partitions with the write-combining scatter instead of
-the LDS counting sort), SGXAMD_CHAIN_HIST=1 (the chain histograms counted in pass 1
-instead of the digit side stream and its histogram pass; measured slower, r04k),
+the LDS counting sort), SGXAMD_CHAIN_HIST=0 (the digit side stream and its histogram
+pass instead of the chain histograms counted in pass 1),
 SGXAMD_NARROW=0 (key partitions stay 4-byte keys where u16 residuals would fit),
 SGXAMD_JOIN_N=0 (narrow relations' build/probe in k_join_x's direct table, one
 workgroup per CU, instead of k_join_n, one task per workgroup), SGXAMD_PLACE=0 (narrow
@@ -86,8 +86,8 @@ print("paths ok")
                                  {"SGXAMD_SMALL_JOIN": "0"}, {"SGXAMD_SMALL_DIRECT": "0"},
                                  {"SGXAMD_POOL": "0"}, {"SGXAMD_POOL_SEGS": "3"}, {"SGXAMD_POOL_SEGS": "100000"},
                                  {"SGXAMD_KEYS": "0"}, {"SGXAMD_SORT2": "0"}, {"SGXAMD_NARROW": "0"}, {"SGXAMD_JOIN_N": "0"}, {"SGXAMD_PLACE": "0"}, {"SGXAMD_PLACE_RUN": "1"}, {"SGXAMD_NARROW_POOL": "1"},
-                                 {"SGXAMD_NARROW_POOL": "1", "SGXAMD_PLACE_RUN": "0"}, {"SGXAMD_CHAIN_HIST": "1"},
-                                 {"SGXAMD_CHAIN_HIST": "1", "SGXAMD_CHAIN_SLOTS": "1"}])
+                                 {"SGXAMD_NARROW_POOL": "1", "SGXAMD_PLACE_RUN": "0"}, {"SGXAMD_CHAIN_HIST": "0"},
+                                 {"SGXAMD_CHAIN_HIST": "0", "SGXAMD_POOL_SEGS": "3"}])
 def test_switch_paths_match_oracle(env):
     e = dict(os.environ, **env)
     e["PYTHONPATH"] = os.pathsep.join([os.path.join(PKG, "python"), os.path.join(ROOT, "oracle"),
@@ -123,7 +123,7 @@ print("wire ok")
 
 @pytest.mark.parametrize("env", [{"SGXAMD_WIRE16": "0"}, {"SGXAMD_NARROW": "0"}, {"SGXAMD_PLACE": "0"}, {"SGXAMD_PLACE_RUN": "1"},
                                  {"SGXAMD_WIRE_GATHER": "1"},
-                                 {"SGXAMD_JOIN_N": "0"}, {"SGXAMD_CHAIN_HIST": "1"}, {"SGXAMD_PASS1_BITS": "6"},
+                                 {"SGXAMD_JOIN_N": "0"}, {"SGXAMD_CHAIN_HIST": "0"}, {"SGXAMD_PASS1_BITS": "6"},
                                  {"SGXAMD_POOL_SEGS": "3"}])
 def test_wire16_switches(env):
     e = dict(os.environ, **env)
@@ -133,10 +133,10 @@ def test_wire16_switches(env):
     assert r.returncode == 0 and "wire ok" in r.stdout, (env, r.stdout[-2000:], r.stderr[-2000:])
 
 
-# Chain histograms under skew (rho_kernels.hip launch_chain_fix / k_sort_blk's list path):
-# every S key has the same pass-1 digit, so with 8 pass-1 workgroups each chain holds
-# 2^19 keys (u16 counts wrap: the chain is recounted from its blocks) and a pass-2
-# segment is one chain of 2,048 blocks (more than the LDS copy of the list holds).
+# Chain histograms under skew (rho_kernels.hip k_hist_chain): every S key has the same
+# pass-1 digit, so with 8 pass-1 workgroups each chain holds 2^19 keys (u16 counts wrap)
+# and every pass-2 segment lies inside one chain (counted from its keys); with 512 a
+# segment holds whole chains of that digit and cut ones at both ends.
 CHAIN_CHILD = r"""
 import numpy as np
 import sgxamd, oracle
@@ -168,7 +168,7 @@ def test_chain_histograms_skewed(segs):
 
 
 # Chain histograms (layout 3) with narrow partitions: BASELINE config 2's 2^28 pk/fk keys
-# over the 14 = 7 + 7-bit plan, pass 2 over chain-aligned segments writing 2-byte residuals.
+# over the 14 = 7 + 7-bit plan, pass 2 writing 2-byte residuals.
 CHAIN_NARROW_CHILD = r"""
 import torch
 import sgxamd

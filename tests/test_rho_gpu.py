@@ -162,15 +162,15 @@ def test_pooled_two_pass_layouts(sgx, orc, gpu, case):
 
 
 def test_key_layout_switch(sgx, orc, gpu):
-    """mi355_set_key_layout: counting joins (RHO and RHT) move 4-byte keys (layout 2 at 14 =
-    7 + 7 bits: keys with the digit side stream) or whole tuples (layout 1) after the input read;
+    """mi355_set_key_layout: counting joins (RHO and RHT) move 4-byte keys (layout 3 at 14 =
+    7 + 7 bits: keys with chain histograms) or whole tuples (layout 1) after the input read;
     the counts are identical, materialising joins keep tuples either way."""
     rng = np.random.default_rng(21)
     R = rel(rng.integers(0, 1 << 21, 400_001).astype(np.uint32))
     S = rel(rng.integers(0, 1 << 21, 300_007).astype(np.uint32))
     exp = orc.count_join_sort(R, S)
     try:
-        for on, layout in ((True, 2), (False, 1), (True, 2)):
+        for on, layout in ((True, 3), (False, 1), (True, 3)):
             sgx.set_key_layout(on)
             for alg in ("RHO", "RHT"):
                 res = gpu_join(sgx, R, S, radix_bits=14, passes=2, algorithm=alg)
@@ -648,7 +648,7 @@ def test_config2_reference_relations_full_size(sgx, gpu):
         res = sgx.rho_join(R, n, S, n)
         st = res.stats
         assert res.matches == n
-        assert (st["radix_bits"], st["passes"], st["layout"]) == (14, 2, 2)  # keys, digit side stream
+        assert (st["radix_bits"], st["passes"], st["layout"]) == (14, 2, 3)  # keys, chain histograms
         assert st["max_part_r"] == st["max_part_s"] == 1 << 14
     finally:
         del R, S
