@@ -161,7 +161,9 @@ int mi355_rho_join_finish(const struct row_t *S, uint64_t nS, const mi355_rho_op
  * Per-kernel timing of the last call on this thread that ran with timing
  * enabled (opts->timing or mi355_timing_enable(1)): names and milliseconds
  * of every recorded kernel, in launch order.  Returns the number of records
- * (up to `cap` are copied).
+ * (up to `cap` are copied).  mi355_timing_enable(2) (sparse): only R's pass-1
+ * scatter and the build/probe are timed, the launches between them as one
+ * span "other" -- four events per join instead of one per kernel.
  */
 void mi355_timing_enable(int on);
 int mi355_timing_get(const char **names, double *ms, int cap);

@@ -2614,124 +2614,176 @@ hipError_t launch_hist_side_blk(const uint8_t *side, const uint64_t *list, const
 // Region r's list holds its chains one after another (chain j = pass-1 segment j's
 // blocks of digit r, k_block_list), so a segment of kPass2Ents blocks is whole chains
 // plus at most a cut chain at either end.  The whole chains' digit counts are summed
-// from the chain histograms pass 1 stored; the cut parts -- and a whole chain of more
-// than 65,535 elements, whose u16 counts may have wrapped (possible only when
-// kPass2Ents > 256) -- are counted from their keys.  Uniform 2^28-key relations: about
-// 16 whole chains (8 KiB of histograms) and 16 blocks of keys (16 KiB) per segment
-// instead of its 64 KiB of side-stream bytes, and 4,096 LDS atomics instead of 65,536.
+// from the chain histograms pass 1 stored; a cut chain's part is counted from its keys,
+// or, when the part outside the segment is the smaller, the chain's histogram less that
+// part (counted from its keys); a chain of more than 65,535 elements, whose u16 counts
+// may have wrapped, always from its keys.  Uniform 2^28-key relations: about 16 whole
+// chains (8 KiB of histograms) and 8 blocks of keys on average per segment, instead of
+// its 64 KiB of side-stream bytes, and 2,048 LDS atomics instead of 65,536.
 constexpr uint32_t kHistChainRanges = 8;  // cut / wrapped chain parts per segment (<= 2 + kPass2Ents / 256)
 static_assert(kPass2Ents <= 1024, "k_hist_chain's range table");
-__global__ __launch_bounds__(kBlock) void k_hist_chain(const uint64_t *__restrict__ rec,
-                                                       const uint64_t *__restrict__ tot, uint32_t nseg,
-                                                       const uint32_t *__restrict__ chain,
-                                                       const uint64_t *__restrict__ list,
-                                                       const uint32_t *__restrict__ keys, SegMap m, uint32_t shift2,
-                                                       uint32_t bits2, uint64_t *__restrict__ hist) {
+// One wave per segment (F2 <= 128): a 2^28-key relation's 4,224 segments are all
+// resident at once, and a segment's work is four dependent round trips -- the segment
+// table; the region's chain records; the whole chains' histogram rows (16 B per lane,
+// F2 / 4 lanes a row) with the cut chains' list entries; their keys.  256-thread
+// workgroups (three rounds of eight per CU) took 0.035 ms per relation against 0.031
+// (profiles/r06p_hist_chain_wave_ab.log).
+constexpr int kHcU = 8;  // chain records per lane per step (512 chains in one step)
+__global__ __launch_bounds__(kWave, 5) void k_hist_chain(const uint64_t *__restrict__ rec,
+                                                           const uint64_t *__restrict__ tot, uint32_t nseg,
+                                                           const uint32_t *__restrict__ chain,
+                                                           const uint64_t *__restrict__ list,
+                                                           const uint32_t *__restrict__ keys, SegMap m,
+                                                           uint32_t shift2, uint32_t bits2,
+                                                           uint64_t *__restrict__ hist) {
     constexpr uint64_t M40 = (1ull << 40) - 1;
     __shared__ uint32_t sbase[kMaxF + 1];
-    __shared__ uint32_t h[kMaxF];
-    __shared__ uint32_t good[kHistChainMaxSegs / 32];  // whole chains read from their histograms
-    __shared__ uint32_t rg[kHistChainRanges][2];         // [p0, p1) region-local list ranges counted from keys
+    __shared__ uint32_t h[kLaneHistF];
+    __shared__ uint32_t good[kHistChainMaxSegs / 32];
+    __shared__ uint32_t rg[kHistChainRanges][3];  // [p0, p1) region-local, subtract
     __shared__ uint32_t jlo, jhi, nrg;
-    const uint32_t g = blockIdx.x, tid = threadIdx.x, lane = __lane_id(), wave = tid / kWave;
-    uint32_t r;
-    uint64_t b, e;
-    if (!seg_lookup(m, g, sbase, r, b, e)) return;
-    const uint32_t F2 = 1u << bits2;
-    const uint64_t lb0 = m.reg_start[r];
-    const uint64_t lb = b - lb0, le = e - lb0;
-    const uint64_t *rc = rec + (uint64_t)r * nseg;
-    for (uint32_t i = tid; i < F2; i += kBlock) h[i] = 0;
-    for (uint32_t i = tid; i < (nseg + 31) / 32; i += kBlock) good[i] = 0;
-    if (tid == 0) {
+    const uint32_t g = blockIdx.x, lane = threadIdx.x;
+    const uint32_t F1 = m.nreg, F2 = 1u << bits2, mask2 = F2 - 1;
+    for (uint32_t i = lane; i <= F1; i += kWave) sbase[i] = m.seg_base[i];
+    for (uint32_t i = lane; i < F2; i += kWave) h[i] = 0;
+    for (uint32_t i = lane; i < (nseg + 31) / 32; i += kWave) good[i] = 0;
+    if (lane == 0) {
         jlo = 0xFFFFFFFFu;
         jhi = 0;
         nrg = 0;
     }
     __syncthreads();
-    // classify the region's chains against [lb, le)
-    for (uint32_t j = tid; j < nseg; j += kBlock) {
-        const uint64_t v0 = rc[j], v1 = j + 1 < nseg ? rc[j + 1] : tot[r];
-        const uint64_t a0 = v0 >> 40, a1 = v1 >> 40;
-        const uint64_t p0 = max(a0, lb), p1 = min(a1, le);
-        if (p0 >= p1) continue;  // outside the segment (or empty)
-        if (a0 >= lb && a1 <= le && (v1 & M40) - (v0 & M40) <= 65535) {
-            atomicOr(&good[j / 32], 1u << (j % 32));
-            atomicMin(&jlo, j);
-            atomicMax(&jhi, j);
-        } else {
-            const uint32_t k = atomicAdd(&nrg, 1u);
-            if (k < kHistChainRanges) {
-                rg[k][0] = (uint32_t)p0;
-                rg[k][1] = (uint32_t)p1;
+    if (g >= sbase[F1]) return;  // wave-uniform
+    uint32_t r = 0, hi = F1;     // largest r with sbase[r] <= g
+    while (hi - r > 1) {
+        const uint32_t mid = (r + hi) >> 1;
+        if (sbase[mid] <= g) r = mid; else hi = mid;
+    }
+    const uint64_t lb0 = m.reg_start[r], lcnt = m.reg_count[r], tr = tot[r];
+    const uint64_t lb = (uint64_t)(g - sbase[r]) * kPass2Ents, le = min(lb + kPass2Ents, lcnt);
+    const uint64_t *rc = rec + (uint64_t)r * nseg;
+    // the region's chains against [lb, le): whole ones (histogram rows), cut ones (ranges)
+    for (uint32_t j0 = 0; j0 < nseg; j0 += kWave * kHcU) {
+        uint64_t v0[kHcU], v1[kHcU];
+#pragma unroll
+        for (int u = 0; u < kHcU; ++u) {
+            const uint32_t j = j0 + u * kWave + lane;
+            v0[u] = j < nseg ? rc[j] : 0ull;
+            v1[u] = j + 1 < nseg ? rc[j + 1] : tr;
+        }
+#pragma unroll
+        for (int u = 0; u < kHcU; ++u) {
+            const uint32_t j = j0 + u * kWave + lane;
+            const uint64_t a0 = v0[u] >> 40, a1 = v1[u] >> 40;
+            const uint64_t p0 = max(a0, lb), p1 = min(a1, le);
+            if (j >= nseg || p0 >= p1) continue;
+            const bool exact = (v1[u] & M40) - (v0[u] & M40) <= 65535;  // its histogram did not wrap
+            const bool whole = a0 >= lb && a1 <= le;
+            // a chain cut at one end of the segment whose part outside is the smaller:
+            // its histogram less the outside part (counted from its keys)
+            const bool sub = exact && !whole && (a0 >= lb || a1 <= le) && (a1 - a0) - (p1 - p0) < p1 - p0;
+            if ((whole && exact) || sub) {
+                atomicOr(&good[j / 32], 1u << (j % 32));
+                atomicMin(&jlo, j);
+                atomicMax(&jhi, j);
+            }
+            if (!(whole && exact)) {
+                const uint32_t k = atomicAdd(&nrg, 1u);
+                if (k < kHistChainRanges) {
+                    rg[k][0] = (uint32_t)(sub ? (a0 < lb ? a0 : le) : p0);
+                    rg[k][1] = (uint32_t)(sub ? (a0 < lb ? lb : a1) : p1);
+                    rg[k][2] = sub ? 1u : 0u;
+                }
             }
         }
     }
     __syncthreads();
-    // whole chains: F2 digits x Q chain groups, the sums folded into h
-    {
-        const uint32_t Q = kBlock / F2, d = tid % F2, q = tid / F2;
-        const uint32_t *ch = chain + (uint64_t)r * nseg * F2 + d;
-        uint32_t sum = 0;
-        if (jlo <= jhi) {
-            constexpr int U = 4;
-            for (uint32_t j0 = jlo + q; j0 <= jhi; j0 += U * Q) {
-                uint32_t c[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const uint32_t j = j0 + u * Q;
-                    c[u] = j <= jhi && ((good[j / 32] >> (j % 32)) & 1u) ? ch[(uint64_t)j * F2] : 0u;
-                }
-#pragma unroll
-                for (int u = 0; u < U; ++u) sum += c[u];
-            }
-        }
-        if (sum) atomicAdd(&h[d], sum);
-    }
-    // cut / wrapped parts from their keys: each wave U blocks per step, a lane 4 keys of one
     const uint32_t nr = min(nrg, kHistChainRanges);
     uint32_t nb = 0;
     for (uint32_t k = 0; k < nr; ++k) nb += rg[k][1] - rg[k][0];
-    const uint32_t mask2 = F2 - 1;
-    constexpr int U = 4;
-    constexpr uint32_t NW = kBlock / kWave;
-    for (uint32_t i0 = wave; i0 < nb; i0 += U * NW) {
+    // block i of the ranges -> its list position (region-local) | subtract << 31, or ~0
+    const auto pos_of = [&](uint32_t i) -> uint32_t {
+        for (uint32_t k = 0; k < nr; ++k) {
+            const uint32_t w = rg[k][1] - rg[k][0];
+            if (i < w) return (rg[k][0] + i) | (rg[k][2] << 31);
+            i -= w;
+        }
+        return 0xFFFFFFFFu;
+    };
+    constexpr int U = 8;  // cut blocks per step
+    uint64_t en[U];
+    uint32_t inc[U];  // 1, or -1 for a subtracted part
+#pragma unroll
+    for (int u = 0; u < U; ++u) {  // the first step's list entries, in flight with the rows below
+        const uint32_t p = pos_of((uint32_t)u);
+        en[u] = p != 0xFFFFFFFFu ? list[lb0 + (p & 0x7FFFFFFFu)] : 0ull;
+        inc[u] = p != 0xFFFFFFFFu && (p >> 31) ? 0xFFFFFFFFu : 1u;
+    }
+    // whole chains: F2 / 4 lanes per histogram row, 256 / F2 rows per load
+    {
+        const uint32_t lpr = F2 / 4, rpi = kWave / lpr, sub = lane / lpr, dq = lane % lpr;
+        const uint32_t *ch = chain + (uint64_t)r * nseg * F2 + 4 * dq;
+        uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+        if (jlo <= jhi) {
+            for (uint32_t j0 = jlo + sub; j0 <= jhi; j0 += U * rpi) {
+                uint4 c[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t j = j0 + u * rpi;
+                    c[u] = j <= jhi && ((good[j / 32] >> (j % 32)) & 1u)
+                               ? *reinterpret_cast<const uint4 *>(ch + (uint64_t)j * F2)
+                               : make_uint4(0, 0, 0, 0);
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    s0 += c[u].x;
+                    s1 += c[u].y;
+                    s2 += c[u].z;
+                    s3 += c[u].w;
+                }
+            }
+        }
+        if (s0) atomicAdd(&h[4 * dq], s0);
+        if (s1) atomicAdd(&h[4 * dq + 1], s1);
+        if (s2) atomicAdd(&h[4 * dq + 2], s2);
+        if (s3) atomicAdd(&h[4 * dq + 3], s3);
+    }
+    // cut parts from their keys: a lane 4 keys of each block
+    for (uint32_t i0 = 0; i0 < nb; i0 += U) {
+        if (i0) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t p = pos_of(i0 + u);
+                en[u] = p != 0xFFFFFFFFu ? list[lb0 + (p & 0x7FFFFFFFu)] : 0ull;
+                inc[u] = p != 0xFFFFFFFFu && (p >> 31) ? 0xFFFFFFFFu : 1u;
+            }
+        }
         uint4 q[U];
-        uint32_t fill[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            uint32_t i = i0 + u * NW, p = 0xFFFFFFFFu;
-            for (uint32_t k = 0; k < nr && p == 0xFFFFFFFFu; ++k) {  // block i of the ranges
-                const uint32_t w = rg[k][1] - rg[k][0];
-                if (i < w) p = rg[k][0] + i; else i -= w;
-            }
-            fill[u] = 0;
-            q[u] = make_uint4(0, 0, 0, 0);
-            if (p != 0xFFFFFFFFu) {
-                const uint64_t en = list[lb0 + p];
-                fill[u] = (uint32_t)(en >> 32);
-                if (lane * 4 < fill[u])
-                    q[u] = ld_nt(reinterpret_cast<const uint4 *>(keys + (uint64_t)(uint32_t)en * kBlk) + lane);
-            }
+            const uint32_t fill = i0 + u < nb ? (uint32_t)(en[u] >> 32) : 0u;
+            q[u] = lane * 4 < fill ? ld_nt(reinterpret_cast<const uint4 *>(keys + (uint64_t)(uint32_t)en[u] * kBlk) + lane)
+                                   : make_uint4(0, 0, 0, 0);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
+            const uint32_t fill = i0 + u < nb ? (uint32_t)(en[u] >> 32) : 0u;
             const uint32_t w[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
 #pragma unroll
             for (int j = 0; j < 4; ++j)
-                if (lane * 4 + j < fill[u]) atomicAdd(&h[(w[j] >> shift2) & mask2], 1u);
+                if (lane * 4 + j < fill) atomicAdd(&h[(w[j] >> shift2) & mask2], inc[u]);
         }
     }
     __syncthreads();
-    for (uint32_t d = tid; d < F2; d += kBlock) hist[(uint64_t)g * F2 + d] = h[d];
+    for (uint32_t d = lane; d < F2; d += kWave) hist[(uint64_t)g * F2 + d] = h[d];
 }
 
 hipError_t launch_hist_chain(const uint64_t *cnt, const uint64_t *tot, uint32_t nseg, const uint32_t *chain,
                              const uint64_t *list, const uint32_t *keys, const SegMap &m, uint32_t grid,
                              uint32_t shift2, uint32_t bits2, uint64_t *hist, hipStream_t s) {
     if (grid == 0) return hipSuccess;
-    if (nseg > kHistChainMaxSegs || bits2 > 9) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_hist_chain, dim3(grid), dim3(kBlock), 0, s, cnt, tot, nseg, chain, list, keys, m, shift2,
+    if (nseg > kHistChainMaxSegs || bits2 < 2 || bits2 > 7) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_hist_chain, dim3(grid), dim3(kWave), 0, s, cnt, tot, nseg, chain, list, keys, m, shift2,
                        bits2, hist);
     return hipGetLastError();
 }

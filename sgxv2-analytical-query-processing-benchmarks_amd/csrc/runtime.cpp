@@ -13,7 +13,7 @@ namespace sgxamd {
 
 namespace {
 thread_local std::string t_last_error;
-thread_local bool t_timing = false;
+thread_local int t_timing = 0;  // 0 off, 1 every kernel, 2 sparse (Timer::mark)
 thread_local void *t_stream = nullptr;
 thread_local Timer t_timer;
 thread_local bool t_overlap = false;
@@ -72,6 +72,7 @@ hipEvent_t Timer::get_event() {
 void Timer::begin_call(hipStream_t s, bool enabled, bool coarse) {
     enabled_ = enabled;
     coarse_ = coarse;
+    sparse_ = enabled && !coarse && t_timing == 2;
     stream_ = s;
     used_ = 0;
     spans_.clear();
@@ -80,13 +81,20 @@ void Timer::begin_call(hipStream_t s, bool enabled, bool coarse) {
     open_ev_ = nullptr;
 }
 
+// Sparse timing (mi355_timing_enable(2)): events only around the spans a roofline reads
+// -- R's pass-1 scatter and the build/probe -- and one "other" span between them, so a
+// timed step carries 4 events instead of one per kernel (each event between two kernels
+// costs 4.5-4.8 us of GPU time even without the system fence: r06q kernel trace).
+static bool sparse_kept(const std::string &n) { return n == "R_pass1_scatter" || n == "join_build_probe"; }
+
 void Timer::mark(const char *name) {
     if (!enabled_ || (coarse_ && open_ev_)) return;
+    if (sparse_ && !sparse_kept(name) && open_ev_ && !sparse_kept(open_name_)) return;
     hipEvent_t ev = get_event();
     if (!ev) return;
     (void)hipEventRecord(ev, stream_);
     if (open_ev_) spans_.push_back({open_name_, {open_ev_, ev}});
-    open_name_ = coarse_ ? "total" : name;
+    open_name_ = coarse_ ? "total" : (sparse_ && !sparse_kept(name)) ? "other" : name;
     open_ev_ = ev;
 }
 
@@ -131,7 +139,7 @@ hipStream_t side_stream(Context *ctx) {
     }
     return ctx->side;
 }
-bool thread_timing_enabled() { return t_timing; }
+bool thread_timing_enabled() { return t_timing != 0; }
 bool thread_partition_overlap() { return t_overlap; }
 bool thread_key_layout() { return t_keys; }
 
@@ -225,7 +233,7 @@ int mi355_device_count(void) {
     return n;
 }
 
-void mi355_timing_enable(int on) { sgxamd::t_timing = on != 0; }
+void mi355_timing_enable(int on) { sgxamd::t_timing = on == 2 ? 2 : on != 0 ? 1 : 0; }
 
 void mi355_set_partition_overlap(int on) { sgxamd::t_overlap = on != 0; }
 

@@ -60,6 +60,7 @@ class Timer {
 
    private:
     bool coarse_ = false;
+    bool sparse_ = false;  // mi355_timing_enable(2): Timer::mark
     hipEvent_t get_event();
     bool enabled_ = false;
     hipStream_t stream_ = nullptr;

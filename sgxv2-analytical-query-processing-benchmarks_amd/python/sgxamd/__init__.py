@@ -555,8 +555,10 @@ def shard_partition(inp, n: int, key_shift: int, dest_bits: int, out, stream: in
     return [int(c) for c in counts]
 
 
-def timing_enable(on: bool = True) -> None:
-    lib.mi355_timing_enable(1 if on else 0)
+def timing_enable(on=True) -> None:
+    """Per-kernel HIP events: True (every kernel), False, or "sparse" (R's pass-1 scatter
+    and the build/probe only, the launches between them as one span "other")."""
+    lib.mi355_timing_enable(2 if on == "sparse" else 1 if on else 0)
 
 
 def set_partition_overlap(on: bool = True) -> None:
