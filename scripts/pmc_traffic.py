@@ -28,6 +28,7 @@ ALIASES = {
     "k_scatter_blk": ["R_pass2_scatter", "S_pass2_scatter"],
     "k_sort_blk": ["R_pass2_scatter", "S_pass2_scatter"],
     "k_hist_side_blk": ["R_pass2_hist", "S_pass2_hist"],
+    "k_hist_chain": ["R_pass2_hist", "S_pass2_hist"],  # chain-histogram plans (round 6)
     "k_join": ["join_build_probe"],
     "k_join_tag": ["join_build_probe"],
     "k_join_x": ["join_build_probe"],

@@ -16,7 +16,8 @@ from collections import defaultdict
 
 def main():
     src, out, commit = sys.argv[1:4]
-    want = sys.argv[4:] or ["k_scatter_pool", "k_scatter_blk", "k_sort_blk", "k_join_x", "k_join_hist_big", "k_hist_side_blk"]
+    want = sys.argv[4:] or ["k_scatter_pool", "k_place_seg", "k_join_n", "k_hist_chain", "k_scatter_blk", "k_sort_blk",
+                            "k_join_x", "k_join_hist_big", "k_hist_side_blk"]
     acc = defaultdict(lambda: defaultdict(list))
     for f in glob.glob(src + "/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):

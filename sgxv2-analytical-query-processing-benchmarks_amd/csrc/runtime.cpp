@@ -89,7 +89,7 @@ static bool sparse_kept(const std::string &n) { return n == "R_pass1_scatter" ||
 
 void Timer::mark(const char *name) {
     if (!enabled_ || (coarse_ && open_ev_)) return;
-    if (sparse_ && !sparse_kept(name) && open_ev_ && !sparse_kept(open_name_)) return;
+    if (sparse_ && !sparse_kept(name) && !(open_ev_ && sparse_kept(open_name_))) return;
     hipEvent_t ev = get_event();
     if (!ev) return;
     (void)hipEventRecord(ev, stream_);
