@@ -243,6 +243,7 @@ struct RelPlan {
     std::vector<uint64_t> piece_off, piece_n;
     std::vector<uint32_t> piece_g0;
     std::vector<hipEvent_t> piece_ev;
+    uint64_t *zero8 = nullptr;  // pooled pass 1: its layout zeroes these 8 words (the join's result block)
 };
 
 #define RHO_HIP(call)                                                                      \
@@ -271,6 +272,7 @@ int partition_relation_pooled(Context *ctx, hipStream_t s, Timer &tm, const std:
         PoolOut po{A.at<uint32_t>(rp.binfo), A.at<uint64_t>(rp.hist1), A.at<uint32_t>(rp.used), rp.pool_blocks,
                    rp.nseg1};
         po.kmax = rp.narrow ? A.at<uint32_t>(rp.kmax) : nullptr;
+        po.zero8 = rp.zero8;
         const DigitSide ds{rp.chain ? nullptr : side, key_shift + pol.b1, pol.b2};
         uint32_t *chist = rp.chain ? A.at<uint32_t>(rp.chist) : nullptr;
         // pass 1 over the relation (one launch, or one per piece as it lands, its segments
@@ -296,10 +298,8 @@ int partition_relation_pooled(Context *ctx, hipStream_t s, Timer &tm, const std:
             return MI355_OK;
         };
         const auto layout = [&](const PoolOut &p) -> int {
-            RHO_HIP(launch_pool_layout(p.cnt, rp.nseg1, pol.b1, A.at<uint64_t>(rp.tot1), start1, cnt1, lbase, lcount,
-                                       segbase2, s, p.kmax, p.guard,
-                                       p.guard_shift));
-            RHO_HIP(launch_block_list(p, lbase, list, pol.b1, s));
+            RHO_HIP(launch_pool_layout_list(p, pol.b1, A.at<uint64_t>(rp.tot1), start1, cnt1, lbase, lcount, segbase2,
+                                            list, s));
             return MI355_OK;
         };
         int rc;
@@ -471,6 +471,7 @@ void plan_relation(Arena &A, RelPlan &rp, uint64_t n, const Policy &pol, int poo
     rp.piece_n.clear();
     rp.piece_g0.clear();
     rp.piece_ev.clear();
+    rp.zero8 = nullptr;
     if (pieces && !pieces->empty()) {  // the input arrives in pieces (every plan waits for them)
         uint64_t off = 0;
         for (uint64_t pn : *pieces) {
@@ -697,6 +698,9 @@ int join_begin(Context *ctx, hipStream_t s, const row_t *dR, uint64_t nR, uint64
         RHO_HIP(hipEventRecord(ctx->ev_t0, s));
         RHO_HIP(hipEventRecord(ctx->ev_fork, s));
     }
+    // R's pooled pass-1 layout zeroes the join's result block (launch_make_tasks then
+    // needs no fill)
+    if (pj.pr.pooled) pj.pr.zero8 = ctx->scratch.at<uint64_t>(pj.off_result);
     int rc;
     for (int pass = 0; pass < (int)pol.passes; ++pass)
         if ((rc = partition_relation(ctx, s, tm, "R_", dR, ctx->t1R.as<row_t>(), ctx->t2R.as<row_t>(),
@@ -828,7 +832,7 @@ int join_finish(Context *ctx, PendingJoin &pj, const row_t *dS, uint64_t nS, mi3
     const bool pieces = given_s && given_s->pieces;
     // (S in pieces: the task list splits each partition's units, 8 per unit)
     RHO_HIP(launch_make_tasks(pcR, pieces ? given_s->w.units8 : pcS, P, over, pj.over_cap, result + 1, pj.s_chunk, s,
-                              nar || pieces ? counts : nullptr, cyc, join_grid));
+                              nar || pieces ? counts : nullptr, cyc, join_grid, pj.pr.zero8 != nullptr));
     if (pieces) {
         if (pj.materialize || pj.algo != kAlgoChaining || pol.rcap != kBigRcap || !pj.pr.narrow || !pj.ps.narrow) {
             set_last_error("u16 wire pieces: the plan is not the narrow counting table");

@@ -162,6 +162,9 @@ struct PoolOut {
     // bits (nullable: unguarded)
     const uint32_t *guard = nullptr;
     uint32_t guard_shift = 0;
+    // (nullable) 8 words the layout's first workgroup zeroes: the join's result block, so
+    // that launch_make_tasks needs no fill of its own
+    uint64_t *zero8 = nullptr;
 };
 // Pass 1 of a pooled plan: contiguous input segments (m), pooled output in out, digit
 // side stream ds beside every stored element.  Elements: in_size-byte input
@@ -192,6 +195,11 @@ hipError_t launch_pool_layout(uint64_t *cnt, uint32_t nseg, uint32_t bits, uint6
 // The block list: region d's blocks at [lbase[d], lbase[d] + lcount[d]) as
 // physical block | fill << 32.
 hipError_t launch_block_list(const PoolOut &po, const uint64_t *lbase, uint64_t *list, uint32_t bits, hipStream_t s);
+// launch_pool_layout + launch_block_list with the layout folded into the block list's
+// launch (pass-1 digits up to 8 bits; wider ones take the two launches).
+hipError_t launch_pool_layout_list(const PoolOut &po, uint32_t bits, uint64_t *totals, uint64_t *start,
+                                   uint64_t *count, uint64_t *lbase, uint64_t *lcount, uint32_t *seg_base,
+                                   uint64_t *list, hipStream_t s);
 // Pass-2 histogram / scatter over block-list segments (m: reg_start = lbase,
 // reg_count = lcount, seg_size = kPass2Ents).
 hipError_t launch_hist_side_blk(const uint8_t *side, const uint64_t *list, const SegMap &m, uint32_t grid,
@@ -258,14 +266,15 @@ constexpr uint64_t kBigSPart = 65536;
 enum JoinMode : int { kJoinCount = 0, kJoinTaskCount = 1, kJoinWrite = 2 };
 // Build/probe algorithm of one task: RHO's bucket chaining or RHT's histogram join.
 enum JoinAlgo : int { kAlgoChaining = 0, kAlgoHistogram = 1 };
-// meta (zeroed here): [0] = largest R partition, [1] = largest S partition,
+// meta (zeroed here, with the word before it, unless `zeroed`: an earlier launch of the
+// call did, PoolOut::zero8): [0] = largest R partition, [1] = largest S partition,
 // [2] = the number of extra tasks (u32 n_over, read by launch_join / launch_excl_scan),
 // [3..5] zero as well ([5]: launch_join's task tickets).
 // zero / zero2 (nullable): nzero / 2 nzero u64 words zeroed as well (k_join_n's count
 // and tick slots).
 hipError_t launch_make_tasks(const uint64_t *r_count, const uint64_t *s_count, uint64_t P, uint64_t *over,
                              uint32_t over_cap, uint64_t *meta, uint64_t s_chunk, hipStream_t s,
-                             uint64_t *zero = nullptr, uint64_t *zero2 = nullptr, uint32_t nzero = 0);
+                             uint64_t *zero = nullptr, uint64_t *zero2 = nullptr, uint32_t nzero = 0, bool zeroed = false);
 // reduce (mode 0, nullable): the last workgroup to finish sums the partial counts and
 // ticks into reduce->result as launch_reduce does (reduce->ticket: a Context::sync word).
 struct JoinReduce {

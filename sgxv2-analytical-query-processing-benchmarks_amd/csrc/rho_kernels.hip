@@ -1880,251 +1880,6 @@ __global__ __launch_bounds__(NT, NT *SGXAMD_PLACE_WGS / 256) void k_place_seg(
     }
 }
 
-// The same placement with one workgroup per CU walking a run of segments (round 6,
-// VERDICT r05 item 5).  k_place_seg's workgroup starts every segment cold: the segment
-// table, the list entries and the cursors are dependent loads, and no key of the segment
-// is read while the previous workgroup's runs are copied out (one workgroup per CU: the
-// segment fills the LDS).  Here the next segment's list entries and cursors are read
-// while the current segment is placed, and its first PF tiles are loaded into registers
-// before the current segment's runs are copied out (loads issued before the copy-out's
-// stores: gfx950 retires both through one in-order vmcnt), so its reads overlap the
-// copy-out's writes; its other tiles stream as in k_place_seg.  The run layout of a
-// segment (counts from the cursors, the slot ranges' scan) is computed by wave 0 alone,
-// F / 64 digits per lane.
-template <int BITS>
-struct PlaceRunLds {
-    static constexpr uint32_t F = 1u << BITS;
-    static constexpr uint32_t CAP = kPass2Ents * kBlk + 14 * F;
-    alignas(16) uint16_t res[CAP];
-    uint64_t ents[2][kPass2Ents];  // list entries of the current and the next segment
-    uint64_t dst[F];
-    uint32_t pos[F], st[F], pb[F + 1], cnt[F];
-    uint32_t sbase[kMaxF + 1];     // segments per region (prefix)
-};
-
-#ifndef SGXAMD_PLACE_PF  // k_place_run: tiles of the next segment loaded during a copy-out
-#define SGXAMD_PLACE_PF 2
-#endif
-template <int BITS, int NT, bool I16>
-__global__ __launch_bounds__(NT, NT / 256) void k_place_run(
-    const uint32_t *__restrict__ in, const uint8_t *__restrict__ side, const uint64_t *__restrict__ list,
-    uint16_t *__restrict__ out, SegMap m, uint32_t shift, const uint64_t *__restrict__ cursors,
-    const uint64_t *__restrict__ part_start, const uint64_t *__restrict__ part_count,
-    const uint32_t *__restrict__ narrow) {
-    using LdsT = PlaceRunLds<BITS>;
-    constexpr uint32_t F = LdsT::F, mask = F - 1, NW = NT / kWave, U = 2;
-    constexpr uint32_t BPT = NW * U;               // blocks per tile
-    constexpr uint32_t NTL = kPass2Ents / BPT;     // tiles per (full) segment
-    constexpr uint32_t PF = SGXAMD_PLACE_PF;
-    constexpr uint32_t DPL = F > kWave ? F / kWave : 1u;  // digits per lane of wave 0
-    static_assert(kBlk == 4 * kWave && F <= NT && kPass2Ents % BPT == 0 && PF < NTL, "placement geometry");
-    __shared__ LdsT L;
-    if (narrow == nullptr || ((*narrow >> (shift + BITS)) >> 16) != 0) return;  // wide: k_sort_blk
-    const uint32_t tid = threadIdx.x, lane = __lane_id(), wave = tid / kWave;
-    const uint32_t rshift = shift + BITS;
-    for (uint32_t i = tid; i <= m.nreg; i += NT) L.sbase[i] = m.seg_base[i];
-    __syncthreads();
-    const uint32_t nseg = L.sbase[m.nreg];
-    // XCD x (workgroups b with b mod 8 = x) takes the x-th contiguous eighth of the
-    // segments, its workgroups in lock step over consecutive segments (workgroup i of the
-    // XCD: segments i, i + WX, ...), so that at any time an XCD places neighbouring
-    // segments -- their shared partial lines meet in its L2, as in k_place_seg's
-    // dispatch order.  (grid: a multiple of 8)
-    const uint32_t WX = gridDim.x / 8, x = blockIdx.x % 8, wi = blockIdx.x / 8;
-    const uint32_t perx = (nseg + 7) / 8;
-    const uint32_t xb = min(nseg, x * perx), xe = min(nseg, xb + perx);
-    const uint32_t g0 = xb + wi, g1 = xe;
-    if (g0 >= g1) return;
-    // segment g: its region, list range and whether it is its region's last
-    struct Seg {
-        uint32_t r, nent, last;
-        uint64_t b;
-    };
-    const auto seg_of = [&](uint32_t g) -> Seg {
-        uint32_t lo = 0, hi = m.nreg;  // largest lo with sbase[lo] <= g
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (L.sbase[mid] <= g) lo = mid; else hi = mid;
-        }
-        Seg s;
-        s.r = lo;
-        const uint64_t rs = m.reg_start[lo], rc = m.reg_count[lo];
-        s.b = rs + (uint64_t)(g - L.sbase[lo]) * m.seg_size;
-        const uint64_t e = min(s.b + m.seg_size, rs + rc);
-        s.nent = e > s.b ? (uint32_t)(e - s.b) : 0u;
-        s.last = g + 1 == L.sbase[lo + 1] ? 1u : 0u;
-        return s;
-    };
-    // wave 0, lane l: digits l + 64 i (i < DPL) -- their cursors and the next ones
-    uint64_t cur[DPL], nxt[DPL];
-    const auto fetch_cursors = [&](uint32_t g, const Seg &s) {
-#pragma unroll
-        for (uint32_t i = 0; i < DPL; ++i) {
-            const uint32_t d = lane + kWave * i;
-            cur[i] = nxt[i] = 0;
-            if (d < F) {
-                cur[i] = cursors[(uint64_t)g * F + d];
-                nxt[i] = s.last ? part_start[(uint64_t)s.r * F + d] + part_count[(uint64_t)s.r * F + d]
-                                : cursors[(uint64_t)(g + 1) * F + d];
-            }
-        }
-    };
-    const auto fetch_ents = [&](const Seg &s, uint32_t slot) {
-        for (uint32_t i = tid; i < kPass2Ents; i += NT) L.ents[slot][i] = i < s.nent ? list[s.b + i] : 0ull;
-    };
-    // tile t of the segment in ents[slot]: item u of wave w = block t * BPT + u * NW + w,
-    // lane l its keys 4l..4l+3 (I16: .x/.y the four residuals, .z their four digits);
-    // entries past the segment are 0 (no block: every key masked out)
-    const auto load_tile = [&](uint32_t slot, uint32_t t, uint4(&k)[U]) -> uint32_t {
-        uint32_t vm = 0;
-#pragma unroll
-        for (uint32_t u = 0; u < U; ++u) {
-            const uint32_t idx = t * BPT + u * NW + wave;
-            const uint64_t en = idx < kPass2Ents ? L.ents[slot][idx] : 0ull;  // one address per wave
-            const uint32_t phys = __builtin_amdgcn_readfirstlane((uint32_t)en);
-            const uint32_t fill = __builtin_amdgcn_readfirstlane((uint32_t)(en >> 32));
-            if constexpr (I16) {
-                const uint16_t *b16 = reinterpret_cast<const uint16_t *>(in) + (uint64_t)phys * kBlk;
-                const uint64_t r = buf_ld_nt_u64(make_rsrc(b16, (fill * 2u + 3u) & ~3u), lane * 8u, 0);
-                const uint32_t dg = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(
-                    make_rsrc(side + (uint64_t)phys * kBlk, (fill + 3u) & ~3u), (int)(lane * 4u), 0, 2);
-                k[u] = make_uint4((uint32_t)r, (uint32_t)(r >> 32), dg, 0u);
-            } else {
-                k[u] = buf_ld_nt_u128(make_rsrc(in + (uint64_t)phys * kBlk, fill * 4u), lane * 16u, 0);
-            }
-            const uint32_t f = fill > 4 * lane ? min(fill - 4 * lane, 4u) : 0u;
-            vm |= ((1u << f) - 1u) << (4 * u);
-        }
-        return vm;
-    };
-    const auto place_tile = [&](const uint4(&k)[U], uint32_t vm) {
-#pragma unroll
-        for (uint32_t u = 0; u < U; ++u) {
-            if constexpr (I16) {
-                const uint32_t rr[2] = {k[u].x, k[u].y};
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    if ((vm >> (4 * u + j)) & 1u)
-                        L.res[atomicAdd(&L.pos[(k[u].z >> (8 * j)) & mask], 1u)] =
-                            (uint16_t)(rr[j >> 1] >> (16 * (j & 1)));
-            } else {
-                const uint32_t x[4] = {k[u].x, k[u].y, k[u].z, k[u].w};
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    if ((vm >> (4 * u + j)) & 1u)
-                        L.res[atomicAdd(&L.pos[(x[j] >> shift) & mask], 1u)] = (uint16_t)(x[j] >> rshift);
-            }
-        }
-    };
-    // the first PF tiles of the next segment load while the current one is copied out
-    uint4 pf[PF][U];
-    uint32_t pm[PF];
-    const auto load_head = [&](uint32_t slot) {
-#pragma unroll
-        for (uint32_t t = 0; t < PF; ++t) pm[t] = load_tile(slot, t, pf[t]);
-    };
-    // the segment's tiles: the head from pf, the rest streamed with one tile in flight
-    // while one is placed (two register sets, loads unconditional)
-    const auto place_segment = [&](uint32_t slot, uint32_t nt) {
-        uint4 ka[U], kb[U];
-        uint32_t ma = load_tile(slot, PF, ka);
-#pragma unroll
-        for (uint32_t t = 0; t < PF; ++t) {
-#pragma unroll
-            for (uint32_t u = 0; u < U; ++u)
-                asm volatile("" ::"v"(pf[t][u].x), "v"(pf[t][u].y), "v"(pf[t][u].z), "v"(pf[t][u].w));
-            place_tile(pf[t], pm[t]);
-        }
-        for (uint32_t t = PF; t < nt; t += 2) {
-            const uint32_t mb = load_tile(slot, t + 1, kb);
-#pragma unroll
-            for (uint32_t u = 0; u < U; ++u) asm volatile("" ::"v"(ka[u].x), "v"(ka[u].y), "v"(ka[u].z), "v"(ka[u].w));
-            place_tile(ka, ma);
-            if (t + 1 >= nt) break;
-            ma = load_tile(slot, t + 2, ka);
-#pragma unroll
-            for (uint32_t u = 0; u < U; ++u) asm volatile("" ::"v"(kb[u].x), "v"(kb[u].y), "v"(kb[u].z), "v"(kb[u].w));
-            place_tile(kb, mb);
-        }
-    };
-    // the run layout of the segment whose cursors are in cur / nxt (wave 0): counts,
-    // slot ranges of round_up8(count + 7) from a multiple of 8, run starts at dst mod 8
-    const auto layout = [&]() {
-        if (wave != 0) return;
-        uint32_t c[DPL], sl[DPL], tot = 0;
-#pragma unroll
-        for (uint32_t i = 0; i < DPL; ++i) {
-            c[i] = (uint32_t)(nxt[i] - cur[i]);
-            sl[i] = c[i] ? (c[i] + 7 + 7) & ~7u : 0u;
-        }
-        uint32_t base = 0;
-#pragma unroll
-        for (uint32_t i = 0; i < DPL; ++i) {
-            const uint32_t d = lane + kWave * i;
-            const uint32_t incl = wave_incl_scan_u32(sl[i]);
-            const uint32_t p = base + incl - sl[i];
-            if (d < F) {
-                L.pb[d] = p;
-                L.st[d] = L.pos[d] = p + (uint32_t)(cur[i] & 7);
-                L.dst[d] = cur[i];
-                L.cnt[d] = c[i];
-            }
-            base += __shfl(incl, kWave - 1, kWave);
-        }
-        (void)tot;
-        if (lane == 0) L.pb[F] = base;
-    };
-    // the runs out (k_place_seg's copy-out)
-    const auto copy_out = [&]() {
-        const uint32_t total = L.pb[F];
-        const uint32_t C = ((total + NW - 1) / NW + 7) & ~7u;
-        const uint32_t q0 = wave * C, q1 = min(total, q0 + C);
-        if (q0 >= q1) return;
-        uint32_t lo = 0, hi = F;
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (L.pb[mid] <= q0) lo = mid; else hi = mid;
-        }
-        for (uint32_t d = __builtin_amdgcn_readfirstlane(lo); d < F; ++d) {
-            if (__builtin_amdgcn_readfirstlane(L.pb[d]) >= q1) break;
-            const uint32_t rs = __builtin_amdgcn_readfirstlane(L.st[d]);
-            const uint32_t re = rs + __builtin_amdgcn_readfirstlane(L.cnt[d]);
-            const uint32_t a = max(rs, q0), z = min(re, q1);
-            if (a >= z) continue;
-            uint16_t *o = out + uni_u64(L.dst[d]);
-            o -= rs;
-            const uint32_t a8 = min((a + 7) & ~7u, z), z8 = max(z & ~7u, a8);
-            if (lane < a8 - a) o[a + lane] = L.res[a + lane];
-            if (lane < z - z8) o[z8 + lane] = L.res[z8 + lane];
-            for (uint32_t q = a8 + 8 * lane; q < z8; q += 8 * kWave)
-                __builtin_nontemporal_store(*reinterpret_cast<const u32x4_t *>(&L.res[q]),
-                                            reinterpret_cast<u32x4_t *>(o + q));
-        }
-    };
-    // prologue: the first segment's entries, cursors and head tiles
-    Seg sc = seg_of(g0);
-    fetch_ents(sc, 0);
-    if (wave == 0) fetch_cursors(g0, sc);
-    __syncthreads();
-    load_head(0);
-    for (uint32_t g = g0, it = 0; g < g1; g += WX, ++it) {
-        const uint32_t slot = it & 1u;
-        layout();  // (cur / nxt of g)
-        __syncthreads();  // pos / st / pb / dst / cnt set; the previous copy-out is done
-        place_segment(slot, (sc.nent + BPT - 1) / BPT);
-        const bool more = g + WX < g1;
-        if (more) {
-            sc = seg_of(g + WX);
-            fetch_ents(sc, slot ^ 1u);
-            if (wave == 0) fetch_cursors(g + WX, sc);
-        }
-        __syncthreads();  // the segment is placed; the next entries are in LDS
-        if (more) load_head(slot ^ 1u);
-        copy_out();
-        __syncthreads();  // the runs are out (res, the layout and ents[slot] are free)
-    }
-}
-
 // Elements per thread per tile: 8 tuples (32 KiB tiles); keys: 12 in the pooled pass 1
 // (24 KiB tiles; 16 spill 17-19 VGPRs at the 128-register cap), 16 in the block-list
 // pass 2 (larger tiles amortise the per-tile work: 0.75 -> 0.69 ms per 2^28 keys).
@@ -2249,20 +2004,6 @@ bool place_enabled() {
     }();
     return on;
 }
-uint32_t cu_count();
-// SGXAMD_PLACE_RUN=1 (development A/B switch, read once): the placement as k_place_run
-// (one workgroup per CU over a run of segments, the next segment's first tiles loaded
-// while the current one's runs are copied out) instead of k_place_seg.  Measured and
-// not the default (round 6, profiles/r06_place_run_ab.log): 0.33 / 0.32 ms per 2^28
-// keys with 2 tiles ahead against k_place_seg's 0.33 / 0.32, 4 ahead 0.34 / 0.33, 6
-// ahead 0.37, the whole next segment in registers 0.39.
-bool place_run_enabled() {
-    static const bool on = [] {
-        const char *e = std::getenv("SGXAMD_PLACE_RUN");
-        return e && std::atoi(e) == 1;
-    }();
-    return on;
-}
 template <typename T>
 hipError_t launch_scatter_blk_t(const void *in, const uint64_t *list, void *out, const SegMap &m, uint32_t grid,
                                 uint32_t shift, uint32_t bits, const uint64_t *cursors, hipStream_t s,
@@ -2281,19 +2022,9 @@ hipError_t launch_scatter_blk_t(const void *in, const uint64_t *list, void *out,
             // 16-byte boundary (each u16-wire destination's pass 2 starts on one)
             if (place && (reinterpret_cast<uintptr_t>(out) & 15u) != 0) return hipErrorInvalidValue;
             const uint32_t skip = place ? 1u : 0u;
-            const bool run = place && place_run_enabled();
-            const uint32_t grid_run = std::max<uint32_t>(8, std::min<uint32_t>(grid, cu_count()) & ~7u);
 #define SORT_CASE(B)                                                                                              \
     case B:                                                                                                       \
-        if (run && side16)                                                                                        \
-            hipLaunchKernelGGL((k_place_run<B, 1024, true>), dim3(grid_run), dim3(1024), 0, s, ik, side16, list,  \
-                               reinterpret_cast<uint16_t *>(out), m, shift, cursors, part_start, part_count,       \
-                               narrow);                                                                           \
-        else if (run)                                                                                             \
-            hipLaunchKernelGGL((k_place_run<B, 1024, false>), dim3(grid_run), dim3(1024), 0, s, ik, nullptr, list, \
-                               reinterpret_cast<uint16_t *>(out), m, shift, cursors, part_start, part_count,       \
-                               narrow);                                                                           \
-        else if (place && side16)                                                                                 \
+        if (place && side16)                                                                                      \
             hipLaunchKernelGGL((k_place_seg<B, SGXAMD_PLACE_NT, SGXAMD_PLACE_U, true>), dim3(grid),             \
                                dim3(SGXAMD_PLACE_NT), 0, s, ik, side16, list, reinterpret_cast<uint16_t *>(out), m, \
                                shift, cursors, part_start, part_count, narrow);                                   \
@@ -2301,7 +2032,7 @@ hipError_t launch_scatter_blk_t(const void *in, const uint64_t *list, void *out,
             hipLaunchKernelGGL((k_place_seg<B, SGXAMD_PLACE_NT, SGXAMD_PLACE_U, false>), dim3(grid),            \
                                dim3(SGXAMD_PLACE_NT), 0, s, ik, nullptr, list, reinterpret_cast<uint16_t *>(out), \
                                m, shift, cursors, part_start, part_count, narrow);                                \
-        if (!place || run) /* (k_place_seg sorts a wide relation itself) */                                      \
+        if (!place) /* (k_place_seg sorts a wide relation itself) */                                             \
             hipLaunchKernelGGL((k_sort_blk<B, SGXAMD_SORT_NT, SGXAMD_SORT_ITEMS>), dim3(grid), dim3(SGXAMD_SORT_NT), 0, \
                                s, ik, list, ok, m, shift, cursors, narrow, skip);                                 \
         break;
@@ -2479,6 +2210,98 @@ __global__ __launch_bounds__(kBlock) void k_block_list(PoolOut po, const uint64_
 hipError_t launch_block_list(const PoolOut &po, const uint64_t *lbase, uint64_t *list, uint32_t bits, hipStream_t s) {
     if (po.nseg == 0) return hipSuccess;
     hipLaunchKernelGGL(k_block_list, dim3(po.nseg), dim3(kBlock), 0, s, po, lbase, list, 1u << bits);
+    return hipGetLastError();
+}
+
+// k_pool_layout folded into the block list (round 6: one launch less per relation): every
+// workgroup scans the F <= 256 digit totals for the regions' list bases itself (one digit
+// per thread), and workgroup 0 also writes the pass-2 layout -- region tuple starts /
+// counts, list bases / lengths, the kPass2Ents-block segment table -- and the relation's
+// largest key, as k_pool_layout does.
+__global__ __launch_bounds__(kBlock) void k_block_list_l(PoolOut po, const uint64_t *__restrict__ totals, uint32_t F,
+                                                         uint64_t *__restrict__ start, uint64_t *__restrict__ count,
+                                                         uint64_t *__restrict__ lbase, uint64_t *__restrict__ lcount,
+                                                         uint32_t *__restrict__ seg_base, uint64_t *__restrict__ list) {
+    __shared__ uint32_t rank[kBlock];
+    __shared__ uint64_t pre[kBlock];  // the segment's first list position per digit
+    __shared__ uint64_t scratch[kBlock / kWave + 1];
+    __shared__ uint32_t kmax_all;
+    if (pool_guard_skip(po)) return;
+    constexpr uint64_t M40 = (1ull << 40) - 1;
+    const uint32_t g = blockIdx.x, d = threadIdx.x;
+    if (d == 0) kmax_all = 0;
+    const uint64_t v = d < F ? totals[d] : 0;
+    const uint64_t c = d < F ? po.cnt[(uint64_t)d * po.nseg + g] : 0;
+    const uint64_t blk = v >> 40;
+    uint64_t tot;
+    const uint64_t ex_b = block_excl_scan_u64(blk, scratch, &tot);
+    if (d < F) {
+        rank[d] = 0;
+        pre[d] = ex_b + (c >> 40);
+    }
+    if (g == 0) {  // (workgroup-uniform) the layout
+        const uint64_t tup = v & M40, ns = (blk + kPass2Ents - 1) / kPass2Ents;
+        const uint64_t ex_t = block_excl_scan_u64(tup, scratch, &tot);
+        uint64_t nsegs;
+        const uint64_t ex_s = block_excl_scan_u64(ns, scratch, &nsegs);
+        if (d < F) {
+            start[d] = ex_t;
+            count[d] = tup;
+            lbase[d] = ex_b;
+            lcount[d] = blk;
+            seg_base[d] = (uint32_t)ex_s;
+        }
+        if (d == 0) seg_base[F] = (uint32_t)nsegs;
+        if (po.zero8 && d < 8) po.zero8[d] = 0;
+        if (po.kmax) {  // the segments' largest keys -> the relation's, kmax[nseg]
+            uint32_t x = 0;
+            for (uint32_t i = d; i < po.nseg; i += kBlock) x = max(x, po.kmax[i]);
+            if (x) atomicMax(&kmax_all, x);
+            __syncthreads();
+            if (d == 0) po.kmax[po.nseg] = kmax_all;
+        }
+    }
+    __syncthreads();
+    const uint32_t used = po.used[g], base = g * po.pool_blocks;
+    constexpr int U = 8;
+    for (uint32_t k0 = threadIdx.x; k0 < used; k0 += U * kBlock) {
+        uint32_t info[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t k = k0 + u * kBlock;
+            info[u] = k < used ? po.binfo[base + k] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t k = k0 + u * kBlock;
+            if (k < used) {
+                const uint32_t dd = info[u] & 0xFFFFu;
+                const uint32_t rk = atomicAdd(&rank[dd], 1u);
+                list[pre[dd] + rk] = (uint64_t)(base + k) | ((uint64_t)(info[u] >> 16) << 32);
+            }
+        }
+    }
+}
+
+hipError_t launch_pool_layout_list(const PoolOut &po, uint32_t bits, uint64_t *totals, uint64_t *start,
+                                   uint64_t *count, uint64_t *lbase, uint64_t *lcount, uint32_t *seg_base,
+                                   uint64_t *list, hipStream_t s) {
+    const uint32_t F = 1u << bits;
+    if (po.zero8 && (F > kBlock || po.nseg == 0)) {  // (no k_block_list_l workgroup 0 to zero them)
+        hipError_t e = hipMemsetAsync(po.zero8, 0, 8 * sizeof(uint64_t), s);
+        if (e != hipSuccess) return e;
+    }
+    if (F > kBlock) {  // (a pass-1 digit past 8 bits: the separate layout workgroup)
+        hipError_t e = launch_pool_layout(po.cnt, po.nseg, bits, totals, start, count, lbase, lcount, seg_base, s,
+                                          po.kmax, po.guard, po.guard_shift);
+        if (e != hipSuccess) return e;
+        return launch_block_list(po, lbase, list, bits, s);
+    }
+    hipLaunchKernelGGL(k_scan_cols, dim3(F), dim3(kBlock), 0, s, po.cnt, po.nseg, totals, po.guard, po.guard_shift);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || po.nseg == 0) return e;
+    hipLaunchKernelGGL(k_block_list_l, dim3(po.nseg), dim3(kBlock), 0, s, po, totals, F, start, count, lbase, lcount,
+                       seg_base, list);
     return hipGetLastError();
 }
 
@@ -2781,8 +2604,8 @@ __global__ __launch_bounds__(kWave, 5) void k_hist_chain(const uint64_t *__restr
 hipError_t launch_hist_chain(const uint64_t *cnt, const uint64_t *tot, uint32_t nseg, const uint32_t *chain,
                              const uint64_t *list, const uint32_t *keys, const SegMap &m, uint32_t grid,
                              uint32_t shift2, uint32_t bits2, uint64_t *hist, hipStream_t s) {
-    if (grid == 0) return hipSuccess;
     if (nseg > kHistChainMaxSegs || bits2 < 2 || bits2 > 7) return hipErrorInvalidValue;
+    if (grid == 0) return hipSuccess;
     hipLaunchKernelGGL(k_hist_chain, dim3(grid), dim3(kWave), 0, s, cnt, tot, nseg, chain, list, keys, m, shift2,
                        bits2, hist);
     return hipGetLastError();
@@ -4646,12 +4469,15 @@ __global__ __launch_bounds__(kBlock) void k_make_tasks(const uint64_t *__restric
 
 hipError_t launch_make_tasks(const uint64_t *r_count, const uint64_t *s_count, uint64_t P, uint64_t *over,
                              uint32_t over_cap, uint64_t *meta, uint64_t s_chunk, hipStream_t s, uint64_t *zero,
-                             uint64_t *zero2, uint32_t nzero) {
+                             uint64_t *zero2, uint32_t nzero, bool zeroed) {
     // meta = result + 1 of the join's 8-word, 256-byte aligned result block: the whole
     // block in one aligned fill (meta's 48 bytes alone, 8-byte aligned, took three fill
-    // kernels: head, body and tail -- 13.7 us per join in the r05g trace)
-    hipError_t e = hipMemsetAsync(meta - 1, 0, 8 * sizeof(uint64_t), s);
-    if (e != hipSuccess) return e;
+    // kernels: head, body and tail -- 13.7 us per join in the r05g trace); none when R's
+    // pass-1 layout zeroed it (round 6, PoolOut::zero8)
+    if (!zeroed) {
+        hipError_t e = hipMemsetAsync(meta - 1, 0, 8 * sizeof(uint64_t), s);
+        if (e != hipSuccess) return e;
+    }
     uint32_t *n_over = reinterpret_cast<uint32_t *>(meta + 2);
     uint64_t blocks = (P + kBlock - 1) / kBlock;
     if (blocks > 1024) blocks = 1024;

@@ -85,8 +85,8 @@ print("paths ok")
                                  {"SGXAMD_DIGIT_SIDE": "1", "SGXAMD_BIG_JOIN": "1"},
                                  {"SGXAMD_SMALL_JOIN": "0"}, {"SGXAMD_SMALL_DIRECT": "0"},
                                  {"SGXAMD_POOL": "0"}, {"SGXAMD_POOL_SEGS": "3"}, {"SGXAMD_POOL_SEGS": "100000"},
-                                 {"SGXAMD_KEYS": "0"}, {"SGXAMD_SORT2": "0"}, {"SGXAMD_NARROW": "0"}, {"SGXAMD_JOIN_N": "0"}, {"SGXAMD_PLACE": "0"}, {"SGXAMD_PLACE_RUN": "1"}, {"SGXAMD_NARROW_POOL": "1"},
-                                 {"SGXAMD_NARROW_POOL": "1", "SGXAMD_PLACE_RUN": "0"}, {"SGXAMD_CHAIN_HIST": "0"},
+                                 {"SGXAMD_KEYS": "0"}, {"SGXAMD_SORT2": "0"}, {"SGXAMD_NARROW": "0"}, {"SGXAMD_JOIN_N": "0"}, {"SGXAMD_PLACE": "0"}, {"SGXAMD_NARROW_POOL": "1"},
+                                 {"SGXAMD_NARROW_POOL": "1", "SGXAMD_PLACE": "0"}, {"SGXAMD_CHAIN_HIST": "0"},
                                  {"SGXAMD_CHAIN_HIST": "0", "SGXAMD_POOL_SEGS": "3"}])
 def test_switch_paths_match_oracle(env):
     e = dict(os.environ, **env)
@@ -121,7 +121,7 @@ print("wire ok")
 """
 
 
-@pytest.mark.parametrize("env", [{"SGXAMD_WIRE16": "0"}, {"SGXAMD_NARROW": "0"}, {"SGXAMD_PLACE": "0"}, {"SGXAMD_PLACE_RUN": "1"},
+@pytest.mark.parametrize("env", [{"SGXAMD_WIRE16": "0"}, {"SGXAMD_NARROW": "0"}, {"SGXAMD_PLACE": "0"},
                                  {"SGXAMD_WIRE_GATHER": "1"},
                                  {"SGXAMD_JOIN_N": "0"}, {"SGXAMD_CHAIN_HIST": "0"}, {"SGXAMD_PASS1_BITS": "6"},
                                  {"SGXAMD_POOL_SEGS": "3"}])
