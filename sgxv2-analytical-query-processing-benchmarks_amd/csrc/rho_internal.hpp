@@ -141,8 +141,14 @@ hipError_t launch_hist_side(const uint8_t *side, const SegMap &m, uint32_t grid,
 // instead of twice (histogram + scatter).
 constexpr uint32_t kBlkShift = 8;
 constexpr uint32_t kBlk = 1u << kBlkShift;          // elements per block (2 KiB of tuples, 1 KiB of keys)
+// 288 blocks (73,728 keys; k_place_seg's LDS copy of a narrow segment, 144 KiB of u16
+// residuals, is the limit): a 2^28-key fk relation's ~8,450 blocks per region make 30
+// segments (3,840, 15 per CU) instead of 33 at 256 (4,224: a 17th, half-empty round of
+// one-workgroup-per-CU placements) -- 2.413-2.422 vs 2.435-2.450 ms per step, round 6
+// (profiles/r06za_pass2_ents288_ab.log); 128 blocks (two placements per CU) measured
+// slower (r06s).
 #ifndef SGXAMD_PASS2_ENTS
-#define SGXAMD_PASS2_ENTS 256
+#define SGXAMD_PASS2_ENTS 288
 #endif
 constexpr uint32_t kPass2Ents = SGXAMD_PASS2_ENTS;  // blocks per pass-2 segment (LDS list copy)
 struct PoolOut {
