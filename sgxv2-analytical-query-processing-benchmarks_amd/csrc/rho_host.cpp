@@ -826,6 +826,7 @@ int join_finish(Context *ctx, PendingJoin &pj, const row_t *dS, uint64_t nS, mi3
     uint64_t *cyc = A.at<uint64_t>(pj.off_cyc);
     uint32_t *n_over = reinterpret_cast<uint32_t *>(result + 3);
     const uint32_t hash_shift = pj.key_shift + pol.bits;
+    uint64_t *fold_host = nullptr;  // (the count reduction's mapped result words)
     tm.mark("join_tasks");
     // narrow plans: k_join_n adds into the count and tick slots, zeroed here
     const bool nar = !pj.materialize && (pj.pr.narrow || pj.ps.narrow) && narrow_join_enabled();
@@ -846,15 +847,26 @@ int join_finish(Context *ctx, PendingJoin &pj, const row_t *dS, uint64_t nS, mi3
                                    A.at<uint32_t>(pj.ps.kmax) + pj.ps.nseg1, result, s));
     } else if (!pj.materialize) {
         tm.mark("join_build_probe");
-        // the 16,384-key table's k_join_x sums the count slots itself (k_reduce folded in)
+        // the 16,384-key table's k_join_x sums the count slots itself (k_reduce folded in),
+        // and writes the result words into mapped host memory too (no copy after it)
         const bool fold = algo == kAlgoChaining && pol.rcap == kBigRcap;
+        if (fold && !ctx->host_fold) {
+            void *dp = nullptr;
+            if (hipHostMalloc(reinterpret_cast<void **>(&ctx->host_fold), 8 * sizeof(uint64_t),
+                              hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
+                hipHostGetDevicePointer(&dp, ctx->host_fold, 0) == hipSuccess)
+                ctx->host_fold_dev = static_cast<uint64_t *>(dp);
+            else
+                (void)hipGetLastError();
+        }
+        fold_host = fold ? ctx->host_fold_dev : nullptr;
         RHO_HIP(launch_join(fR, fS, psR, pcR, psS, pcS, P, over, n_over, hash_shift, pol.rcap, pj.s_chunk, join_grid,
                             kJoinCount, algo, counts, nullptr, nullptr, cyc, s, nullptr, pj.pr.keys ? 1 : 2,
                             reinterpret_cast<uint32_t *>(result + 6),
                             pj.pr.narrow ? A.at<uint32_t>(pj.pr.kmax) + pj.pr.nseg1 : nullptr,
                             pj.ps.narrow ? A.at<uint32_t>(pj.ps.kmax) + pj.ps.nseg1 : nullptr,
                             (uint32_t)std::min<uint64_t>(P + pj.over_cap - 1, 0xFFFFFFFFull), nullptr,
-                            fold ? result : nullptr));
+                            fold ? result : nullptr, fold_host));
         if (!fold) {
             tm.mark("join_reduce");
             RHO_HIP(launch_reduce(counts, join_grid, result, cyc, join_grid, s));
@@ -888,8 +900,9 @@ int join_finish(Context *ctx, PendingJoin &pj, const row_t *dS, uint64_t nS, mi3
     }
     tm.end_call();
     if (s2) RHO_HIP(hipEventRecord(ctx->ev_t1, s));
-    RHO_HIP(hipMemcpyAsync(ctx->host_result, result, 7 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    if (!fold_host) RHO_HIP(hipMemcpyAsync(ctx->host_result, result, 7 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     RHO_HIP(hipStreamSynchronize(s));
+    if (fold_host) std::memcpy(ctx->host_result, ctx->host_fold, 7 * sizeof(uint64_t));
     if (std::getenv("SGXAMD_DEBUG_WG_TICKS") && !pj.materialize) {
         // development: the build/probe workgroups' wall-clock ticks (load balance)
         const uint32_t ng = std::min<uint32_t>(join_grid, 4096);

@@ -294,10 +294,13 @@ hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, 
                        uint64_t *cyc, hipStream_t s, const JoinReduce *reduce = nullptr, int key_stride = 2,
                        uint32_t *tickets = nullptr, const uint32_t *narrow_r = nullptr,
                        const uint32_t *narrow_s = nullptr, uint32_t tasks_max = 0,
-                       const uint64_t *small_kmax = nullptr, uint64_t *fold = nullptr);
+                       const uint64_t *small_kmax = nullptr, uint64_t *fold = nullptr,
+                       uint64_t *fold_host = nullptr);
 // fold (nullable; counting joins on the 16,384-key table, k_join_x): the join's 8-word
 // result block -- k_join_x's last workgroup sums the count and tick slots into
 // fold[0] / [4] / [5] (k_reduce's job; fold[7], zeroed by launch_make_tasks, is the
+// fold_host (nullable, with fold): mapped host memory that also receives the result
+// block's words 0..6 (the caller reads them after the stream synchronisation: no copy).
 // arrival ticket), whether k_join_x joined or k_join_n did.  Returns
 // hipErrorNotSupported (nothing launched) when the plan takes another kernel.
 // small_kmax (nullable; tuples, counting, the small joins' 1,024-thread chaining table):

@@ -3389,10 +3389,19 @@ __device__ __forceinline__ void join_x_body(
 // relations, idle): every workgroup arrives on res[7] after its slots are written; the
 // last sums the ncounts count slots and tick pairs (k_join_n's or k_join_x's) into
 // res[0] / [4] / [5].  Called by every thread of the workgroup.
+// x_fold_sum: the sums alone, by one workgroup (the narrow relations' path, whose count
+// slots an earlier launch, k_join_n, wrote: workgroup 0 sums them while the others return,
+// instead of every workgroup arriving on the ticket -- 256 device atomics on one word).
+// host (nullable): mapped host memory that also receives the result block's words 0..6
+// (the caller then needs no copy of them after the stream synchronisation).
+template <int BLOCK>
+__device__ __forceinline__ void x_fold_sum(const uint64_t *__restrict__ counts, const uint64_t *__restrict__ cyc,
+                                           uint32_t ncounts, uint64_t *__restrict__ res, uint64_t *red,
+                                           uint64_t *host);
 template <int BLOCK>
 __device__ __forceinline__ void x_fold_reduce(const uint64_t *__restrict__ counts, const uint64_t *__restrict__ cyc,
-                                              uint32_t ncounts, uint64_t *__restrict__ res, uint64_t *red) {
-    constexpr uint32_t NW = BLOCK / kWave;
+                                              uint32_t ncounts, uint64_t *__restrict__ res, uint64_t *red,
+                                              uint64_t *host) {
     __shared__ uint32_t last;
     __syncthreads();  // this workgroup's slot writes are issued
     if (threadIdx.x == 0) {
@@ -3402,6 +3411,13 @@ __device__ __forceinline__ void x_fold_reduce(const uint64_t *__restrict__ count
     __syncthreads();
     if (!last) return;
     __threadfence();
+    x_fold_sum<BLOCK>(counts, cyc, ncounts, res, red, host);
+}
+template <int BLOCK>
+__device__ __forceinline__ void x_fold_sum(const uint64_t *__restrict__ counts, const uint64_t *__restrict__ cyc,
+                                           uint32_t ncounts, uint64_t *__restrict__ res, uint64_t *red,
+                                           uint64_t *host) {
+    constexpr uint32_t NW = BLOCK / kWave;
     uint64_t c = 0, b = 0, p = 0;
     for (uint32_t i = threadIdx.x; i < ncounts; i += BLOCK) {
         c += __hip_atomic_load(&counts[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -3421,12 +3437,20 @@ __device__ __forceinline__ void x_fold_reduce(const uint64_t *__restrict__ count
         red[2 * NW + w] = p;
     }
     __syncthreads();
-    if (threadIdx.x < 3) {
+    const uint32_t tid = threadIdx.x;
+    if (tid < 3) {
         uint64_t t = 0;
-        for (uint32_t k = 0; k < NW; ++k) t += red[threadIdx.x * NW + k];
-        if (threadIdx.x == 0) res[0] = t;
-        else if (cyc) res[3 + threadIdx.x] = t;
+        for (uint32_t k = 0; k < NW; ++k) t += red[tid * NW + k];
+        if (tid == 0) res[0] = t;
+        else if (cyc) res[3 + tid] = t;
+        if (host && (tid == 0 || cyc)) host[tid == 0 ? 0 : 3 + tid] = t;
+    } else if (host && tid >= kWave && tid < kWave + 7) {
+        // the words earlier launches wrote (largest partitions, extra tasks, the widths)
+        const uint32_t w = tid - kWave;
+        if (!(w == 0 || (cyc && (w == 4 || w == 5))))
+            host[w] = __hip_atomic_load(&res[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    if (host) __threadfence_system();
 }
 
 template <int RCAP, int BLOCK, int UP, int KS = 1>
@@ -3437,13 +3461,14 @@ __global__ __launch_bounds__(BLOCK, 1) void k_join_x(
     uint64_t s_chunk, uint64_t *__restrict__ counts, uint64_t *__restrict__ cyc, uint64_t *__restrict__ red_result,
     uint64_t *__restrict__ red_ticket, uint32_t ncounts, uint32_t *__restrict__ tickets,
     const uint32_t *__restrict__ narrow_r, const uint32_t *__restrict__ narrow_s, uint32_t skip_narrow,
-    uint64_t *__restrict__ fold) {
+    uint64_t *__restrict__ fold, uint64_t *fold_host) {
     __shared__ JoinLdsX<RCAP, BLOCK / kWave> L;
     // (the same test as k_sort_blk's, which wrote the partitions)
     const bool nr = narrow_r != nullptr && ((*narrow_r >> hash_shift) >> 16) == 0;
     const bool ns = narrow_s != nullptr && ((*narrow_s >> hash_shift) >> 16) == 0;
     if (skip_narrow && (nr || ns)) {  // k_join_n, launched beside it, joined them
-        if (fold) x_fold_reduce<BLOCK>(counts, cyc, ncounts, fold, reinterpret_cast<uint64_t *>(L.head));
+        if (fold && blockIdx.x == 0)
+            x_fold_sum<BLOCK>(counts, cyc, ncounts, fold, reinterpret_cast<uint64_t *>(L.head), fold_host);
         return;
     }
     // the direct table's counters: residuals below 2^(the fewest residual bits of a narrow
@@ -3474,7 +3499,7 @@ __global__ __launch_bounds__(BLOCK, 1) void k_join_x(
     }
 #undef JOIN_X_BODY
 #undef JOIN_X_BODY_U
-    if (fold) x_fold_reduce<BLOCK>(counts, cyc, ncounts, fold, reinterpret_cast<uint64_t *>(L.head));
+    if (fold) x_fold_reduce<BLOCK>(counts, cyc, ncounts, fold, reinterpret_cast<uint64_t *>(L.head), fold_host);
 }
 
 // ------------------------------------------- narrow build/probe (round 5) ---
@@ -4257,7 +4282,7 @@ hipError_t launch_join_keys(const void *R, const void *S, const uint64_t *r_star
                             const uint32_t *n_over, uint32_t hash_shift, uint32_t rcap, uint64_t s_chunk,
                             uint32_t grid, int mode, int algo, uint64_t *counts, uint64_t *cyc, hipStream_t s,
                             const JoinReduce *reduce, uint32_t *tickets, const uint32_t *narrow_r,
-                            const uint32_t *narrow_s, uint32_t tasks_max, uint64_t *fold) {
+                            const uint32_t *narrow_s, uint32_t tasks_max, uint64_t *fold, uint64_t *fold_host) {
     if (mode != kJoinCount) return hipErrorInvalidValue;
     if (fold && (reduce || algo != kAlgoChaining || rcap != kBigRcap)) return hipErrorNotSupported;
     // narrow partitions are read by the 16,384-key chaining table only
@@ -4305,7 +4330,7 @@ hipError_t launch_join_keys(const void *R, const void *S, const uint64_t *r_star
         }
         hipLaunchKernelGGL((k_join_x<kBigRcap, 1024, 8, 1>), dim3(std::min<uint32_t>(grid, cu_count())), dim3(1024), 0,
                            s, R64, S64, r_start, r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts,
-                           cyc, rres, rtick, grid, tickets, narrow_r, narrow_s, nar ? 1u : 0u, fold);
+                           cyc, rres, rtick, grid, tickets, narrow_r, narrow_s, nar ? 1u : 0u, fold, fold ? fold_host : nullptr);
         return hipGetLastError();
     }
 #define KEYS_CASE(RC)                                                                                                   case RC:                                                                                                                hipLaunchKernelGGL((k_join<RC, kJoinCount, kBlock, 1>), dim3(grid), dim3(kBlock), 0, s, R64, S64, r_start,                            r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts, nullptr, nullptr,                             cyc, rres, rtick);                                                                               break;
@@ -4339,7 +4364,7 @@ hipError_t launch_join_pieces(const void *R, const uint64_t *r_start, const uint
     hipLaunchKernelGGL((k_join_x<kBigRcap, 1024, 8, 1>), dim3(std::min<uint32_t>(grid, cu_count())), dim3(1024), 0, s,
                        R64, reinterpret_cast<const uint64_t *>(s16), r_start, r_count, r_start, r_count, P, over,
                        n_over, hash_shift, s_chunk, counts, cyc, nullptr, nullptr, grid, tickets, narrow_r, narrow_s,
-                       1u, fold);
+                       1u, fold, nullptr);
     return hipGetLastError();
 }
 
@@ -4349,10 +4374,11 @@ hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, 
                        int mode, int algo, uint64_t *counts, const uint64_t *task_off, output_triple_t *out,
                        uint64_t *cyc, hipStream_t s, const JoinReduce *reduce, int key_stride, uint32_t *tickets,
                        const uint32_t *narrow_r, const uint32_t *narrow_s, uint32_t tasks_max,
-                       const uint64_t *small_kmax, uint64_t *fold) {
+                       const uint64_t *small_kmax, uint64_t *fold, uint64_t *fold_host) {
     if (key_stride == 1)
         return launch_join_keys(R, S, r_start, r_count, s_start, s_count, P, over, n_over, hash_shift, rcap, s_chunk,
-                                grid, mode, algo, counts, cyc, s, reduce, tickets, narrow_r, narrow_s, tasks_max, fold);
+                                grid, mode, algo, counts, cyc, s, reduce, tickets, narrow_r, narrow_s, tasks_max, fold,
+                                fold_host);
     if (fold && (mode != kJoinCount || reduce || algo == kAlgoHistogram || rcap != kBigRcap))
         return hipErrorNotSupported;
     if (narrow_r || narrow_s) return hipErrorInvalidValue;
@@ -4388,7 +4414,7 @@ hipError_t launch_join(const row_t *R, const row_t *S, const uint64_t *r_start, 
         if (mode != kJoinCount) return hipErrorInvalidValue;
         hipLaunchKernelGGL((k_join_x<kBigRcap, 1024, 8, 2>), dim3(std::min<uint32_t>(grid, cu_count())), dim3(1024), 0,
                            s, R64, S64, r_start, r_count, s_start, s_count, P, over, n_over, hash_shift, s_chunk, counts,
-                           cyc, rres, rtick, grid, tickets, nullptr, nullptr, 0u, fold);
+                           cyc, rres, rtick, grid, tickets, nullptr, nullptr, 0u, fold, fold ? fold_host : nullptr);
     } else if (mode == kJoinCount && grid <= 512 && rcap <= 4096) {
         // few tasks (small joins: one workgroup per CU at most): 1,024 threads per table
         // instead of 256, so that a CU holds 16 waves to hide the load latencies

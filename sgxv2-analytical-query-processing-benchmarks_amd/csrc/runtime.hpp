@@ -91,6 +91,9 @@ struct Context {
     DeviceBuffer scan_in, scan_out, scan_aux, scan_dict;
     uint64_t *host_result = nullptr;  // pinned 64 x u64
     uint64_t *host_join = nullptr;    // coherent, mapped 8 x u64: written by the small join's kernel
+    // coherent, mapped 8 x u64 (and its device address): the result words the large join's
+    // count reduction writes (k_join_x's fold), read after the stream synchronisation
+    uint64_t *host_fold = nullptr, *host_fold_dev = nullptr;
     // multi-GPU exchange workspace (multi_host.cpp): shard-partitioned send buffers and
     // the receive buffers the peers' pieces land in
     DeviceBuffer xsendR, xsendS, xrecvR, xrecvS;
