@@ -119,6 +119,14 @@ class _LibraryLocalJoin:
             res = rho_join(self.R, self.nR, S, nS, key_shift=self.shift, algorithm=self.algorithm)
         return res.matches, res.stats
 
+    def join(self, R, S):
+        """One rank: the whole join in one library call (no exchange to overlap R's passes
+        with; 2.396 vs 2.402 ms per config-2 step for begin + finish, and bench.py's step
+        was 2.413 through them, scripts/dev/host_gap.py)."""
+        res = rho_join(R, R.numel(), S, S.numel(), stream=_stream_of(R) if R.is_cuda else None,
+                       algorithm=self.algorithm)
+        return res.matches, res.stats
+
 
 class _InjectedLocalJoin:
     """A caller-supplied local_join_fn(R, nR, S, nS, shift) seen through begin/finish."""
@@ -328,9 +336,12 @@ def sharded_rho_join(R: torch.Tensor, S: torch.Tensor, *, group=None, partition_
     sync = (lambda: torch.cuda.synchronize()) if R.is_cuda else (lambda: None)
     t0 = time.perf_counter()
     if world == 1:
-        local.begin(R, R.numel(), S.numel(), 0)
-        m, st = local.finish(S, S.numel())
-        sync()
+        if isinstance(local, _LibraryLocalJoin):  # (blocking: no device synchronisation after it)
+            m, st = local.join(R, S)
+        else:
+            local.begin(R, R.numel(), S.numel(), 0)
+            m, st = local.finish(S, S.numel())
+            sync()
         ms["local_join"] = (time.perf_counter() - t0) * 1e3
         return ShardedJoinResult(int(m), int(m), R.numel(), S.numel(), ms, st)
 
