@@ -30,7 +30,7 @@ sys.path.insert(0, os.path.join(PKG, "python"))
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 TABLE_STEPS = 3  # untimed full-timing steps after a timed region (per-kernel table)
 METRIC = "M probed tuples/sec (RHO join) + scan GB/s vs HBM roofline, 1/2/4/8 MI355X"
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic_r06t.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic_r06zm.json")
 
 
 def log(*a):
