@@ -448,10 +448,20 @@ __global__ __launch_bounds__(kMaxF) void k_scan_regions(uint64_t *__restrict__ h
     const uint32_t r = blockIdx.x, tid = threadIdx.x;
     const uint32_t S = kMaxF / F, d = tid % F, j = tid / F;
     const uint32_t sb = seg_base[r], se = seg_base[r + 1];
+    const uint64_t rs = reg_start[r];
     const uint32_t per = (se - sb + S - 1) / S;
     const uint32_t g0 = min(se, sb + j * per), g1 = min(se, g0 + per);
+    // The first kKeep counts of the chunk stay in registers for the cursor pass below
+    // (all of them at the bench's ~31 segments per region), so the column is read once.
+    constexpr uint32_t kKeep = 12;
+    uint64_t keep[kKeep];
     uint64_t sum = 0;
-    for (uint32_t g = g0; g < g1; ++g) sum += hist[(uint64_t)g * F + d];
+#pragma unroll
+    for (uint32_t i = 0; i < kKeep; ++i) {
+        keep[i] = g0 + i < g1 ? hist[(uint64_t)(g0 + i) * F + d] : 0;
+        sum += keep[i];
+    }
+    for (uint32_t g = g0 + kKeep; g < g1; ++g) sum += hist[(uint64_t)g * F + d];
     part[tid] = sum;
     __syncthreads();
     uint64_t total = 0;
@@ -466,14 +476,20 @@ __global__ __launch_bounds__(kMaxF) void k_scan_regions(uint64_t *__restrict__ h
     const uint64_t ex = block_excl_scan_u64(j == 0 ? (pad ? (total + 7) & ~7ull : total) : 0, scratch,
                                             &tot);  // digits are tids 0..F-1
     if (j == 0) {
-        const uint64_t start = (pad ? (reg_start[r] + 8ull * F * r + 7) & ~7ull : reg_start[r]) + ex;
+        const uint64_t start = (pad ? (rs + 8ull * F * r + 7) & ~7ull : rs) + ex;
         startd[d] = start;
         part_start[(uint64_t)r * F + d] = start;
         part_count[(uint64_t)r * F + d] = total;
     }
     __syncthreads();
     uint64_t run = startd[d] + part[tid];
-    for (uint32_t g = g0; g < g1; ++g) {
+#pragma unroll
+    for (uint32_t i = 0; i < kKeep; ++i)
+        if (g0 + i < g1) {
+            hist[(uint64_t)(g0 + i) * F + d] = run;
+            run += keep[i];
+        }
+    for (uint32_t g = g0 + kKeep; g < g1; ++g) {
         const uint64_t c = hist[(uint64_t)g * F + d];
         hist[(uint64_t)g * F + d] = run;
         run += c;
